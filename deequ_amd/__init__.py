@@ -1,0 +1,22 @@
+"""deequ_amd -- MI355X-native backend for deequ's metric-computation hot path.
+
+The public names mirror the reference's Scala API (`com.amazon.deequ.analyzers`,
+`...analyzers.runners`): analyzers, states, `AnalysisRunner`, `AnalyzerContext`.  All compute
+goes through the C-ABI library `libdeequ_amd.so` (hand-written gfx950 HIP kernels); there is
+no CPU fallback.
+"""
+from .analyzers import (Analyzer, ApproxCountDistinct, Completeness, Compliance, Maximum, Mean,
+                        Minimum, Preconditions, ScanShareableAnalyzer, Size, StandardDeviation,
+                        StandardScanShareableAnalyzer, Sum)
+from .engine import Plan, current_device, run_scan, set_device
+from .metrics import (DoubleMetric, EmptyStateException, Entity, Failure,
+                      IllegalAnalyzerParameterException, MetricCalculationException,
+                      MetricCalculationRuntimeException, NoSuchColumnException, Success,
+                      WrongColumnTypeException)
+from .runner import (Analysis, AnalysisRunBuilder, AnalysisRunner, AnalyzerContext,
+                     InMemoryStateProvider)
+from .states import (ApproxCountDistinctState, MaxState, MeanState, MinState, NumMatches,
+                     NumMatchesAndCount, StandardDeviationState, State, SumState)
+from .table import Column, PartitionedTable, Table
+
+__all__ = [n for n in dir() if not n.startswith("_")]

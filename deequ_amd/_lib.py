@@ -1,0 +1,147 @@
+"""ctypes binding of the deequ_amd C-ABI (include/deequ_amd.h).
+
+The shared library is built in-tree (`deequ_amd/libdeequ_amd.so`, see
+`deequ_amd/csrc/Makefile` / `__graft_entry__.build()`).  There is no fallback: if the
+library is missing, importing the compute entry points raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (POINTER, Structure, c_char_p, c_double, c_int, c_int32, c_int64, c_size_t,
+                    c_uint8, c_uint64, c_void_p)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdeequ_amd.so")
+
+# ---------------------------------------------------------------- enums (mirror the header)
+DQ_OK, DQ_ERR_INVALID, DQ_ERR_UNSUPPORTED, DQ_ERR_DEVICE, DQ_ERR_OOM, DQ_ERR_STATE = range(6)
+
+DQ_T_BOOL, DQ_T_INT8, DQ_T_INT16, DQ_T_INT32, DQ_T_INT64, DQ_T_FLOAT32, DQ_T_FLOAT64, DQ_T_UTF8 = range(1, 9)
+DQ_COL_DEVICE = 0x1
+
+(DQ_OP_SIZE, DQ_OP_COMPLETENESS, DQ_OP_COMPLIANCE, DQ_OP_SUM, DQ_OP_MEAN, DQ_OP_STDDEV,
+ DQ_OP_MINIMUM, DQ_OP_MAXIMUM, DQ_OP_APPROX_COUNT_DISTINCT) = range(1, 10)
+
+DQ_P_COLUMN, DQ_P_LIT_INT, DQ_P_LIT_FLOAT, DQ_P_LIT_NULL, DQ_P_COALESCE, DQ_P_LIT_STRING = 1, 2, 3, 4, 5, 6
+DQ_P_EQ, DQ_P_NE, DQ_P_LT, DQ_P_LE, DQ_P_GT, DQ_P_GE, DQ_P_EQ_NULLSAFE = 10, 11, 12, 13, 14, 15, 16
+DQ_P_IS_NULL, DQ_P_IS_NOT_NULL = 20, 21
+DQ_P_AND, DQ_P_OR, DQ_P_NOT, DQ_P_TRUE, DQ_P_FALSE = 30, 31, 32, 33, 34
+DQ_CMP_AS_INT64, DQ_CMP_AS_FLOAT64 = 0, 1
+
+DQ_HLL_NUM_WORDS = 52
+
+TYPE_CODES = {
+    "bool": DQ_T_BOOL, "int8": DQ_T_INT8, "int16": DQ_T_INT16, "int32": DQ_T_INT32,
+    "int64": DQ_T_INT64, "float32": DQ_T_FLOAT32, "float64": DQ_T_FLOAT64, "string": DQ_T_UTF8,
+}
+
+
+class DqColumn(Structure):
+    _fields_ = [("type", c_int32), ("flags", c_int32), ("length", c_int64), ("offset", c_int64),
+                ("validity", c_void_p), ("values", c_void_p), ("offsets", c_void_p)]
+
+
+class DqPredInsn(Structure):
+    _fields_ = [("opcode", c_int32), ("arg", c_int32), ("i64", c_int64), ("f64", c_double)]
+
+
+class DqPredicate(Structure):
+    _fields_ = [("code", POINTER(DqPredInsn)), ("n_insns", c_int32), ("strings_len", c_int32),
+                ("strings", c_void_p)]
+
+
+class DqOp(Structure):
+    _fields_ = [("kind", c_int32), ("column", c_int32), ("predicate", DqPredicate),
+                ("where", DqPredicate)]
+
+
+class DqState(Structure):
+    _fields_ = [("kind", c_int32), ("has_value", c_int32), ("num_matches", c_int64),
+                ("count", c_int64), ("sum", c_double), ("n", c_double), ("avg", c_double),
+                ("m2", c_double), ("value", c_double), ("words", c_int64 * DQ_HLL_NUM_WORDS)]
+
+
+# every symbol include/deequ_amd.h declares, with its ctypes signature
+SIGNATURES = {
+    "dq_last_error": (c_char_p, []),
+    "dq_abi_version": (c_int, []),
+    "dq_device_count": (c_int, [POINTER(c_int)]),
+    "dq_ctx_create": (c_int, [c_int, c_int, POINTER(c_void_p)]),
+    "dq_ctx_destroy": (c_int, [c_void_p]),
+    "dq_plan_create": (c_int, [c_void_p, POINTER(DqOp), c_int, POINTER(c_int32), c_int, POINTER(c_void_p)]),
+    "dq_plan_destroy": (c_int, [c_void_p]),
+    "dq_op_supported": (c_int, [POINTER(DqOp), POINTER(c_int32), c_int]),
+    "dq_plan_consume": (c_int, [c_void_p, POINTER(DqColumn), c_int, c_int64]),
+    "dq_plan_finish": (c_int, [c_void_p, POINTER(DqState), c_int]),
+    "dq_plan_reset": (c_int, [c_void_p]),
+    "dq_plan_stream": (c_void_p, [c_void_p]),
+    "dq_state_merge": (c_int, [POINTER(DqState), POINTER(DqState), POINTER(DqState)]),
+    "dq_state_metric": (c_int, [POINTER(DqState), POINTER(c_double)]),
+    "dq_hll_count": (c_double, [POINTER(c_int64)]),
+    "dq_hll_merge": (None, [POINTER(c_int64), POINTER(c_int64), POINTER(c_int64)]),
+    "dq_hll_words_to_bytes": (None, [POINTER(c_int64), POINTER(c_uint8)]),
+    "dq_hll_words_from_bytes": (None, [POINTER(c_uint8), POINTER(c_int64)]),
+    "dq_xxh64": (c_uint64, [c_void_p, c_size_t, c_uint64]),
+}
+
+_lib = None
+
+
+class DeequAmdError(RuntimeError):
+    """A non-OK dq_status from the C-ABI (message from dq_last_error)."""
+
+    def __init__(self, status: int, message: str):
+        super().__init__("deequ_amd status %d: %s" % (status, message))
+        self.status = status
+
+
+class UnsupportedOnGpu(DeequAmdError):
+    """DQ_ERR_UNSUPPORTED: the reference would run this analyzer on Spark instead."""
+
+
+def lib():
+    """Load libdeequ_amd.so (raises if it has not been built -- there is no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("deequ_amd native library not built: %s (run "
+                              "`python -c 'import __graft_entry__ as g; g.build()'`)" % LIB_PATH)
+        l = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(l, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = l
+    return _lib
+
+
+def check(status: int):
+    if status != DQ_OK:
+        msg = lib().dq_last_error().decode("utf-8", "replace")
+        if status == DQ_ERR_UNSUPPORTED:
+            raise UnsupportedOnGpu(status, msg)
+        raise DeequAmdError(status, msg)
+
+
+def device_count() -> int:
+    n = c_int(0)
+    check(lib().dq_device_count(ctypes.byref(n)))
+    return n.value
+
+
+class Context:
+    """One dq_ctx per (process, device); created lazily."""
+
+    _by_device = {}
+
+    def __init__(self, device: int):
+        self.device = device
+        h = c_void_p()
+        check(lib().dq_ctx_create(device, 0, ctypes.byref(h)))
+        self.handle = h
+
+    @classmethod
+    def get(cls, device: int = 0) -> "Context":
+        if device not in cls._by_device:
+            cls._by_device[device] = Context(device)
+        return cls._by_device[device]

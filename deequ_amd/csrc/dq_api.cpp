@@ -1,0 +1,1138 @@
+// dq_api.cpp -- host side of the deequ_amd C-ABI (include/deequ_amd.h).
+//
+// Plays the role of AnalysisRunner.runScanningAnalyzers (runners/AnalysisRunner.scala:289-336)
+// for GPU-eligible analyzers: it groups the requested analyzers into fused scan tasks (one
+// per (column, where) pair, Compliance predicates riding along), HLL tasks and predicate
+// mask programs, launches one fused pass per batch, and maps the device aggregates back to
+// the exact Scala State values (fromAggregationResult in Size/Completeness/Compliance/Sum/
+// Mean/StandardDeviation/Minimum/Maximum/ApproxCountDistinct .scala) including Spark's NULL
+// -> None rules.  It also implements the State algebra (State.sum / metricValue) so GPU
+// states from several devices merge exactly like Spark partial states.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "dq_internal.h"
+#include "hll_p9_tables.h"
+
+using namespace dq;
+
+// ------------------------------------------------------------------------------ errors
+static thread_local std::string g_last_error;
+
+static dq_status fail(dq_status s, const std::string& msg) {
+  g_last_error = msg;
+  return s;
+}
+
+#define DQ_HIP(expr)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return fail(e_ == hipErrorOutOfMemory ? DQ_ERR_OOM : DQ_ERR_DEVICE,              \
+                  std::string(#expr) + " failed: " + hipGetErrorString(e_));           \
+  } while (0)
+
+#define DQ_TRY(expr)                 \
+  do {                               \
+    dq_status s_ = (expr);           \
+    if (s_ != DQ_OK) return s_;      \
+  } while (0)
+
+extern "C" const char* dq_last_error(void) { return g_last_error.c_str(); }
+extern "C" int dq_abi_version(void) { return DQ_ABI_VERSION; }
+
+// ------------------------------------------------------------------------------ helpers
+static int type_size(int t) {
+  switch (t) {
+    case DQ_T_INT8: return 1;
+    case DQ_T_INT16: return 2;
+    case DQ_T_INT32: return 4;
+    case DQ_T_INT64: return 8;
+    case DQ_T_FLOAT32: return 4;
+    case DQ_T_FLOAT64: return 8;
+    default: return 0;  // BOOL (bits), UTF8 (variable)
+  }
+}
+static bool is_numeric(int t) { return t >= DQ_T_INT8 && t <= DQ_T_FLOAT64; }
+static bool is_integral(int t) { return t >= DQ_T_INT8 && t <= DQ_T_INT64; }
+static bool valid_type(int t) { return t >= DQ_T_BOOL && t <= DQ_T_UTF8; }
+
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t cap = 0;
+  ~DevBuf() {
+    if (ptr) (void)hipFree(ptr);
+  }
+  dq_status ensure(size_t bytes) {
+    if (bytes <= cap) return DQ_OK;
+    if (ptr) {
+      (void)hipFree(ptr);
+      ptr = nullptr;
+      cap = 0;
+    }
+    size_t want = std::max<size_t>(bytes, 256);
+    want = (want + 255) & ~(size_t)255;  // padded: kernels may read whole aligned words
+    DQ_HIP(hipMalloc(&ptr, want));
+    cap = want;
+    return DQ_OK;
+  }
+};
+
+// ------------------------------------------------------------------------------ context
+struct dq_ctx {
+  int device = 0;
+};
+
+extern "C" dq_status dq_device_count(int* out) {
+  if (!out) return fail(DQ_ERR_INVALID, "out is NULL");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) n = 0;
+  int gfx950 = 0;
+  for (int d = 0; d < n; ++d) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, d) == hipSuccess && std::strncmp(p.gcnArchName, "gfx950", 6) == 0)
+      ++gfx950;
+  }
+  *out = gfx950;
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_ctx_create(int device, int flags, dq_ctx** out) {
+  (void)flags;
+  if (!out) return fail(DQ_ERR_INVALID, "out is NULL");
+  *out = nullptr;
+  int n = 0;
+  DQ_HIP(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(DQ_ERR_INVALID, "device index out of range");
+  hipDeviceProp_t p;
+  DQ_HIP(hipGetDeviceProperties(&p, device));
+  if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0)
+    return fail(DQ_ERR_DEVICE, std::string("device is not gfx950 (MI355X): ") + p.gcnArchName);
+  dq_ctx* c = new dq_ctx();
+  c->device = device;
+  *out = c;
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_ctx_destroy(dq_ctx* ctx) {
+  delete ctx;
+  return DQ_OK;
+}
+
+// ------------------------------------------------------------------------------ predicates
+enum VT { V_INT = 0, V_FLT = 1, V_BOOL = 2, V_STR = 3 };
+
+struct Program {
+  std::vector<PredInsn> code;
+  std::vector<int> columns;  // referenced batch columns (sorted, unique)
+  std::string pool;          // string literals (DQ_P_LIT_STRING), offsets relative to this
+  std::string key;           // byte image for de-duplication
+};
+
+static dq_status validate_predicate(const dq_predicate& p, const int32_t* types, int n_cols,
+                                    Program* out) {
+  if (!p.code || p.n_insns <= 0) return fail(DQ_ERR_INVALID, "empty predicate");
+  if (p.n_insns > 256) return fail(DQ_ERR_UNSUPPORTED, "predicate too long");
+  std::vector<int> st;  // value types
+  Program prog;
+  for (int i = 0; i < p.n_insns; ++i) {
+    const dq_pred_insn& in = p.code[i];
+    PredInsn pi{in.opcode, in.arg, in.i64, in.f64};
+    switch (in.opcode) {
+      case DQ_P_COLUMN: {
+        if (in.arg < 0 || in.arg >= n_cols) return fail(DQ_ERR_INVALID, "predicate column out of range");
+        const int t = types[in.arg];
+        st.push_back(t == DQ_T_UTF8 ? V_STR : t == DQ_T_BOOL ? V_BOOL : (is_integral(t) ? V_INT : V_FLT));
+        prog.columns.push_back(in.arg);
+        break;
+      }
+      case DQ_P_LIT_STRING: {
+        if (in.i64 < 0 || in.arg < 0 || !p.strings || in.i64 + in.arg > (int64_t)p.strings_len)
+          return fail(DQ_ERR_INVALID, "string literal outside the predicate's string pool");
+        st.push_back(V_STR);
+        break;
+      }
+      case DQ_P_LIT_INT: st.push_back(V_INT); break;
+      case DQ_P_LIT_FLOAT: st.push_back(V_FLT); break;
+      case DQ_P_LIT_NULL: st.push_back(V_INT); break;
+      case DQ_P_TRUE: case DQ_P_FALSE: st.push_back(V_BOOL); break;
+      case DQ_P_COALESCE: {
+        if (st.size() < 2) return fail(DQ_ERR_INVALID, "predicate stack underflow");
+        const int b = st.back(); st.pop_back();
+        const int a = st.back(); st.pop_back();
+        if ((a == V_BOOL) != (b == V_BOOL)) return fail(DQ_ERR_UNSUPPORTED, "COALESCE of mixed boolean/numeric");
+        if ((a == V_STR) != (b == V_STR)) return fail(DQ_ERR_UNSUPPORTED, "COALESCE of mixed string/numeric");
+        st.push_back((a == V_FLT || b == V_FLT) ? V_FLT : a);
+        break;
+      }
+      case DQ_P_EQ: case DQ_P_NE: case DQ_P_LT: case DQ_P_LE: case DQ_P_GT: case DQ_P_GE:
+      case DQ_P_EQ_NULLSAFE: {
+        if (st.size() < 2) return fail(DQ_ERR_INVALID, "predicate stack underflow");
+        const int b = st.back(); st.pop_back();
+        const int a = st.back(); st.pop_back();
+        if (in.arg != DQ_CMP_AS_INT64 && in.arg != DQ_CMP_AS_FLOAT64)
+          return fail(DQ_ERR_INVALID, "comparison type must be DQ_CMP_AS_INT64 or DQ_CMP_AS_FLOAT64");
+        if (in.arg == DQ_CMP_AS_INT64 && (a == V_FLT || b == V_FLT))
+          return fail(DQ_ERR_INVALID, "int64 comparison of a floating-point operand");
+        if ((a == V_STR) != (b == V_STR))  // Spark would cast the string to double: not here
+          return fail(DQ_ERR_UNSUPPORTED, "comparison of a string with a non-string");
+        st.push_back(V_BOOL);
+        break;
+      }
+      case DQ_P_IS_NULL: case DQ_P_IS_NOT_NULL:
+        if (st.empty()) return fail(DQ_ERR_INVALID, "predicate stack underflow");
+        st.back() = V_BOOL;
+        break;
+      case DQ_P_NOT:
+        if (st.empty() || st.back() != V_BOOL) return fail(DQ_ERR_INVALID, "NOT of a non-boolean");
+        break;
+      case DQ_P_AND: case DQ_P_OR: {
+        if (st.size() < 2) return fail(DQ_ERR_INVALID, "predicate stack underflow");
+        const int b = st.back(); st.pop_back();
+        const int a = st.back(); st.pop_back();
+        if (a != V_BOOL || b != V_BOOL) return fail(DQ_ERR_INVALID, "AND/OR of a non-boolean");
+        st.push_back(V_BOOL);
+        break;
+      }
+      default:
+        return fail(DQ_ERR_UNSUPPORTED, "unknown predicate opcode " + std::to_string(in.opcode));
+    }
+    if ((int)st.size() > kMaxStack) return fail(DQ_ERR_UNSUPPORTED, "predicate stack too deep");
+    prog.code.push_back(pi);
+  }
+  if (st.size() != 1 || st.back() != V_BOOL)
+    return fail(DQ_ERR_INVALID, "predicate must leave exactly one boolean");
+  std::sort(prog.columns.begin(), prog.columns.end());
+  prog.columns.erase(std::unique(prog.columns.begin(), prog.columns.end()), prog.columns.end());
+  if (p.strings && p.strings_len > 0) prog.pool.assign(reinterpret_cast<const char*>(p.strings), p.strings_len);
+  prog.key.assign(reinterpret_cast<const char*>(prog.code.data()), prog.code.size() * sizeof(PredInsn));
+  prog.key += prog.pool;
+  if (out) *out = std::move(prog);
+  return DQ_OK;
+}
+
+static int cmp_of(int opcode) {
+  switch (opcode) {
+    case DQ_P_EQ: return CMP_EQ;
+    case DQ_P_NE: return CMP_NE;
+    case DQ_P_LT: return CMP_LT;
+    case DQ_P_LE: return CMP_LE;
+    case DQ_P_GT: return CMP_GT;
+    case DQ_P_GE: return CMP_GE;
+    case DQ_P_EQ_NULLSAFE: return CMP_EQNS;
+    default: return -1;
+  }
+}
+static int flip_cmp(int c) {
+  switch (c) {
+    case CMP_LT: return CMP_GT;
+    case CMP_LE: return CMP_GE;
+    case CMP_GT: return CMP_LT;
+    case CMP_GE: return CMP_LE;
+    default: return c;
+  }
+}
+
+// Recognise the forms the fused kernel evaluates inline on its primary column.  Returns the
+// referenced column (or -2 for a column-free constant) when `fp` was filled, else -1.
+static int fast_form(const Program& prog, const int32_t* types, FastPred* fp) {
+  const auto& c = prog.code;
+  std::memset(fp, 0, sizeof(*fp));
+  auto lit_ok = [](const PredInsn& in) { return in.opcode == DQ_P_LIT_INT || in.opcode == DQ_P_LIT_FLOAT; };
+  auto set_lit = [](const PredInsn& in, bool as_f64, int64_t* li, double* lf) -> bool {
+    if (as_f64) {
+      *lf = in.opcode == DQ_P_LIT_FLOAT ? in.f64 : (double)in.i64;
+      return true;
+    }
+    if (in.opcode != DQ_P_LIT_INT) return false;
+    *li = in.i64;
+    return true;
+  };
+  auto numeric_col = [&](const PredInsn& in) { return in.opcode == DQ_P_COLUMN && is_numeric(types[in.arg]); };
+  if (c.size() == 1 && (c[0].opcode == DQ_P_TRUE || c[0].opcode == DQ_P_FALSE)) {
+    fp->kind = FP_CONST;
+    fp->lit_i = c[0].opcode == DQ_P_TRUE ? 1 : 0;
+    return -2;
+  }
+  if (c.size() == 2 && c[0].opcode == DQ_P_COLUMN &&
+      (c[1].opcode == DQ_P_IS_NULL || c[1].opcode == DQ_P_IS_NOT_NULL)) {
+    fp->kind = c[1].opcode == DQ_P_IS_NULL ? FP_IS_NULL : FP_IS_NOT_NULL;
+    return c[0].arg;
+  }
+  if (c.size() == 3 && cmp_of(c[2].opcode) >= 0 && c[2].opcode != DQ_P_EQ_NULLSAFE) {
+    const bool as_f64 = c[2].arg == DQ_CMP_AS_FLOAT64;
+    int col = -1, op = cmp_of(c[2].opcode);
+    const PredInsn* lit = nullptr;
+    if (numeric_col(c[0]) && lit_ok(c[1])) {
+      col = c[0].arg;
+      lit = &c[1];
+    } else if (lit_ok(c[0]) && numeric_col(c[1])) {
+      col = c[1].arg;
+      lit = &c[0];
+      op = flip_cmp(op);
+    }
+    if (col < 0) return -1;
+    if (!as_f64 && !is_integral(types[col])) return -1;
+    fp->kind = FP_CMP;
+    fp->op = op;
+    fp->as_f64 = as_f64 ? 1 : 0;
+    if (!set_lit(*lit, as_f64, &fp->lit_i, &fp->lit_f)) return -1;
+    return col;
+  }
+  if (c.size() == 5 && numeric_col(c[0]) && lit_ok(c[1]) && c[2].opcode == DQ_P_COALESCE &&
+      lit_ok(c[3]) && cmp_of(c[4].opcode) >= 0 && c[4].opcode != DQ_P_EQ_NULLSAFE) {
+    const bool as_f64 = c[4].arg == DQ_CMP_AS_FLOAT64;
+    const int col = c[0].arg;
+    if (!as_f64 && !is_integral(types[col])) return -1;
+    fp->kind = FP_COALESCE_CMP;
+    fp->op = cmp_of(c[4].opcode);
+    fp->as_f64 = as_f64 ? 1 : 0;
+    if (!set_lit(c[3], as_f64, &fp->lit_i, &fp->lit_f)) return -1;
+    if (!set_lit(c[1], as_f64, &fp->coal_i, &fp->coal_f)) return -1;
+    return col;
+  }
+  return -1;
+}
+
+// ------------------------------------------------------------------------------ plan
+enum Target { TGT_HOST_SIZE = 0, TGT_SCAN = 1, TGT_HLL = 2 };
+
+struct OpSlot {
+  int kind;
+  int target;
+  int task;
+  int pred;        // COMPLIANCE: predicate slot within the task
+  bool has_where;
+};
+
+struct TaskBuild {
+  int primary;
+  int where_prog;  // -1 = none
+  ScanTask t;
+};
+
+// Scan tasks launched by one kernel specialisation (see launch_scan_group).
+struct ScanGroup {
+  int kind;   // 0 = validity/mask only, 1 = reads values
+  int ptype;  // value type (kind 1)
+  int np;     // inline predicates (kind 1)
+  std::vector<int32_t> tasks;
+  size_t dev_offset = 0;  // first entry in d_groups
+};
+
+struct dq_plan {
+  dq_ctx* ctx = nullptr;
+  hipStream_t stream = nullptr;
+  std::vector<int32_t> col_types;
+  std::vector<bool> col_used;
+  std::vector<OpSlot> slots;
+  std::vector<ScanTask> scan_tasks;
+  std::vector<ScanGroup> groups;
+  std::vector<HllTask> hll_tasks;
+  std::vector<Program> programs;  // generic predicate programs -> batch masks
+  // device state
+  DevBuf d_tasks, d_groups, d_ranges, d_hll, d_progs, d_insns, d_pool, d_acc, d_partials, d_regs,
+      d_cols, d_masks, d_mask_words;
+  std::vector<DevBuf> stage_values, stage_validity, stage_offsets;
+  int64_t mask_words = 0;
+  // pinned descriptor staging (DevColumn + DevMask arrays) guarded by an event
+  void* h_desc = nullptr;
+  size_t h_desc_size = 0;
+  hipEvent_t desc_done = nullptr;
+  bool desc_pending = false;
+  std::vector<std::vector<uint8_t>> host_tmp;  // realigned host buffers alive until sync
+  int64_t total_rows = 0;
+  int target_blocks = 2048;
+
+  ~dq_plan() {
+    if (stream) {
+      (void)hipStreamSynchronize(stream);
+    }
+    if (desc_done) (void)hipEventDestroy(desc_done);
+    if (h_desc) (void)hipHostFree(h_desc);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+static dq_status check_op(const dq_op& op, const int32_t* types, int n_cols) {
+  auto need_col = [&](bool numeric) -> dq_status {
+    if (op.column < 0 || op.column >= n_cols) return fail(DQ_ERR_INVALID, "op column out of range");
+    if (!valid_type(types[op.column])) return fail(DQ_ERR_INVALID, "invalid column type");
+    if (numeric && !is_numeric(types[op.column]))
+      return fail(DQ_ERR_UNSUPPORTED, "analyzer needs a numeric column (Preconditions.isNumeric)");
+    return DQ_OK;
+  };
+  switch (op.kind) {
+    case DQ_OP_SIZE: break;
+    case DQ_OP_COMPLETENESS: DQ_TRY(need_col(false)); break;
+    case DQ_OP_COMPLIANCE:
+      DQ_TRY(validate_predicate(op.predicate, types, n_cols, nullptr));
+      break;
+    case DQ_OP_SUM: case DQ_OP_MEAN: case DQ_OP_STDDEV: case DQ_OP_MINIMUM: case DQ_OP_MAXIMUM:
+      DQ_TRY(need_col(true));
+      break;
+    case DQ_OP_APPROX_COUNT_DISTINCT: DQ_TRY(need_col(false)); break;
+    default: return fail(DQ_ERR_UNSUPPORTED, "unknown op kind " + std::to_string(op.kind));
+  }
+  if (op.where.code && op.where.n_insns > 0)
+    DQ_TRY(validate_predicate(op.where, types, n_cols, nullptr));
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_op_supported(const dq_op* op, const int32_t* column_types, int n_columns) {
+  if (!op || (n_columns > 0 && !column_types)) return fail(DQ_ERR_INVALID, "NULL argument");
+  return check_op(*op, column_types, n_columns);
+}
+
+static int add_program(dq_plan* plan, Program&& prog) {
+  for (size_t i = 0; i < plan->programs.size(); ++i)
+    if (plan->programs[i].key == prog.key) return (int)i;
+  plan->programs.push_back(std::move(prog));
+  return (int)plan->programs.size() - 1;
+}
+
+extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
+                                    const int32_t* column_types, int n_columns, dq_plan** out) {
+  if (!out) return fail(DQ_ERR_INVALID, "out is NULL");
+  *out = nullptr;
+  if (!ctx || (n_ops > 0 && !ops) || n_columns < 0 || (n_columns > 0 && !column_types))
+    return fail(DQ_ERR_INVALID, "NULL argument");
+  for (int c = 0; c < n_columns; ++c)
+    if (!valid_type(column_types[c])) return fail(DQ_ERR_INVALID, "invalid column type");
+  for (int i = 0; i < n_ops; ++i) DQ_TRY(check_op(ops[i], column_types, n_columns));
+
+  DQ_HIP(hipSetDevice(ctx->device));
+  dq_plan* plan = new dq_plan();
+  plan->ctx = ctx;
+  plan->col_types.assign(column_types, column_types + n_columns);
+  plan->col_used.assign(n_columns, false);
+
+  std::vector<TaskBuild> tasks;
+  auto find_or_add_task = [&](int primary, int where_prog) -> int {
+    for (size_t i = 0; i < tasks.size(); ++i)
+      if (tasks[i].primary == primary && tasks[i].where_prog == where_prog) return (int)i;
+    TaskBuild tb;
+    tb.primary = primary;
+    tb.where_prog = where_prog;
+    std::memset(&tb.t, 0, sizeof(tb.t));
+    tb.t.primary = primary;
+    tb.t.ptype = primary >= 0 ? column_types[primary] : 0;
+    tb.t.where_mask = where_prog;
+    tb.t.flags = where_prog >= 0 ? TF_WHERE : 0;
+    if (primary >= 0) tb.t.flags |= TF_VALIDITY;
+    tasks.push_back(tb);
+    return (int)tasks.size() - 1;
+  };
+
+  dq_status st = DQ_OK;
+  for (int i = 0; i < n_ops && st == DQ_OK; ++i) {
+    const dq_op& op = ops[i];
+    OpSlot slot{op.kind, TGT_SCAN, -1, -1, false};
+    int where_prog = -1;
+    if (op.where.code && op.where.n_insns > 0) {
+      Program wp;
+      validate_predicate(op.where, column_types, n_columns, &wp);
+      for (int c : wp.columns) plan->col_used[c] = true;
+      where_prog = add_program(plan, std::move(wp));
+      slot.has_where = true;
+    }
+    switch (op.kind) {
+      case DQ_OP_SIZE: {
+        if (where_prog < 0) {
+          slot.target = TGT_HOST_SIZE;
+        } else {
+          int t = -1;  // any task with the same filter can count its rows
+          for (size_t k = 0; k < tasks.size(); ++k)
+            if (tasks[k].where_prog == where_prog) t = (int)k;
+          slot.task = t >= 0 ? t : find_or_add_task(-1, where_prog);
+        }
+        break;
+      }
+      case DQ_OP_COMPLETENESS:
+        plan->col_used[op.column] = true;
+        slot.task = find_or_add_task(op.column, where_prog);
+        break;
+      case DQ_OP_SUM: case DQ_OP_MEAN: case DQ_OP_STDDEV: case DQ_OP_MINIMUM: case DQ_OP_MAXIMUM: {
+        plan->col_used[op.column] = true;
+        slot.task = find_or_add_task(op.column, where_prog);
+        tasks[slot.task].t.flags |= TF_VALUES | TF_STATS;
+        break;
+      }
+      case DQ_OP_COMPLIANCE: {
+        Program pp;
+        validate_predicate(op.predicate, column_types, n_columns, &pp);
+        for (int c : pp.columns) plan->col_used[c] = true;
+        FastPred fp;
+        const int fcol = fast_form(pp, column_types, &fp);
+        int t;
+        if (fcol >= 0) {
+          t = find_or_add_task(fcol, where_prog);
+          if (fp.kind == FP_CMP || fp.kind == FP_COALESCE_CMP) tasks[t].t.flags |= TF_VALUES;
+        } else if (fcol == -2) {
+          t = -1;
+          for (size_t k = 0; k < tasks.size(); ++k)
+            if (tasks[k].where_prog == where_prog) t = (int)k;
+          if (t < 0) t = find_or_add_task(-1, where_prog);
+        } else {
+          const int prog = add_program(plan, std::move(pp));
+          fp.kind = FP_MASK;
+          fp.mask = prog;
+          t = -1;  // prefer an existing task with the same filter: masks need no values
+          for (size_t k = 0; k < tasks.size(); ++k)
+            if (tasks[k].where_prog == where_prog && tasks[k].t.n_preds < kMaxPreds) t = (int)k;
+          if (t < 0) t = find_or_add_task(-1, where_prog);
+        }
+        if (tasks[t].t.n_preds >= kMaxPreds) {
+          // task full: open a sibling task on the same column/filter
+          TaskBuild tb = tasks[t];
+          tb.t.n_preds = 0;
+          tb.t.flags &= ~TF_STATS;
+          tasks.push_back(tb);
+          t = (int)tasks.size() - 1;
+        }
+        slot.task = t;
+        slot.pred = tasks[t].t.n_preds;
+        tasks[t].t.preds[tasks[t].t.n_preds++] = fp;
+        break;
+      }
+      case DQ_OP_APPROX_COUNT_DISTINCT: {
+        plan->col_used[op.column] = true;
+        slot.target = TGT_HLL;
+        int t = -1;
+        for (size_t k = 0; k < plan->hll_tasks.size(); ++k)
+          if (plan->hll_tasks[k].column == op.column && plan->hll_tasks[k].where_mask == where_prog)
+            t = (int)k;
+        if (t < 0) {
+          plan->hll_tasks.push_back(HllTask{op.column, column_types[op.column], where_prog, 0});
+          t = (int)plan->hll_tasks.size() - 1;
+        }
+        slot.task = t;
+        break;
+      }
+      default: st = fail(DQ_ERR_UNSUPPORTED, "unknown op kind");
+    }
+    plan->slots.push_back(slot);
+  }
+  if (st != DQ_OK) {
+    delete plan;
+    return st;
+  }
+  for (auto& tb : tasks) plan->scan_tasks.push_back(tb.t);
+  // group tasks by kernel specialisation: (needs values, value type, #inline predicates)
+  std::vector<int32_t> group_ids;
+  for (size_t i = 0; i < plan->scan_tasks.size(); ++i) {
+    const ScanTask& t = plan->scan_tasks[i];
+    const int kind = (t.flags & TF_VALUES) ? 1 : 0;
+    const int ptype = kind ? t.ptype : 0;
+    const int np = kind ? (t.n_preds <= 4 ? t.n_preds : kMaxPreds) : 0;
+    ScanGroup* g = nullptr;
+    for (auto& gg : plan->groups)
+      if (gg.kind == kind && gg.ptype == ptype && gg.np == np) g = &gg;
+    if (!g) {
+      plan->groups.push_back(ScanGroup{kind, ptype, np, {}, 0});
+      g = &plan->groups.back();
+    }
+    g->tasks.push_back((int32_t)i);
+  }
+  for (auto& g : plan->groups) {
+    g.dev_offset = group_ids.size();
+    group_ids.insert(group_ids.end(), g.tasks.begin(), g.tasks.end());
+  }
+
+  // device-resident plan tables
+  auto upload = [&](DevBuf& buf, const void* src, size_t bytes) -> dq_status {
+    if (bytes == 0) return DQ_OK;
+    DQ_TRY(buf.ensure(bytes));
+    DQ_HIP(hipMemcpy(buf.ptr, src, bytes, hipMemcpyHostToDevice));
+    return DQ_OK;
+  };
+  std::vector<PredProgram> progs;
+  std::vector<PredInsn> insns;
+  std::string pool;
+  for (const auto& p : plan->programs) {
+    progs.push_back(PredProgram{(int32_t)insns.size(), (int32_t)p.code.size()});
+    for (PredInsn in : p.code) {
+      if (in.opcode == DQ_P_LIT_STRING) in.i64 += (int64_t)pool.size();  // plan-wide pool offset
+      insns.push_back(in);
+    }
+    pool += p.pool;
+  }
+  pool.append(8, '\0');
+  dq_status s = DQ_OK;
+  if ((s = upload(plan->d_tasks, plan->scan_tasks.data(), plan->scan_tasks.size() * sizeof(ScanTask))) != DQ_OK ||
+      (s = upload(plan->d_groups, group_ids.data(), group_ids.size() * sizeof(int32_t))) != DQ_OK ||
+      (s = plan->d_ranges.ensure(std::max<size_t>(1, plan->scan_tasks.size()) * sizeof(PartRange))) != DQ_OK ||
+      (s = upload(plan->d_hll, plan->hll_tasks.data(), plan->hll_tasks.size() * sizeof(HllTask))) != DQ_OK ||
+      (s = upload(plan->d_progs, progs.data(), progs.size() * sizeof(PredProgram))) != DQ_OK ||
+      (s = upload(plan->d_insns, insns.data(), insns.size() * sizeof(PredInsn))) != DQ_OK ||
+      (s = upload(plan->d_pool, pool.data(), pool.size())) != DQ_OK ||
+      (s = plan->d_acc.ensure(std::max<size_t>(1, plan->scan_tasks.size()) * sizeof(ScanAcc))) != DQ_OK ||
+      (s = plan->d_regs.ensure(std::max<size_t>(1, plan->hll_tasks.size()) * kHllM * sizeof(uint32_t))) != DQ_OK ||
+      (s = plan->d_cols.ensure(std::max(1, n_columns) * sizeof(DevColumn))) != DQ_OK ||
+      (s = plan->d_masks.ensure(std::max<size_t>(1, plan->programs.size()) * sizeof(DevMask))) != DQ_OK) {
+    delete plan;
+    return s;
+  }
+  hipError_t e = hipStreamCreateWithFlags(&plan->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&plan->desc_done, hipEventDisableTiming);
+  plan->h_desc_size = std::max(1, n_columns) * sizeof(DevColumn) +
+                      std::max<size_t>(1, plan->programs.size()) * sizeof(DevMask) +
+                      std::max<size_t>(1, plan->scan_tasks.size()) * sizeof(PartRange);
+  if (e == hipSuccess) e = hipHostMalloc(&plan->h_desc, plan->h_desc_size, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    delete plan;
+    return fail(DQ_ERR_DEVICE, std::string("stream/event/pinned allocation failed: ") + hipGetErrorString(e));
+  }
+  plan->stage_values.resize(n_columns);
+  plan->stage_validity.resize(n_columns);
+  plan->stage_offsets.resize(n_columns);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess)
+    plan->target_blocks = std::max(256, prop.multiProcessorCount * 8);
+  if ((s = dq_plan_reset(plan)) != DQ_OK) {
+    delete plan;
+    return s;
+  }
+  *out = plan;
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_plan_destroy(dq_plan* plan) {
+  delete plan;
+  return DQ_OK;
+}
+
+extern "C" void* dq_plan_stream(dq_plan* plan) { return plan ? (void*)plan->stream : nullptr; }
+
+extern "C" dq_status dq_plan_reset(dq_plan* plan) {
+  if (!plan) return fail(DQ_ERR_INVALID, "plan is NULL");
+  DQ_HIP(hipSetDevice(plan->ctx->device));
+  DQ_HIP(launch_init_acc(static_cast<ScanAcc*>(plan->d_acc.ptr), (int)plan->scan_tasks.size(), plan->stream));
+  if (!plan->hll_tasks.empty())
+    DQ_HIP(hipMemsetAsync(plan->d_regs.ptr, 0, plan->hll_tasks.size() * kHllM * sizeof(uint32_t), plan->stream));
+  DQ_HIP(hipStreamSynchronize(plan->stream));
+  plan->total_rows = 0;
+  return DQ_OK;
+}
+
+// Realign an LSB-first bitmap on the host: out bit i = in bit (off + i).
+static void host_realign(const uint8_t* src, int64_t off, int64_t n, std::vector<uint8_t>& dst) {
+  const int64_t nb = (n + 7) >> 3;
+  dst.assign((size_t)nb + 8, 0);
+  for (int64_t i = 0; i < n; ++i)
+    if ((src[(off + i) >> 3] >> ((off + i) & 7)) & 1u) dst[i >> 3] |= (uint8_t)(1u << (i & 7));
+}
+
+static dq_status prepare_column(dq_plan* plan, int c, const dq_column& col, int64_t n_rows,
+                                DevColumn* dc) {
+  const int t = plan->col_types[c];
+  if (col.type != t) return fail(DQ_ERR_INVALID, "column " + std::to_string(c) + " type differs from plan");
+  if (col.length < n_rows) return fail(DQ_ERR_INVALID, "column shorter than n_rows");
+  if (col.offset < 0) return fail(DQ_ERR_INVALID, "negative column offset");
+  if (!col.values && n_rows > 0) return fail(DQ_ERR_INVALID, "column values are NULL");
+  if (t == DQ_T_UTF8 && !col.offsets) return fail(DQ_ERR_INVALID, "utf8 column without offsets");
+  const bool device = (col.flags & DQ_COL_DEVICE) != 0;
+  const int64_t off = col.offset;
+  dc->type = t;
+  dc->pad = 0;
+  dc->offsets = nullptr;
+  dc->validity = nullptr;
+  const size_t vbytes = (size_t)((n_rows + 7) >> 3);
+
+  // ---- validity
+  if (col.validity) {
+    if (device) {
+      if ((off & 7) == 0) {
+        dc->validity = col.validity + (off >> 3);
+      } else {
+        DQ_TRY(plan->stage_validity[c].ensure(vbytes + 8));
+        DQ_HIP(launch_realign_bitmap(col.validity, off, n_rows,
+                                     static_cast<uint8_t*>(plan->stage_validity[c].ptr), plan->stream));
+        dc->validity = static_cast<const uint8_t*>(plan->stage_validity[c].ptr);
+      }
+    } else {
+      DQ_TRY(plan->stage_validity[c].ensure(vbytes + 8));
+      const uint8_t* src = col.validity + (off >> 3);
+      if (off & 7) {
+        plan->host_tmp.emplace_back();
+        host_realign(col.validity, off, n_rows, plan->host_tmp.back());
+        src = plan->host_tmp.back().data();
+      }
+      if (vbytes)
+        DQ_HIP(hipMemcpyAsync(plan->stage_validity[c].ptr, src, vbytes, hipMemcpyHostToDevice, plan->stream));
+      dc->validity = static_cast<const uint8_t*>(plan->stage_validity[c].ptr);
+    }
+  }
+  // ---- values
+  if (t == DQ_T_BOOL) {
+    if (device && (off & 7) == 0) {
+      dc->values = static_cast<const uint8_t*>(col.values) + (off >> 3);
+    } else if (device) {
+      DQ_TRY(plan->stage_values[c].ensure(vbytes + 8));
+      DQ_HIP(launch_realign_bitmap(static_cast<const uint8_t*>(col.values), off, n_rows,
+                                   static_cast<uint8_t*>(plan->stage_values[c].ptr), plan->stream));
+      dc->values = plan->stage_values[c].ptr;
+    } else {
+      DQ_TRY(plan->stage_values[c].ensure(vbytes + 8));
+      const uint8_t* src = static_cast<const uint8_t*>(col.values) + (off >> 3);
+      if (off & 7) {
+        plan->host_tmp.emplace_back();
+        host_realign(static_cast<const uint8_t*>(col.values), off, n_rows, plan->host_tmp.back());
+        src = plan->host_tmp.back().data();
+      }
+      if (vbytes)
+        DQ_HIP(hipMemcpyAsync(plan->stage_values[c].ptr, src, vbytes, hipMemcpyHostToDevice, plan->stream));
+      dc->values = plan->stage_values[c].ptr;
+    }
+  } else if (t == DQ_T_UTF8) {
+    const int32_t* offs = col.offsets + off;
+    if (device) {
+      dc->offsets = offs;
+      dc->values = col.values;
+    } else {
+      // rebase offsets to the batch's first byte and copy only the referenced bytes
+      int32_t first = n_rows > 0 ? offs[0] : 0;
+      int32_t last = n_rows > 0 ? offs[n_rows] : 0;
+      plan->host_tmp.emplace_back((size_t)(n_rows + 1) * sizeof(int32_t));
+      int32_t* reb = reinterpret_cast<int32_t*>(plan->host_tmp.back().data());
+      for (int64_t i = 0; i <= n_rows; ++i) reb[i] = offs[i] - first;
+      DQ_TRY(plan->stage_offsets[c].ensure((size_t)(n_rows + 1) * sizeof(int32_t)));
+      DQ_TRY(plan->stage_values[c].ensure((size_t)(last - first) + 16));
+      DQ_HIP(hipMemcpyAsync(plan->stage_offsets[c].ptr, reb, (size_t)(n_rows + 1) * sizeof(int32_t),
+                            hipMemcpyHostToDevice, plan->stream));
+      if (last > first)
+        DQ_HIP(hipMemcpyAsync(plan->stage_values[c].ptr, static_cast<const uint8_t*>(col.values) + first,
+                              (size_t)(last - first), hipMemcpyHostToDevice, plan->stream));
+      dc->offsets = static_cast<const int32_t*>(plan->stage_offsets[c].ptr);
+      dc->values = plan->stage_values[c].ptr;
+    }
+  } else {
+    const size_t es = (size_t)type_size(t);
+    const uint8_t* src = static_cast<const uint8_t*>(col.values) + (size_t)off * es;
+    const size_t bytes = (size_t)n_rows * es;
+    if (device && ((uintptr_t)src & 15) == 0) {
+      dc->values = src;
+    } else {
+      DQ_TRY(plan->stage_values[c].ensure(bytes + 16));
+      if (bytes)
+        DQ_HIP(hipMemcpyAsync(plan->stage_values[c].ptr, src, bytes,
+                              device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, plan->stream));
+      dc->values = plan->stage_values[c].ptr;
+    }
+  }
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, int n_columns,
+                                     int64_t n_rows) {
+  if (!plan) return fail(DQ_ERR_INVALID, "plan is NULL");
+  if (n_columns != (int)plan->col_types.size()) return fail(DQ_ERR_INVALID, "column count differs from plan");
+  if (n_rows < 0) return fail(DQ_ERR_INVALID, "negative n_rows");
+  if (n_columns > 0 && !columns) return fail(DQ_ERR_INVALID, "columns is NULL");
+  if (n_rows == 0) return DQ_OK;
+  if (n_rows > (int64_t)1 << 40) return fail(DQ_ERR_INVALID, "batch too large (split it)");
+  DQ_HIP(hipSetDevice(plan->ctx->device));
+
+  // the pinned descriptor block may still be in flight from the previous batch
+  if (plan->desc_pending) {
+    DQ_HIP(hipEventSynchronize(plan->desc_done));
+    plan->desc_pending = false;
+  }
+  DevColumn* h_cols = static_cast<DevColumn*>(plan->h_desc);
+  DevMask* h_masks = reinterpret_cast<DevMask*>(static_cast<uint8_t*>(plan->h_desc) +
+                                                std::max(1, n_columns) * sizeof(DevColumn));
+  bool any_host = false;
+  for (int c = 0; c < n_columns; ++c) {
+    std::memset(&h_cols[c], 0, sizeof(DevColumn));
+    if (!plan->col_used[c]) continue;
+    if (!(columns[c].flags & DQ_COL_DEVICE)) any_host = true;
+    DQ_TRY(prepare_column(plan, c, columns[c], n_rows, &h_cols[c]));
+  }
+  // generic predicates -> masks
+  const int n_progs = (int)plan->programs.size();
+  if (n_progs > 0) {
+    const int64_t wpm = ((n_rows + 63) >> 6) + 1;
+    DQ_TRY(plan->d_mask_words.ensure((size_t)wpm * 2 * n_progs * sizeof(uint64_t)));
+    plan->mask_words = wpm;
+    uint64_t* base = static_cast<uint64_t*>(plan->d_mask_words.ptr);
+    for (int p = 0; p < n_progs; ++p) {
+      h_masks[p].t = base + (int64_t)(2 * p) * wpm;
+      h_masks[p].nn = base + (int64_t)(2 * p + 1) * wpm;
+    }
+  }
+  // per-group grid sizes and where each task's block partials go for this batch
+  const int64_t chunks = (n_rows + kScanRowAlign - 1) / kScanRowAlign;
+  const int n_scan = (int)plan->scan_tasks.size();
+  PartRange* h_ranges = reinterpret_cast<PartRange*>(reinterpret_cast<uint8_t*>(h_masks) +
+                                                     std::max<size_t>(1, plan->programs.size()) * sizeof(DevMask));
+  std::vector<int64_t> group_bpt(plan->groups.size()), group_base(plan->groups.size());
+  int64_t part_total = 0;
+  for (size_t g = 0; g < plan->groups.size(); ++g) {
+    const int64_t ng = (int64_t)plan->groups[g].tasks.size();
+    int64_t bpt = (plan->target_blocks + ng - 1) / ng;
+    bpt = std::max<int64_t>(1, std::min<int64_t>(bpt, chunks));
+    group_bpt[g] = bpt;
+    group_base[g] = part_total;
+    for (int64_t i = 0; i < ng; ++i)
+      h_ranges[plan->groups[g].tasks[i]] = PartRange{part_total + i * bpt, (int32_t)bpt, 0};
+    part_total += bpt * ng;
+  }
+  if (n_scan > 0) DQ_TRY(plan->d_partials.ensure((size_t)part_total * sizeof(ScanAcc)));
+
+  DQ_HIP(hipMemcpyAsync(plan->d_cols.ptr, h_cols, n_columns * sizeof(DevColumn), hipMemcpyHostToDevice, plan->stream));
+  if (n_progs > 0)
+    DQ_HIP(hipMemcpyAsync(plan->d_masks.ptr, h_masks, n_progs * sizeof(DevMask), hipMemcpyHostToDevice, plan->stream));
+  if (n_scan > 0)
+    DQ_HIP(hipMemcpyAsync(plan->d_ranges.ptr, h_ranges, n_scan * sizeof(PartRange), hipMemcpyHostToDevice, plan->stream));
+  DQ_HIP(hipEventRecord(plan->desc_done, plan->stream));
+  plan->desc_pending = true;
+
+  const DevColumn* d_cols = static_cast<const DevColumn*>(plan->d_cols.ptr);
+  const DevMask* d_masks = static_cast<const DevMask*>(plan->d_masks.ptr);
+  if (n_progs > 0)
+    DQ_HIP(launch_predicates(static_cast<const PredProgram*>(plan->d_progs.ptr), n_progs,
+                             static_cast<const PredInsn*>(plan->d_insns.ptr),
+                             static_cast<const uint8_t*>(plan->d_pool.ptr), d_cols, n_rows,
+                             static_cast<uint64_t*>(plan->d_mask_words.ptr), plan->mask_words, plan->stream));
+
+  if (n_scan > 0) {
+    ScanAcc* parts = static_cast<ScanAcc*>(plan->d_partials.ptr);
+    const ScanTask* d_tasks = static_cast<const ScanTask*>(plan->d_tasks.ptr);
+    const int32_t* d_groups = static_cast<const int32_t*>(plan->d_groups.ptr);
+    for (size_t g = 0; g < plan->groups.size(); ++g) {
+      const ScanGroup& G = plan->groups[g];
+      DQ_HIP(launch_scan_group(G.kind, G.ptype, G.np, d_tasks, d_groups + G.dev_offset, (int)G.tasks.size(),
+                               d_cols, d_masks, n_rows, (int)group_bpt[g], parts + group_base[g], plan->stream));
+    }
+    DQ_HIP(launch_scan_reduce(parts, static_cast<const PartRange*>(plan->d_ranges.ptr), n_scan,
+                              static_cast<ScanAcc*>(plan->d_acc.ptr), plan->stream));
+  }
+  const int n_hll = (int)plan->hll_tasks.size();
+  if (n_hll > 0) {
+    int64_t bpt = std::max<int64_t>(1, plan->target_blocks / n_hll);
+    bpt = std::min<int64_t>(bpt, chunks);
+    DQ_HIP(launch_hll(static_cast<const HllTask*>(plan->d_hll.ptr), n_hll, d_cols, d_masks, n_rows, (int)bpt,
+                      static_cast<uint32_t*>(plan->d_regs.ptr), plan->stream));
+  }
+  plan->total_rows += n_rows;
+  if (any_host) {  // caller's host buffers may be released once we return
+    DQ_HIP(hipStreamSynchronize(plan->stream));
+    plan->host_tmp.clear();
+    plan->desc_pending = false;
+  }
+  return DQ_OK;
+}
+
+static double fsum_value(const ScanAcc& a) {
+  if (!std::isfinite(a.fs)) return a.fs;  // Inf/NaN: the plain running sum is Spark's answer
+  return a.fs + a.fc;
+}
+
+static void pack_hll(const uint32_t* regs, int64_t words[DQ_HLL_NUM_WORDS]) {
+  for (int w = 0; w < DQ_HLL_NUM_WORDS; ++w) {
+    uint64_t word = 0;
+    for (int i = 0; i < 10; ++i) {
+      const int idx = w * 10 + i;
+      if (idx < kHllM) word |= ((uint64_t)(regs[idx] & 63u)) << (6 * i);
+    }
+    words[w] = (int64_t)word;
+  }
+}
+
+extern "C" dq_status dq_plan_finish(dq_plan* plan, dq_state* out, int n_out) {
+  if (!plan) return fail(DQ_ERR_INVALID, "plan is NULL");
+  if (n_out < (int)plan->slots.size() || (!out && !plan->slots.empty()))
+    return fail(DQ_ERR_INVALID, "output array too small");
+  DQ_HIP(hipSetDevice(plan->ctx->device));
+  std::vector<ScanAcc> acc(plan->scan_tasks.size());
+  std::vector<uint32_t> regs(plan->hll_tasks.size() * kHllM);
+  if (!acc.empty())
+    DQ_HIP(hipMemcpyAsync(acc.data(), plan->d_acc.ptr, acc.size() * sizeof(ScanAcc), hipMemcpyDeviceToHost, plan->stream));
+  if (!regs.empty())
+    DQ_HIP(hipMemcpyAsync(regs.data(), plan->d_regs.ptr, regs.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, plan->stream));
+  DQ_HIP(hipStreamSynchronize(plan->stream));
+  plan->desc_pending = false;
+  plan->host_tmp.clear();
+
+  const int64_t rows = plan->total_rows;
+  for (size_t i = 0; i < plan->slots.size(); ++i) {
+    const OpSlot& s = plan->slots[i];
+    dq_state& o = out[i];
+    std::memset(&o, 0, sizeof(o));
+    o.kind = s.kind;
+    if (s.target == TGT_HOST_SIZE) {  // count(*) is never NULL
+      o.has_value = 1;
+      o.num_matches = rows;
+      continue;
+    }
+    if (s.target == TGT_HLL) {  // never NULL (StatefulHyperloglogPlus.nullable = false)
+      o.has_value = 1;
+      pack_hll(&regs[(size_t)s.task * kHllM], o.words);
+      continue;
+    }
+    const ScanAcc& a = acc[s.task];
+    const int ptype = plan->scan_tasks[s.task].ptype;
+    const bool count_ok = s.has_where ? (a.n_wnn > 0) : true;  // conditionalCount non-NULL
+    const int64_t count = s.has_where ? a.n_rows : rows;
+    switch (s.kind) {
+      case DQ_OP_SIZE:
+        o.has_value = count_ok ? 1 : 0;
+        o.num_matches = count;
+        break;
+      case DQ_OP_COMPLETENESS:
+        o.has_value = (rows > 0 && count_ok) ? 1 : 0;  // sum over zero rows is NULL
+        o.num_matches = a.n_sel;
+        o.count = count;
+        break;
+      case DQ_OP_COMPLIANCE:
+        o.has_value = (a.pn[s.pred] > 0 && count_ok) ? 1 : 0;
+        o.num_matches = a.pm[s.pred];
+        o.count = count;
+        break;
+      case DQ_OP_SUM:
+        o.has_value = a.n_sel > 0;
+        o.sum = is_integral(ptype) ? (double)a.isum : fsum_value(a);
+        break;
+      case DQ_OP_MEAN:
+        o.has_value = a.n_sel > 0;
+        o.sum = is_integral(ptype) ? (double)a.isum : fsum_value(a);
+        o.count = a.n_sel;
+        break;
+      case DQ_OP_STDDEV:
+        o.has_value = a.n_sel > 0;
+        o.n = (double)a.n_sel;
+        o.avg = a.mean;
+        o.m2 = a.m2;
+        break;
+      case DQ_OP_MINIMUM:
+        o.has_value = a.n_sel > 0;
+        if (is_integral(ptype)) o.value = (double)a.imin;
+        else o.value = (a.nnan == a.n_sel) ? std::numeric_limits<double>::quiet_NaN() : a.fmin;
+        break;
+      case DQ_OP_MAXIMUM:
+        o.has_value = a.n_sel > 0;
+        if (is_integral(ptype)) o.value = (double)a.imax;
+        else o.value = a.nnan > 0 ? std::numeric_limits<double>::quiet_NaN() : a.fmax;
+        break;
+      default: break;
+    }
+  }
+  return DQ_OK;
+}
+
+// ------------------------------------------------------------------------------ HLL host
+static const double kAlphaM2 = (0.7213 / (1.0 + 1.079 / 512)) * 512.0 * 512.0;
+
+static double estimate_bias(double e) {  // StatefulHyperloglogPlus.scala:259-297
+  const double* est = kDqHllRawEstimateP9;
+  const int n = DQ_HLL_P9_NUM_ESTIMATES;
+  int low = 0, high = n - 1, found = -1;
+  while (low <= high) {  // java.util.Arrays.binarySearch(double[], ...)
+    const int mid = (low + high) >> 1;
+    const double mv = est[mid];
+    if (mv < e) low = mid + 1;
+    else if (mv > e) high = mid - 1;
+    else {
+      int64_t mb, kb;
+      std::memcpy(&mb, &mv, 8);
+      std::memcpy(&kb, &e, 8);
+      if (mb == kb) { found = mid; break; }
+      if (mb < kb) low = mid + 1;
+      else high = mid - 1;
+    }
+  }
+  const int nearest = found >= 0 ? found : low;
+  auto dist = [&](int i) { const double d = e - est[i]; return d * d; };
+  int lo = std::max(nearest - 6 + 1, 0);
+  int hi = std::min(lo + 6, n);
+  while (hi < n && dist(hi) < dist(lo)) {
+    ++lo;
+    ++hi;
+  }
+  double bias_sum = 0.0;
+  for (int i = lo; i < hi; ++i) bias_sum += kDqHllBiasP9[i];
+  return bias_sum / (double)(hi - lo);
+}
+
+static double java_round(double a) {  // java.lang.Math.round(double) (JDK 8), as a double
+  if (std::isnan(a)) return 0.0;
+  if (a == 0x1.fffffffffffffp-2) return 0.0;
+  const double r = std::floor(a + 0.5);
+  if (r >= 9.223372036854775807e18) return 9.223372036854775807e18;
+  if (r <= -9.223372036854775808e18) return -9.223372036854775808e18;
+  return r;
+}
+
+extern "C" double dq_hll_count(const int64_t words[DQ_HLL_NUM_WORDS]) {
+  double z_inverse = 0.0, v = 0.0;
+  for (int idx = 0; idx < kHllM; ++idx) {
+    const uint64_t w = (uint64_t)words[idx / 10];
+    const uint32_t m = (uint32_t)((w >> (6 * (idx % 10))) & 63u);
+    const int32_t pow2 = (int32_t)(1u << (m & 31u));  // Java int shift of 1 by a Long count
+    z_inverse += 1.0 / (double)pow2;
+    if (m == 0) v += 1.0;
+  }
+  auto e_bias_corrected = [&]() {
+    const double e = kAlphaM2 / z_inverse;
+    return (e < 5.0 * kHllM) ? e - estimate_bias(e) : e;  // P < 19 always holds (P = 9)
+  };
+  double estimate;
+  if (v > 0) {
+    const double h = kHllM * std::log((double)kHllM / v);
+    estimate = (h <= kDqHllThresholdP9) ? h : e_bias_corrected();
+  } else {
+    estimate = e_bias_corrected();
+  }
+  return java_round(estimate);
+}
+
+extern "C" void dq_hll_merge(const int64_t a[DQ_HLL_NUM_WORDS], const int64_t b[DQ_HLL_NUM_WORDS],
+                             int64_t out[DQ_HLL_NUM_WORDS]) {
+  for (int w = 0; w < DQ_HLL_NUM_WORDS; ++w) {
+    const uint64_t wa = (uint64_t)a[w], wb = (uint64_t)b[w];
+    uint64_t word = 0, mask = 63;
+    for (int i = 0; i < 10 && w * 10 + i < kHllM; ++i) {
+      word |= std::max(wa & mask, wb & mask);
+      mask <<= 6;
+    }
+    out[w] = (int64_t)word;
+  }
+}
+
+extern "C" void dq_hll_words_to_bytes(const int64_t words[DQ_HLL_NUM_WORDS], uint8_t out[416]) {
+  for (int w = 0; w < DQ_HLL_NUM_WORDS; ++w)
+    for (int b = 0; b < 8; ++b) out[w * 8 + b] = (uint8_t)((uint64_t)words[w] >> (56 - 8 * b));
+}
+
+extern "C" void dq_hll_words_from_bytes(const uint8_t in[416], int64_t words[DQ_HLL_NUM_WORDS]) {
+  for (int w = 0; w < DQ_HLL_NUM_WORDS; ++w) {
+    uint64_t v = 0;
+    for (int b = 0; b < 8; ++b) v = (v << 8) | in[w * 8 + b];
+    words[w] = (int64_t)v;
+  }
+}
+
+extern "C" uint64_t dq_xxh64(const void* data, size_t len, uint64_t seed) {
+  const uint8_t* p = static_cast<const uint8_t*>(data);
+  const uint8_t* end = p + len;
+  auto rd64 = [](const uint8_t* q) { uint64_t v; std::memcpy(&v, q, 8); return v; };
+  auto rd32 = [](const uint8_t* q) { uint32_t v; std::memcpy(&v, q, 4); return v; };
+  uint64_t h;
+  if (len >= 32) {
+    uint64_t v1 = seed + kP1 + kP2, v2 = seed + kP2, v3 = seed, v4 = seed - kP1;
+    const uint8_t* limit = end - 32;
+    do {
+      v1 = xxh_round(v1, rd64(p));
+      v2 = xxh_round(v2, rd64(p + 8));
+      v3 = xxh_round(v3, rd64(p + 16));
+      v4 = xxh_round(v4, rd64(p + 24));
+      p += 32;
+    } while (p <= limit);
+    h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+    h ^= xxh_round(0, v1); h = h * kP1 + kP4;
+    h ^= xxh_round(0, v2); h = h * kP1 + kP4;
+    h ^= xxh_round(0, v3); h = h * kP1 + kP4;
+    h ^= xxh_round(0, v4); h = h * kP1 + kP4;
+  } else {
+    h = seed + kP5;
+  }
+  h += (uint64_t)len;
+  while (p + 8 <= end) {
+    h ^= xxh_round(0, rd64(p));
+    h = rotl64(h, 27) * kP1 + kP4;
+    p += 8;
+  }
+  if (p + 4 <= end) {
+    h ^= (uint64_t)rd32(p) * kP1;
+    h = rotl64(h, 23) * kP2 + kP3;
+    p += 4;
+  }
+  while (p < end) {
+    h ^= (uint64_t)(*p) * kP5;
+    h = rotl64(h, 11) * kP1;
+    ++p;
+  }
+  return xxh_avalanche(h);
+}
+
+// ------------------------------------------------------------------------------ state algebra
+static double java_min(double a, double b) {  // java.lang.Math.min(double, double)
+  if (a != a) return a;
+  if (b != b) return b;
+  if (a == 0.0 && b == 0.0) return std::signbit(a) ? a : b;
+  return a <= b ? a : b;
+}
+static double java_max(double a, double b) {
+  if (a != a) return a;
+  if (b != b) return b;
+  if (a == 0.0 && b == 0.0) return std::signbit(a) ? b : a;
+  return a >= b ? a : b;
+}
+
+extern "C" dq_status dq_state_merge(const dq_state* a, const dq_state* b, dq_state* out) {
+  if (!a || !b || !out) return fail(DQ_ERR_INVALID, "NULL argument");
+  if (a->kind != b->kind) return fail(DQ_ERR_INVALID, "cannot merge states of different kinds");
+  if (!a->has_value || !b->has_value) {  // Analyzers.merge: None is the identity
+    const dq_state* pick = a->has_value ? a : b;
+    if (out != pick) *out = *pick;
+    return DQ_OK;
+  }
+  dq_state r = *a;
+  switch (a->kind) {
+    case DQ_OP_SIZE:  // NumMatches.sum (Size.scala:25-27)
+      r.num_matches = (int64_t)((uint64_t)a->num_matches + (uint64_t)b->num_matches);
+      break;
+    case DQ_OP_COMPLETENESS: case DQ_OP_COMPLIANCE:  // NumMatchesAndCount.sum (Analyzer.scala:233-235)
+      r.num_matches = (int64_t)((uint64_t)a->num_matches + (uint64_t)b->num_matches);
+      r.count = (int64_t)((uint64_t)a->count + (uint64_t)b->count);
+      break;
+    case DQ_OP_SUM:  // SumState.sum (Sum.scala:27-29)
+      r.sum = a->sum + b->sum;
+      break;
+    case DQ_OP_MEAN:  // MeanState.sum (Mean.scala:27-29)
+      r.sum = a->sum + b->sum;
+      r.count = (int64_t)((uint64_t)a->count + (uint64_t)b->count);
+      break;
+    case DQ_OP_STDDEV: {  // StandardDeviationState.sum (StandardDeviation.scala:37-44)
+      const double new_n = a->n + b->n;
+      const double delta = b->avg - a->avg;
+      const double delta_n = new_n == 0.0 ? 0.0 : delta / new_n;
+      r.n = new_n;
+      r.avg = a->avg + delta_n * b->n;
+      r.m2 = a->m2 + b->m2 + delta * delta_n * a->n * b->n;
+      break;
+    }
+    case DQ_OP_MINIMUM: r.value = java_min(a->value, b->value); break;  // Minimum.scala:27-29
+    case DQ_OP_MAXIMUM: r.value = java_max(a->value, b->value); break;  // Maximum.scala:27-29
+    case DQ_OP_APPROX_COUNT_DISTINCT: dq_hll_merge(a->words, b->words, r.words); break;
+    default: return fail(DQ_ERR_INVALID, "unknown state kind");
+  }
+  *out = r;
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_state_metric(const dq_state* s, double* out) {
+  if (!s || !out) return fail(DQ_ERR_INVALID, "NULL argument");
+  if (!s->has_value) return fail(DQ_ERR_STATE, "empty state (all input values were NULL)");
+  switch (s->kind) {
+    case DQ_OP_SIZE: *out = (double)s->num_matches; break;
+    case DQ_OP_COMPLETENESS: case DQ_OP_COMPLIANCE:
+      *out = s->count == 0 ? std::numeric_limits<double>::quiet_NaN() : (double)s->num_matches / (double)s->count;
+      break;
+    case DQ_OP_SUM: *out = s->sum; break;
+    case DQ_OP_MEAN:
+      *out = s->count == 0 ? std::numeric_limits<double>::quiet_NaN() : s->sum / (double)s->count;
+      break;
+    case DQ_OP_STDDEV: *out = std::sqrt(s->m2 / s->n); break;
+    case DQ_OP_MINIMUM: case DQ_OP_MAXIMUM: *out = s->value; break;
+    case DQ_OP_APPROX_COUNT_DISTINCT: *out = dq_hll_count(s->words); break;
+    default: return fail(DQ_ERR_INVALID, "unknown state kind");
+  }
+  return DQ_OK;
+}

@@ -1,0 +1,221 @@
+// dq_hll.hip -- HLL++ register update for ApproxCountDistinct, bit-exact with deequ.
+//
+// Reproduces StatefulHyperloglogPlus.update (catalyst/StatefulHyperloglogPlus.scala:89-115):
+//   x   = XxHash64Function.hash(v, type, 42)        (Spark 2.2.2 type dispatch)
+//   idx = x >>> 55                                   (top p = 9 bits)
+//   pw  = numberOfLeadingZeros((x << 9) | 0x100) + 1
+//   M[idx] = max(M[idx], pw)
+// and the merge (:121-139) = per-register max.  Because max is order-independent the result
+// is bitwise identical whatever the block/wave schedule.
+//
+// Layout: blockIdx.y = HLL task (column, where), blockIdx.x = contiguous row chunk.  Each
+// workgroup keeps its 512 registers as u32 in LDS (2 KiB) and updates them with ds_max_u32,
+// skipping the atomic when the register already holds >= pw (after a few thousand rows almost
+// every update is a no-op, so the LDS traffic is one ds_read per row).  At the end every
+// non-zero register is folded into the task's global registers with one atomicMax.  The host
+// packs the 512 registers into the 52 Long words of ApproxCountDistinctState.
+#include "dq_internal.h"
+
+namespace dq {
+
+namespace {
+
+struct alignas(16) Vec16 {
+  uint32_t w[4];
+};
+
+__device__ inline void hll_update(uint32_t* regs, uint64_t x) {
+  uint32_t idx, pw;
+  hll_idx_rank(x, &idx, &pw);
+  if (pw > regs[idx]) atomicMax(&regs[idx], pw);
+}
+
+// Spark 2.2.2 hash by type (InterpretedHashFunction / XxHash64Function).
+template <typename T> __device__ inline uint64_t spark_hash(T v);
+template <> __device__ inline uint64_t spark_hash<int8_t>(int8_t v) { return xxh64_u32((uint32_t)(int32_t)v, 42); }
+template <> __device__ inline uint64_t spark_hash<int16_t>(int16_t v) { return xxh64_u32((uint32_t)(int32_t)v, 42); }
+template <> __device__ inline uint64_t spark_hash<int32_t>(int32_t v) { return xxh64_u32((uint32_t)v, 42); }
+template <> __device__ inline uint64_t spark_hash<int64_t>(int64_t v) { return xxh64_u64((uint64_t)v, 42); }
+template <> __device__ inline uint64_t spark_hash<float>(float v) {
+  uint32_t bits = __float_as_uint(v);
+  if (v != v) bits = 0x7fc00000u;  // Float.floatToIntBits canonical NaN
+  return xxh64_u32(bits, 42);
+}
+template <> __device__ inline uint64_t spark_hash<double>(double v) {
+  uint64_t bits = (uint64_t)__double_as_longlong(v);
+  if (v != v) bits = 0x7ff8000000000000ull;  // Double.doubleToLongBits canonical NaN
+  return xxh64_u64(bits, 42);
+}
+
+template <int RPL>
+__device__ inline uint32_t load_bits(const uint8_t* bm, int64_t row0, int64_t left) {
+  if constexpr (RPL == 16) {
+    if (left > 8) return (uint32_t)(*reinterpret_cast<const uint16_t*>(bm + (row0 >> 3)));
+    return (uint32_t)bm[row0 >> 3];
+  } else {
+    const uint32_t byte = bm[row0 >> 3];
+    return (byte >> (uint32_t)(row0 & 7)) & ((1u << RPL) - 1u);
+  }
+}
+
+template <typename T>
+__device__ void hll_fixed(uint32_t* regs, const DevColumn& col, const uint8_t* wt_bm,
+                          int64_t row_begin, int64_t row_end) {
+  constexpr int RPL = 16 / (int)sizeof(T);
+  constexpr uint32_t FULL = (1u << RPL) - 1u;
+  const T* __restrict__ values = static_cast<const T*>(col.values);
+  for (int64_t row0 = row_begin + (int64_t)threadIdx.x * RPL; row0 < row_end;
+       row0 += (int64_t)kBlock * RPL) {
+    const int64_t left = row_end - row0;
+    const uint32_t in = left >= RPL ? FULL : ((1u << (uint32_t)left) - 1u);
+    Vec16 vec;
+    if (left >= RPL) {
+      vec = *reinterpret_cast<const Vec16*>(values + row0);
+    } else {
+      T tmp[RPL];
+#pragma unroll
+      for (int k = 0; k < RPL; ++k) tmp[k] = k < left ? values[row0 + k] : T(0);
+      __builtin_memcpy(&vec, tmp, 16);
+    }
+    uint32_t sel = in;
+    if (col.validity) sel &= load_bits<RPL>(col.validity, row0, left);
+    if (wt_bm) sel &= load_bits<RPL>(wt_bm, row0, left);
+    const T* vals = reinterpret_cast<const T*>(&vec);
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {
+      if ((sel >> k) & 1u) hll_update(regs, spark_hash<T>(vals[k]));
+    }
+  }
+}
+
+__device__ void hll_bool(uint32_t* regs, const DevColumn& col, const uint8_t* wt_bm,
+                         int64_t row_begin, int64_t row_end) {
+  const uint8_t* bits = static_cast<const uint8_t*>(col.values);
+  const uint64_t h1 = xxh64_u32(1u, 42), h0 = xxh64_u32(0u, 42);
+  for (int64_t row = row_begin + threadIdx.x; row < row_end; row += kBlock) {
+    bool sel = !col.validity || ((col.validity[row >> 3] >> (row & 7)) & 1u);
+    if (wt_bm) sel = sel && ((wt_bm[row >> 3] >> (row & 7)) & 1u);
+    if (sel) hll_update(regs, ((bits[row >> 3] >> (row & 7)) & 1u) ? h1 : h0);
+  }
+}
+
+// Unaligned little-endian loads that only touch aligned words containing at least one byte
+// of [p, end): such a word never leaves the page of that byte, so this is memory safe.
+__device__ inline uint64_t ld64(const uint8_t* p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(a & ~(uintptr_t)7);
+  const uint32_t sh = (uint32_t)(a & 7) * 8u;
+  if (sh == 0) return w[0];
+  return (w[0] >> sh) | (w[1] << (64u - sh));
+}
+__device__ inline uint32_t ld32(const uint8_t* p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3) * 8u;
+  if (sh == 0) return w[0];
+  return (w[0] >> sh) | (w[1] << (32u - sh));
+}
+
+// XXH64 (Spark XXH64.hashUnsafeBytes) over [p, p + len).
+__device__ uint64_t xxh64_bytes(const uint8_t* p, int64_t len, uint64_t seed) {
+  const uint8_t* end = p + len;
+  uint64_t h;
+  if (len >= 32) {
+    uint64_t v1 = seed + kP1 + kP2, v2 = seed + kP2, v3 = seed, v4 = seed - kP1;
+    const uint8_t* limit = end - 32;
+    do {
+      v1 = xxh_round(v1, ld64(p));
+      v2 = xxh_round(v2, ld64(p + 8));
+      v3 = xxh_round(v3, ld64(p + 16));
+      v4 = xxh_round(v4, ld64(p + 24));
+      p += 32;
+    } while (p <= limit);
+    h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+    h ^= xxh_round(0, v1); h = h * kP1 + kP4;
+    h ^= xxh_round(0, v2); h = h * kP1 + kP4;
+    h ^= xxh_round(0, v3); h = h * kP1 + kP4;
+    h ^= xxh_round(0, v4); h = h * kP1 + kP4;
+  } else {
+    h = seed + kP5;
+  }
+  h += (uint64_t)len;
+  while (p + 8 <= end) {
+    h ^= xxh_round(0, ld64(p));
+    h = rotl64(h, 27) * kP1 + kP4;
+    p += 8;
+  }
+  if (p + 4 <= end) {
+    h ^= (uint64_t)ld32(p) * kP1;
+    h = rotl64(h, 23) * kP2 + kP3;
+    p += 4;
+  }
+  while (p < end) {
+    h ^= (uint64_t)(*p) * kP5;
+    h = rotl64(h, 11) * kP1;
+    ++p;
+  }
+  return xxh_avalanche(h);
+}
+
+__device__ void hll_utf8(uint32_t* regs, const DevColumn& col, const uint8_t* wt_bm,
+                         int64_t row_begin, int64_t row_end) {
+  const uint8_t* chars = static_cast<const uint8_t*>(col.values);
+  const int32_t* offs = col.offsets;
+  for (int64_t row = row_begin + threadIdx.x; row < row_end; row += kBlock) {
+    bool sel = !col.validity || ((col.validity[row >> 3] >> (row & 7)) & 1u);
+    if (wt_bm) sel = sel && ((wt_bm[row >> 3] >> (row & 7)) & 1u);
+    if (sel) {
+      const int32_t b = offs[row], e = offs[row + 1];
+      hll_update(regs, xxh64_bytes(chars + b, (int64_t)(e - b), 42));
+    }
+  }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kBlock) void dq_hll_kernel(const HllTask* __restrict__ tasks,
+                                                        const DevColumn* __restrict__ cols,
+                                                        const DevMask* __restrict__ masks,
+                                                        int64_t n_rows, uint32_t* registers) {
+  __shared__ uint32_t regs[kHllM];
+  const HllTask task = tasks[blockIdx.y];
+  for (int r = threadIdx.x; r < kHllM; r += kBlock) regs[r] = 0u;
+  __syncthreads();
+
+  const int64_t n_chunks = (n_rows + kScanRowAlign - 1) / kScanRowAlign;
+  const int64_t per_block = (n_chunks + gridDim.x - 1) / gridDim.x;
+  const int64_t row_begin = min((int64_t)blockIdx.x * per_block * kScanRowAlign, n_rows);
+  const int64_t row_end = min(row_begin + per_block * kScanRowAlign, n_rows);
+  const DevColumn& col = cols[task.column];
+  const uint8_t* wt_bm =
+      task.where_mask >= 0 ? reinterpret_cast<const uint8_t*>(masks[task.where_mask].t) : nullptr;
+
+  switch (task.ctype) {
+    case DQ_T_BOOL: hll_bool(regs, col, wt_bm, row_begin, row_end); break;
+    case DQ_T_INT8: hll_fixed<int8_t>(regs, col, wt_bm, row_begin, row_end); break;
+    case DQ_T_INT16: hll_fixed<int16_t>(regs, col, wt_bm, row_begin, row_end); break;
+    case DQ_T_INT32: hll_fixed<int32_t>(regs, col, wt_bm, row_begin, row_end); break;
+    case DQ_T_INT64: hll_fixed<int64_t>(regs, col, wt_bm, row_begin, row_end); break;
+    case DQ_T_FLOAT32: hll_fixed<float>(regs, col, wt_bm, row_begin, row_end); break;
+    case DQ_T_FLOAT64: hll_fixed<double>(regs, col, wt_bm, row_begin, row_end); break;
+    case DQ_T_UTF8: hll_utf8(regs, col, wt_bm, row_begin, row_end); break;
+    default: break;
+  }
+  __syncthreads();
+  uint32_t* out = registers + (int64_t)blockIdx.y * kHllM;
+  for (int r = threadIdx.x; r < kHllM; r += kBlock) {
+    const uint32_t v = regs[r];
+    if (v) atomicMax(&out[r], v);
+  }
+}
+
+hipError_t launch_hll(const HllTask* d_tasks, int n_tasks, const DevColumn* d_cols,
+                      const DevMask* d_masks, int64_t n_rows, int blocks_per_task,
+                      uint32_t* d_registers, hipStream_t stream) {
+  if (n_tasks <= 0 || n_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(dq_hll_kernel, dim3(blocks_per_task, n_tasks), dim3(kBlock), 0, stream,
+                     d_tasks, d_cols, d_masks, n_rows, d_registers);
+  return hipGetLastError();
+}
+
+}  // namespace dq

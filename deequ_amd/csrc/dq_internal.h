@@ -1,0 +1,190 @@
+// dq_internal.h -- structures shared by the host planner (dq_api.cpp) and the gfx950
+// kernels (dq_scan.hip, dq_hll.hip, dq_pred.hip).  Not part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/deequ_amd.h"
+
+namespace dq {
+
+constexpr int kBlock = 256;          // threads per workgroup (4 waves of 64)
+constexpr int kMaxPreds = 8;         // predicates evaluated per scan task
+constexpr int kMaxStack = 8;         // generic predicate interpreter stack depth
+constexpr int kHllM = 512;           // 2^p registers, p = 9 (StatefulHyperloglogPlus.scala:157-161)
+constexpr int kHllIdxShift = 55;     // 64 - p
+constexpr uint64_t kHllWPadding = 1ull << 8;
+constexpr int kScanRowAlign = 2048;  // chunk granularity: keeps every lane's bitmap word aligned
+
+// A batch column after host preparation: row 0 of the batch is at values[0] and at bit 0 of
+// validity[0] (the host realigns sliced Arrow bitmaps).  Device pointers.
+struct DevColumn {
+  const uint8_t* validity;  // nullptr = all valid
+  const void* values;
+  const int32_t* offsets;   // utf8
+  int32_t type;             // dq_type
+  int32_t pad;
+};
+
+// Mask produced by the generic predicate kernel: bit r of `t` = predicate TRUE at row r,
+// bit r of `nn` = predicate NOT NULL at row r.  64-bit words, LSB-first.
+struct DevMask {
+  const uint64_t* t;
+  const uint64_t* nn;
+};
+
+enum FastPredKind : int32_t {
+  FP_NONE = 0,
+  FP_CMP = 1,           // primary CMP literal
+  FP_COALESCE_CMP = 2,  // COALESCE(primary, coalesce literal) CMP literal
+  FP_IS_NULL = 3,
+  FP_IS_NOT_NULL = 4,
+  FP_CONST = 5,         // constant TRUE/FALSE/NULL (lit_i: 1 true, 0 false, -1 null)
+  FP_MASK = 6           // precomputed DevMask[mask]
+};
+
+enum CmpOp : int32_t { CMP_EQ = 0, CMP_NE, CMP_LT, CMP_LE, CMP_GT, CMP_GE, CMP_EQNS };
+
+struct FastPred {
+  int32_t kind;    // FastPredKind
+  int32_t op;      // CmpOp
+  int32_t as_f64;  // compare in fp64 (else int64)
+  int32_t mask;    // FP_MASK: index into the batch mask table
+  int64_t lit_i;
+  double lit_f;
+  int64_t coal_i;
+  double coal_f;
+};
+
+enum ScanTaskFlags : int32_t {
+  TF_VALUES = 1,      // the task must read the primary column's values
+  TF_STATS = 2,       // sum/mean/stddev/min/max wanted
+  TF_WHERE = 4,       // filter rows by batch mask `where_mask`
+  TF_VALIDITY = 8     // primary column is read for validity (completeness / null tests)
+};
+
+struct ScanTask {
+  int32_t primary;     // batch column index or -1 (row-count only task)
+  int32_t ptype;       // dq_type of the primary column
+  int32_t flags;       // ScanTaskFlags
+  int32_t where_mask;  // batch mask index when TF_WHERE
+  int32_t n_preds;
+  int32_t pad;
+  FastPred preds[kMaxPreds];
+};
+
+// Per-(task, block) partial aggregate and the per-task running accumulator.  Every field is
+// 8 bytes; the layout is mirrored by nothing outside this library.
+struct ScanAcc {
+  int64_t n_rows;   // rows in scope: Σ where TRUE (or all rows)
+  int64_t n_wnn;    // Σ where NOT NULL (or all rows)
+  int64_t n_sel;    // Σ valid & where TRUE
+  int64_t isum;     // wrapping int64 sum of integral values
+  int64_t imin, imax;
+  double fs, fc;    // Neumaier-compensated fp64 sum: value = fs + fc
+  double fmin, fmax;
+  int64_t nnan;     // NaNs among selected floats
+  double mean, m2;  // moments about the mean over the n_sel selected values
+  int64_t pm[kMaxPreds];  // predicate TRUE & where TRUE
+  int64_t pn[kMaxPreds];  // predicate NOT NULL & where TRUE
+};
+
+// Where a task's block partials live for the current batch.
+struct PartRange {
+  int64_t offset;
+  int32_t count;
+  int32_t pad;
+};
+
+struct HllTask {
+  int32_t column;
+  int32_t ctype;
+  int32_t where_mask;  // -1 = none
+  int32_t pad;
+};
+
+// One instruction of the generic predicate interpreter (dq_pred_insn after validation).
+struct PredInsn {
+  int32_t opcode;
+  int32_t arg;
+  int64_t i64;
+  double f64;
+};
+
+struct PredProgram {
+  int32_t first;   // index of first PredInsn in the plan's instruction table
+  int32_t n;
+};
+
+// ---------------------------------------------------------------- launchers (.hip files)
+// kind 0 = validity/mask-only tasks, 1 = value tasks of column type `ptype` with exactly
+// `np` inline predicates (np > 4 uses the 8-slot kernel).  Partials of the group's i-th task
+// go to d_partials[i * blocks_per_task + b].
+hipError_t launch_scan_group(int kind, int ptype, int np, const ScanTask* d_tasks,
+                             const int32_t* d_group, int n_group, const DevColumn* d_cols,
+                             const DevMask* d_masks, int64_t n_rows, int blocks_per_task,
+                             ScanAcc* d_partials, hipStream_t stream);
+hipError_t launch_scan_reduce(const ScanAcc* d_partials, const PartRange* d_ranges, int n_tasks,
+                              ScanAcc* d_acc, hipStream_t stream);
+hipError_t launch_hll(const HllTask* d_tasks, int n_tasks, const DevColumn* d_cols,
+                      const DevMask* d_masks, int64_t n_rows, int blocks_per_task,
+                      uint32_t* d_registers, hipStream_t stream);
+hipError_t launch_predicates(const PredProgram* d_progs, int n_progs, const PredInsn* d_insns,
+                             const uint8_t* d_pool, const DevColumn* d_cols, int64_t n_rows,
+                             uint64_t* d_mask_words,
+                             int64_t words_per_mask, hipStream_t stream);
+hipError_t launch_realign_bitmap(const uint8_t* src, int64_t bit_offset, int64_t n_bits,
+                                 uint8_t* dst, hipStream_t stream);
+hipError_t launch_init_acc(ScanAcc* d_acc, int n, hipStream_t stream);
+
+// ---------------------------------------------------------------- XXH64 (host + device)
+constexpr uint64_t kP1 = 0x9E3779B185EBCA87ull;
+constexpr uint64_t kP2 = 0xC2B2AE3D27D4EB4Full;
+constexpr uint64_t kP3 = 0x165667B19E3779F9ull;
+constexpr uint64_t kP4 = 0x85EBCA77C2B2AE63ull;
+constexpr uint64_t kP5 = 0x27D4EB2F165667C5ull;
+
+__host__ __device__ inline uint64_t rotl64(uint64_t x, int r) {
+  return (x << r) | (x >> (64 - r));
+}
+__host__ __device__ inline uint64_t xxh_round(uint64_t acc, uint64_t lane) {
+  acc += lane * kP2;
+  acc = rotl64(acc, 31);
+  return acc * kP1;
+}
+__host__ __device__ inline uint64_t xxh_avalanche(uint64_t h) {
+  h ^= h >> 33;
+  h *= kP2;
+  h ^= h >> 29;
+  h *= kP3;
+  h ^= h >> 32;
+  return h;
+}
+// Spark XXH64.hashLong(v, seed): XXH64 of the 8 little-endian bytes of v.
+__host__ __device__ inline uint64_t xxh64_u64(uint64_t v, uint64_t seed) {
+  uint64_t h = seed + kP5 + 8;
+  h ^= xxh_round(0, v);
+  h = rotl64(h, 27) * kP1 + kP4;
+  return xxh_avalanche(h);
+}
+// Spark XXH64.hashInt(i, seed): XXH64 of the 4 little-endian bytes of i.
+__host__ __device__ inline uint64_t xxh64_u32(uint32_t v, uint64_t seed) {
+  uint64_t h = seed + kP5 + 4;
+  h ^= (uint64_t)v * kP1;
+  h = rotl64(h, 23) * kP2 + kP3;
+  return xxh_avalanche(h);
+}
+
+// HLL register index and rank (StatefulHyperloglogPlus.scala:96-99).
+__host__ __device__ inline void hll_idx_rank(uint64_t x, uint32_t* idx, uint32_t* pw) {
+  *idx = (uint32_t)(x >> kHllIdxShift);
+  uint64_t w = (x << 9) | kHllWPadding;
+#if defined(__HIP_DEVICE_COMPILE__)
+  *pw = (uint32_t)__clzll((long long)w) + 1u;
+#else
+  *pw = (uint32_t)__builtin_clzll(w) + 1u;
+#endif
+}
+
+}  // namespace dq

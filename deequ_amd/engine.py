@@ -1,0 +1,157 @@
+"""Plan execution over the C-ABI: the replacement for the fused `data.agg(...)` job.
+
+`AnalysisRunner.runScanningAnalyzers` (runners/AnalysisRunner.scala:306-313) concatenates
+every scan-shareable analyzer's aggregation columns into ONE Spark job.  Here the same set
+of analyzers becomes ONE `dq_plan`; every batch (partition) of the table is consumed by one
+fused pass of the gfx950 kernels, and `dq_plan_finish` returns one POD state per analyzer.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, List, Optional, Sequence
+
+from . import _lib as L
+from .predicates import compile_predicate
+from .states import State, state_from_dq
+
+_DEVICE: Optional[int] = None
+
+
+def set_device(device: int) -> None:
+    """Select the GPU used by subsequent plans in this process (one process per GPU)."""
+    global _DEVICE
+    _DEVICE = int(device)
+
+
+def current_device() -> int:
+    if _DEVICE is not None:
+        return _DEVICE
+    return int(os.environ.get("DEEQU_AMD_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+
+
+def _pred_array(pred):
+    if not pred:
+        return None
+    code = list(pred)
+    arr = (L.DqPredInsn * len(code))()
+    for i, (op, arg, i64, f64) in enumerate(code):
+        arr[i].opcode, arr[i].arg, arr[i].i64, arr[i].f64 = op, arg, i64, f64
+    pool = getattr(pred, "pool", b"")
+    return arr, (ctypes.create_string_buffer(pool, max(1, len(pool))) if pool else None), len(pool)
+
+
+def _fill_pred(dst: L.DqPredicate, packed) -> None:
+    arr, pool, n_pool = packed
+    dst.code = arr
+    dst.n_insns = len(arr)
+    if pool is not None:
+        dst.strings = ctypes.cast(pool, ctypes.c_void_p)
+        dst.strings_len = n_pool
+
+
+class OpSpec:
+    """One dq_op: kind, column index, compiled predicate / where programs."""
+
+    def __init__(self, kind: int, column: int = -1, predicate=None, where=None):
+        self.kind = kind
+        self.column = column
+        self.predicate = _pred_array(predicate)
+        self.where = _pred_array(where)
+
+    def fill(self, op: L.DqOp) -> None:
+        op.kind = self.kind
+        op.column = self.column
+        if self.predicate is not None:
+            _fill_pred(op.predicate, self.predicate)
+        if self.where is not None:
+            _fill_pred(op.where, self.where)
+
+
+def schema_index(schema: Dict[str, str]) -> Dict[str, tuple]:
+    return {name: (i, dtype) for i, (name, dtype) in enumerate(schema.items())}
+
+
+def op_spec_for(analyzer, schema: Dict[str, str]) -> OpSpec:
+    idx = schema_index(schema)
+    where = compile_predicate(analyzer.where, idx) if getattr(analyzer, "where", None) else None
+    kind = analyzer.DQ_KIND
+    if kind == L.DQ_OP_SIZE:
+        return OpSpec(kind, -1, None, where)
+    if kind == L.DQ_OP_COMPLIANCE:
+        return OpSpec(kind, -1, compile_predicate(analyzer.predicate, idx), where)
+    return OpSpec(kind, idx[analyzer.column][0], None, where)
+
+
+def op_supported(spec: OpSpec, schema: Dict[str, str]) -> None:
+    """Raises UnsupportedOnGpu / DeequAmdError if the op is not GPU-eligible."""
+    types = (ctypes.c_int32 * max(1, len(schema)))(*[L.TYPE_CODES[t] for t in schema.values()])
+    op = L.DqOp()
+    spec.fill(op)
+    L.check(L.lib().dq_op_supported(ctypes.byref(op), types, len(schema)))
+
+
+class Plan:
+    """Owns a dq_plan for a fixed analyzer list and schema; reusable across datasets."""
+
+    def __init__(self, specs: Sequence[OpSpec], schema: Dict[str, str], device: Optional[int] = None):
+        self.device = current_device() if device is None else device
+        self.ctx = L.Context.get(self.device)
+        self.schema = dict(schema)
+        self.names = list(schema.keys())
+        self.specs = list(specs)  # keep predicate arrays alive
+        self.n_ops = len(self.specs)
+        ops = (L.DqOp * max(1, self.n_ops))()
+        for i, s in enumerate(self.specs):
+            s.fill(ops[i])
+        types = (ctypes.c_int32 * max(1, len(self.names)))(*[L.TYPE_CODES[schema[n]] for n in self.names])
+        h = ctypes.c_void_p()
+        L.check(L.lib().dq_plan_create(self.ctx.handle, ops, self.n_ops, types, len(self.names),
+                                       ctypes.byref(h)))
+        self.handle = h
+        self._out = (L.DqState * max(1, self.n_ops))()
+
+    def consume(self, batch) -> None:
+        from .table import dq_columns
+        cols = dq_columns(batch, self.names)
+        L.check(L.lib().dq_plan_consume(self.handle, cols, len(self.names), batch.num_rows))
+
+    def finish_raw(self):
+        L.check(L.lib().dq_plan_finish(self.handle, self._out, self.n_ops))
+        return self._out
+
+    def finish(self) -> List[Optional[State]]:
+        out = self.finish_raw()
+        return [state_from_dq(out[i]) for i in range(self.n_ops)]
+
+    def reset(self) -> None:
+        L.check(L.lib().dq_plan_reset(self.handle))
+
+    @property
+    def stream(self) -> int:
+        return L.lib().dq_plan_stream(self.handle) or 0
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            L.lib().dq_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def run_scan(analyzers: Sequence, data) -> Dict[object, Optional[State]]:
+    """One fused GPU pass over every batch of `data` for all `analyzers`."""
+    schema = data.schema
+    specs = [op_spec_for(a, schema) for a in analyzers]
+    plan = Plan(specs, schema)
+    try:
+        for batch in data.batches():
+            plan.consume(batch)
+        states = plan.finish()
+    finally:
+        plan.close()
+    return dict(zip(analyzers, states))

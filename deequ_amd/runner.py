@@ -1,0 +1,208 @@
+"""AnalysisRunner / AnalyzerContext / state providers -- the reference's runner on the GPU path.
+
+Follows `runners/AnalysisRunner.scala`:
+* doAnalysisRun (:97-203): de-duplicate, schema-only precondition failures (:137-145,
+  :242-257), scan-shareable analyzers in ONE fused pass (:289-336) with the same failure
+  scoping (an aggregation error fails every shareable analyzer :320-323, an extraction error
+  fails one :340-353), then the non-shareable ones.
+* runOnAggregatedStates (:385-460): metrics from persisted states only, no data scan.
+Plus `AnalyzerContext` (AnalyzerContext.scala:29-105) and `InMemoryStateProvider`
+(StateProvider.scala:47-70).
+"""
+from __future__ import annotations
+
+import json
+import math
+import threading
+from collections import OrderedDict
+from typing import Dict, Iterable, List, Optional, Sequence
+
+from . import _lib as L
+from .analyzers import Analyzer, Preconditions, ScanShareableAnalyzer
+from .metrics import DoubleMetric, Entity
+
+
+class AnalyzerContext:
+    def __init__(self, metricMap: Optional[Dict[Analyzer, object]] = None):
+        self.metricMap = OrderedDict(metricMap or {})
+
+    @staticmethod
+    def empty() -> "AnalyzerContext":
+        return AnalyzerContext()
+
+    def allMetrics(self) -> List:
+        return list(self.metricMap.values())
+
+    def metric(self, analyzer) -> Optional[object]:
+        return self.metricMap.get(analyzer)
+
+    def __add__(self, other: "AnalyzerContext") -> "AnalyzerContext":
+        m = OrderedDict(self.metricMap)
+        m.update(other.metricMap)
+        return AnalyzerContext(m)
+
+    def successMetricsAsJson(self, forAnalyzers: Sequence[Analyzer] = ()) -> str:
+        """AnalyzerContext.successMetricsAsJson (AnalyzerContext.scala:61-76)."""
+        rows = []
+        for analyzer, metric in self.metricMap.items():
+            if forAnalyzers and analyzer not in forAnalyzers:
+                continue
+            for m in metric.flatten():
+                if m.value.isSuccess:
+                    rows.append(OrderedDict([("entity", m.entity.value), ("instance", m.instance),
+                                             ("name", m.name), ("value", m.value.get())]))
+        return json.dumps(rows)
+
+
+class InMemoryStateProvider:
+    """StateLoader + StatePersister backed by a dict (StateProvider.scala:47-70)."""
+
+    def __init__(self):
+        self._states = {}
+        self._lock = threading.Lock()
+
+    def load(self, analyzer):
+        with self._lock:
+            return self._states.get(analyzer)
+
+    def persist(self, analyzer, state) -> None:
+        with self._lock:
+            self._states[analyzer] = state
+
+    def __str__(self):
+        return "InMemoryStateProvider(%s)" % ", ".join("%s -> %r" % kv for kv in self._states.items())
+
+
+def _distinct(analyzers: Iterable[Analyzer]) -> List[Analyzer]:
+    seen, out = set(), []
+    for a in analyzers:
+        if a not in seen:
+            seen.add(a)
+            out.append(a)
+    return out
+
+
+class AnalysisRunner:
+    @staticmethod
+    def onData(data) -> "AnalysisRunBuilder":
+        return AnalysisRunBuilder(data)
+
+    @staticmethod
+    def run(data, analysis: "Analysis", aggregateWith=None, saveStatesWith=None) -> AnalyzerContext:
+        return AnalysisRunner.doAnalysisRun(data, analysis.analyzers, aggregateWith, saveStatesWith)
+
+    @staticmethod
+    def doAnalysisRun(data, analyzers: Sequence[Analyzer], aggregateWith=None,
+                      saveStatesWith=None) -> AnalyzerContext:
+        analyzers = _distinct(analyzers)
+        if not analyzers:
+            return AnalyzerContext.empty()
+        schema = data.schema
+        passed, failed = [], OrderedDict()
+        for a in analyzers:
+            err = Preconditions.findFirstFailing(schema, a.preconditions())
+            if err is None:
+                passed.append(a)
+            else:
+                failed[a] = a.toFailureMetric(err)
+        ctx = AnalyzerContext(failed)
+        ctx = ctx + AnalysisRunner._runScanningAnalyzers(data, passed, aggregateWith, saveStatesWith)
+        # keep the caller's order
+        return AnalyzerContext(OrderedDict((a, ctx.metricMap[a]) for a in analyzers if a in ctx.metricMap))
+
+    @staticmethod
+    def _runScanningAnalyzers(data, analyzers, aggregateWith, saveStatesWith) -> AnalyzerContext:
+        from .engine import op_spec_for, op_supported, run_scan
+        shareable = [a for a in analyzers if isinstance(a, ScanShareableAnalyzer)]
+        others = [a for a in analyzers if not isinstance(a, ScanShareableAnalyzer)]
+        results = OrderedDict()
+        # GPU eligibility is decided per analyzer at plan time (the reference's JNI shim
+        # would leave an ineligible analyzer on Spark; here it becomes a failure metric)
+        eligible = []
+        for a in shareable:
+            try:
+                op_supported(op_spec_for(a, data.schema), data.schema)
+                eligible.append(a)
+            except Exception as e:  # noqa: BLE001
+                results[a] = a.toFailureMetric(e)
+        if eligible:
+            try:
+                states = run_scan(eligible, data)
+                for a in eligible:
+                    try:
+                        results[a] = a.calculateMetric(states[a], aggregateWith, saveStatesWith)
+                    except Exception as e:  # noqa: BLE001 - one analyzer fails (:348-352)
+                        results[a] = a.toFailureMetric(e)
+            except Exception as e:  # noqa: BLE001 - the whole pass fails (:320-323)
+                for a in eligible:
+                    results[a] = a.toFailureMetric(e)
+        for a in others:
+            results[a] = a.calculate(data, aggregateWith, saveStatesWith)
+        return AnalyzerContext(results)
+
+    @staticmethod
+    def runOnAggregatedStates(schema: Dict[str, str], analysis: "Analysis", stateLoaders,
+                              saveStatesWith=None) -> AnalyzerContext:
+        """Metrics from the merge of persisted states (AnalysisRunner.scala:385-460)."""
+        analyzers = _distinct(analysis.analyzers)
+        results = OrderedDict()
+        for a in analyzers:
+            err = Preconditions.findFirstFailing(schema, a.preconditions())
+            if err is not None:
+                results[a] = a.toFailureMetric(err)
+                continue
+            try:
+                from .states import merge
+                state = merge(*[loader.load(a) for loader in stateLoaders])
+                if state is not None and saveStatesWith is not None:
+                    saveStatesWith.persist(a, state)
+                results[a] = a.computeMetricFrom(state)
+            except Exception as e:  # noqa: BLE001
+                results[a] = a.toFailureMetric(e)
+        return AnalyzerContext(results)
+
+
+class AnalysisRunBuilder:
+    """AnalysisRunBuilder (runners/AnalysisRunBuilder.scala:25-116)."""
+
+    def __init__(self, data):
+        self.data = data
+        self.analyzers: List[Analyzer] = []
+        self._aggregate_with = None
+        self._save_states_with = None
+
+    def addAnalyzer(self, analyzer: Analyzer) -> "AnalysisRunBuilder":
+        self.analyzers.append(analyzer)
+        return self
+
+    def addAnalyzers(self, analyzers: Sequence[Analyzer]) -> "AnalysisRunBuilder":
+        self.analyzers.extend(analyzers)
+        return self
+
+    def aggregateWith(self, loader) -> "AnalysisRunBuilder":
+        self._aggregate_with = loader
+        return self
+
+    def saveStatesWith(self, persister) -> "AnalysisRunBuilder":
+        self._save_states_with = persister
+        return self
+
+    def run(self) -> AnalyzerContext:
+        return AnalysisRunner.doAnalysisRun(self.data, self.analyzers, self._aggregate_with,
+                                            self._save_states_with)
+
+
+class Analysis:
+    """Analysis (analyzers/Analysis.scala): a list of analyzers run together."""
+
+    def __init__(self, analyzers: Sequence[Analyzer] = ()):
+        self.analyzers = list(analyzers)
+
+    def addAnalyzer(self, analyzer: Analyzer) -> "Analysis":
+        return Analysis(self.analyzers + [analyzer])
+
+    def addAnalyzers(self, analyzers: Sequence[Analyzer]) -> "Analysis":
+        return Analysis(self.analyzers + list(analyzers))
+
+    def run(self, data, aggregateWith=None, saveStatesWith=None) -> AnalyzerContext:
+        return AnalysisRunner.doAnalysisRun(data, self.analyzers, aggregateWith, saveStatesWith)

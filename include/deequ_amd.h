@@ -1,0 +1,224 @@
+/*
+ * deequ_amd.h -- C-ABI of the MI355X-native backend for deequ's metric hot path.
+ *
+ * This is the drop-in boundary named by SURVEY.md §8(b).  In the reference there is no
+ * FFI: the seam is the Scala trait pair
+ *     ScanShareableAnalyzer.aggregationFunctions() / fromAggregationResult()
+ *         (src/main/scala/com/amazon/deequ/analyzers/Analyzer.scala:169-197)
+ *     State.sum                                    (Analyzer.scala:34-48)
+ * and the single launch site of the fused scan
+ *     data.agg(aggs.head, aggs.tail: _*).collect().head   (runners/AnalysisRunner.scala:313)
+ * plus the grouping launch site
+ *     FrequencyBasedAnalyzer.computeFrequencies   (analyzers/GroupingAnalyzers.scala:53-80).
+ * A JNI shim replaces those call sites for GPU-eligible analyzers: it
+ * creates a plan from the analyzers, feeds Arrow-layout column batches, and turns the POD
+ * states returned here into the unchanged Scala `State` case classes, which then flow into
+ * Analyzer.calculateMetric (Analyzer.scala:107-128) exactly as Spark-produced states do.
+ *
+ * Conventions
+ *   - Every function returns dq_status (0 = OK).  No C++ exception crosses the ABI.
+ *     dq_last_error() returns a thread-local message for the last failure.
+ *   - Columns use the Arrow layout: validity bitmap LSB-first, 1 = valid (NULL pointer = no
+ *     nulls), fixed-width values, utf8 = int32 offsets + bytes.  A column's buffers are either
+ *     host memory (copied to HBM by the library) or device memory on the context's GPU
+ *     (DQ_COL_DEVICE; used in place, never copied).
+ *   - Plans are not thread-safe; use one plan per calling thread.  Contexts may be shared.
+ */
+#ifndef DEEQU_AMD_H
+#define DEEQU_AMD_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DQ_ABI_VERSION 1
+
+/* ---------------------------------------------------------------- status codes */
+typedef enum dq_status {
+  DQ_OK = 0,
+  DQ_ERR_INVALID = 1,      /* bad argument (maps to IllegalArgumentException)           */
+  DQ_ERR_UNSUPPORTED = 2,  /* op/type/predicate not on the GPU path: route it to Spark   */
+  DQ_ERR_DEVICE = 3,       /* HIP runtime failure or no usable gfx950 device             */
+  DQ_ERR_OOM = 4,          /* device allocation failed                                   */
+  DQ_ERR_STATE = 5         /* call out of order (e.g. consume after finish without reset)*/
+} dq_status;
+
+/* ---------------------------------------------------------------- column types */
+typedef enum dq_type {
+  DQ_T_BOOL = 1,     /* Arrow bit-packed boolean                    (Spark BooleanType) */
+  DQ_T_INT8 = 2,     /*                                             (ByteType)          */
+  DQ_T_INT16 = 3,    /*                                             (ShortType)         */
+  DQ_T_INT32 = 4,    /*                                             (IntegerType)       */
+  DQ_T_INT64 = 5,    /*                                             (LongType)          */
+  DQ_T_FLOAT32 = 6,  /*                                             (FloatType)         */
+  DQ_T_FLOAT64 = 7,  /*                                             (DoubleType)        */
+  DQ_T_UTF8 = 8      /* int32 offsets + UTF-8 bytes                 (StringType)        */
+} dq_type;
+
+#define DQ_COL_DEVICE 0x1 /* validity/values/offsets are device pointers on ctx's GPU */
+
+typedef struct dq_column {
+  int32_t type;             /* dq_type                                                   */
+  int32_t flags;            /* DQ_COL_*                                                  */
+  int64_t length;           /* number of rows in this batch                             */
+  int64_t offset;           /* Arrow slot offset of row 0 (elements; bits for bitmaps)  */
+  const uint8_t* validity;  /* LSB-first bitmap, 1 = valid; NULL = no nulls             */
+  const void* values;       /* fixed-width values, bit-packed bools, or utf8 bytes      */
+  const int32_t* offsets;   /* utf8 only: length+1 offsets (from `offset`)              */
+} dq_column;
+
+/* ---------------------------------------------------------------- analyzer ops */
+typedef enum dq_op_kind {
+  DQ_OP_SIZE = 1,                  /* Size(where)                       Size.scala:35-47        */
+  DQ_OP_COMPLETENESS = 2,          /* Completeness(column, where)       Completeness.scala:26-46*/
+  DQ_OP_COMPLIANCE = 3,            /* Compliance(instance, pred, where) Compliance.scala:37-53  */
+  DQ_OP_SUM = 4,                   /* Sum(column, where)                Sum.scala:35-52         */
+  DQ_OP_MEAN = 5,                  /* Mean(column, where)               Mean.scala:36-54        */
+  DQ_OP_STDDEV = 6,                /* StandardDeviation(column, where)  StandardDeviation.scala:47-73 */
+  DQ_OP_MINIMUM = 7,               /* Minimum(column, where)            Minimum.scala:35-53     */
+  DQ_OP_MAXIMUM = 8,               /* Maximum(column, where)            Maximum.scala:35-53     */
+  DQ_OP_APPROX_COUNT_DISTINCT = 9  /* ApproxCountDistinct(column, where) ApproxCountDistinct.scala:47-64 */
+} dq_op_kind;
+
+/*
+ * Predicate IR: an analyzed Catalyst boolean expression (casts resolved) in postfix form.
+ * It covers what deequ's Check DSL emits for numeric columns (Check.scala:594-943:
+ * comparisons, COALESCE, IN, BETWEEN, IS [NOT] NULL, AND/OR/NOT) with SQL three-valued
+ * logic.  Anything else is rejected with DQ_ERR_UNSUPPORTED at plan time.
+ *
+ * Value instructions push a typed value (int64, fp64 or UTF-8 string, each with a NULL flag);
+ * boolean instructions pop/push three-valued booleans.  Numeric comparisons compare in the type
+ * given by `arg` (DQ_CMP_AS_INT64 / DQ_CMP_AS_FLOAT64), converting operands first; two strings
+ * compare byte-wise (unsigned, then by length), as Spark's UTF8String.compareTo.
+ */
+typedef enum dq_pred_opcode {
+  DQ_P_COLUMN = 1,     /* push value of batch column `arg`                                  */
+  DQ_P_LIT_INT = 2,    /* push int64 literal `i64`                                          */
+  DQ_P_LIT_FLOAT = 3,  /* push fp64 literal `f64`                                           */
+  DQ_P_LIT_NULL = 4,   /* push NULL                                                         */
+  DQ_P_COALESCE = 5,   /* pop b, a; push a if a non-NULL else b                             */
+  DQ_P_LIT_STRING = 6, /* push UTF-8 literal strings[i64 .. i64 + arg) of the predicate      */
+  DQ_P_EQ = 10, DQ_P_NE = 11, DQ_P_LT = 12, DQ_P_LE = 13, DQ_P_GT = 14, DQ_P_GE = 15,
+  DQ_P_EQ_NULLSAFE = 16, /* <=>                                                             */
+  DQ_P_IS_NULL = 20,   /* pop value; push boolean (never NULL)                              */
+  DQ_P_IS_NOT_NULL = 21,
+  DQ_P_AND = 30, DQ_P_OR = 31, DQ_P_NOT = 32,
+  DQ_P_TRUE = 33, DQ_P_FALSE = 34
+} dq_pred_opcode;
+
+#define DQ_CMP_AS_INT64 0
+#define DQ_CMP_AS_FLOAT64 1
+
+typedef struct dq_pred_insn {
+  int32_t opcode;  /* dq_pred_opcode                                   */
+  int32_t arg;     /* column index (DQ_P_COLUMN) or DQ_CMP_AS_* (cmp)  */
+  int64_t i64;
+  double f64;
+} dq_pred_insn;
+
+typedef struct dq_predicate {
+  const dq_pred_insn* code;  /* NULL/0 = no predicate                     */
+  int32_t n_insns;
+  int32_t strings_len;       /* bytes in `strings`                        */
+  const uint8_t* strings;    /* pool for DQ_P_LIT_STRING (may be NULL)    */
+} dq_predicate;
+
+typedef struct dq_op {
+  int32_t kind;              /* dq_op_kind                                     */
+  int32_t column;            /* batch column index; ignored for SIZE/COMPLIANCE */
+  dq_predicate predicate;    /* COMPLIANCE only                                */
+  dq_predicate where;        /* optional filter (Analyzers.conditionalSelection) */
+} dq_op;
+
+/* ---------------------------------------------------------------- states */
+#define DQ_HLL_NUM_WORDS 52   /* StatefulHyperloglogPlus.scala:154 */
+
+/*
+ * POD image of the Scala State returned for one op.  `has_value` = 0 is Scala `None`
+ * (Spark returned SQL NULL, e.g. Mean over an all-NULL column).  Which fields are meaningful
+ * depends on `kind`:
+ *   SIZE                         NumMatches(num_matches)
+ *   COMPLETENESS, COMPLIANCE     NumMatchesAndCount(num_matches, count)
+ *   SUM                          SumState(sum)
+ *   MEAN                         MeanState(sum, count)
+ *   STDDEV                       StandardDeviationState(n, avg, m2)
+ *   MINIMUM / MAXIMUM            MinState(value) / MaxState(value)
+ *   APPROX_COUNT_DISTINCT        ApproxCountDistinctState(words)  (always has_value = 1)
+ */
+typedef struct dq_state {
+  int32_t kind;
+  int32_t has_value;
+  int64_t num_matches;
+  int64_t count;
+  double sum;
+  double n, avg, m2;
+  double value;
+  int64_t words[DQ_HLL_NUM_WORDS];
+} dq_state;
+
+/* ---------------------------------------------------------------- context / plan */
+typedef struct dq_ctx dq_ctx;
+typedef struct dq_plan dq_plan;
+
+const char* dq_last_error(void);
+int dq_abi_version(void);
+
+/* Number of gfx950 devices visible to this process (0 on a host without a GPU). */
+dq_status dq_device_count(int* out);
+
+dq_status dq_ctx_create(int device, int flags, dq_ctx** out);
+dq_status dq_ctx_destroy(dq_ctx* ctx);
+
+/* Build a plan for `n_ops` analyzers over batches with `n_columns` columns of the given
+ * types.  All scan-shareable ops of a plan run in one fused pass per batch
+ * (AnalysisRunner.scala:306-313).  Returns DQ_ERR_UNSUPPORTED (and sets *out = NULL) if any
+ * op cannot run on the GPU; the caller then routes that op to Spark. */
+dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
+                         const int32_t* column_types, int n_columns, dq_plan** out);
+dq_status dq_plan_destroy(dq_plan* plan);
+
+/* Check whether a single op is GPU-eligible for the given schema without building a plan. */
+dq_status dq_op_supported(const dq_op* op, const int32_t* column_types, int n_columns);
+
+/* Enqueue one batch (a row partition).  Asynchronous on the plan's HIP stream; host buffers
+ * must stay valid until the next dq_plan_* call on this plan returns.  May be called any
+ * number of times; results accumulate in HBM in call order (deterministic). */
+dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, int n_columns,
+                          int64_t n_rows);
+
+/* Wait for all consumed batches and write one dq_state per op (in op order). */
+dq_status dq_plan_finish(dq_plan* plan, dq_state* out, int n_out);
+
+/* Clear accumulated results so the plan can scan a new dataset. */
+dq_status dq_plan_reset(dq_plan* plan);
+
+/* The HIP stream (hipStream_t) the plan launches on, for external timing/sync. */
+void* dq_plan_stream(dq_plan* plan);
+
+/* ---------------------------------------------------------------- state algebra (host) */
+/* `Analyzers.merge` (Analyzer.scala:367-386) over Option[State]: out = a + b with None
+ * handling; `a` and `b` must have the same kind.  Mirrors each State.sum. */
+dq_status dq_state_merge(const dq_state* a, const dq_state* b, dq_state* out);
+
+/* `DoubleValuedState.metricValue()` of a state with has_value = 1. */
+dq_status dq_state_metric(const dq_state* s, double* out);
+
+/* DeequHyperLogLogPlusPlusUtils.count (StatefulHyperloglogPlus.scala:210-257). */
+double dq_hll_count(const int64_t words[DQ_HLL_NUM_WORDS]);
+/* DeequHyperLogLogPlusPlusUtils.merge (StatefulHyperloglogPlus.scala:188-208). */
+void dq_hll_merge(const int64_t a[DQ_HLL_NUM_WORDS], const int64_t b[DQ_HLL_NUM_WORDS],
+                  int64_t out[DQ_HLL_NUM_WORDS]);
+/* wordsToBytes / wordsFromBytes (StatefulHyperloglogPlus.scala:170-186): 416 big-endian bytes. */
+void dq_hll_words_to_bytes(const int64_t words[DQ_HLL_NUM_WORDS], uint8_t out[416]);
+void dq_hll_words_from_bytes(const uint8_t in[416], int64_t words[DQ_HLL_NUM_WORDS]);
+
+/* Spark 2.2.2 XxHash64Function with seed 42 for one value (host reference, used by tests). */
+uint64_t dq_xxh64(const void* data, size_t len, uint64_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DEEQU_AMD_H */

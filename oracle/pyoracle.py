@@ -1,0 +1,1054 @@
+"""TEST INFRASTRUCTURE ONLY -- CPU restatement ("oracle") of deequ's metric hot path.
+
+Only `tests/`, `__graft_entry__.smoke()` and `bench.py`'s cpu_baseline leg may
+import this module, and only as the checker.  The product (`deequ_amd`) never
+imports it and has no CPU fallback.
+
+What is restated (reference = /root/reference, deequ 1.0.3-SNAPSHOT on Spark 2.2.2):
+
+* States and their algebra (`State.sum`, `metricValue`):
+  NumMatches `Size.scala:23-31`, NumMatchesAndCount `Analyzer.scala:230-244`,
+  SumState `Sum.scala:25-33`, MeanState `Mean.scala:25-34`,
+  StandardDeviationState `StandardDeviation.scala:25-45`, MinState `Minimum.scala:25-33`,
+  MaxState `Maximum.scala:25-33`, ApproxCountDistinctState `ApproxCountDistinct.scala:26-40`,
+  FrequenciesAndNumRows `GroupingAnalyzers.scala:124-157`, Option merge `Analyzer.scala:367-386`.
+* Aggregations with Spark 2.2.2 NULL semantics:
+  Size `Size.scala:35-47`, Completeness `Completeness.scala:26-46`,
+  Compliance `Compliance.scala:37-53`, Sum/Mean/Min/Max (`sum/count/min/max ... cast`),
+  StandardDeviation = Spark `CentralMomentAgg` update/merge (row a-7 of SURVEY §8),
+  conditionalSelection / conditionalCount `Analyzer.scala:409-432`.
+* HLL++: `StatefulHyperloglogPlus.scala:89-115` (update), `:121-139`/`:188-208` (merge),
+  `:210-297` (count / estimateBias), `:170-186` (words <-> bytes), constants
+  `HLLConstants.scala:27-37` + the p=9 bias tables (`hll_p9_tables.py`).
+  Hash: Spark 2.2.2 `XxHash64Function` = XXH64 with seed 42 over the 4-byte (int
+  family, float bits), 8-byte (long, double bits) little-endian value or UTF-8 bytes.
+  XXH64 itself is the third-party algorithm (Spark `XXH64` port of Yann Collet's
+  xxHash64, not vendored); it is restated here from the published spec and pinned
+  against the `xxhash` 3.8.1 Python binding.
+* Frequency family: `GroupingAnalyzers.scala:53-80` (group-by, NULL rows dropped,
+  numRows = all rows), Uniqueness `Uniqueness.scala:29-31`, Distinctness
+  `Distinctness.scala:32-34`, Entropy `Entropy.scala:31-41`, CountDistinct
+  `CountDistinct.scala:27-33`, UniqueValueRatio `UniqueValueRatio.scala:28-37`,
+  Histogram `Histogram.scala:54-96` (cast to string, NULL -> "NullValue").
+
+Parity pins: every known answer of the reference tests listed in SURVEY §8(c) is
+encoded in `tests/golden/reference_known_answers.json` and checked against this
+module by `tests/test_oracle_golden.py`.
+"""
+from __future__ import annotations
+
+import math
+import struct
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+try:  # the oracle directory may be imported as a package or via sys.path
+    from .hll_p9_tables import BIAS_P9, RAW_ESTIMATE_P9, THRESHOLD_P9
+except ImportError:  # pragma: no cover
+    from hll_p9_tables import BIAS_P9, RAW_ESTIMATE_P9, THRESHOLD_P9
+
+MASK64 = (1 << 64) - 1
+
+# ----------------------------------------------------------------------------
+# XXH64 (published spec) + Spark 2.2.2 type dispatch
+# ----------------------------------------------------------------------------
+P1 = 0x9E3779B185EBCA87
+P2 = 0xC2B2AE3D27D4EB4F
+P3 = 0x165667B19E3779F9
+P4 = 0x85EBCA77C2B2AE63
+P5 = 0x27D4EB2F165667C5
+
+
+def _rotl(x: int, r: int) -> int:
+    return ((x << r) | (x >> (64 - r))) & MASK64
+
+
+def _round(acc: int, lane: int) -> int:
+    acc = (acc + lane * P2) & MASK64
+    acc = _rotl(acc, 31)
+    return (acc * P1) & MASK64
+
+
+def _merge_round(acc: int, val: int) -> int:
+    acc ^= _round(0, val)
+    return (acc * P1 + P4) & MASK64
+
+
+def xxh64(data: bytes, seed: int = 42) -> int:
+    """XXH64 over `data` (unsigned 64-bit result)."""
+    n = len(data)
+    seed &= MASK64
+    i = 0
+    if n >= 32:
+        v1 = (seed + P1 + P2) & MASK64
+        v2 = (seed + P2) & MASK64
+        v3 = seed
+        v4 = (seed - P1) & MASK64
+        while i + 32 <= n:
+            a, b, c, d = struct.unpack_from("<4Q", data, i)
+            v1 = _round(v1, a)
+            v2 = _round(v2, b)
+            v3 = _round(v3, c)
+            v4 = _round(v4, d)
+            i += 32
+        h = (_rotl(v1, 1) + _rotl(v2, 7) + _rotl(v3, 12) + _rotl(v4, 18)) & MASK64
+        h = _merge_round(h, v1)
+        h = _merge_round(h, v2)
+        h = _merge_round(h, v3)
+        h = _merge_round(h, v4)
+    else:
+        h = (seed + P5) & MASK64
+    h = (h + n) & MASK64
+    while i + 8 <= n:
+        (k,) = struct.unpack_from("<Q", data, i)
+        h ^= _round(0, k)
+        h = (_rotl(h, 27) * P1 + P4) & MASK64
+        i += 8
+    if i + 4 <= n:
+        (k,) = struct.unpack_from("<I", data, i)
+        h ^= (k * P1) & MASK64
+        h = (_rotl(h, 23) * P2 + P3) & MASK64
+        i += 4
+    while i < n:
+        h ^= (data[i] * P5) & MASK64
+        h = (_rotl(h, 11) * P1) & MASK64
+        i += 1
+    h ^= h >> 33
+    h = (h * P2) & MASK64
+    h ^= h >> 29
+    h = (h * P3) & MASK64
+    h ^= h >> 32
+    return h
+
+
+try:  # the reference C implementation, used for speed once xxh64() is pinned against it
+    import xxhash as _xxhash
+
+    def _xxh(data: bytes, seed: int) -> int:
+        return _xxhash.xxh64_intdigest(data, seed)
+except ImportError:  # pragma: no cover
+    _xxh = None
+
+
+def spark_hash(value, dtype: str, seed: int = 42) -> int:
+    """Spark 2.2.2 `XxHash64Function.hash(value, dataType, seed)` for the types deequ
+    feeds into HLL (unsigned 64-bit result; the caller reinterprets as signed)."""
+    xxh64 = _xxh if _xxh is not None else globals()["xxh64"]
+    if dtype in ("int8", "int16", "int32", "date32"):
+        return xxh64(struct.pack("<i", int(value)), seed)
+    if dtype == "bool":
+        return xxh64(struct.pack("<i", 1 if value else 0), seed)
+    if dtype in ("int64", "timestamp"):
+        return xxh64(struct.pack("<q", int(value)), seed)
+    if dtype == "float32":
+        f = float(value)
+        bits = 0x7FC00000 if math.isnan(f) else struct.unpack("<I", struct.pack("<f", f))[0]
+        return xxh64(struct.pack("<I", bits), seed)
+    if dtype == "float64":
+        d = float(value)
+        bits = 0x7FF8000000000000 if math.isnan(d) else struct.unpack("<Q", struct.pack("<d", d))[0]
+        return xxh64(struct.pack("<Q", bits), seed)
+    if dtype == "string":
+        return xxh64(value.encode("utf-8") if isinstance(value, str) else bytes(value), seed)
+    raise ValueError("unsupported hash type " + dtype)
+
+
+# ----------------------------------------------------------------------------
+# HLL++ (p = 9) exactly as StatefulHyperloglogPlus / DeequHyperLogLogPlusPlusUtils
+# ----------------------------------------------------------------------------
+HLL_P = 9
+HLL_M = 1 << HLL_P
+HLL_IDX_SHIFT = 64 - HLL_P
+HLL_W_PADDING = 1 << (HLL_P - 1)
+HLL_NUM_WORDS = 52
+HLL_REGISTER_SIZE = 6
+HLL_REGISTERS_PER_WORD = 10
+HLL_REGISTER_WORD_MASK = (1 << HLL_REGISTER_SIZE) - 1
+HLL_ALPHA_M2 = (0.7213 / (1.0 + 1.079 / HLL_M)) * HLL_M * HLL_M
+HLL_K = 6
+
+
+def _nlz64(x: int) -> int:
+    return 64 - x.bit_length() if x else 64
+
+
+def hll_index_and_rank(x: int) -> Tuple[int, int]:
+    """`StatefulHyperloglogPlus.scala:96,99`: idx = x >>> 55; pw = nlz((x << 9) | 256) + 1."""
+    idx = x >> HLL_IDX_SHIFT
+    pw = _nlz64(((x << HLL_P) & MASK64) | HLL_W_PADDING) + 1
+    return idx, pw
+
+
+def hll_registers(values: Sequence, dtype: str) -> List[int]:
+    """512 registers after updating with every non-null value (`:89-115`)."""
+    regs = [0] * HLL_M
+    for v in values:
+        if v is None:
+            continue
+        idx, pw = hll_index_and_rank(spark_hash(v, dtype))
+        if pw > regs[idx]:
+            regs[idx] = pw
+    return regs
+
+
+def _to_signed64(u: int) -> int:
+    return u - (1 << 64) if u >= (1 << 63) else u
+
+
+def hll_pack(regs: Sequence[int]) -> List[int]:
+    """Registers -> 52 signed Long words, 10 six-bit registers per word (`:102-113`)."""
+    words = []
+    for w in range(HLL_NUM_WORDS):
+        word = 0
+        for i in range(HLL_REGISTERS_PER_WORD):
+            idx = w * HLL_REGISTERS_PER_WORD + i
+            if idx < HLL_M:
+                word |= (regs[idx] & HLL_REGISTER_WORD_MASK) << (HLL_REGISTER_SIZE * i)
+        words.append(_to_signed64(word))
+    return words
+
+
+def hll_unpack(words: Sequence[int]) -> List[int]:
+    regs = []
+    for idx in range(HLL_M):
+        w = words[idx // HLL_REGISTERS_PER_WORD] & MASK64
+        regs.append((w >> (HLL_REGISTER_SIZE * (idx % HLL_REGISTERS_PER_WORD))) & HLL_REGISTER_WORD_MASK)
+    return regs
+
+
+def hll_merge(words1: Sequence[int], words2: Sequence[int]) -> List[int]:
+    """`DeequHyperLogLogPlusPlusUtils.merge` (`:188-208`): per-register max."""
+    return hll_pack([max(a, b) for a, b in zip(hll_unpack(words1), hll_unpack(words2))])
+
+
+def _java_int_shift_one(m: int) -> int:
+    """Java `1 << m` for Int with a Long shift count: the count is masked to 5 bits and
+    the result is a signed 32-bit int (so 1 << 31 is negative, 1 << 32 == 1)."""
+    r = (1 << (m & 31)) & 0xFFFFFFFF
+    return r - (1 << 32) if r >= (1 << 31) else r
+
+
+def _estimate_bias(e: float) -> float:
+    """`DeequHyperLogLogPlusPlusUtils.estimateBias` (`:259-297`)."""
+    estimates = RAW_ESTIMATE_P9
+    n = len(estimates)
+    # java.util.Arrays.binarySearch: index if found, else -(insertion point) - 1
+    lo, hi, found = 0, n - 1, None
+    while lo <= hi:
+        mid = (lo + hi) >> 1
+        if estimates[mid] < e:
+            lo = mid + 1
+        elif estimates[mid] > e:
+            hi = mid - 1
+        else:
+            found = mid
+            break
+    nearest = found if found is not None else lo
+
+    def distance(i):
+        d = e - estimates[i]
+        return d * d
+
+    low = max(nearest - HLL_K + 1, 0)
+    high = min(low + HLL_K, n)
+    while high < n and distance(high) < distance(low):
+        low += 1
+        high += 1
+    bias_sum = 0.0
+    for i in range(low, high):
+        bias_sum += BIAS_P9[i]
+    return bias_sum / (high - low)
+
+
+def _java_round(x: float) -> float:
+    """Java `Math.round(double)` (floor(x + 0.5), saturating), returned as a double."""
+    if math.isnan(x):
+        return 0.0
+    r = math.floor(x + 0.5)
+    return float(max(min(r, 2 ** 63 - 1), -(2 ** 63)))
+
+
+def hll_count(words: Sequence[int]) -> float:
+    """`DeequHyperLogLogPlusPlusUtils.count` (`:210-257`), sequential order kept."""
+    z_inverse = 0.0
+    v = 0.0
+    for idx in range(HLL_M):
+        w = words[idx // HLL_REGISTERS_PER_WORD] & MASK64
+        m = (w >> (HLL_REGISTER_SIZE * (idx % HLL_REGISTERS_PER_WORD))) & HLL_REGISTER_WORD_MASK
+        z_inverse += 1.0 / _java_int_shift_one(m)
+        if m == 0:
+            v += 1.0
+
+    def e_bias_corrected():
+        e = HLL_ALPHA_M2 / z_inverse
+        if HLL_P < 19 and e < 5.0 * HLL_M:
+            return e - _estimate_bias(e)
+        return e
+
+    if v > 0:
+        h = HLL_M * math.log(HLL_M / v)
+        estimate = h if h <= THRESHOLD_P9 else e_bias_corrected()
+    else:
+        estimate = e_bias_corrected()
+    return _java_round(estimate)
+
+
+def hll_words_to_bytes(words: Sequence[int]) -> bytes:
+    """`wordsToBytes` (`:170-178`): big-endian longs."""
+    return struct.pack(">52q", *words)
+
+
+def hll_words_from_bytes(b: bytes) -> List[int]:
+    return list(struct.unpack(">52q", b))
+
+
+# ----------------------------------------------------------------------------
+# States (Scala case classes) and their algebra
+# ----------------------------------------------------------------------------
+@dataclass(frozen=True)
+class NumMatches:
+    num_matches: int
+
+    def sum(self, o):
+        return NumMatches(_wrap64(self.num_matches + o.num_matches))
+
+    def metric_value(self):
+        return float(self.num_matches)
+
+
+@dataclass(frozen=True)
+class NumMatchesAndCount:
+    num_matches: int
+    count: int
+
+    def sum(self, o):
+        return NumMatchesAndCount(_wrap64(self.num_matches + o.num_matches), _wrap64(self.count + o.count))
+
+    def metric_value(self):
+        return float("nan") if self.count == 0 else float(self.num_matches) / self.count
+
+
+@dataclass(frozen=True)
+class SumState:
+    sum_: float
+
+    def sum(self, o):
+        return SumState(self.sum_ + o.sum_)
+
+    def metric_value(self):
+        return self.sum_
+
+
+@dataclass(frozen=True)
+class MeanState:
+    sum_: float
+    count: int
+
+    def sum(self, o):
+        return MeanState(self.sum_ + o.sum_, _wrap64(self.count + o.count))
+
+    def metric_value(self):
+        return float("nan") if self.count == 0 else self.sum_ / self.count
+
+
+@dataclass(frozen=True)
+class StandardDeviationState:
+    n: float
+    avg: float
+    m2: float
+
+    def __post_init__(self):
+        if not self.n > 0.0:
+            raise ValueError("Standard deviation is undefined for n = 0.")
+
+    def sum(self, o):  # StandardDeviation.scala:37-44
+        new_n = self.n + o.n
+        delta = o.avg - self.avg
+        delta_n = 0.0 if new_n == 0.0 else delta / new_n
+        return StandardDeviationState(new_n, self.avg + delta_n * o.n,
+                                      self.m2 + o.m2 + delta * delta_n * self.n * o.n)
+
+    def metric_value(self):
+        return math.sqrt(self.m2 / self.n)
+
+
+def _java_min(a: float, b: float) -> float:
+    """java.lang.Math.min(double, double): NaN-propagating, -0.0 < 0.0."""
+    if a != a:
+        return a
+    if b != b:
+        return b
+    if a == 0.0 and b == 0.0:
+        return a if math.copysign(1.0, a) < 0 else b
+    return a if a <= b else b
+
+
+def _java_max(a: float, b: float) -> float:
+    if a != a:
+        return a
+    if b != b:
+        return b
+    if a == 0.0 and b == 0.0:
+        return a if math.copysign(1.0, a) > 0 else b
+    return a if a >= b else b
+
+
+@dataclass(frozen=True)
+class MinState:
+    min_value: float
+
+    def sum(self, o):
+        return MinState(_java_min(self.min_value, o.min_value))
+
+    def metric_value(self):
+        return self.min_value
+
+
+@dataclass(frozen=True)
+class MaxState:
+    max_value: float
+
+    def sum(self, o):
+        return MaxState(_java_max(self.max_value, o.max_value))
+
+    def metric_value(self):
+        return self.max_value
+
+
+@dataclass(frozen=True)
+class ApproxCountDistinctState:
+    words: Tuple[int, ...]
+
+    def sum(self, o):
+        return ApproxCountDistinctState(tuple(hll_merge(self.words, o.words)))
+
+    def metric_value(self):
+        return hll_count(self.words)
+
+
+@dataclass
+class FrequenciesAndNumRows:
+    frequencies: Dict[tuple, int]
+    num_rows: int
+
+    def sum(self, o):  # null-safe outer join, counts added (GroupingAnalyzers.scala:128-148)
+        out = dict(self.frequencies)
+        for k, c in o.frequencies.items():
+            out[k] = out.get(k, 0) + c
+        return FrequenciesAndNumRows(out, self.num_rows + o.num_rows)
+
+
+def merge_options(*states):
+    """`Analyzers.merge` (`Analyzer.scala:367-386`)."""
+    acc = None
+    for s in states:
+        if acc is None:
+            acc = s
+        elif s is not None:
+            acc = acc.sum(s)
+    return acc
+
+
+def _wrap64(x: int) -> int:
+    x &= MASK64
+    return x - (1 << 64) if x >= (1 << 63) else x
+
+
+# ----------------------------------------------------------------------------
+# Columns and the SQL predicate subset (independent evaluator, 3-valued logic)
+# ----------------------------------------------------------------------------
+@dataclass
+class OColumn:
+    """A column as Spark would see it: python values, None = SQL NULL."""
+    dtype: str            # int8/int16/int32/int64/float32/float64/bool/string
+    values: list
+
+    @staticmethod
+    def from_numpy(dtype: str, values: np.ndarray, valid: Optional[np.ndarray]):
+        vals = values.tolist()
+        if valid is not None:
+            vals = [v if ok else None for v, ok in zip(vals, valid.tolist())]
+        return OColumn(dtype, vals)
+
+
+OTable = Dict[str, OColumn]
+
+_INTEGRAL = ("int8", "int16", "int32", "int64")
+_FRACTIONAL = ("float32", "float64")
+
+
+class _Tok:
+    def __init__(self, text: str):
+        self.toks = self._lex(text)
+        self.i = 0
+
+    @staticmethod
+    def _lex(s: str):
+        out, i = [], 0
+        while i < len(s):
+            c = s[i]
+            if c.isspace():
+                i += 1
+            elif c == "'":
+                j = s.index("'", i + 1)
+                out.append(("str", s[i + 1:j]))
+                i = j + 1
+            elif c.isdigit() or (c == "." and i + 1 < len(s) and s[i + 1].isdigit()):
+                j = i
+                while j < len(s) and (s[j].isdigit() or s[j] == "."):
+                    j += 1
+                if j < len(s) and s[j] in "eE":
+                    j += 1
+                    if s[j] in "+-":
+                        j += 1
+                    while j < len(s) and s[j].isdigit():
+                        j += 1
+                out.append(("num", s[i:j]))
+                i = j
+            elif c.isalpha() or c == "_" or c == "`":
+                if c == "`":
+                    j = s.index("`", i + 1)
+                    out.append(("id", s[i + 1:j]))
+                    i = j + 1
+                    continue
+                j = i
+                while j < len(s) and (s[j].isalnum() or s[j] == "_"):
+                    j += 1
+                out.append(("id", s[i:j]))
+                i = j
+            else:
+                for op in ("<=>", "<=", ">=", "!=", "<>", "==", "<", ">", "=", "(", ")", ",", "-"):
+                    if s.startswith(op, i):
+                        out.append(("op", op))
+                        i += len(op)
+                        break
+                else:
+                    raise ValueError("cannot lex %r" % s[i:])
+        return out
+
+    def peek(self):
+        return self.toks[self.i] if self.i < len(self.toks) else (None, None)
+
+    def next(self):
+        t = self.peek()
+        self.i += 1
+        return t
+
+    def kw(self, word):
+        t = self.peek()
+        if t[0] == "id" and t[1].upper() == word:
+            self.i += 1
+            return True
+        return False
+
+
+def eval_predicate(text: str, table: OTable) -> List[Optional[bool]]:
+    """Evaluate a deequ SQL predicate string (the numeric subset deequ's checks emit:
+    comparisons, IN, BETWEEN, IS [NOT] NULL, COALESCE, AND/OR/NOT, string equality)
+    row by row with SQL three-valued logic.  Returns True/False/None per row."""
+    nrows = len(next(iter(table.values())).values)
+    tk = _Tok(text)
+
+    def operand():
+        t = tk.next()
+        if t[0] == "op" and t[1] == "-":
+            v = operand()
+            return ("neg", v)
+        if t[0] == "op" and t[1] == "(":
+            e = or_expr()
+            assert tk.next() == ("op", ")")
+            return ("paren", e)
+        if t[0] == "num":
+            return ("lit", ("int" if all(ch.isdigit() for ch in t[1]) else
+                            ("double" if "e" in t[1].lower() else "decimal")), t[1])
+        if t[0] == "str":
+            return ("lit", "string", t[1])
+        if t[0] == "id":
+            if t[1].upper() == "COALESCE":
+                assert tk.next() == ("op", "(")
+                args = [operand()]
+                while tk.peek() == ("op", ","):
+                    tk.next()
+                    args.append(operand())
+                assert tk.next() == ("op", ")")
+                return ("coalesce", args)
+            if t[1].upper() in ("TRUE", "FALSE"):
+                return ("lit", "bool", t[1].upper() == "TRUE")
+            if t[1].upper() == "NULL":
+                return ("lit", "null", None)
+            return ("col", t[1])
+        raise ValueError("bad operand %r" % (t,))
+
+    def comparison():
+        left = operand()
+        t = tk.peek()
+        if t[0] == "op" and t[1] in ("<", "<=", ">", ">=", "=", "==", "!=", "<>", "<=>"):
+            tk.next()
+            return ("cmp", t[1], left, operand())
+        negate = False
+        if tk.kw("NOT"):
+            negate = True
+        if tk.kw("IN"):
+            assert tk.next() == ("op", "(")
+            items = [operand()]
+            while tk.peek() == ("op", ","):
+                tk.next()
+                items.append(operand())
+            assert tk.next() == ("op", ")")
+            e = ("in", left, items)
+            return ("not", e) if negate else e
+        if tk.kw("BETWEEN"):
+            lo = operand()
+            assert tk.kw("AND")
+            hi = operand()
+            e = ("and", ("cmp", ">=", left, lo), ("cmp", "<=", left, hi))
+            return ("not", e) if negate else e
+        if tk.kw("IS"):
+            neg = tk.kw("NOT")
+            assert tk.kw("NULL")
+            return ("isnotnull" if neg else "isnull", left)
+        assert not negate
+        return ("bool", left)
+
+    def not_expr():
+        if tk.kw("NOT"):
+            return ("not", not_expr())
+        return comparison()
+
+    def and_expr():
+        e = not_expr()
+        while tk.kw("AND"):
+            e = ("and", e, not_expr())
+        return e
+
+    def or_expr():
+        e = and_expr()
+        while tk.kw("OR"):
+            e = ("or", e, and_expr())
+        return e
+
+    tree = or_expr()
+    assert tk.peek() == (None, None), "trailing tokens in %r" % text
+
+    def typed(node):
+        """Returns (kind, getter) where kind in int/decimal/double/string/bool."""
+        if node[0] == "lit":
+            kind, v = node[1], node[2]
+            if kind == "int":
+                return "int", lambda r, x=int(v): x
+            if kind == "decimal":
+                from fractions import Fraction
+                return "decimal", lambda r, x=Fraction(v): x
+            if kind == "double":
+                return "double", lambda r, x=float(v): x
+            if kind == "string":
+                return "string", lambda r, x=v: x
+            if kind == "bool":
+                return "bool", lambda r, x=v: x
+            return "null", lambda r: None
+        if node[0] == "col":
+            col = table[node[1]]
+            kind = ("int" if col.dtype in _INTEGRAL else "double" if col.dtype in _FRACTIONAL
+                    else col.dtype)
+            return kind, lambda r, c=col: c.values[r]
+        if node[0] == "paren":
+            return typed(node[1])
+        if node[0] == "neg":
+            k, g = typed(node[1])
+            return k, lambda r: None if g(r) is None else -g(r)
+        if node[0] == "coalesce":
+            parts = [typed(a) for a in node[1]]
+            kinds = [k for k, _ in parts if k != "null"]
+            kind = _common(kinds)
+
+            def get(r):
+                for _, g in parts:
+                    v = g(r)
+                    if v is not None:
+                        return v
+                return None
+            return kind, get
+        return "bool", lambda r, n=node: ev(n, r)
+
+    def _common(kinds):
+        if "double" in kinds:
+            return "double"
+        if "decimal" in kinds:
+            return "decimal"
+        if "int" in kinds:
+            return "int"
+        return kinds[0] if kinds else "null"
+
+    def conv(v, src, dst):
+        if v is None:
+            return None
+        if dst == "double":
+            return float(v)
+        if dst == "decimal":
+            from fractions import Fraction
+            return Fraction(v) if not isinstance(v, float) else Fraction(v)
+        if dst == "int":
+            return int(v)
+        if dst == "string" and src in ("int", "double", "decimal"):
+            return str(v)
+        return v
+
+    def coerced_pair(a, b):
+        ka, ga = typed(a)
+        kb, gb = typed(b)
+        if ka == kb:
+            return ka, ga, kb, gb, ka
+        if "string" in (ka, kb) and ka in ("int", "double", "decimal", "string") and kb in (
+                "int", "double", "decimal", "string"):
+            # Spark 2.2 PromoteStrings: numeric vs string compares as double
+            return ka, ga, kb, gb, "double_from_string"
+        target = _common([ka, kb])
+        return ka, ga, kb, gb, target
+
+    def cmp_values(op, x, y):
+        if op in ("=", "==", "<=>"):
+            return x == y
+        if op in ("!=", "<>"):
+            return x != y
+        if op == "<":
+            return x < y
+        if op == "<=":
+            return x <= y
+        if op == ">":
+            return x > y
+        if op == ">=":
+            return x >= y
+        raise ValueError(op)
+
+    def ev(node, r):
+        t = node[0]
+        if t == "cmp":
+            op = node[1]
+            ka, ga, kb, gb, target = coerced_pair(node[2], node[3])
+            x, y = ga(r), gb(r)
+            if op == "<=>":
+                if x is None or y is None:
+                    return x is None and y is None
+            if x is None or y is None:
+                return None
+            if target == "double_from_string":
+                try:
+                    x, y = float(x), float(y)
+                except ValueError:
+                    return None
+            else:
+                x, y = conv(x, ka, target), conv(y, kb, target)
+            if isinstance(x, float) and isinstance(y, float) and (x != x or y != y):
+                # Spark double comparison: NaN = NaN is true and NaN is the largest value
+                xn, yn = x != x, y != y
+                if op in ("=", "==", "<=>"):
+                    return xn and yn
+                if op in ("!=", "<>"):
+                    return not (xn and yn)
+                order = (1 if xn else 0) - (1 if yn else 0)
+                return {"<": order < 0, "<=": order <= 0, ">": order > 0, ">=": order >= 0}[op]
+            return cmp_values(op, x, y)
+        if t == "in":
+            kx, gx = typed(node[1])
+            x = gx(r)
+            if x is None:
+                return None
+            saw_null = False
+            for item in node[2]:
+                res = ev(("cmp", "=", node[1], item), r)
+                if res is True:
+                    return True
+                if res is None:
+                    saw_null = True
+            return None if saw_null else False
+        if t == "and":
+            a, b = ev(node[1], r), ev(node[2], r)
+            if a is False or b is False:
+                return False
+            if a is None or b is None:
+                return None
+            return True
+        if t == "or":
+            a, b = ev(node[1], r), ev(node[2], r)
+            if a is True or b is True:
+                return True
+            if a is None or b is None:
+                return None
+            return False
+        if t == "not":
+            a = ev(node[1], r)
+            return None if a is None else (not a)
+        if t == "isnull":
+            return typed(node[1])[1](r) is None
+        if t == "isnotnull":
+            return typed(node[1])[1](r) is not None
+        if t == "bool":
+            return typed(node[1])[1](r)
+        if t == "paren":
+            return ev(node[1], r)
+        raise ValueError(t)
+
+    return [ev(tree, r) for r in range(nrows)]
+
+
+# ----------------------------------------------------------------------------
+# Analyzer aggregations (Spark 2.2.2 semantics) -> Optional[State]
+# ----------------------------------------------------------------------------
+def _where_mask(table: OTable, where: Optional[str]):
+    n = len(next(iter(table.values())).values)
+    if where is None:
+        return [True] * n
+    return eval_predicate(where, table)
+
+
+def _selected_values(table: OTable, column: str, where: Optional[str]):
+    """`conditionalSelection` (`Analyzer.scala:413-426`): when(cond, col) is NULL when the
+    condition is false or NULL."""
+    w = _where_mask(table, where)
+    return [v if w[i] is True else None for i, v in enumerate(table[column].values)]
+
+
+def _conditional_count(table: OTable, where: Optional[str]) -> Optional[int]:
+    """`conditionalCount` (`Analyzer.scala:428-432`): count(*) or sum(cast(where as long))."""
+    n = len(next(iter(table.values())).values)
+    if where is None:
+        return n
+    w = _where_mask(table, where)
+    nonnull = [x for x in w if x is not None]
+    if not nonnull:
+        return None
+    return sum(1 for x in nonnull if x)
+
+
+def size_state(table: OTable, where: Optional[str] = None):
+    c = _conditional_count(table, where)
+    return None if c is None else NumMatches(c)
+
+
+def completeness_state(table: OTable, column: str, where: Optional[str] = None):
+    n = len(table[column].values)
+    if n == 0:
+        return None  # sum over zero rows is NULL
+    sel = _selected_values(table, column, where)
+    matches = sum(1 for v in sel if v is not None)
+    count = _conditional_count(table, where)
+    return None if count is None else NumMatchesAndCount(matches, count)
+
+
+def compliance_state(table: OTable, predicate: str, where: Optional[str] = None):
+    pred = eval_predicate(predicate, table)
+    w = _where_mask(table, where)
+    sel = [p if w[i] is True else None for i, p in enumerate(pred)]
+    nonnull = [p for p in sel if p is not None]
+    if not nonnull:
+        return None
+    count = _conditional_count(table, where)
+    if count is None:
+        return None
+    return NumMatchesAndCount(sum(1 for p in nonnull if p), count)
+
+
+def _numeric_selected(table, column, where):
+    col = table[column]
+    vals = [v for v in _selected_values(table, column, where) if v is not None]
+    return col.dtype, vals
+
+
+def _spark_sum(dtype, vals):
+    if dtype in _INTEGRAL:
+        return float(_wrap64(sum(int(v) for v in vals)))
+    acc = 0.0
+    for v in vals:  # sequential fp64 as Spark's Sum within one partition
+        acc += float(v)
+    return acc
+
+
+def sum_state(table: OTable, column: str, where: Optional[str] = None):
+    dtype, vals = _numeric_selected(table, column, where)
+    return None if not vals else SumState(_spark_sum(dtype, vals))
+
+
+def mean_state(table: OTable, column: str, where: Optional[str] = None):
+    dtype, vals = _numeric_selected(table, column, where)
+    return None if not vals else MeanState(_spark_sum(dtype, vals), len(vals))
+
+
+def stddev_state(table: OTable, column: str, where: Optional[str] = None):
+    """Spark `CentralMomentAgg` (momentOrder 2) per-row update, one partition."""
+    _, vals = _numeric_selected(table, column, where)
+    n = avg = m2 = 0.0
+    for v in vals:
+        x = float(v)
+        n += 1.0
+        delta = x - avg
+        delta_n = delta / n
+        avg += delta_n
+        m2 += delta * (delta - delta_n)
+    return None if n == 0.0 else StandardDeviationState(n, avg, m2)
+
+
+def _spark_double_lt(a: float, b: float) -> bool:
+    """Spark NaN-safe ordering for doubles: NaN is the largest value, -0.0 == 0.0."""
+    an, bn = a != a, b != b
+    if an or bn:
+        return (not an) and bn
+    return a < b
+
+
+def min_state(table: OTable, column: str, where: Optional[str] = None):
+    dtype, vals = _numeric_selected(table, column, where)
+    if not vals:
+        return None
+    if dtype in _INTEGRAL:
+        return MinState(float(min(int(v) for v in vals)))
+    best = float(vals[0])
+    for v in vals[1:]:
+        if _spark_double_lt(float(v), best):
+            best = float(v)
+    return MinState(best)
+
+
+def max_state(table: OTable, column: str, where: Optional[str] = None):
+    dtype, vals = _numeric_selected(table, column, where)
+    if not vals:
+        return None
+    if dtype in _INTEGRAL:
+        return MaxState(float(max(int(v) for v in vals)))
+    best = float(vals[0])
+    for v in vals[1:]:
+        if _spark_double_lt(best, float(v)):
+            best = float(v)
+    return MaxState(best)
+
+
+def approx_count_distinct_state(table: OTable, column: str, where: Optional[str] = None):
+    """Never None: the HLL aggregate is non-nullable (`StatefulHyperloglogPlus.scala:59`)."""
+    col = table[column]
+    vals = _selected_values(table, column, where)
+    return ApproxCountDistinctState(tuple(hll_pack(hll_registers(vals, col.dtype))))
+
+
+def frequencies_state(table: OTable, columns: Sequence[str]) -> FrequenciesAndNumRows:
+    """`computeFrequencies` (`GroupingAnalyzers.scala:53-80`)."""
+    n = len(table[columns[0]].values)
+    freq: Dict[tuple, int] = {}
+    for r in range(n):
+        key = tuple(table[c].values[r] for c in columns)
+        if any(k is None for k in key):
+            continue
+        key = tuple(_group_key(k, table[c].dtype) for k, c in zip(key, columns))
+        freq[key] = freq.get(key, 0) + 1
+    return FrequenciesAndNumRows(freq, n)
+
+
+def _group_key(v, dtype):
+    if dtype in _FRACTIONAL:
+        v = float(v)
+        if v != v:
+            return "NaN"  # Spark groups all NaNs together
+        if v == 0.0:
+            return 0.0  # -0.0 and 0.0 group together
+    return v
+
+
+def uniqueness_metric(state: FrequenciesAndNumRows) -> Optional[float]:
+    if not state.frequencies:
+        return None  # sum over an empty frequency table is NULL -> empty-state failure
+    return sum(1.0 for c in state.frequencies.values() if c == 1) / state.num_rows
+
+
+def distinctness_metric(state: FrequenciesAndNumRows) -> Optional[float]:
+    if not state.frequencies:
+        return None
+    return sum(1.0 for c in state.frequencies.values() if c >= 1) / state.num_rows
+
+
+def count_distinct_metric(state: FrequenciesAndNumRows) -> float:
+    return float(len(state.frequencies))
+
+
+def unique_value_ratio_metric(state: FrequenciesAndNumRows) -> float:
+    uniq = sum(1.0 for c in state.frequencies.values() if c == 1)
+    return uniq / float(len(state.frequencies)) if state.frequencies else float("nan")
+
+
+def entropy_metric(state: FrequenciesAndNumRows, ordered_counts: Optional[Sequence[int]] = None):
+    """Σ −(c/N)·ln(c/N); `ordered_counts` fixes the fp64 summation order."""
+    counts = list(ordered_counts) if ordered_counts is not None else list(state.frequencies.values())
+    if not counts:
+        return None
+    n = state.num_rows
+    total = 0.0
+    for c in counts:
+        c = float(c)
+        total += 0.0 if c == 0.0 else -(c / n) * math.log(c / n)
+    return total
+
+
+def entropy_exact(state: FrequenciesAndNumRows) -> Optional[float]:
+    if not state.frequencies:
+        return None
+    n = state.num_rows
+    return math.fsum(-(c / n) * math.log(c / n) for c in state.frequencies.values())
+
+
+def java_double_to_string(d: float) -> str:
+    """Java `Double.toString` (shortest-repr digits; the JDK 19+ rule, identical to JDK 8
+    for the values in the reference tests)."""
+    from decimal import Decimal
+    if d != d:
+        return "NaN"
+    if d == math.inf:
+        return "Infinity"
+    if d == -math.inf:
+        return "-Infinity"
+    if d == 0.0:
+        return "-0.0" if math.copysign(1.0, d) < 0 else "0.0"
+    a = abs(d)
+    t = Decimal(repr(a)).normalize().as_tuple()
+    digits = "".join(map(str, t.digits))
+    point = len(digits) + t.exponent  # digits before the decimal point
+    sign = "-" if d < 0 else ""
+    if 1e-3 <= a < 1e7:
+        if point <= 0:
+            body = "0." + "0" * (-point) + digits
+        elif point >= len(digits):
+            body = digits + "0" * (point - len(digits)) + ".0"
+        else:
+            body = digits[:point] + "." + digits[point:]
+        return sign + body
+    return sign + digits[0] + "." + (digits[1:] or "0") + "E" + str(point - 1)
+
+
+def histogram_state(table: OTable, column: str) -> FrequenciesAndNumRows:
+    """`Histogram.computeStateFrom` (`Histogram.scala:54-69`): cast to string, NULL ->
+    "NullValue", group-by count, numRows = data.count()."""
+    col = table[column]
+    freq: Dict[tuple, int] = {}
+    for v in col.values:
+        key = "NullValue" if v is None else _spark_cast_string(v, col.dtype)
+        freq[(key,)] = freq.get((key,), 0) + 1
+    return FrequenciesAndNumRows(freq, len(col.values))
+
+
+def _spark_cast_string(v, dtype):
+    if dtype in _INTEGRAL:
+        return str(int(v))
+    if dtype in _FRACTIONAL:
+        return java_double_to_string(float(v)) if dtype == "float64" else java_double_to_string(float(v))
+    if dtype == "bool":
+        return "true" if v else "false"
+    return str(v)
+
+
+def histogram_metric(state: FrequenciesAndNumRows, max_detail_bins: int = 1000):
+    """Distribution(values: top-N by count, numberOfBins).  Ties at the cut are broken by
+    key (ascending) here; Spark's `rdd.top` breaks them arbitrarily."""
+    items = sorted(state.frequencies.items(), key=lambda kv: (-kv[1], kv[0]))
+    top = items[:max_detail_bins]
+    return {
+        "number_of_bins": len(state.frequencies),
+        "values": {k[0]: (c, c / state.num_rows) for k, c in top},
+    }

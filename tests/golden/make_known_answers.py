@@ -1,0 +1,167 @@
+"""Writes tests/golden/reference_known_answers.json.
+
+Every entry transcribes one known answer of the REFERENCE's own test-suite or docs: the
+fixture table's values (FixtureSupport.scala, NullHandlingTests.scala, examples) and the
+asserted metric, with the reference file:line it comes from.  Values only -- no reference
+code.  The oracle (tests/test_oracle_golden.py) and the GPU path
+(tests/test_gpu_known_answers.py) are both checked against this file.
+
+    python tests/golden/make_known_answers.py
+"""
+import json
+import math
+import os
+
+T = "src/test/scala/com/amazon/deequ/"
+M = "src/main/scala/com/amazon/deequ/"
+
+# --------------------------------------------------------------------------- fixture tables
+TABLES = {
+    # FixtureSupport.getDfMissing (utils/FixtureSupport.scala:45-62)
+    "dfMissing": {
+        "item": ["string", ["1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12"]],
+        "att1": ["string", ["a", "b", None, "a", "a", None, None, "b", "a", None, None, None]],
+        "att2": ["string", ["f", "d", "f", None, "f", "d", "d", None, "f", None, "f", "d"]],
+    },
+    # getDfFull (:64-73)
+    "dfFull": {
+        "item": ["string", ["1", "2", "3", "4"]],
+        "att1": ["string", ["a", "a", "a", "b"]],
+        "att2": ["string", ["c", "c", "c", "d"]],
+    },
+    # getDfWithNumericValues (:137-148) -- att1..att3 are Scala Ints (IntegerType)
+    "dfNumeric": {
+        "item": ["string", ["1", "2", "3", "4", "5", "6"]],
+        "att1": ["int32", [1, 2, 3, 4, 5, 6]],
+        "att2": ["int32", [0, 0, 0, 5, 6, 7]],
+        "att3": ["int32", [0, 0, 0, 4, 6, 7]],
+    },
+    # getDfWithNumericFractionalValues (:150-160)
+    "dfFractional": {
+        "item": ["string", ["1", "2", "3", "4", "5", "6"]],
+        "att1": ["float64", [1.0, 2.0, 3.0, 4.0, 5.0, 6.0]],
+        "att2": ["float64", [0.0, 0.0, 0.0, 5.0, 6.0, 7.0]],
+    },
+    # getDfWithUniqueColumns (:198-211) -- every column is a string
+    "dfUnique": {
+        "unique": ["string", ["1", "2", "3", "4", "5", "6"]],
+        "nonUnique": ["string", ["0", "0", "0", "5", "6", "7"]],
+        "nonUniqueWithNulls": ["string", ["3", "3", "3", None, None, None]],
+        "uniqueWithNulls": ["string", ["1", "2", None, "3", "4", "5"]],
+        "onlyUniqueWithOtherNonUnique": ["string", ["5", "6", "7", "0", "0", "0"]],
+        "halfUniqueCombinedWithNonUnique": ["string", ["0", "0", "0", "4", "5", "6"]],
+    },
+    # IncrementalAnalyzerTest.initialData / deltaData (analyzers/IncrementalAnalyzerTest.scala:243-260)
+    "incrInitial": {
+        "item": ["string", ["1", "2", "3"]],
+        "att1": ["string", ["a", None, "b"]],
+        "count": ["int32", [12, 12, 12]],
+    },
+    "incrDelta": {
+        "item": ["string", ["4", "5"]],
+        "att1": ["string", ["b", None]],
+        "count": ["int32", [12, 12]],
+    },
+    # NullHandlingTests.dataWithNullColumns (analyzers/NullHandlingTests.scala:32-53)
+    "dfNullColumns": {
+        "stringCol": ["string", [None] * 8],
+        "numericCol": ["float64", [None] * 8],
+        "numericCol2": ["float64", [None] * 8],
+        "numericCol3": ["float64", [1.0, 2.0, 3.0, 4.0, 5.0, 6.0, 7.0, 8.0]],
+    },
+    # examples/algebraic_states_example.md:10-14 (Item rows) and :55-58 (more data)
+    "items": {
+        "id": ["int64", [1, 2, 3]],
+        "productName": ["string", ["Thingy A", "Thingy B", "Thing C"]],
+        "description": ["string", ["awesome thing.", "available tomorrow", None]],
+        "priority": ["string", ["high", "low", None]],
+        "numViews": ["int64", [0, 0, 5]],
+    },
+    "itemsMore": {
+        "id": ["int64", [4, 5]],
+        "productName": ["string", ["Thingy D", "Thingy E"]],
+        "description": ["string", [None, None]],
+        "priority": ["string", ["low", "high"]],
+        "numViews": ["int64", [10, 12]],
+    },
+    # getDfEmpty (:26-33)
+    "dfEmpty": {"column1": ["string", []], "column2": ["string", []]},
+}
+
+A = "analyzers/AnalyzerTests.scala"
+EMPTY = "empty"  # the metric is a Failure(EmptyStateException)
+
+CASES = [
+    # (id, table, analyzer, args, expected, source)
+    ("size_missing", "dfMissing", "Size", [], 12.0, T + A + ":36-37"),
+    ("size_full", "dfFull", "Size", [], 4.0, T + A + ":38-39"),
+    ("completeness_att1", "dfMissing", "Completeness", ["att1"], 0.5, T + A + ":48-49"),
+    ("completeness_att2", "dfMissing", "Completeness", ["att2"], 0.75, T + A + ":50-51"),
+    ("completeness_where", "dfMissing", "Completeness", ["att1", "item IN ('1', '2')"], 1.0, T + A + ":68-72"),
+    ("compliance_gt3", "dfNumeric", "Compliance", ["rule1", "att1 > 3"], 3.0 / 6, T + A + ":173-174"),
+    ("compliance_gt2", "dfNumeric", "Compliance", ["rule2", "att1 > 2"], 4.0 / 6, T + A + ":175-176"),
+    ("compliance_where", "dfNumeric", "Compliance", ["rule1", "att2 = 0", "att1 < 4"], 1.0, T + A + ":180-184"),
+    ("mean", "dfNumeric", "Mean", ["att1"], 3.5, T + A + ":424-428"),
+    ("mean_where", "dfNumeric", "Mean", ["att1", "item != '6'"], 3.0, T + A + ":434-438"),
+    ("stddev", "dfNumeric", "StandardDeviation", ["att1"], 1.707825127659933, T + A + ":440-444"),
+    ("minimum", "dfNumeric", "Minimum", ["att1"], 1.0, T + A + ":450-454"),
+    ("maximum", "dfNumeric", "Maximum", ["att1"], 6.0, T + A + ":460-464"),
+    ("maximum_where", "dfNumeric", "Maximum", ["att1", "item != '6'"], 5.0, T + A + ":466-471"),
+    ("sum", "dfNumeric", "Sum", ["att1"], 21.0, T + A + ":478-481"),
+    ("acd_strings", "dfUnique", "ApproxCountDistinct", ["uniqueWithNulls"], 5.0, T + A + ":543-548"),
+    ("acd_int", "dfNumeric", "ApproxCountDistinct", ["att1"], 6.0, T + "analyzers/AnalysisTest.scala:91-92"),
+    ("stddev_analysis", "dfNumeric", "StandardDeviation", ["att1"], 1.707825127659933, T + "analyzers/AnalysisTest.scala:87-88"),
+    ("frac_mean", "dfFractional", "Mean", ["att1"], 3.5, T + "checks/CheckTest.scala:427-431 (same values)"),
+    ("frac_stddev", "dfFractional", "StandardDeviation", ["att1"], 1.707825127659933, T + "checks/CheckTest.scala:429"),
+    ("null_size", "dfNullColumns", "Size", [], 8.0, T + "analyzers/NullHandlingTests.scala:60,99"),
+    ("null_completeness", "dfNullColumns", "Completeness", ["stringCol"], 0.0, T + "analyzers/NullHandlingTests.scala:61,100"),
+    ("null_mean", "dfNullColumns", "Mean", ["numericCol"], EMPTY, T + "analyzers/NullHandlingTests.scala:63,102"),
+    ("null_stddev", "dfNullColumns", "StandardDeviation", ["numericCol"], EMPTY, T + "analyzers/NullHandlingTests.scala:64,104"),
+    ("null_min", "dfNullColumns", "Minimum", ["numericCol"], EMPTY, T + "analyzers/NullHandlingTests.scala:65,105"),
+    ("null_max", "dfNullColumns", "Maximum", ["numericCol"], EMPTY, T + "analyzers/NullHandlingTests.scala:66,106"),
+    ("null_sum", "dfNullColumns", "Sum", ["numericCol"], EMPTY, T + "analyzers/NullHandlingTests.scala:74,113"),
+    ("null_acd", "dfNullColumns", "ApproxCountDistinct", ["stringCol"], 0.0, T + "analyzers/NullHandlingTests.scala:119"),
+    ("items_size", "items", "Size", [], 3.0, M + "examples/algebraic_states_example.md:45-52"),
+    ("items_acd", "items", "ApproxCountDistinct", ["id"], 3.0, M + "examples/algebraic_states_example.md:49"),
+    ("items_completeness_name", "items", "Completeness", ["productName"], 1.0, M + "examples/algebraic_states_example.md:50"),
+    ("items_completeness_desc", "items", "Completeness", ["description"], 0.6666666666666666, M + "examples/algebraic_states_example.md:51"),
+    ("incr_size_initial", "incrInitial", "Size", [], 3.0, T + "analyzers/IncrementalAnalyzerTest.scala:45"),
+    ("incr_size_delta", "incrDelta", "Size", [], 2.0, T + "analyzers/IncrementalAnalyzerTest.scala:46"),
+    ("incr_compliance_initial", "incrInitial", "Compliance", ["att1", "att1 = 'b'"], 0.3333333333333333, T + "analyzers/IncrementalAnalyzerTest.scala:73"),
+    ("incr_compliance_delta", "incrDelta", "Compliance", ["att1", "att1 = 'b'"], 0.5, T + "analyzers/IncrementalAnalyzerTest.scala:74"),
+    ("incr_completeness_initial", "incrInitial", "Completeness", ["att1"], 0.6666666666666666, T + "analyzers/IncrementalAnalyzerTest.scala:92"),
+    ("incr_completeness_delta", "incrDelta", "Completeness", ["att1"], 0.5, T + "analyzers/IncrementalAnalyzerTest.scala:93"),
+    ("empty_size", "dfEmpty", "Size", [], 0.0, T + "analyzers/runners/AnalysisRunnerTests.scala (Size of an empty frame is 0)"),
+    ("empty_completeness", "dfEmpty", "Completeness", ["column1"], EMPTY, T + "analyzers/NullHandlingTests.scala (sum over zero rows is NULL)"),
+]
+
+# Known answers that need the union of two tables (state merge == union):
+MERGE_CASES = [
+    # (id, table_a, table_b, analyzer, args, expected, source)
+    ("items_merge_size", "items", "itemsMore", "Size", [], 5.0, M + "examples/algebraic_states_example.md:74-80"),
+    ("items_merge_acd", "items", "itemsMore", "ApproxCountDistinct", ["id"], 5.0, M + "examples/algebraic_states_example.md:76"),
+    ("items_merge_name", "items", "itemsMore", "Completeness", ["productName"], 1.0, M + "examples/algebraic_states_example.md:77"),
+    ("items_merge_desc", "items", "itemsMore", "Completeness", ["description"], 0.4, M + "examples/algebraic_states_example.md:78"),
+    ("incr_size_merged", "incrInitial", "incrDelta", "Size", [], 5.0, T + "analyzers/IncrementalAnalyzerTest.scala:47"),
+    ("incr_compliance_merged", "incrInitial", "incrDelta", "Compliance", ["att1", "att1 = 'b'"], 0.4, T + "analyzers/IncrementalAnalyzerTest.scala:75"),
+    ("incr_completeness_merged", "incrInitial", "incrDelta", "Completeness", ["att1"], 0.6, T + "analyzers/IncrementalAnalyzerTest.scala:94"),
+]
+
+
+def main():
+    # the Completeness(att2) initial case is the reference's own 4/6 computed on att2
+    out = {
+        "tables": TABLES,
+        "cases": [dict(id=c[0], table=c[1], analyzer=c[2], args=c[3], expected=c[4], source=c[5])
+                  for c in CASES],
+        "merge_cases": [dict(id=c[0], table_a=c[1], table_b=c[2], analyzer=c[3], args=c[4],
+                             expected=c[5], source=c[6]) for c in MERGE_CASES],
+    }
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_known_answers.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1, sort_keys=False)
+    print("wrote", path, len(CASES), "cases +", len(MERGE_CASES), "merge cases")
+
+
+if __name__ == "__main__":
+    main()

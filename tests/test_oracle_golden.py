@@ -1,0 +1,97 @@
+"""The oracle (oracle/pyoracle.py) against the reference's own known answers and the
+third-party XXH64 implementation it restates.  CPU only."""
+import math
+import random
+import struct
+
+import pytest
+import xxhash
+
+import pyoracle as O
+from helpers import known_answers, oracle_metric, oracle_state, oracle_table
+
+KA = known_answers()
+
+
+@pytest.mark.parametrize("case", KA["cases"], ids=[c["id"] for c in KA["cases"]])
+def test_oracle_reproduces_reference_known_answer(case):
+    table = oracle_table(KA["tables"][case["table"]])
+    got = oracle_metric(oracle_state(case["analyzer"], case["args"], table))
+    assert got == case["expected"], (case["source"], got)
+
+
+@pytest.mark.parametrize("case", KA["merge_cases"], ids=[c["id"] for c in KA["merge_cases"]])
+def test_oracle_merge_equals_reference(case):
+    ta = oracle_table(KA["tables"][case["table_a"]])
+    tb = oracle_table(KA["tables"][case["table_b"]])
+    sa = oracle_state(case["analyzer"], case["args"], ta)
+    sb = oracle_state(case["analyzer"], case["args"], tb)
+    assert O.merge_options(sa, sb).metric_value() == case["expected"], case["source"]
+    union = {k: O.OColumn(ta[k].dtype, ta[k].values + tb[k].values) for k in ta}
+    assert oracle_state(case["analyzer"], case["args"], union).metric_value() == case["expected"]
+
+
+def test_oracle_xxh64_matches_reference_implementation():
+    rnd = random.Random(7)
+    for n in list(range(0, 80)) + [127, 128, 129, 1000]:
+        data = bytes(rnd.getrandbits(8) for _ in range(n))
+        for seed in (0, 42, 2 ** 63 + 5):
+            assert O.xxh64(data, seed) == xxhash.xxh64_intdigest(data, seed % 2 ** 64)
+
+
+def test_spark_hash_dispatch():
+    # hashInt/hashLong are XXH64 over the 4/8 little-endian bytes (Spark 2.2.2 XXH64)
+    assert O.spark_hash(5, "int32") == xxhash.xxh64_intdigest(struct.pack("<i", 5), 42)
+    assert O.spark_hash(-5, "int64") == xxhash.xxh64_intdigest(struct.pack("<q", -5), 42)
+    assert O.spark_hash(True, "bool") == O.spark_hash(1, "int32")
+    assert O.spark_hash(float("nan"), "float64") == O.spark_hash(struct.unpack("<d", struct.pack("<Q", 0x7FF8000000000000))[0], "float64")
+    assert O.spark_hash("é", "string") == xxhash.xxh64_intdigest("é".encode("utf-8"), 42)
+
+
+def test_hll_pack_roundtrip_and_merge():
+    rnd = random.Random(3)
+    regs_a = [rnd.randint(0, 40) for _ in range(512)]
+    regs_b = [rnd.randint(0, 40) for _ in range(512)]
+    wa, wb = O.hll_pack(regs_a), O.hll_pack(regs_b)
+    assert O.hll_unpack(wa) == regs_a
+    assert O.hll_unpack(O.hll_merge(wa, wb)) == [max(x, y) for x, y in zip(regs_a, regs_b)]
+    assert O.hll_words_from_bytes(O.hll_words_to_bytes(wa)) == wa
+
+
+def test_hll_count_java_int_shift_quirk():
+    # a register >= 32 wraps Java's `1 << m` (int shift masks the count to 5 bits)
+    regs = [0] * 512
+    regs[0] = 32  # 1 << 32 == 1 in Java
+    regs[1] = 31  # 1 << 31 == Int.MinValue
+    words = O.hll_pack(regs)
+    z = 510.0 + 1.0 / 1 + 1.0 / -2147483648
+    assert math.isclose(O.hll_count(words), float(math.floor(512 * math.log(512 / 510.0) + 0.5)))
+    assert z != 0
+
+
+def test_hll_relative_error_large():
+    rnd = random.Random(11)
+    vals = [rnd.getrandbits(63) for _ in range(100000)]
+    est = O.hll_count(O.hll_pack(O.hll_registers(vals, "int64")))
+    assert abs(est - 100000) / 100000 < 0.1  # RELATIVE_SD = 0.05
+
+
+def test_welford_state_algebra():
+    # StandardDeviationState.sum of two halves equals the single-pass state (within fp64)
+    vals = [float(x) for x in range(1, 7)]
+    t = {"x": O.OColumn("float64", vals)}
+    a = O.stddev_state({"x": O.OColumn("float64", vals[:3])}, "x")
+    b = O.stddev_state({"x": O.OColumn("float64", vals[3:])}, "x")
+    assert a.sum(b).metric_value() == pytest.approx(O.stddev_state(t, "x").metric_value(), rel=1e-15)
+
+
+def test_predicate_three_valued_logic():
+    t = {"a": O.OColumn("int64", [1, None, 3]), "s": O.OColumn("string", ["x", "y", None])}
+    assert O.eval_predicate("a > 2", t) == [False, None, True]
+    assert O.eval_predicate("a > 2 OR s = 'y'", t) == [False, True, True]
+    assert O.eval_predicate("a > 2 AND s = 'y'", t) == [False, None, None]
+    assert O.eval_predicate("NOT (a > 2)", t) == [True, None, False]
+    assert O.eval_predicate("COALESCE(a, 0.0) >= 0", t) == [True, True, True]
+    assert O.eval_predicate("a IN (1, 3)", t) == [True, None, True]
+    assert O.eval_predicate("a > 1.5", t) == [False, None, True]
+    assert O.eval_predicate("a IS NULL", t) == [False, True, False]
