@@ -106,6 +106,14 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError("deequ_amd native library not built: %s (run "
                               "`python -c 'import __graft_entry__ as g; g.build()'`)" % LIB_PATH)
+        # PyTorch-ROCm bundles its own libamdhip64.so.7 (same SONAME as /opt/rocm's).  Only one
+        # HIP runtime can live in a process; whichever is loaded first serves everyone, and
+        # torch cannot run on a newer one.  So when torch is installed, let it load its runtime
+        # first and bind this library to that same runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         l = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(l, name)

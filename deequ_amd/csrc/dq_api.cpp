@@ -229,6 +229,42 @@ static int cmp_of(int opcode) {
     default: return -1;
   }
 }
+// Derive the branch-free selectors of FastPred (see dq_internal.h) from kind / op.
+static void finalize_fast_pred(FastPred* fp) {
+  const uint32_t ON = ~0u;
+  fp->m_lt = fp->m_eq = fp->m_gt = 0;
+  fp->f_cmp = fp->f_coal = fp->f_isnull = fp->f_isnotnull = fp->f_true = fp->f_mask = 0;
+  fp->f_nn_valid = fp->f_nn_one = fp->pad = 0;
+  switch (fp->kind) {
+    case FP_CMP:
+    case FP_COALESCE_CMP:
+      fp->f_cmp = ON;
+      if (fp->kind == FP_COALESCE_CMP) {
+        fp->f_coal = ON;
+        fp->f_nn_one = ON;
+      } else {
+        fp->f_nn_valid = ON;
+      }
+      switch (fp->op) {
+        case CMP_EQ: fp->m_eq = ON; break;
+        case CMP_NE: fp->m_lt = fp->m_gt = ON; break;
+        case CMP_LT: fp->m_lt = ON; break;
+        case CMP_LE: fp->m_lt = fp->m_eq = ON; break;
+        case CMP_GT: fp->m_gt = ON; break;
+        default: fp->m_gt = fp->m_eq = ON; break;  // CMP_GE
+      }
+      break;
+    case FP_IS_NULL: fp->f_isnull = ON; fp->f_nn_one = ON; break;
+    case FP_IS_NOT_NULL: fp->f_isnotnull = ON; fp->f_nn_one = ON; break;
+    case FP_CONST:
+      if (fp->lit_i == 1) fp->f_true = ON;
+      if (fp->lit_i != -1) fp->f_nn_one = ON;
+      break;
+    case FP_MASK: fp->f_mask = ON; break;
+    default: break;
+  }
+}
+
 static int flip_cmp(int c) {
   switch (c) {
     case CMP_LT: return CMP_GT;
@@ -283,6 +319,7 @@ static int fast_form(const Program& prog, const int32_t* types, FastPred* fp) {
     fp->op = op;
     fp->as_f64 = as_f64 ? 1 : 0;
     if (!set_lit(*lit, as_f64, &fp->lit_i, &fp->lit_f)) return -1;
+    if (as_f64 && fp->lit_f != fp->lit_f) return -1;  // NaN literal: generic path
     return col;
   }
   if (c.size() == 5 && numeric_col(c[0]) && lit_ok(c[1]) && c[2].opcode == DQ_P_COALESCE &&
@@ -294,6 +331,7 @@ static int fast_form(const Program& prog, const int32_t* types, FastPred* fp) {
     fp->op = cmp_of(c[4].opcode);
     fp->as_f64 = as_f64 ? 1 : 0;
     if (!set_lit(c[3], as_f64, &fp->lit_i, &fp->lit_f)) return -1;
+    if (as_f64 && fp->lit_f != fp->lit_f) return -1;  // NaN literal: generic path
     if (!set_lit(c[1], as_f64, &fp->coal_i, &fp->coal_f)) return -1;
     return col;
   }
@@ -498,6 +536,7 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
         }
         slot.task = t;
         slot.pred = tasks[t].t.n_preds;
+        finalize_fast_pred(&fp);
         tasks[t].t.preds[tasks[t].t.n_preds++] = fp;
         break;
       }
@@ -530,7 +569,10 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
     const ScanTask& t = plan->scan_tasks[i];
     const int kind = (t.flags & TF_VALUES) ? 1 : 0;
     const int ptype = kind ? t.ptype : 0;
-    const int np = kind ? (t.n_preds <= 4 ? t.n_preds : kMaxPreds) : 0;
+    bool ext = (t.flags & TF_WHERE) != 0;
+    for (int p = 0; p < t.n_preds; ++p) ext = ext || t.preds[p].kind == FP_MASK;
+    // np = exact inline-predicate count of a plain task, -1 = the EXT kernel (where/masks)
+    const int np = kind ? (ext ? -1 : (t.n_preds <= 4 ? t.n_preds : kMaxPreds)) : 0;
     ScanGroup* g = nullptr;
     for (auto& gg : plan->groups)
       if (gg.kind == kind && gg.ptype == ptype && gg.np == np) g = &gg;
@@ -777,6 +819,9 @@ extern "C" dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, in
     const int64_t ng = (int64_t)plan->groups[g].tasks.size();
     int64_t bpt = (plan->target_blocks + ng - 1) / ng;
     bpt = std::max<int64_t>(1, std::min<int64_t>(bpt, chunks));
+    // a block's rows are addressed by 32-bit buffer offsets: keep its span <= 2^27 rows
+    bpt = std::max<int64_t>(bpt, (chunks + (((int64_t)1 << 27) / kScanRowAlign) - 1) /
+                                     (((int64_t)1 << 27) / kScanRowAlign));
     group_bpt[g] = bpt;
     group_base[g] = part_total;
     for (int64_t i = 0; i < ng; ++i)

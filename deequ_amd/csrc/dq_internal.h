@@ -55,6 +55,13 @@ struct FastPred {
   double lit_f;
   int64_t coal_i;
   double coal_f;
+  // Branch-free evaluation (filled by the host from kind/op; each is 0 or ~0u):
+  //   cmp  = (x < lit & m_lt) | (x == lit & m_eq) | (!(x < lit | x == lit) & m_gt)
+  //   TRUE = cmp & f_cmp | ~valid & f_isnull | valid & f_isnotnull | f_true | mask_t & f_mask
+  //   NOT NULL = valid & f_nn_valid | f_nn_one | mask_nn & f_mask
+  // (a NaN x is neither < nor == a non-NaN literal, so it lands in "greater": Spark's order)
+  uint32_t m_lt, m_eq, m_gt;
+  uint32_t f_cmp, f_coal, f_isnull, f_isnotnull, f_true, f_mask, f_nn_valid, f_nn_one, pad;
 };
 
 enum ScanTaskFlags : int32_t {
@@ -119,8 +126,9 @@ struct PredProgram {
 
 // ---------------------------------------------------------------- launchers (.hip files)
 // kind 0 = validity/mask-only tasks, 1 = value tasks of column type `ptype` with exactly
-// `np` inline predicates (np > 4 uses the 8-slot kernel).  Partials of the group's i-th task
-// go to d_partials[i * blocks_per_task + b].
+// `np` inline predicates (np > 4 uses the 8-slot kernel; np < 0 = tasks with a where mask
+// or mask predicates).  Partials of the group's i-th task go to
+// d_partials[i * blocks_per_task + b].
 hipError_t launch_scan_group(int kind, int ptype, int np, const ScanTask* d_tasks,
                              const int32_t* d_group, int n_group, const DevColumn* d_cols,
                              const DevMask* d_masks, int64_t n_rows, int blocks_per_task,

@@ -347,111 +347,267 @@ __device__ inline void chunk_of_block(int64_t n_rows, int64_t& row_begin, int64_
   row_end = min(row_begin + per_block * kScanRowAlign, n_rows);
 }
 
+typedef uint32_t dq_v4u __attribute__((ext_vector_type(4)));
+
+__device__ inline __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+
+// `RPL` validity/mask bits of the rows starting at chunk row `r0` (r0 % RPL == 0).
+template <int RPL>
+__device__ inline uint32_t buf_bits(__amdgpu_buffer_rsrc_t rs, uint32_t r0) {
+  if constexpr (RPL == 16) {
+    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rs, (int)(r0 >> 3), 0, 0);
+  } else {
+    const uint32_t byte = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)(r0 >> 3), 0, 0);
+    return (byte >> (r0 & 7u)) & ((1u << RPL) - 1u);
+  }
+}
+
+template <typename T>
+__device__ inline T buf_elem(__amdgpu_buffer_rsrc_t rs, uint32_t row) {
+  if constexpr (sizeof(T) == 8) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(row * 8u), 0, 0);
+    return __builtin_bit_cast(T, (uint64_t)v[0] | ((uint64_t)v[1] << 32));
+  } else if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(row * 4u), 0, 0));
+  } else if constexpr (sizeof(T) == 2) {
+    return __builtin_bit_cast(T, (uint16_t)__builtin_amdgcn_raw_buffer_load_b16(rs, (int)(row * 2u), 0, 0));
+  } else {
+    return __builtin_bit_cast(T, (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)row, 0, 0));
+  }
+}
+
+// Statistics over R rows of one lane (selection bits `sel`), against the wave's shift.
+template <typename T, int NP, int R>
+__device__ inline void accumulate_rows(ThreadAcc<NP>& a, const T* vals, uint32_t sel, double shift,
+                                       double& psum) {
+  a.n_sel += __builtin_popcount(sel);
+  if constexpr (IsIntegral<T>::value) {
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const bool s = (sel >> k) & 1u;
+      const int64_t xi = (int64_t)vals[k];
+      a.isum += s ? xi : 0;
+      const int64_t vmn = s ? xi : INT64_MAX;
+      const int64_t vmx = s ? xi : INT64_MIN;
+      a.imin = vmn < a.imin ? vmn : a.imin;
+      a.imax = vmx > a.imax ? vmx : a.imax;
+      const double d = s ? ((double)xi - shift) : 0.0;
+      a.s1 += d;
+      a.s2 = fma(d, d, a.s2);
+    }
+  } else {
+    uint32_t nanb = 0u;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const bool s = (sel >> k) & 1u;
+      const double x = (double)vals[k];
+      psum += s ? x : 0.0;
+      const double d = s ? (x - shift) : 0.0;
+      a.s1 += d;
+      a.s2 = fma(d, d, a.s2);
+      // minnum/maxnum drop a NaN operand: NaN never wins min (Spark's NaN-safe order); a NaN
+      // max is restored from `nnan` when the state is built.
+      a.fmin = __builtin_fmin(a.fmin, s ? x : __builtin_huge_val());
+      a.fmax = __builtin_fmax(a.fmax, s ? x : -__builtin_huge_val());
+      nanb |= (s && x != x) ? (1u << k) : 0u;
+    }
+    a.nnan += __builtin_popcount(nanb);
+  }
+}
+
+// Compare bits of R values against the literal, branch-free in the operator: lt / eq are
+// computed, "greater" is neither (which also puts a NaN x above every literal, Spark's
+// NaN-safe order), and the uniform selectors pick the operator's answer.
+template <typename V, int R>
+__device__ inline uint32_t cmp_bits(const V* x, V lit, const FastPred& fp) {
+  uint32_t r = 0u;
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const uint32_t lt = x[k] < lit ? ~0u : 0u;
+    const uint32_t eq = x[k] == lit ? ~0u : 0u;
+    const uint32_t b = (lt & fp.m_lt) | (eq & fp.m_eq) | (~(lt | eq) & fp.m_gt);
+    r |= b & (1u << k);
+  }
+  return r;
+}
+
+// Inline predicates over R rows: counts TRUE and NOT NULL among where-TRUE rows.
+template <typename T, int NP, int R>
+__device__ inline void predicate_rows(ThreadAcc<NP>& a, const FastPred* fps, const T* vals,
+                                      uint32_t valid, uint32_t wt, const uint32_t* mt,
+                                      const uint32_t* mn) {
+  constexpr uint32_t FULL = (R == 32) ? 0xffffffffu : ((1u << R) - 1u);
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const FastPred& fp = fps[p];
+    uint32_t c = 0u;
+    if (fp.f_cmp) {  // uniform
+      if (IsIntegral<T>::value && !fp.as_f64) {
+        int64_t x[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k)
+          x[k] = (fp.f_coal && !((valid >> k) & 1u)) ? fp.coal_i : (int64_t)vals[k];
+        c = cmp_bits<int64_t, R>(x, fp.lit_i, fp);
+      } else {
+        double x[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k)
+          x[k] = (fp.f_coal && !((valid >> k) & 1u)) ? fp.coal_f : (double)vals[k];
+        c = cmp_bits<double, R>(x, fp.lit_f, fp);
+      }
+    }
+    const uint32_t r = ((c & fp.f_cmp) | (~valid & fp.f_isnull) | (valid & fp.f_isnotnull) |
+                        fp.f_true | (mt[p] & fp.f_mask)) & FULL;
+    const uint32_t nn = ((valid & fp.f_nn_valid) | fp.f_nn_one | (mn[p] & fp.f_mask)) & FULL;
+    a.pm[p] += __builtin_popcount(wt & nn & r);
+    a.pn[p] += __builtin_popcount(wt & nn);
+  }
+}
+
 }  // namespace
 
 // Tasks that read the primary column's values.  NP = number of inline predicates (exact).
-template <typename T, int NP>
+// The block's row chunk is addressed through buffer descriptors (32-bit offsets, hardware
+// range check), the main loop runs over whole iterations with no bounds checks, and the
+// ragged end of the chunk is finished element by element.
+// EXT = the task has a `where` mask or mask-based predicates.  Every load of the main loop is
+// unconditional: an absent buffer gets a zero-size descriptor (the hardware range check
+// returns 0 without touching memory) and a uniform "absent" mask is OR-ed in afterwards, so
+// no load sits behind a branch (which would force a vmcnt(0) per load).
+template <typename T, int NP, bool EXT>
 __global__ __launch_bounds__(kBlock) void dq_scan_values_kernel(
     const ScanTask* __restrict__ tasks, const int32_t* __restrict__ group,
     const DevColumn* __restrict__ cols, const DevMask* __restrict__ masks, int64_t n_rows,
     ScanAcc* partials) {
   constexpr int RPL = 16 / (int)sizeof(T);
   constexpr int UNROLL = sizeof(T) >= 8 ? 4 : (sizeof(T) == 4 ? 2 : 1);
-  constexpr int64_t ROWS_PER_ITER = (int64_t)kBlock * RPL * UNROLL;
+  constexpr uint32_t ROWS_PER_ITER = (uint32_t)kBlock * RPL * UNROLL;
   constexpr uint32_t FULL = (1u << RPL) - 1u;
+  constexpr int NPS = NP > 0 ? NP : 1;
 
   const int task_id = group[blockIdx.y];
   const ScanTask& task = tasks[task_id];
   int64_t row_begin, row_end;
   chunk_of_block(n_rows, row_begin, row_end);
+  const uint32_t span = (uint32_t)(row_end - row_begin);  // host keeps span * 8 < 4 GiB
 
   const DevColumn& col = cols[task.primary];
-  const T* __restrict__ values = static_cast<const T*>(col.values);
-  const uint8_t* __restrict__ validity = col.validity;
-  const bool has_where = (task.flags & TF_WHERE) != 0;
-  const uint8_t* wt_bm = nullptr;
-  const uint8_t* wn_bm = nullptr;
+  const __amdgpu_buffer_rsrc_t rv =
+      make_rsrc(static_cast<const T*>(col.values) + row_begin, span * (uint32_t)sizeof(T));
+  const bool has_valid = col.validity != nullptr;
+  const uint32_t no_valid = has_valid ? 0u : ~0u;
+  const uint32_t bm_bytes = (span + 7u) >> 3;
+  const __amdgpu_buffer_rsrc_t rvalid =
+      make_rsrc(has_valid ? col.validity + (row_begin >> 3) : nullptr, has_valid ? bm_bytes : 0u);
+  const bool has_where = EXT && (task.flags & TF_WHERE) != 0;
+  const uint32_t no_where = has_where ? 0u : ~0u;
+  __amdgpu_buffer_rsrc_t rwt = make_rsrc(nullptr, 0), rwn = make_rsrc(nullptr, 0);
   if (has_where) {
-    wt_bm = reinterpret_cast<const uint8_t*>(masks[task.where_mask].t);
-    wn_bm = reinterpret_cast<const uint8_t*>(masks[task.where_mask].nn);
+    rwt = make_rsrc(reinterpret_cast<const uint8_t*>(masks[task.where_mask].t) + (row_begin >> 3), bm_bytes);
+    rwn = make_rsrc(reinterpret_cast<const uint8_t*>(masks[task.where_mask].nn) + (row_begin >> 3), bm_bytes);
   }
-  FastPred fps[NP > 0 ? NP : 1];
-  const uint8_t* mt_bm[NP > 0 ? NP : 1];
-  const uint8_t* mn_bm[NP > 0 ? NP : 1];
+  FastPred fps[NPS];
+  __amdgpu_buffer_rsrc_t rmt[NPS], rmn[NPS];
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     fps[p] = task.preds[p];
-    mt_bm[p] = mn_bm[p] = nullptr;
-    if (fps[p].kind == FP_MASK) {
-      mt_bm[p] = reinterpret_cast<const uint8_t*>(masks[fps[p].mask].t);
-      mn_bm[p] = reinterpret_cast<const uint8_t*>(masks[fps[p].mask].nn);
+    rmt[p] = rmn[p] = make_rsrc(nullptr, 0);
+    if (EXT && fps[p].kind == FP_MASK) {
+      rmt[p] = make_rsrc(reinterpret_cast<const uint8_t*>(masks[fps[p].mask].t) + (row_begin >> 3), bm_bytes);
+      rmn[p] = make_rsrc(reinterpret_cast<const uint8_t*>(masks[fps[p].mask].nn) + (row_begin >> 3), bm_bytes);
+    }
+  }
+
+  // Wave-uniform shift for the moments: the first valid, finite value among the wave's
+  // first rows (any sample of the column keeps Σ(x - c)² well conditioned).
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = threadIdx.x >> 6;
+  double shift = 0.0;
+  for (uint32_t probe = 0; probe < 4; ++probe) {
+    const uint32_t r = (probe * (kBlock / 64) + wave) * 64u + lane;
+    bool ok = false;
+    double x = 0.0;
+    if (r < span) {
+      x = (double)buf_elem<T>(rv, r);
+      ok = (has_valid ? ((buf_bits<1>(rvalid, r)) & 1u) : 1u) && (x - x == 0.0);
+    }
+    const uint64_t m = __ballot(ok);
+    if (m) {
+      const int src = __builtin_ctzll(m);
+      shift = __shfl(x, src, 64);
+      break;
     }
   }
 
   ThreadAcc<NP> a;
   thread_acc_init(a);
-  const int tid = threadIdx.x;
-  for (int64_t base = row_begin; base < row_end; base += ROWS_PER_ITER) {
-    Vec16 vec[UNROLL];
-    uint32_t vb[UNROLL], wtb[UNROLL], wnb[UNROLL], inb[UNROLL];
-    // ---- load phase: every load of the group is issued before any use
+  const uint32_t tid = threadIdx.x;
+  const uint32_t full_iters = span / ROWS_PER_ITER;
+  for (uint32_t it = 0; it < full_iters; ++it) {
+    dq_v4u vec[UNROLL];
+    uint32_t vb[UNROLL], wtb[UNROLL], wnb[UNROLL];
+    uint32_t mtb[UNROLL][NPS], mnb[UNROLL][NPS];
+    // ---- load phase: every load of the iteration is issued before any use
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-      const int64_t row0 = base + ((int64_t)u * kBlock + tid) * RPL;
-      const int64_t left = row_end - row0;
-      inb[u] = left >= RPL ? FULL : (left > 0 ? ((1u << (uint32_t)left) - 1u) : 0u);
-      vec[u] = Vec16{{0u, 0u, 0u, 0u}};
-      vb[u] = wtb[u] = wnb[u] = 0u;
-      if (left >= RPL) {
-        vec[u] = *reinterpret_cast<const Vec16*>(values + row0);
-      } else if (left > 0) {  // last partial vector: element loads, nothing past the end
-        T tmp[RPL];
+      const uint32_t r0 = it * ROWS_PER_ITER + ((uint32_t)u * kBlock + tid) * RPL;
+      vec[u] = __builtin_amdgcn_raw_buffer_load_b128(rv, (int)(r0 * (uint32_t)sizeof(T)), 0, 0);
+      vb[u] = buf_bits<RPL>(rvalid, r0);
+      if constexpr (EXT) {
+        wtb[u] = buf_bits<RPL>(rwt, r0);
+        wnb[u] = buf_bits<RPL>(rwn, r0);
 #pragma unroll
-        for (int k = 0; k < RPL; ++k) tmp[k] = k < left ? values[row0 + k] : T(0);
-        __builtin_memcpy(&vec[u], tmp, 16);
-      }
-      if (left > 0) {
-        vb[u] = validity ? load_bits<RPL>(validity, row0, left) : FULL;
-        if (has_where) {
-          wtb[u] = load_bits<RPL>(wt_bm, row0, left);
-          wnb[u] = load_bits<RPL>(wn_bm, row0, left);
-        } else {
-          wtb[u] = wnb[u] = FULL;
+        for (int p = 0; p < NPS; ++p) {
+          mtb[u][p] = buf_bits<RPL>(rmt[p], r0);
+          mnb[u][p] = buf_bits<RPL>(rmn[p], r0);
         }
+      } else {
+        wtb[u] = wnb[u] = FULL;
+#pragma unroll
+        for (int p = 0; p < NPS; ++p) mtb[u][p] = mnb[u][p] = 0u;
       }
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {  // absent buffers read as 0: restore "all valid/TRUE"
+      vb[u] = (vb[u] | no_valid) & FULL;
+      wtb[u] = (wtb[u] | no_where) & FULL;
+      wnb[u] = (wnb[u] | no_where) & FULL;
     }
     // ---- compute phase
+    double psum = 0.0;
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-      const uint32_t wt = wtb[u] & inb[u];
-      const uint32_t sel = vb[u] & wt;
-      a.n_rows += __builtin_popcount(wt);
-      a.n_wnn += __builtin_popcount(wnb[u] & inb[u]);
       const T* vals = reinterpret_cast<const T*>(&vec[u]);
-#pragma unroll
-      for (int k = 0; k < RPL; ++k) accumulate_element<T, NP>(a, vals[k], (sel >> k) & 1u);
-#pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        uint32_t mtb = 0u, mnb = 0u;
-        if (fps[p].kind == FP_MASK && inb[u]) {
-          const int64_t row0 = base + ((int64_t)u * kBlock + tid) * RPL;
-          mtb = load_bits<RPL>(mt_bm[p], row0, row_end - row0);
-          mnb = load_bits<RPL>(mn_bm[p], row0, row_end - row0);
-        }
-        uint32_t cm = 0u, cn = 0u;
-#pragma unroll
-        for (int k = 0; k < RPL; ++k) {
-          uint32_t r, nn;
-          eval_fast_pred<T>(fps[p], vals[k], (vb[u] >> k) & 1u, (mtb >> k) & 1u, (mnb >> k) & 1u, r, nn);
-          const uint32_t w = (wt >> k) & 1u;
-          cm += w & nn & r;
-          cn += w & nn;
-        }
-        a.pm[p] += cm;
-        a.pn[p] += cn;
-      }
+      const uint32_t sel = vb[u] & wtb[u];
+      a.n_rows += __builtin_popcount(wtb[u]);
+      a.n_wnn += __builtin_popcount(wnb[u]);
+      accumulate_rows<T, NP, RPL>(a, vals, sel, shift, psum);
+      predicate_rows<T, NP, RPL>(a, fps, vals, vb[u], wtb[u], mtb[u], mnb[u]);
     }
+    if constexpr (!IsIntegral<T>::value) neumaier_add(a.fs, a.fc, psum);
   }
+  // ---- ragged end of the chunk: one row per lane
+  double psum = 0.0;
+  for (uint32_t r = full_iters * ROWS_PER_ITER + tid; r < span; r += kBlock) {
+    const T v = buf_elem<T>(rv, r);
+    const uint32_t valid = (buf_bits<1>(rvalid, r) | no_valid) & 1u;
+    const uint32_t wt = (buf_bits<1>(rwt, r) | no_where) & 1u;
+    const uint32_t wn = (buf_bits<1>(rwn, r) | no_where) & 1u;
+    uint32_t mt[NPS], mn[NPS];
+#pragma unroll
+    for (int p = 0; p < NPS; ++p) {
+      mt[p] = buf_bits<1>(rmt[p], r) & 1u;
+      mn[p] = buf_bits<1>(rmn[p], r) & 1u;
+    }
+    a.n_rows += wt;
+    a.n_wnn += wn;
+    accumulate_rows<T, NP, 1>(a, &v, valid & wt, shift, psum);
+    predicate_rows<T, NP, 1>(a, fps, &v, valid, wt, mt, mn);
+  }
+  if constexpr (!IsIntegral<T>::value) neumaier_add(a.fs, a.fc, psum);
+  a.shift = shift;
   thread_finish<NP>(a, NP, &partials[(int64_t)blockIdx.y * gridDim.x + blockIdx.x]);
 }
 
@@ -566,13 +722,17 @@ template <typename T>
 static hipError_t launch_values_np(int np, dim3 grid, hipStream_t s, const ScanTask* t,
                                    const int32_t* g, const DevColumn* c, const DevMask* m,
                                    int64_t n, ScanAcc* part) {
+  if (np < 0) {  // EXT: where masks / mask predicates, all predicate slots
+    hipLaunchKernelGGL((dq_scan_values_kernel<T, kMaxPreds, true>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part);
+    return hipGetLastError();
+  }
   switch (np) {
-    case 0: hipLaunchKernelGGL((dq_scan_values_kernel<T, 0>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part); break;
-    case 1: hipLaunchKernelGGL((dq_scan_values_kernel<T, 1>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part); break;
-    case 2: hipLaunchKernelGGL((dq_scan_values_kernel<T, 2>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part); break;
-    case 3: hipLaunchKernelGGL((dq_scan_values_kernel<T, 3>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part); break;
-    case 4: hipLaunchKernelGGL((dq_scan_values_kernel<T, 4>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part); break;
-    default: hipLaunchKernelGGL((dq_scan_values_kernel<T, kMaxPreds>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part); break;
+    case 0: hipLaunchKernelGGL((dq_scan_values_kernel<T, 0, false>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part); break;
+    case 1: hipLaunchKernelGGL((dq_scan_values_kernel<T, 1, false>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part); break;
+    case 2: hipLaunchKernelGGL((dq_scan_values_kernel<T, 2, false>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part); break;
+    case 3: hipLaunchKernelGGL((dq_scan_values_kernel<T, 3, false>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part); break;
+    case 4: hipLaunchKernelGGL((dq_scan_values_kernel<T, 4, false>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part); break;
+    default: hipLaunchKernelGGL((dq_scan_values_kernel<T, kMaxPreds, false>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part); break;
   }
   return hipGetLastError();
 }
