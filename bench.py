@@ -35,7 +35,7 @@ def parse_args():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--rows", type=int, default=1_000_000_000, help="rows per GPU")
-    p.add_argument("--cpu-sample-rows", type=int, default=64_000_000)
+    p.add_argument("--cpu-sample-rows", type=int, default=256_000_000)
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, nproc)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
