@@ -1,0 +1,132 @@
+"""Multi-rank state exchange (deequ_amd/distributed.py) on CPU with gloo, world_size 2.
+
+Each rank holds the states of its own row shard (built here with the oracle, since these CPU
+tests run no GPU compute), the ranks all-gather the POD states and fold them in rank order
+with dq_state_merge.  The result must equal the states of the whole table: exactly for counts,
+int sums, min/max and HLL registers, and as the State.sum formulas prescribe for fp64 moments.
+"""
+import ctypes
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+import pyoracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _to_dq(kind, st):
+    import deequ_amd as d
+    from deequ_amd import _lib as L
+    if st is None:
+        s = L.DqState()
+        s.kind = kind
+        return s
+    mapping = {
+        L.DQ_OP_SIZE: lambda: d.NumMatches(st.num_matches),
+        L.DQ_OP_COMPLETENESS: lambda: d.NumMatchesAndCount(st.num_matches, st.count),
+        L.DQ_OP_SUM: lambda: d.SumState(st.sum_),
+        L.DQ_OP_MEAN: lambda: d.MeanState(st.sum_, st.count),
+        L.DQ_OP_STDDEV: lambda: d.StandardDeviationState(st.n, st.avg, st.m2),
+        L.DQ_OP_MINIMUM: lambda: d.MinState(st.min_value),
+        L.DQ_OP_MAXIMUM: lambda: d.MaxState(st.max_value),
+        L.DQ_OP_APPROX_COUNT_DISTINCT: lambda: d.ApproxCountDistinctState(st.words),
+    }
+    out = mapping[kind]().to_dq()
+    out.kind = kind
+    return out
+
+
+def _states_for(table):
+    from deequ_amd import _lib as L
+    return [
+        (L.DQ_OP_SIZE, O.size_state(table)),
+        (L.DQ_OP_COMPLETENESS, O.completeness_state(table, "x")),
+        (L.DQ_OP_SUM, O.sum_state(table, "x")),
+        (L.DQ_OP_MEAN, O.mean_state(table, "f")),
+        (L.DQ_OP_STDDEV, O.stddev_state(table, "f")),
+        (L.DQ_OP_MINIMUM, O.min_state(table, "x")),
+        (L.DQ_OP_MAXIMUM, O.max_state(table, "f")),
+        (L.DQ_OP_APPROX_COUNT_DISTINCT, O.approx_count_distinct_state(table, "x")),
+        (L.DQ_OP_SUM, O.sum_state(table, "empty")),  # None on every rank
+    ]
+
+
+def _table(lo, hi):
+    xs = [None if i % 7 == 0 else (i * 37) % 1000 - 300 for i in range(lo, hi)]
+    fs = [None if i % 11 == 0 else 0.5 * i for i in range(lo, hi)]
+    return {"x": O.OColumn("int64", xs), "f": O.OColumn("float64", fs),
+            "empty": O.OColumn("int64", [None] * (hi - lo))}
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+    import torch.distributed as dist
+    from deequ_amd import _lib as L
+    from deequ_amd.distributed import allgather_merge
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank,
+                            world_size=world)
+    n = 3000
+    lo, hi = rank * n // world, (rank + 1) * n // world
+    local = _states_for(_table(lo, hi))
+    arr = (L.DqState * len(local))()
+    for i, (kind, st) in enumerate(local):
+        arr[i] = _to_dq(kind, st)
+    merged = allgather_merge(arr, len(local))
+    q.put((rank, bytes(merged)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_allgather_merge_equals_whole_table(world):
+    from deequ_amd import _lib as L
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    whole = _states_for(_table(0, 3000))
+    n_ops = len(whole)
+    size = ctypes.sizeof(L.DqState)
+    for r in range(world):
+        blob = results[r]
+        assert blob == results[0]  # every rank holds the same merged states
+        for i, (kind, want) in enumerate(whole):
+            got = L.DqState.from_buffer_copy(blob, i * size)
+            if want is None:
+                assert not got.has_value
+                continue
+            assert got.has_value
+            if kind == L.DQ_OP_SIZE:
+                assert got.num_matches == want.num_matches
+            elif kind == L.DQ_OP_COMPLETENESS:
+                assert (got.num_matches, got.count) == (want.num_matches, want.count)
+            elif kind == L.DQ_OP_SUM:
+                assert got.sum == want.sum_  # integral sum: exact
+            elif kind == L.DQ_OP_MEAN:
+                assert got.count == want.count and got.sum == pytest.approx(want.sum_, rel=1e-15)
+            elif kind == L.DQ_OP_STDDEV:
+                assert got.n == want.n
+                assert got.avg == pytest.approx(want.avg, rel=1e-13)
+                assert got.m2 == pytest.approx(want.m2, rel=1e-12)
+            elif kind == L.DQ_OP_MINIMUM:
+                assert got.value == want.min_value
+            elif kind == L.DQ_OP_MAXIMUM:
+                assert got.value == want.max_value
+            elif kind == L.DQ_OP_APPROX_COUNT_DISTINCT:
+                assert list(got.words) == list(want.words)
