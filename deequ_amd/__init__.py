@@ -5,11 +5,16 @@ The public names mirror the reference's Scala API (`com.amazon.deequ.analyzers`,
 goes through the C-ABI library `libdeequ_amd.so` (hand-written gfx950 HIP kernels); there is
 no CPU fallback.
 """
-from .analyzers import (Analyzer, ApproxCountDistinct, Completeness, Compliance, Maximum, Mean,
-                        Minimum, Preconditions, ScanShareableAnalyzer, Size, StandardDeviation,
-                        StandardScanShareableAnalyzer, Sum)
+from .analyzers import (Analyzer, ApproxCountDistinct, Completeness, Compliance, CountDistinct,
+                        Distinctness, Entropy, FrequencyBasedAnalyzer, GroupingAnalyzer, Histogram,
+                        Maximum, Mean, Minimum, MutualInformation, Preconditions,
+                        ScanShareableAnalyzer, ScanShareableFrequencyBasedAnalyzer, Size,
+                        StandardDeviation, StandardScanShareableAnalyzer, Sum, Uniqueness,
+                        UniqueValueRatio)
+from .frequencies import FrequenciesAndNumRows, FrequencyTable
 from .engine import Plan, current_device, run_scan, set_device
-from .metrics import (DoubleMetric, EmptyStateException, Entity, Failure,
+from .metrics import (Distribution, DistributionValue, DoubleMetric, EmptyStateException, Entity,
+                      Failure, HistogramMetric,
                       IllegalAnalyzerParameterException, MetricCalculationException,
                       MetricCalculationRuntimeException, NoSuchColumnException, Success,
                       WrongColumnTypeException)

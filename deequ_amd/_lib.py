@@ -14,7 +14,7 @@ from ctypes import (POINTER, Structure, c_char_p, c_double, c_int, c_int32, c_in
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdeequ_amd.so")
 
 # ---------------------------------------------------------------- enums (mirror the header)
-DQ_OK, DQ_ERR_INVALID, DQ_ERR_UNSUPPORTED, DQ_ERR_DEVICE, DQ_ERR_OOM, DQ_ERR_STATE = range(6)
+DQ_OK, DQ_ERR_INVALID, DQ_ERR_UNSUPPORTED, DQ_ERR_DEVICE, DQ_ERR_OOM, DQ_ERR_STATE, DQ_ERR_SPACE = range(7)
 
 DQ_T_BOOL, DQ_T_INT8, DQ_T_INT16, DQ_T_INT32, DQ_T_INT64, DQ_T_FLOAT32, DQ_T_FLOAT64, DQ_T_UTF8 = range(1, 9)
 DQ_COL_DEVICE = 0x1
@@ -29,6 +29,7 @@ DQ_P_AND, DQ_P_OR, DQ_P_NOT, DQ_P_TRUE, DQ_P_FALSE = 30, 31, 32, 33, 34
 DQ_CMP_AS_INT64, DQ_CMP_AS_FLOAT64 = 0, 1
 
 DQ_HLL_NUM_WORDS = 52
+DQ_FREQ_NULL_AS_KEY = 0x1
 
 TYPE_CODES = {
     "bool": DQ_T_BOOL, "int8": DQ_T_INT8, "int16": DQ_T_INT16, "int32": DQ_T_INT32,
@@ -61,6 +62,16 @@ class DqState(Structure):
                 ("m2", c_double), ("value", c_double), ("words", c_int64 * DQ_HLL_NUM_WORDS)]
 
 
+class DqFreqSummary(Structure):
+    _fields_ = [("num_rows", c_int64), ("num_groups", c_int64), ("num_unique", c_int64),
+                ("grouped_rows", c_int64), ("entropy", c_double)]
+
+
+class DqFreqGroup(Structure):
+    _fields_ = [("count", c_int64), ("key_offset", c_int64), ("key_len", c_int32),
+                ("reserved", c_int32)]
+
+
 # every symbol include/deequ_amd.h declares, with its ctypes signature
 SIGNATURES = {
     "dq_last_error": (c_char_p, []),
@@ -82,6 +93,19 @@ SIGNATURES = {
     "dq_hll_words_to_bytes": (None, [POINTER(c_int64), POINTER(c_uint8)]),
     "dq_hll_words_from_bytes": (None, [POINTER(c_uint8), POINTER(c_int64)]),
     "dq_xxh64": (c_uint64, [c_void_p, c_size_t, c_uint64]),
+    "dq_freq_create": (c_int, [c_void_p, POINTER(c_int32), c_int, POINTER(c_int32), c_int, c_int,
+                               POINTER(c_void_p)]),
+    "dq_freq_destroy": (c_int, [c_void_p]),
+    "dq_freq_reset": (c_int, [c_void_p]),
+    "dq_freq_consume": (c_int, [c_void_p, POINTER(DqColumn), c_int, c_int64]),
+    "dq_freq_get_summary": (c_int, [c_void_p, POINTER(DqFreqSummary)]),
+    "dq_freq_size": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64)]),
+    "dq_freq_export": (c_int, [c_void_p, POINTER(DqFreqGroup), c_int64, c_void_p, c_int64,
+                               POINTER(c_int64)]),
+    "dq_freq_top": (c_int, [c_void_p, c_int, POINTER(DqFreqGroup), c_int64, c_void_p, c_int64,
+                            POINTER(c_int64), POINTER(c_int64)]),
+    "dq_freq_merge": (c_int, [c_void_p, c_void_p]),
+    "dq_freq_import": (c_int, [c_void_p, POINTER(DqFreqGroup), c_int64, c_void_p, c_int64]),
 }
 
 _lib = None

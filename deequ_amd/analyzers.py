@@ -13,12 +13,15 @@ Names, constructor arguments, preconditions, NULL -> None rules and failure metr
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional
 
 from . import _lib as L
-from .metrics import (DoubleMetric, Entity, NoSuchColumnException, WrongColumnTypeException,
-                      empty_state_exception, metric_from_failure, metric_from_value)
+from .metrics import (DoubleMetric, Entity, Failure, IllegalAnalyzerParameterException,
+                      MetricCalculationRuntimeException, NoColumnsSpecifiedException,
+                      NoSuchColumnException, NumberOfSpecifiedColumnsException,
+                      WrongColumnTypeException, empty_state_exception, metric_from_failure,
+                      metric_from_value, wrap_if_necessary)
 from .states import State, merge
 
 NUMERIC_TYPES = ("int8", "int16", "int32", "int64", "float32", "float64")
@@ -44,6 +47,22 @@ class Preconditions:
                 raise WrongColumnTypeException(
                     "Expected type of column %s to be one of (ByteType,ShortType,IntegerType,"
                     "LongType,FloatType,DoubleType,DecimalType), but found %s instead!" % (column, t))
+        return check
+
+    @staticmethod
+    def atLeastOne(columns) -> Callable[[Dict[str, str]], None]:
+        def check(_schema):
+            if len(columns) == 0:
+                raise NoColumnsSpecifiedException("At least one column needs to be specified!")
+        return check
+
+    @staticmethod
+    def exactlyNColumns(columns, n: int) -> Callable[[Dict[str, str]], None]:
+        def check(_schema):
+            if len(columns) != n:
+                raise NumberOfSpecifiedColumnsException(
+                    "%d columns have to be specified! Currently, columns contains only %d column(s): %s!"
+                    % (n, len(columns), ",".join(columns)))
         return check
 
     @staticmethod
@@ -252,3 +271,281 @@ class ApproxCountDistinct(StandardScanShareableAnalyzer):
 
     def __str__(self):
         return "ApproxCountDistinct(%s,%s)" % (self.column, _opt(self.where))
+
+
+# ---------------------------------------------------------------- frequency-based analyzers
+def _columns_tuple(columns) -> tuple:
+    return (columns,) if isinstance(columns, str) else tuple(columns)
+
+
+def _scala_seq(columns) -> str:
+    return "List(%s)" % ", ".join(columns)
+
+
+class GroupingAnalyzer(Analyzer):
+    """GroupingAnalyzer (Analyzer.scala:273-282)."""
+
+    def groupingColumns(self) -> List[str]:
+        raise NotImplementedError
+
+    def preconditions(self):
+        return [Preconditions.hasColumn(c) for c in self.groupingColumns()]
+
+
+class FrequencyBasedAnalyzer(GroupingAnalyzer):
+    """FrequencyBasedAnalyzer (GroupingAnalyzers.scala:29-42): the state is the GPU group-by
+    of the grouping columns (deequ_amd.frequencies)."""
+
+    columns: tuple = ()
+
+    def __post_init__(self):
+        object.__setattr__(self, "columns", _columns_tuple(self.columns))
+
+    def groupingColumns(self) -> List[str]:
+        return list(self.columns)
+
+    @property
+    def entity(self):
+        return Entity.Column if len(self.columns) == 1 else Entity.Mutlicolumn
+
+    def instance(self) -> str:
+        return ",".join(self.columns)
+
+    def computeStateFrom(self, data):
+        from .frequencies import compute_frequencies
+        return compute_frequencies(data, self.groupingColumns())
+
+    def preconditions(self):
+        return [Preconditions.atLeastOne(self.columns)] + \
+            [Preconditions.hasColumn(c) for c in self.columns]
+
+    def __str__(self):
+        return "%s(%s)" % (self.name, _scala_seq(self.columns))
+
+
+class ScanShareableFrequencyBasedAnalyzer(FrequencyBasedAnalyzer):
+    """ScanShareableFrequencyBasedAnalyzer (GroupingAnalyzers.scala:84-121).  The Spark job
+    `frequencies.agg(...)` becomes the device summary (#groups, #count==1, entropy) of the
+    frequency table; `metric_from_summary` restates each analyzer's aggregation."""
+
+    def metric_from_summary(self, s) -> Optional[float]:
+        raise NotImplementedError
+
+    def computeMetricFrom(self, state):
+        if state is None:
+            return metric_from_failure(empty_state_exception(self), self.name, self.instance(), self.entity)
+        value = self.metric_from_summary(state.summary())
+        if value is None:  # the aggregation over the frequency table is NULL (:113-119)
+            return metric_from_failure(empty_state_exception(self), self.name, self.instance(), self.entity)
+        return metric_from_value(value, self.name, self.instance(), self.entity)
+
+
+@dataclass(frozen=True)
+class Uniqueness(ScanShareableFrequencyBasedAnalyzer):
+    """Σ[count == 1] / numRows (Uniqueness.scala:29-31)."""
+    columns: tuple
+    name = "Uniqueness"
+
+    def metric_from_summary(self, s):
+        return None if s.num_groups == 0 else float(s.num_unique) / s.num_rows
+
+    __str__ = FrequencyBasedAnalyzer.__str__
+
+
+@dataclass(frozen=True)
+class Distinctness(ScanShareableFrequencyBasedAnalyzer):
+    """Σ[count >= 1] / numRows (Distinctness.scala:32-34)."""
+    columns: tuple
+    name = "Distinctness"
+
+    def metric_from_summary(self, s):
+        return None if s.num_groups == 0 else float(s.num_groups) / s.num_rows
+
+    __str__ = FrequencyBasedAnalyzer.__str__
+
+
+@dataclass(frozen=True)
+class CountDistinct(ScanShareableFrequencyBasedAnalyzer):
+    """count(*) over the frequency table (CountDistinct.scala:27-33): never NULL."""
+    columns: tuple
+    name = "CountDistinct"
+
+    def metric_from_summary(self, s):
+        return float(s.num_groups)
+
+    __str__ = FrequencyBasedAnalyzer.__str__
+
+
+@dataclass(frozen=True)
+class UniqueValueRatio(ScanShareableFrequencyBasedAnalyzer):
+    """Σ[count == 1] / count(*) (UniqueValueRatio.scala:28-37).  With no groups the sum is
+    NULL and the reference's `Row.getDouble` throws, which surfaces as a failure metric."""
+    columns: tuple
+    name = "UniqueValueRatio"
+
+    def metric_from_summary(self, s):
+        if s.num_groups == 0:
+            raise MetricCalculationRuntimeException("Value at index 0 is null")
+        return float(s.num_unique) / float(s.num_groups)
+
+    __str__ = FrequencyBasedAnalyzer.__str__
+
+
+@dataclass(frozen=True)
+class Entropy(ScanShareableFrequencyBasedAnalyzer):
+    """Σ −(c/N)·ln(c/N) over the groups (Entropy.scala:31-41)."""
+    column: str
+    name = "Entropy"
+
+    def __post_init__(self):
+        object.__setattr__(self, "columns", (self.column,))
+
+    def metric_from_summary(self, s):
+        return None if s.num_groups == 0 else s.entropy
+
+    def __str__(self):
+        return "Entropy(%s)" % self.column
+
+
+@dataclass(frozen=True)
+class MutualInformation(FrequencyBasedAnalyzer):
+    """Mutual information of two columns from their joint frequencies (MutualInformation.scala:
+    34-84).  The joint table is the GPU group-by; the marginals and the sum are taken over the
+    exported groups in a fixed (encoded-key) order."""
+    columns: tuple
+    columnB: Optional[str] = field(default=None, compare=False, repr=False)  # MutualInformation(a, b)
+    name = "MutualInformation"
+
+    def __post_init__(self):
+        cols = _columns_tuple(self.columns)
+        if self.columnB is not None:
+            cols = cols + (self.columnB,)
+            object.__setattr__(self, "columnB", None)
+        object.__setattr__(self, "columns", cols)
+
+    @property
+    def entity(self):
+        return Entity.Mutlicolumn
+
+    def preconditions(self):
+        return [Preconditions.exactlyNColumns(self.columns, 2)] + super().preconditions()
+
+    def computeMetricFrom(self, state):
+        if state is None:
+            return metric_from_failure(empty_state_exception(self), self.name, self.instance(), self.entity)
+        import math
+        from .frequencies import decode_key
+        total = state.numRows
+        counts, keys = state.table.export()
+        if len(keys) == 0:
+            return metric_from_failure(empty_state_exception(self), self.name, self.instance(), self.entity)
+        cols = state.columns
+        i1, i2 = cols.index(self.columns[0]), cols.index(self.columns[1])
+        order = sorted(range(len(keys)), key=lambda i: keys[i])
+        joint = [(decode_key(keys[i], state.table.dtypes), int(counts[i])) for i in order]
+        m1, m2 = {}, {}
+        for k, c in joint:
+            m1[k[i1]] = m1.get(k[i1], 0) + c
+            m2[k[i2]] = m2.get(k[i2], 0) + c
+        value = 0.0
+        for k, c in joint:
+            px, py, pxy = float(m1[k[i1]]), float(m2[k[i2]]), float(c)
+            value += (pxy / total) * math.log((pxy / total) / ((px / total) * (py / total)))
+        return metric_from_value(value, self.name, self.instance(), self.entity)
+
+    def __str__(self):
+        return "MutualInformation(%s)" % _scala_seq(self.columns)
+
+
+MAXIMUM_ALLOWED_DETAIL_BINS = 1000  # Histogram.MaximumAllowedDetailBins (Histogram.scala:109)
+
+
+@dataclass(frozen=True)
+class Histogram(Analyzer):
+    """Histogram (Histogram.scala:41-116): value counts of `column` cast to string (NULL ->
+    "NullValue"), the top `maxDetailBins` by count and the number of bins.
+
+    The group-by runs on the GPU over the raw values (DQ_FREQ_NULL_AS_KEY: NULL is a group,
+    NaNs are one group); values become Java strings only for the few reported bins.  A
+    `binningUdf` (a Python callable on the column's values, None for NULL) is applied per
+    distinct value after the group-by -- the same result as binning every row first, since
+    the UDF is a function of the value."""
+    column: str
+    binningUdf: Optional[Callable] = None
+    maxDetailBins: int = MAXIMUM_ALLOWED_DETAIL_BINS
+    name = "Histogram"
+
+    def instance(self):
+        return self.column
+
+    def preconditions(self):
+        def param_check(_schema):
+            if self.maxDetailBins > MAXIMUM_ALLOWED_DETAIL_BINS:
+                raise IllegalAnalyzerParameterException(
+                    "Cannot return histogram values for more than %d values" % MAXIMUM_ALLOWED_DETAIL_BINS)
+        return [param_check, Preconditions.hasColumn(self.column)]
+
+    def computeStateFrom(self, data):
+        from .frequencies import FrequenciesAndNumRows, compute_frequencies, decode_key
+        if self.binningUdf is None:
+            return compute_frequencies(data, [self.column], histogram=True)
+        state = compute_frequencies(data, [self.column])
+        dtype = state.table.dtypes[0]
+        s = state.summary()
+        counts, keys = state.table.export()
+        binned: Dict[tuple, int] = {}
+
+        def add(value, c):
+            b = self.binningUdf(value)
+            key = NULL_FIELD_REPLACEMENT if b is None else _udf_result_to_string(b)
+            binned[(key,)] = binned.get((key,), 0) + c
+        for k, c in zip(keys, counts.tolist()):
+            add(decode_key(k, [dtype])[0], c)
+        if s.num_rows > s.grouped_rows:
+            add(None, s.num_rows - s.grouped_rows)
+        return FrequenciesAndNumRows.from_frequencies([self.column], ["string"], binned, s.num_rows,
+                                                      histogram=True)
+
+    def computeMetricFrom(self, state):
+        from .metrics import Distribution, DistributionValue, HistogramMetric, Success as _S
+        if state is None:
+            return HistogramMetric(self.column, Failure(wrap_if_necessary(empty_state_exception(self))))
+        try:
+            from .frequencies import decode_key
+            from .javafmt import spark_cast_to_string
+            dtype = state.table.dtypes[0]
+            n_rows = state.numRows
+            counts, keys = state.table.top(self.maxDetailBins)
+            items = []
+            for k, c in zip(keys, counts.tolist()):
+                v = decode_key(k, [dtype], histogram=True)[0]
+                items.append((NULL_FIELD_REPLACEMENT if v is None else spark_cast_to_string(v, dtype), c))
+            items.sort(key=lambda kv: (-kv[1], kv[0].encode("utf-8")))
+            values = {k: DistributionValue(c, c / n_rows) for k, c in items[:self.maxDetailBins]}
+            return HistogramMetric(self.column, _S(Distribution(values, state.summary().num_groups)))
+        except Exception as e:  # noqa: BLE001
+            return self.toFailureMetric(e)
+
+    def toFailureMetric(self, error):
+        from .metrics import HistogramMetric
+        return HistogramMetric(self.column, Failure(wrap_if_necessary(error)))
+
+    def __str__(self):
+        return "Histogram(%s,%s,%d)" % (self.column, "None" if self.binningUdf is None else
+                                        "Some(%r)" % self.binningUdf, self.maxDetailBins)
+
+
+NULL_FIELD_REPLACEMENT = "NullValue"
+
+
+def _udf_result_to_string(b) -> str:
+    from .javafmt import spark_cast_to_string
+    if isinstance(b, str):
+        return b
+    if isinstance(b, bool):
+        return spark_cast_to_string(b, "bool")
+    if isinstance(b, int):
+        return str(b)
+    if isinstance(b, float):
+        return spark_cast_to_string(b, "float64")
+    return str(b)

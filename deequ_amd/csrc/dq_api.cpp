@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <string>
@@ -364,10 +365,18 @@ struct ScanGroup {
   size_t dev_offset = 0;  // first entry in d_groups
 };
 
-struct dq_plan {
-  dq_ctx* ctx = nullptr;
+// Per-batch column staging shared by scan plans and frequency tables: host buffers are copied
+// (and sliced bitmaps realigned) into device buffers owned here; device buffers are used in
+// place when their layout allows.
+struct Stager {
   hipStream_t stream = nullptr;
   std::vector<int32_t> col_types;
+  std::vector<DevBuf> stage_values, stage_validity, stage_offsets;
+  std::vector<std::vector<uint8_t>> host_tmp;  // realigned host buffers alive until sync
+};
+
+struct dq_plan : Stager {
+  dq_ctx* ctx = nullptr;
   std::vector<bool> col_used;
   std::vector<OpSlot> slots;
   std::vector<ScanTask> scan_tasks;
@@ -377,14 +386,12 @@ struct dq_plan {
   // device state
   DevBuf d_tasks, d_groups, d_ranges, d_hll, d_progs, d_insns, d_pool, d_acc, d_partials, d_regs,
       d_cols, d_masks, d_mask_words;
-  std::vector<DevBuf> stage_values, stage_validity, stage_offsets;
   int64_t mask_words = 0;
   // pinned descriptor staging (DevColumn + DevMask arrays) guarded by an event
   void* h_desc = nullptr;
   size_t h_desc_size = 0;
   hipEvent_t desc_done = nullptr;
   bool desc_pending = false;
-  std::vector<std::vector<uint8_t>> host_tmp;  // realigned host buffers alive until sync
   int64_t total_rows = 0;
   int target_blocks = 2048;
 
@@ -671,7 +678,7 @@ static void host_realign(const uint8_t* src, int64_t off, int64_t n, std::vector
     if ((src[(off + i) >> 3] >> ((off + i) & 7)) & 1u) dst[i >> 3] |= (uint8_t)(1u << (i & 7));
 }
 
-static dq_status prepare_column(dq_plan* plan, int c, const dq_column& col, int64_t n_rows,
+static dq_status prepare_column(Stager* plan, int c, const dq_column& col, int64_t n_rows,
                                 DevColumn* dc) {
   const int t = plan->col_types[c];
   if (col.type != t) return fail(DQ_ERR_INVALID, "column " + std::to_string(c) + " type differs from plan");
@@ -1181,3 +1188,6 @@ extern "C" dq_status dq_state_metric(const dq_state* s, double* out) {
   }
   return DQ_OK;
 }
+
+// The frequency group-by shares the staging helpers above.
+#include "dq_freq_api.inc"

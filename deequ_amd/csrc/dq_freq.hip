@@ -1,0 +1,540 @@
+// dq_freq.hip -- GPU hash group-by for the frequency-based analyzers.
+//
+// Replaces FrequencyBasedAnalyzer.computeFrequencies (analyzers/GroupingAnalyzers.scala:53-80):
+//   SELECT cols, COUNT(*) FROM data WHERE cols NOT NULL GROUP BY cols
+// and the group-by of Histogram.computeStateFrom (Histogram.scala:54-69, NULL -> "NullValue").
+// The metrics (Uniqueness, Distinctness, CountDistinct, UniqueValueRatio, Entropy,
+// Histogram) depend only on the multiset of group counts, so after the group-by a second
+// kernel builds a count-of-counts histogram (integer, order independent); the host turns it
+// into metrics in a fixed order -- bitwise reproducible whatever the insert schedule.
+//
+// Table: open addressing with linear probing in HBM, 32-byte slots
+//   ctrl  = tag(32) << 32 | READY | HEAP | len(24)     (0 = empty)
+//   count = number of rows in the group
+//   k0,k1 = the key bytes when len <= 16, else {heap offset, 0} into the key heap
+// Every access to another workgroup's slot is a device-scope atomic RMW (CAS to probe/claim,
+// atomic exchange to write the key, fetch-or to read it, fetch-add for the count): RMW
+// atomics are coherent across the eight XCDs, plain loads of another XCD's stores are not
+// (MI355X_MICROARCH.md "Workgroup dispatch, XCD placement & inter-workgroup visibility").
+//
+// Each workgroup first aggregates in an LDS table (kLdsSlots keys); rows whose key does not
+// find room there go straight to the global table.  Low-cardinality / skewed columns therefore
+// cost one global atomic per (workgroup, key) instead of one per row.
+#include "dq_internal.h"
+
+namespace dq {
+
+namespace {
+
+constexpr unsigned long long kReady = 1ull << 31;
+constexpr unsigned long long kHeapKey = 1ull << 30;
+constexpr unsigned long long kLenMask = (1ull << 24) - 1;
+constexpr int kLdsSlots = 1024;       // LDS pre-aggregation slots per workgroup
+constexpr int kLdsProbe = 8;          // linear probes in LDS before going global
+constexpr int kMaxLocalKey = 64;      // encoded multi-column keys are built in registers/scratch
+
+__device__ inline unsigned long long atom_or(unsigned long long* p, unsigned long long v) {
+  return __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline unsigned long long atom_read(unsigned long long* p) { return atom_or(p, 0ull); }
+
+// Unaligned little-endian 8-byte read of p[0..n) (n <= 8), zero padded, touching only aligned
+// words that contain at least one byte of the range (never leaves the page of a valid byte).
+__device__ inline uint64_t ld_partial(const uint8_t* p, uint32_t n) {
+  if (n == 0) return 0;
+  const uintptr_t a = (uintptr_t)p;
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(a & ~(uintptr_t)7);
+  const uint32_t sh = (uint32_t)(a & 7) * 8u;
+  uint64_t v = w[0] >> sh;
+  if (sh && (a & 7) + n > 8) v |= w[1] << (64u - sh);
+  return n >= 8 ? v : (v & ((1ull << (8u * n)) - 1ull));
+}
+
+__device__ uint64_t xxh64_any(const uint8_t* p, uint32_t len, uint64_t seed) {
+  const uint8_t* end = p + len;
+  uint64_t h;
+  if (len >= 32) {
+    uint64_t v1 = seed + kP1 + kP2, v2 = seed + kP2, v3 = seed, v4 = seed - kP1;
+    while (p + 32 <= end) {
+      v1 = xxh_round(v1, ld_partial(p, 8));
+      v2 = xxh_round(v2, ld_partial(p + 8, 8));
+      v3 = xxh_round(v3, ld_partial(p + 16, 8));
+      v4 = xxh_round(v4, ld_partial(p + 24, 8));
+      p += 32;
+    }
+    h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+    h ^= xxh_round(0, v1); h = h * kP1 + kP4;
+    h ^= xxh_round(0, v2); h = h * kP1 + kP4;
+    h ^= xxh_round(0, v3); h = h * kP1 + kP4;
+    h ^= xxh_round(0, v4); h = h * kP1 + kP4;
+  } else {
+    h = seed + kP5;
+  }
+  h += (uint64_t)len;
+  while (p + 8 <= end) {
+    h ^= xxh_round(0, ld_partial(p, 8));
+    h = rotl64(h, 27) * kP1 + kP4;
+    p += 8;
+  }
+  if (p < end) {  // tail <= 7 bytes folded as one word (a deterministic variant, not XXH64)
+    h ^= ld_partial(p, (uint32_t)(end - p)) * kP5;
+    h = rotl64(h, 11) * kP1;
+  }
+  return xxh_avalanche(h);
+}
+
+__device__ inline uint64_t hash_inline(uint64_t k0, uint64_t k1, uint32_t len) {
+  uint64_t h = (uint64_t)len * kP5 + 42u;
+  h ^= xxh_round(0, k0);
+  h = rotl64(h, 27) * kP1 + kP4;
+  h ^= xxh_round(0, k1);
+  h = rotl64(h, 27) * kP1 + kP4;
+  return xxh_avalanche(h);
+}
+
+// One row's grouping key.  Inline (len <= 16) keys live in k0/k1; longer keys point at their
+// bytes (`ptr`, in the batch or in thread-local scratch).
+struct Key {
+  uint64_t k0, k1;
+  const uint8_t* ptr;
+  uint32_t len;
+  uint64_t hash;
+};
+
+__device__ inline bool col_valid(const DevColumn& c, int64_t row) {
+  return c.validity == nullptr || ((c.validity[row >> 3] >> (row & 7)) & 1u);
+}
+
+__device__ inline int width_of(int t) {
+  switch (t) {
+    case DQ_T_BOOL: case DQ_T_INT8: return 1;
+    case DQ_T_INT16: return 2;
+    case DQ_T_INT32: case DQ_T_FLOAT32: return 4;
+    default: return 8;
+  }
+}
+
+__device__ inline uint64_t fixed_bits(const DevColumn& c, int64_t row) {
+  switch (c.type) {
+    case DQ_T_BOOL: return (static_cast<const uint8_t*>(c.values)[row >> 3] >> (row & 7)) & 1u;
+    case DQ_T_INT8: return static_cast<const uint8_t*>(c.values)[row];
+    case DQ_T_INT16: return static_cast<const uint16_t*>(c.values)[row];
+    case DQ_T_INT32: case DQ_T_FLOAT32: return static_cast<const uint32_t*>(c.values)[row];
+    default: return static_cast<const uint64_t*>(c.values)[row];
+  }
+}
+
+// Builds the key of `row`; false if the row is excluded (a NULL grouping value and NULLs are
+// not a key).  Encodings: fixed-width columns = little-endian value bits (floats as raw bits,
+// Spark 2.2 groups by UnsafeRow bytes); strings = UTF-8 bytes, prefixed by a u32 length when
+// several columns are combined; Histogram NULLs = "NullValue" for strings (merging with a
+// literal "NullValue", Histogram.scala:63-64) and the empty key for other types.
+__device__ bool make_key(const FreqKeySpec& ks, const DevColumn* cols, int64_t row, Key& k,
+                         uint8_t* scratch, bool& too_long) {
+  k.k0 = k.k1 = 0;
+  k.ptr = nullptr;
+  k.len = 0;
+  too_long = false;
+  if (ks.n_keys == 1) {
+    const DevColumn& c = cols[ks.key_cols[0]];
+    const bool valid = col_valid(c, row);
+    if (!valid && !ks.null_as_key) return false;
+    if (c.type == DQ_T_UTF8) {
+      const uint8_t* p;
+      uint32_t n;
+      if (!valid) {
+        p = reinterpret_cast<const uint8_t*>("NullValue");
+        n = 9;
+      } else {
+        const int32_t b = c.offsets[row], e = c.offsets[row + 1];
+        p = static_cast<const uint8_t*>(c.values) + b;
+        n = (uint32_t)(e - b);
+      }
+      k.len = n;
+      if (n <= 16) {
+        k.k0 = ld_partial(p, n < 8 ? n : 8);
+        k.k1 = n > 8 ? ld_partial(p + 8, n - 8) : 0;
+        k.hash = hash_inline(k.k0, k.k1, n);
+      } else {
+        k.ptr = p;
+        k.hash = xxh64_any(p, n, 42);
+      }
+      return true;
+    }
+    if (!valid) {  // Histogram NULL of a non-string column: the empty key
+      k.hash = hash_inline(0, 0, 0);
+      return true;
+    }
+    k.k0 = fixed_bits(c, row);
+    if (ks.null_as_key) {  // Histogram groups cast-to-string values: every NaN is "NaN"
+      if (c.type == DQ_T_FLOAT64 && (k.k0 & 0x7fffffffffffffffull) > 0x7ff0000000000000ull) k.k0 = 0x7ff8000000000000ull;
+      if (c.type == DQ_T_FLOAT32 && (k.k0 & 0x7fffffffull) > 0x7f800000ull) k.k0 = 0x7fc00000ull;
+    }
+    k.len = (uint32_t)width_of(c.type);
+    k.hash = hash_inline(k.k0, 0, k.len);
+    return true;
+  }
+  // several columns: concatenate into scratch
+  uint32_t n = 0;
+  for (int i = 0; i < ks.n_keys; ++i) {
+    const DevColumn& c = cols[ks.key_cols[i]];
+    if (!col_valid(c, row)) return false;
+    if (c.type == DQ_T_UTF8) {
+      const int32_t b = c.offsets[row], e = c.offsets[row + 1];
+      const uint32_t sl = (uint32_t)(e - b);
+      if (n + 4 + sl > (uint32_t)kMaxLocalKey) {
+        too_long = true;
+        return false;
+      }
+      for (int j = 0; j < 4; ++j) scratch[n + j] = (uint8_t)(sl >> (8 * j));
+      n += 4;
+      const uint8_t* p = static_cast<const uint8_t*>(c.values) + b;
+      for (uint32_t j = 0; j < sl; ++j) scratch[n + j] = p[j];
+      n += sl;
+    } else {
+      const int w = width_of(c.type);
+      const uint64_t bits = fixed_bits(c, row);
+      for (int j = 0; j < w; ++j) scratch[n + j] = (uint8_t)(bits >> (8 * j));
+      n += (uint32_t)w;
+    }
+  }
+  k.len = n;
+  if (n <= 16) {
+    for (uint32_t j = 0; j < n && j < 8; ++j) k.k0 |= (uint64_t)scratch[j] << (8 * j);
+    for (uint32_t j = 8; j < n; ++j) k.k1 |= (uint64_t)scratch[j] << (8 * (j - 8));
+    k.hash = hash_inline(k.k0, k.k1, n);
+  } else {
+    k.ptr = scratch;
+    k.hash = xxh64_any(scratch, n, 42);
+  }
+  return true;
+}
+
+__device__ inline uint32_t tag_of(uint64_t h) {
+  const uint32_t t = (uint32_t)(h >> 32);
+  return t ? t : 1u;
+}
+
+// Compare a long key with heap bytes (heap words written by atomic exchange: read coherently).
+__device__ bool heap_equal(const FreqTable& T, uint64_t off, const uint8_t* p, uint32_t len) {
+  unsigned long long* hw = reinterpret_cast<unsigned long long*>(T.heap) + (off >> 3);
+  for (uint32_t i = 0; i < len; i += 8) {
+    const uint32_t n = len - i < 8 ? len - i : 8;
+    if (atom_read(hw + (i >> 3)) != ld_partial(p + i, n)) return false;
+  }
+  return true;
+}
+
+// Insert `cnt` rows of key k into the global table.  Returns false on table/heap overflow.
+__device__ bool global_insert(const FreqTable& T, const Key& k, unsigned long long cnt) {
+  const uint32_t tag = tag_of(k.hash);
+  const bool inl = k.len <= 16;
+  const unsigned long long want = ((unsigned long long)tag << 32) | (inl ? 0ull : kHeapKey) | k.len;
+  uint64_t slot = k.hash & T.mask;
+  uint32_t waits = 0;
+  for (uint64_t probes = 0; probes <= T.mask;) {
+    FreqSlot* e = &T.slots[slot];
+    unsigned long long c = atomicCAS(&e->ctrl, 0ull, want);
+    if (c == 0ull) {  // claimed: publish key, count, then READY
+      if (inl) {
+        atomicExch(&e->k0, (unsigned long long)k.k0);
+        atomicExch(&e->k1, (unsigned long long)k.k1);
+      } else {
+        const unsigned long long bytes = ((unsigned long long)k.len + 7ull) & ~7ull;
+        const unsigned long long off = atomicAdd(T.heap_used, bytes);
+        if (off + bytes > T.heap_cap) {  // publish anyway so that no reader waits on the slot
+          atomicOr(T.overflow, 2u);
+          atomicExch(&e->k0, ~0ull);
+          atomicAdd(&e->count, cnt);
+          __hip_atomic_fetch_or(&e->ctrl, kReady, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          return false;
+        }
+        unsigned long long* hw = reinterpret_cast<unsigned long long*>(T.heap) + (off >> 3);
+        for (uint32_t i = 0; i < k.len; i += 8) {
+          const uint32_t n = k.len - i < 8 ? k.len - i : 8;
+          atomicExch(hw + (i >> 3), (unsigned long long)ld_partial(k.ptr + i, n));
+        }
+        atomicExch(&e->k0, off);
+      }
+      atomicAdd(&e->count, cnt);
+      atomicAdd(T.n_groups, 1ull);
+      __hip_atomic_fetch_or(&e->ctrl, kReady, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      return true;
+    }
+    if ((uint32_t)(c >> 32) == tag && (c & (kLenMask | kHeapKey)) == (want & (kLenMask | kHeapKey))) {
+      if (!(c & kReady)) {  // being published by another lane/wave: re-read this slot
+        if (++waits > (1u << 24)) break;
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      bool eq;
+      if (inl) {
+        eq = atom_read(&e->k0) == k.k0 && atom_read(&e->k1) == k.k1;
+      } else {
+        const unsigned long long off = atom_read(&e->k0);
+        eq = off + k.len <= T.heap_cap && heap_equal(T, off, k.ptr, k.len);
+      }
+      if (eq) {
+        atomicAdd(&e->count, cnt);
+        return true;
+      }
+    }
+    slot = (slot + 1) & T.mask;
+    ++probes;
+  }
+  atomicOr(T.overflow, 1u);
+  return false;
+}
+
+struct LdsSlot {
+  unsigned long long ctrl;  // as the global ctrl (READY unused: LDS keys are written before ctrl)
+  unsigned long long k0, k1;
+  unsigned int count;
+  unsigned int pad;
+};
+
+}  // namespace
+
+// Group-by of one batch: LDS pre-aggregation per workgroup, overflow rows to the global table.
+__global__ __launch_bounds__(kBlock) void dq_freq_insert_kernel(FreqKeySpec ks,
+                                                                const DevColumn* __restrict__ cols,
+                                                                int64_t n_rows, FreqTable T) {
+  __shared__ LdsSlot lds[kLdsSlots];
+  __shared__ int lds_open;
+  for (int i = threadIdx.x; i < kLdsSlots; i += kBlock) {
+    lds[i].ctrl = 0;
+    lds[i].count = 0;
+  }
+  if (threadIdx.x == 0) lds_open = 1;
+  __syncthreads();
+
+  const int64_t per_block = (n_rows + gridDim.x - 1) / gridDim.x;
+  const int64_t row_begin = (int64_t)blockIdx.x * per_block;
+  const int64_t row_end = row_begin + per_block < n_rows ? row_begin + per_block : n_rows;
+  alignas(8) uint8_t scratch[kMaxLocalKey];
+  unsigned long long lds_misses = 0;
+  for (int64_t row = row_begin + threadIdx.x; row < row_end; row += kBlock) {
+    Key k;
+    bool too_long;
+    if (!make_key(ks, cols, row, k, scratch, too_long)) {
+      if (too_long) atomicOr(T.overflow, 4u);
+      continue;
+    }
+    bool done = false;
+    if (k.len <= 16 && lds_open) {
+      // LDS table: claim by CAS on ctrl after the key words are known; a racing claimer of the
+      // same slot either wins (and writes the same-or-other key) or re-probes.  Keys are written
+      // BEFORE ctrl by the winner, so readers compare after seeing a non-zero ctrl... which needs
+      // the key in the same atomic: LDS slots therefore publish k0/k1 first under a per-slot
+      // two-phase (ctrl = BUSY, then ctrl = want) and readers re-probe the slot while BUSY.
+      const uint32_t tag = tag_of(k.hash);
+      const unsigned long long want = ((unsigned long long)tag << 32) | kReady | k.len;
+      uint32_t s = (uint32_t)(k.hash & (kLdsSlots - 1));
+      for (int probe = 0; probe < kLdsProbe * 4 && !done; ) {
+        unsigned long long c = atomicCAS(&lds[s].ctrl, 0ull, 1ull);  // 1 = BUSY
+        if (c == 0ull) {
+          lds[s].k0 = k.k0;
+          lds[s].k1 = k.k1;
+          atomicAdd(&lds[s].count, 1u);
+          __threadfence_block();
+          atomicExch(&lds[s].ctrl, want);
+          done = true;
+        } else if (c == 1ull) {
+          ++probe;  // another lane is publishing this slot: look again
+        } else if (c == want && __hip_atomic_load(&lds[s].k0, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == k.k0 &&
+                   __hip_atomic_load(&lds[s].k1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == k.k1) {
+          atomicAdd(&lds[s].count, 1u);
+          done = true;
+        } else {
+          s = (s + 1) & (kLdsSlots - 1);
+          probe += 4;
+        }
+      }
+      if (!done && ++lds_misses > 32) lds_open = 0;  // LDS is full of other keys: stop probing it
+    }
+    if (!done && !global_insert(T, k, 1ull)) break;
+  }
+  __syncthreads();
+  // flush the LDS groups
+  for (int i = threadIdx.x; i < kLdsSlots; i += kBlock) {
+    const unsigned long long c = lds[i].ctrl;
+    if (c > 1ull && lds[i].count) {
+      Key k;
+      k.k0 = lds[i].k0;
+      k.k1 = lds[i].k1;
+      k.len = (uint32_t)(c & kLenMask);
+      k.ptr = nullptr;
+      k.hash = hash_inline(k.k0, k.k1, k.len);
+      global_insert(T, k, lds[i].count);
+    }
+  }
+}
+
+// Count-of-counts over the table: hist[c] for c < kFreqHist, larger counts appended to a list.
+__global__ __launch_bounds__(kBlock) void dq_freq_hist_kernel(FreqTable T, unsigned long long* hist,
+                                                              unsigned long long* big,
+                                                              unsigned long long* n_big,
+                                                              unsigned long long big_cap) {
+  __shared__ unsigned int lh[kFreqLdsHist];
+  for (int i = threadIdx.x; i < kFreqLdsHist; i += kBlock) lh[i] = 0;
+  __syncthreads();
+  const uint64_t n = T.mask + 1;
+  for (uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x; s < n; s += (uint64_t)gridDim.x * kBlock) {
+    const FreqSlot& e = T.slots[s];
+    if (e.ctrl & kReady) {
+      const unsigned long long c = e.count;  // launch boundary: all inserts are visible
+      if (c < (unsigned long long)kFreqLdsHist) {
+        atomicAdd(&lh[c], 1u);
+      } else if (c < (unsigned long long)kFreqHist) {
+        atomicAdd(&hist[c], 1ull);
+      } else {
+        const unsigned long long i = atomicAdd(n_big, 1ull);
+        if (i < big_cap) big[i] = c;
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kFreqLdsHist; i += kBlock)
+    if (lh[i]) atomicAdd(&hist[i], (unsigned long long)lh[i]);
+}
+
+// Export groups: slots with count >= min_count (and, for count == tie_count, all of them).
+__global__ __launch_bounds__(kBlock) void dq_freq_export_kernel(FreqTable T, unsigned long long min_count,
+                                                                FreqOut out) {
+  const uint64_t n = T.mask + 1;
+  for (uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x; s < n; s += (uint64_t)gridDim.x * kBlock) {
+    const FreqSlot& e = T.slots[s];
+    if ((e.ctrl & kReady) && e.count >= min_count) {
+      const unsigned long long i = atomicAdd(out.n, 1ull);
+      if (i < out.cap) {
+        out.ctrl[i] = e.ctrl;
+        out.count[i] = e.count;
+        out.k0[i] = e.k0;
+        out.k1[i] = e.k1;
+      }
+    }
+  }
+}
+
+// Insert exported groups (another table, a loaded state, another GPU's partition).
+__global__ __launch_bounds__(kBlock) void dq_freq_import_kernel(FreqTable T, FreqIn in) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < in.n; i += (uint64_t)gridDim.x * kBlock) {
+    Key k;
+    k.len = (uint32_t)(in.ctrl[i] & kLenMask);
+    if (in.ctrl[i] & kHeapKey) {
+      k.ptr = in.heap + in.k0[i];
+      k.k0 = k.k1 = 0;
+      k.hash = xxh64_any(k.ptr, k.len, 42);
+    } else {
+      k.ptr = nullptr;
+      k.k0 = in.k0[i];
+      k.k1 = in.k1[i];
+      k.hash = hash_inline(k.k0, k.k1, k.len);
+    }
+    if (!global_insert(T, k, in.count[i])) return;
+  }
+}
+
+// Table growth: move every group of `old_slots` into the (empty, larger) table T.  All keys
+// are distinct, so a slot is claimed with its final ctrl word and nobody compares keys.
+__global__ __launch_bounds__(kBlock) void dq_freq_rehash_kernel(const FreqSlot* __restrict__ old_slots,
+                                                                uint64_t old_n, FreqTable T) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < old_n; i += (uint64_t)gridDim.x * kBlock) {
+    const FreqSlot e = old_slots[i];
+    if (!(e.ctrl & kReady)) continue;
+    const uint32_t len = (uint32_t)(e.ctrl & kLenMask);
+    const uint64_t h = (e.ctrl & kHeapKey) ? xxh64_any(T.heap + e.k0, len, 42) : hash_inline(e.k0, e.k1, len);
+    uint64_t slot = h & T.mask;
+    for (uint64_t it = 0; it <= T.mask; ++it) {
+      if (atomicCAS(&T.slots[slot].ctrl, 0ull, e.ctrl) == 0ull) {
+        T.slots[slot].count = e.count;
+        T.slots[slot].k0 = e.k0;
+        T.slots[slot].k1 = e.k1;
+        break;
+      }
+      slot = (slot + 1) & T.mask;
+    }
+  }
+}
+
+hipError_t launch_freq_rehash(const FreqSlot* d_old, uint64_t old_n, const FreqTable& T, hipStream_t stream) {
+  uint64_t blocks = (old_n + kBlock * 8 - 1) / (kBlock * 8);
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(dq_freq_rehash_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, d_old, old_n, T);
+  return hipGetLastError();
+}
+
+// Bytes of long (> 16 B) single-string keys in a batch: the key heap is grown to fit first.
+__global__ __launch_bounds__(kBlock) void dq_freq_heap_need_kernel(FreqKeySpec ks, const DevColumn* __restrict__ cols,
+                                                                   int64_t n_rows, unsigned long long* need) {
+  unsigned long long local = 0;
+  for (int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x; row < n_rows; row += (int64_t)gridDim.x * kBlock) {
+    uint32_t n = 0;
+    bool any_null = false;
+    for (int i = 0; i < ks.n_keys; ++i) {
+      const DevColumn& c = cols[ks.key_cols[i]];
+      if (!col_valid(c, row)) {
+        any_null = true;
+        continue;
+      }
+      if (c.type == DQ_T_UTF8) n += (uint32_t)(c.offsets[row + 1] - c.offsets[row]) + (ks.n_keys > 1 ? 4u : 0u);
+      else n += (uint32_t)width_of(c.type);
+    }
+    if (any_null && !(ks.null_as_key && ks.n_keys == 1)) n = 0;
+    if (n > 16) local += (n + 7u) & ~7u;
+  }
+  for (int d = 32; d >= 1; d >>= 1) local += __shfl_down(local, d, 64);
+  if ((threadIdx.x & 63) == 0 && local) atomicAdd(need, local);
+}
+
+hipError_t launch_freq_insert(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
+                              const FreqTable& T, hipStream_t stream) {
+  if (n_rows <= 0) return hipSuccess;
+  int64_t blocks = (n_rows + 4095) / 4096;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(dq_freq_insert_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, ks, d_cols,
+                     n_rows, T);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_hist(const FreqTable& T, unsigned long long* d_hist, unsigned long long* d_big,
+                            unsigned long long* d_nbig, unsigned long long big_cap, hipStream_t stream) {
+  const uint64_t n = T.mask + 1;
+  uint64_t blocks = (n + kBlock * 16 - 1) / (kBlock * 16);
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(dq_freq_hist_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, d_hist, d_big,
+                     d_nbig, big_cap);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_export(const FreqTable& T, unsigned long long min_count, const FreqOut& out,
+                              hipStream_t stream) {
+  const uint64_t n = T.mask + 1;
+  uint64_t blocks = (n + kBlock * 16 - 1) / (kBlock * 16);
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(dq_freq_export_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, min_count, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_import(const FreqTable& T, const FreqIn& in, hipStream_t stream) {
+  if (in.n == 0) return hipSuccess;
+  uint64_t blocks = (in.n + kBlock * 4 - 1) / (kBlock * 4);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(dq_freq_import_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, in);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_heap_need(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
+                                 unsigned long long* d_need, hipStream_t stream) {
+  if (n_rows <= 0) return hipSuccess;
+  int64_t blocks = (n_rows + kBlock * 16 - 1) / (kBlock * 16);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(dq_freq_heap_need_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, ks, d_cols,
+                     n_rows, d_need);
+  return hipGetLastError();
+}
+
+}  // namespace dq

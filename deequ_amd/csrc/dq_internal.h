@@ -124,6 +124,60 @@ struct PredProgram {
   int32_t n;
 };
 
+// ---------------------------------------------------------------- frequency group-by
+constexpr int kMaxKeyCols = 8;
+constexpr int kFreqHist = 1 << 16;   // count-of-counts bins kept on the device
+constexpr int kFreqLdsHist = 2048;   // ... of which the first are aggregated in LDS
+
+struct FreqSlot {  // 32 B; see dq_freq.hip for the ctrl word
+  unsigned long long ctrl, count, k0, k1;
+};
+
+struct FreqTable {
+  FreqSlot* slots;
+  uint64_t mask;                   // capacity - 1 (capacity is a power of two)
+  unsigned long long* n_groups;    // device counter of claimed slots
+  uint8_t* heap;                   // key bytes of keys longer than 16 B
+  unsigned long long* heap_used;
+  unsigned long long heap_cap;
+  unsigned int* overflow;          // bit 0 table full, bit 1 heap full, bit 2 key too long
+};
+
+struct FreqKeySpec {
+  int32_t key_cols[kMaxKeyCols];
+  int32_t n_keys;
+  int32_t null_as_key;  // Histogram: NULL is a group ("NullValue")
+};
+
+struct FreqOut {  // exported groups (device arrays of capacity `cap`)
+  unsigned long long* ctrl;
+  unsigned long long* count;
+  unsigned long long* k0;
+  unsigned long long* k1;
+  unsigned long long* n;
+  unsigned long long cap;
+};
+
+struct FreqIn {  // groups to merge in; heap offsets in k0 refer to `heap`
+  const unsigned long long* ctrl;
+  const unsigned long long* count;
+  const unsigned long long* k0;
+  const unsigned long long* k1;
+  const uint8_t* heap;
+  uint64_t n;
+};
+
+hipError_t launch_freq_insert(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
+                              const FreqTable& T, hipStream_t stream);
+hipError_t launch_freq_hist(const FreqTable& T, unsigned long long* d_hist, unsigned long long* d_big,
+                            unsigned long long* d_nbig, unsigned long long big_cap, hipStream_t stream);
+hipError_t launch_freq_export(const FreqTable& T, unsigned long long min_count, const FreqOut& out,
+                              hipStream_t stream);
+hipError_t launch_freq_import(const FreqTable& T, const FreqIn& in, hipStream_t stream);
+hipError_t launch_freq_heap_need(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
+                                 unsigned long long* d_need, hipStream_t stream);
+hipError_t launch_freq_rehash(const FreqSlot* d_old, uint64_t old_n, const FreqTable& T, hipStream_t stream);
+
 // ---------------------------------------------------------------- launchers (.hip files)
 // kind 0 = validity/mask-only tasks, 1 = value tasks of column type `ptype` with exactly
 // `np` inline predicates (np > 4 uses the 8-slot kernel; np < 0 = tasks with a where mask

@@ -1,0 +1,262 @@
+"""Frequency group-by on the GPU: the state `FrequenciesAndNumRows` and its table handle.
+
+Replaces `FrequencyBasedAnalyzer.computeFrequencies` (analyzers/GroupingAnalyzers.scala:53-80):
+
+    SELECT cols, COUNT(*) FROM data WHERE cols NOT NULL GROUP BY cols      (+ data.count())
+
+and the group-by of `Histogram.computeStateFrom` (Histogram.scala:54-69).  The table lives in
+HBM (an open-addressing hash table built by deequ_amd/csrc/dq_freq.hip); the metrics of the
+frequency family are derived on the device from a count-of-counts histogram, so a 200M-group
+table never leaves the GPU unless the caller exports it (state persistence, Spark interop).
+
+Group keys cross the C-ABI in an encoded form (see include/deequ_amd.h): fixed-width values
+as their little-endian bytes (floats as raw bits -- Spark 2.2 groups by the UnsafeRow bytes),
+strings as UTF-8; several columns concatenated, string parts prefixed by a u32 length.
+"""
+from __future__ import annotations
+
+import ctypes
+import struct
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib as L
+from .states import State
+
+_FIXED = {"bool": ("<B", 1), "int8": ("<b", 1), "int16": ("<h", 2), "int32": ("<i", 4),
+          "int64": ("<q", 8), "float32": ("<f", 4), "float64": ("<d", 8)}
+NULL_FIELD_REPLACEMENT = "NullValue"  # Histogram.NullFieldReplacement (Histogram.scala:108)
+
+
+# ---------------------------------------------------------------- key codec
+def encode_key(values: Sequence, dtypes: Sequence[str], histogram: bool = False) -> bytes:
+    """Python values (None = NULL, histogram tables only) -> encoded key bytes."""
+    if histogram:
+        (v,), (t,) = values, dtypes
+        if v is None:
+            return NULL_FIELD_REPLACEMENT.encode() if t == "string" else b""
+        if t == "float64" and v != v:
+            return struct.pack("<Q", 0x7FF8000000000000)
+        if t == "float32" and v != v:
+            return struct.pack("<I", 0x7FC00000)
+    multi = len(dtypes) > 1
+    out = []
+    for v, t in zip(values, dtypes):
+        if t == "string":
+            b = v.encode("utf-8")
+            out.append((struct.pack("<I", len(b)) if multi else b"") + b)
+        elif t == "bool":
+            out.append(b"\x01" if v else b"\x00")
+        else:
+            out.append(struct.pack(_FIXED[t][0], v))
+    return b"".join(out)
+
+
+def decode_key(key: bytes, dtypes: Sequence[str], histogram: bool = False) -> tuple:
+    """Encoded key bytes -> tuple of Python values (floats keep their bits)."""
+    if histogram and len(key) == 0 and dtypes[0] != "string":
+        return (None,)
+    if len(dtypes) == 1 and dtypes[0] == "string":
+        return (key.decode("utf-8"),)
+    out, pos, multi = [], 0, len(dtypes) > 1
+    for t in dtypes:
+        if t == "string":
+            n = struct.unpack_from("<I", key, pos)[0] if multi else len(key) - pos
+            pos += 4 if multi else 0
+            out.append(key[pos:pos + n].decode("utf-8"))
+            pos += n
+        elif t == "bool":
+            out.append(key[pos] != 0)
+            pos += 1
+        else:
+            fmt, w = _FIXED[t]
+            out.append(struct.unpack_from(fmt, key, pos)[0])
+            pos += w
+    return tuple(out)
+
+
+# ---------------------------------------------------------------- device table
+class FrequencyTable:
+    """A dq_freq handle: device-resident (group key -> count) table plus numRows.
+
+    `schema` is the batch schema handed to `consume` (defaults to the key columns alone);
+    `histogram=True` is Histogram's NULL-as-"NullValue" grouping (DQ_FREQ_NULL_AS_KEY)."""
+
+    def __init__(self, key_columns: Sequence[str], schema: Dict[str, str], histogram: bool = False,
+                 device: Optional[int] = None):
+        from .engine import current_device
+        self.key_columns = list(key_columns)
+        self.schema = dict(schema)
+        self.names = list(self.schema.keys())
+        self.dtypes = [self.schema[c] for c in self.key_columns]
+        self.histogram = histogram
+        self.device = current_device() if device is None else device
+        ctx = L.Context.get(self.device)
+        idx = (ctypes.c_int32 * len(self.key_columns))(*[self.names.index(c) for c in self.key_columns])
+        types = (ctypes.c_int32 * len(self.names))(*[L.TYPE_CODES[self.schema[n]] for n in self.names])
+        h = ctypes.c_void_p()
+        L.check(L.lib().dq_freq_create(ctx.handle, idx, len(self.key_columns), types, len(self.names),
+                                       L.DQ_FREQ_NULL_AS_KEY if histogram else 0, ctypes.byref(h)))
+        self.handle = h
+
+    @classmethod
+    def like(cls, other: "FrequencyTable") -> "FrequencyTable":
+        """An empty table with the same key columns (and a key-only schema)."""
+        return cls(other.key_columns, {c: t for c, t in zip(other.key_columns, other.dtypes)},
+                   other.histogram, other.device)
+
+    def consume(self, batch) -> None:
+        from .table import dq_columns
+        cols = dq_columns(batch, self.names)
+        L.check(L.lib().dq_freq_consume(self.handle, cols, len(self.names), batch.num_rows))
+
+    def summary(self) -> L.DqFreqSummary:
+        s = L.DqFreqSummary()
+        L.check(L.lib().dq_freq_get_summary(self.handle, ctypes.byref(s)))
+        return s
+
+    @property
+    def num_rows(self) -> int:
+        return self.summary().num_rows
+
+    def export(self) -> Tuple[np.ndarray, List[bytes]]:
+        """Every group: (counts int64[n], encoded keys), in an unspecified order."""
+        n, kb = ctypes.c_int64(), ctypes.c_int64()
+        L.check(L.lib().dq_freq_size(self.handle, ctypes.byref(n), ctypes.byref(kb)))
+        groups = (L.DqFreqGroup * max(1, n.value))()
+        keys = ctypes.create_string_buffer(max(1, kb.value))
+        got = ctypes.c_int64()
+        L.check(L.lib().dq_freq_export(self.handle, groups, n.value, keys, kb.value, ctypes.byref(got)))
+        return _unpack_groups(groups, got.value, keys.raw)
+
+    def top(self, n: int) -> Tuple[np.ndarray, List[bytes]]:
+        """Groups whose count is at least the n-th largest count (ties at the cut included),
+        count descending then encoded key ascending."""
+        cap_g, cap_k = max(16, 2 * n), max(4096, 64 * n)
+        while True:
+            groups = (L.DqFreqGroup * cap_g)()
+            keys = ctypes.create_string_buffer(cap_k)
+            got, kb = ctypes.c_int64(), ctypes.c_int64()
+            st = L.lib().dq_freq_top(self.handle, n, groups, cap_g, keys, cap_k, ctypes.byref(got),
+                                     ctypes.byref(kb))
+            if st == L.DQ_ERR_SPACE:
+                cap_g, cap_k = max(cap_g, got.value), max(cap_k, kb.value)
+                continue
+            L.check(st)
+            return _unpack_groups(groups, got.value, keys.raw)
+
+    def import_groups(self, counts: Sequence[int], keys: Sequence[bytes], num_rows: int) -> None:
+        """FrequenciesAndNumRows.sum for the given groups (GroupingAnalyzers.scala:128-148)."""
+        n = len(keys)
+        groups = (L.DqFreqGroup * max(1, n))()
+        off = 0
+        for i, (c, k) in enumerate(zip(counts, keys)):
+            groups[i].count = int(c)
+            groups[i].key_offset = off
+            groups[i].key_len = len(k)
+            off += len(k)
+        blob = b"".join(keys)
+        buf = ctypes.create_string_buffer(blob, max(1, len(blob)))
+        L.check(L.lib().dq_freq_import(self.handle, groups, n, buf, int(num_rows)))
+
+    def merge_from(self, other: "FrequencyTable") -> None:
+        """self += other, device to device."""
+        L.check(L.lib().dq_freq_merge(self.handle, other.handle))
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            L.lib().dq_freq_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_GROUP_DTYPE = np.dtype([("count", "<i8"), ("key_offset", "<i8"), ("key_len", "<i4"), ("reserved", "<i4")])
+
+
+def _unpack_groups(groups, n: int, raw: bytes) -> Tuple[np.ndarray, List[bytes]]:
+    g = np.frombuffer(groups, dtype=_GROUP_DTYPE, count=n)
+    offs, lens = g["key_offset"].tolist(), g["key_len"].tolist()
+    return g["count"].copy(), [raw[o:o + m] for o, m in zip(offs, lens)]
+
+
+def compute_frequencies(data, grouping_columns: Sequence[str], histogram: bool = False) -> "FrequenciesAndNumRows":
+    """FrequencyBasedAnalyzer.computeFrequencies over every batch of `data` (one pass)."""
+    schema = data.schema
+    table = FrequencyTable(grouping_columns, {c: schema[c] for c in schema}, histogram)
+    for batch in data.batches():
+        table.consume(batch)
+    return FrequenciesAndNumRows(table)
+
+
+# ---------------------------------------------------------------- the state
+class FrequenciesAndNumRows(State):
+    """FrequenciesAndNumRows(frequencies, numRows) (GroupingAnalyzers.scala:124-157), with the
+    frequencies held in HBM."""
+
+    def __init__(self, table: FrequencyTable):
+        self.table = table
+        self._summary = None
+
+    @property
+    def columns(self) -> List[str]:
+        return self.table.key_columns
+
+    @property
+    def numRows(self) -> int:
+        return self.summary().num_rows
+
+    def summary(self) -> L.DqFreqSummary:
+        if self._summary is None:
+            self._summary = self.table.summary()
+        return self._summary
+
+    def sum(self, other: "FrequenciesAndNumRows") -> "FrequenciesAndNumRows":
+        """Null-safe outer join adding counts (GroupingAnalyzers.scala:128-148)."""
+        if not isinstance(other, FrequenciesAndNumRows):
+            raise TypeError("cannot sum FrequenciesAndNumRows with %s" % type(other).__name__)
+        if other.table.dtypes != self.table.dtypes or other.table.histogram != self.table.histogram:
+            raise ValueError("frequency states over different key columns cannot be summed")
+        out = FrequencyTable.like(self.table)
+        out.merge_from(self.table)
+        out.merge_from(other.table)
+        return FrequenciesAndNumRows(out)
+
+    __add__ = sum
+
+    def frequencies(self, raw: bool = False) -> Dict:
+        """{key tuple: count} on the host (decoded Python values), or with `raw` the encoded
+        key bytes -- the exact group identity (decoded floats conflate 0.0 and -0.0)."""
+        counts, keys = self.table.export()
+        if raw:
+            return {k: int(c) for k, c in zip(keys, counts.tolist())}
+        return {decode_key(k, self.table.dtypes, self.table.histogram): int(c)
+                for k, c in zip(keys, counts.tolist())}
+
+    @staticmethod
+    def from_frequencies(columns: Sequence[str], dtypes: Sequence[str], frequencies: Dict[tuple, int],
+                         numRows: int, histogram: bool = False) -> "FrequenciesAndNumRows":
+        """Build a device state from host groups (e.g. a state persisted by Spark deequ)."""
+        t = FrequencyTable(columns, dict(zip(columns, dtypes)), histogram)
+        keys = [encode_key(k, dtypes, histogram) for k in frequencies]
+        t.import_groups(list(frequencies.values()), keys, numRows)
+        return FrequenciesAndNumRows(t)
+
+    def metricValue(self):
+        raise NotImplementedError("frequency metrics are computed by the analyzers")
+
+    def __eq__(self, o):
+        return (isinstance(o, FrequenciesAndNumRows) and o.columns == self.columns
+                and o.numRows == self.numRows and o.frequencies(raw=True) == self.frequencies(raw=True))
+
+    __hash__ = None
+
+    def __repr__(self):
+        s = self.summary()
+        return "FrequenciesAndNumRows(columns=%s, groups=%d, numRows=%d)" % (
+            ",".join(self.columns), s.num_groups, s.num_rows)

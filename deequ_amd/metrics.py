@@ -134,3 +134,53 @@ def metric_from_failure(error: BaseException, name: str, instance: str,
 def empty_state_exception(analyzer) -> EmptyStateException:
     """Analyzers.emptyStateException (Analyzer.scala:444-446)."""
     return EmptyStateException("Empty state for analyzer %s, all input values were NULL." % analyzer)
+
+
+@dataclass(frozen=True)
+class DistributionValue:
+    """DistributionValue(absolute, ratio) (metrics/HistogramMetric.scala:21)."""
+    absolute: int
+    ratio: float
+
+
+@dataclass(frozen=True)
+class Distribution:
+    """Distribution(values, numberOfBins) (metrics/HistogramMetric.scala:23-36)."""
+    values: Any  # Dict[str, DistributionValue]
+    numberOfBins: int
+
+    def __getitem__(self, key: str) -> DistributionValue:
+        return self.values[key]
+
+    def argmax(self) -> str:
+        return max(self.values.items(), key=lambda kv: kv[1].absolute)[0]
+
+    def __hash__(self):
+        return hash((tuple(sorted(self.values.items())), self.numberOfBins))
+
+
+@dataclass(frozen=True)
+class HistogramMetric:
+    """HistogramMetric(column, value: Try[Distribution]) (metrics/HistogramMetric.scala:38-64)."""
+    column: str
+    value: Try
+
+    entity = Entity.Column
+    name = "Histogram"
+
+    @property
+    def instance(self) -> str:
+        return self.column
+
+    def flatten(self):
+        if not self.value.isSuccess:
+            return [DoubleMetric(self.entity, "%s.bins" % self.name, self.instance, self.value)]
+        dist = self.value.get()
+        out = [DoubleMetric(self.entity, "%s.bins" % self.name, self.instance,
+                            Success(float(dist.numberOfBins)))]
+        for key, dv in dist.values.items():
+            out.append(DoubleMetric(self.entity, "%s.abs.%s" % (self.name, key), self.instance,
+                                    Success(float(dv.absolute))))
+            out.append(DoubleMetric(self.entity, "%s.ratio.%s" % (self.name, key), self.instance,
+                                    Success(dv.ratio)))
+        return out

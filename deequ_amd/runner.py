@@ -111,10 +111,40 @@ class AnalysisRunner:
         return AnalyzerContext(OrderedDict((a, ctx.metricMap[a]) for a in analyzers if a in ctx.metricMap))
 
     @staticmethod
+    def _runGroupingAnalyzers(data, analyzers, aggregateWith, saveStatesWith) -> AnalyzerContext:
+        """One GPU group-by per sorted grouping-column set (AnalysisRunner.scala:172-186,
+        259-287), metrics of all analyzers of that grouping from the one table (:480-548)."""
+        from .frequencies import compute_frequencies
+        from .states import merge
+        groups = OrderedDict()
+        for a in analyzers:
+            groups.setdefault(tuple(sorted(a.groupingColumns())), []).append(a)
+        results = OrderedDict()
+        for cols, group in groups.items():
+            try:
+                state = compute_frequencies(data, list(cols))
+                if aggregateWith is not None:
+                    state = merge(state, aggregateWith.load(group[0]))
+            except Exception as e:  # noqa: BLE001 - the group-by itself failed
+                for a in group:
+                    results[a] = a.toFailureMetric(e)
+                continue
+            for a in group:
+                try:
+                    results[a] = a.computeMetricFrom(state)
+                except Exception as e:  # noqa: BLE001 (:517-520, :528-531)
+                    results[a] = a.toFailureMetric(e)
+            if saveStatesWith is not None:
+                saveStatesWith.persist(group[0], state)
+        return AnalyzerContext(results)
+
+    @staticmethod
     def _runScanningAnalyzers(data, analyzers, aggregateWith, saveStatesWith) -> AnalyzerContext:
+        from .analyzers import GroupingAnalyzer
         from .engine import op_spec_for, op_supported, run_scan
         shareable = [a for a in analyzers if isinstance(a, ScanShareableAnalyzer)]
-        others = [a for a in analyzers if not isinstance(a, ScanShareableAnalyzer)]
+        grouping = [a for a in analyzers if isinstance(a, GroupingAnalyzer)]
+        others = [a for a in analyzers if not isinstance(a, (ScanShareableAnalyzer, GroupingAnalyzer))]
         results = OrderedDict()
         # GPU eligibility is decided per analyzer at plan time (the reference's JNI shim
         # would leave an ineligible analyzer on Spark; here it becomes a failure metric)
@@ -136,6 +166,9 @@ class AnalysisRunner:
             except Exception as e:  # noqa: BLE001 - the whole pass fails (:320-323)
                 for a in eligible:
                     results[a] = a.toFailureMetric(e)
+        if grouping:
+            results.update(AnalysisRunner._runGroupingAnalyzers(
+                data, grouping, aggregateWith, saveStatesWith).metricMap)
         for a in others:
             results[a] = a.calculate(data, aggregateWith, saveStatesWith)
         return AnalyzerContext(results)

@@ -43,7 +43,8 @@ typedef enum dq_status {
   DQ_ERR_UNSUPPORTED = 2,  /* op/type/predicate not on the GPU path: route it to Spark   */
   DQ_ERR_DEVICE = 3,       /* HIP runtime failure or no usable gfx950 device             */
   DQ_ERR_OOM = 4,          /* device allocation failed                                   */
-  DQ_ERR_STATE = 5         /* call out of order (e.g. consume after finish without reset)*/
+  DQ_ERR_STATE = 5,        /* call out of order (e.g. consume after finish without reset)*/
+  DQ_ERR_SPACE = 6         /* caller's output buffer too small: required sizes returned  */
 } dq_status;
 
 /* ---------------------------------------------------------------- column types */
@@ -217,6 +218,62 @@ void dq_hll_words_from_bytes(const uint8_t in[416], int64_t words[DQ_HLL_NUM_WOR
 
 /* Spark 2.2.2 XxHash64Function with seed 42 for one value (host reference, used by tests). */
 uint64_t dq_xxh64(const void* data, size_t len, uint64_t seed);
+
+/* ---------------------------------------------------------------- frequency group-by
+ * Replaces FrequencyBasedAnalyzer.computeFrequencies (GroupingAnalyzers.scala:53-80) and the
+ * group-by of Histogram (Histogram.scala:54-69).  A dq_freq is the device-resident state
+ * FrequenciesAndNumRows(frequencies, numRows) (GroupingAnalyzers.scala:124-157): consuming a
+ * batch groups its rows (rows with a NULL grouping value are dropped, numRows counts every
+ * row); importing groups is FrequenciesAndNumRows.sum (outer join adding counts).
+ *
+ * Group keys are exchanged in an encoded form: fixed-width columns as little-endian value bytes
+ * (1 B bool/int8, 2 B int16, 4 B int32/float32, 8 B int64/float64; floats as raw bits), strings
+ * as UTF-8 bytes; with several grouping columns the parts are concatenated in column order and
+ * every string part is prefixed with its u32 length.  With DQ_FREQ_NULL_AS_KEY (Histogram), a
+ * NULL string is the key "NullValue" and a NULL of any other type is the empty key. */
+typedef struct dq_freq dq_freq;
+
+#define DQ_FREQ_NULL_AS_KEY 0x1
+
+typedef struct dq_freq_summary {
+  int64_t num_rows;      /* FrequenciesAndNumRows.numRows: every consumed row          */
+  int64_t num_groups;    /* number of groups (CountDistinct, Distinctness numerator)   */
+  int64_t num_unique;    /* groups with count == 1 (Uniqueness numerator)              */
+  int64_t grouped_rows;  /* sum of the group counts                                    */
+  double entropy;        /* sum over groups of -(c/num_rows) ln(c/num_rows)            */
+} dq_freq_summary;
+
+typedef struct dq_freq_group {
+  int64_t count;
+  int64_t key_offset;    /* into the caller's key byte buffer                         */
+  int32_t key_len;
+  int32_t reserved;
+} dq_freq_group;
+
+dq_status dq_freq_create(dq_ctx* ctx, const int32_t* key_columns, int n_keys,
+                         const int32_t* column_types, int n_columns, int flags, dq_freq** out);
+dq_status dq_freq_destroy(dq_freq* f);
+dq_status dq_freq_reset(dq_freq* f);
+dq_status dq_freq_consume(dq_freq* f, const dq_column* columns, int n_columns, int64_t n_rows);
+dq_status dq_freq_get_summary(dq_freq* f, dq_freq_summary* out);
+/* Number of groups and total encoded key bytes (to size dq_freq_export's buffers). */
+dq_status dq_freq_size(dq_freq* f, int64_t* n_groups, int64_t* key_bytes);
+/* Every group, in an unspecified order. */
+dq_status dq_freq_export(dq_freq* f, dq_freq_group* groups, int64_t max_groups, uint8_t* key_bytes,
+                         int64_t key_cap, int64_t* n_out);
+/* The most frequent groups for Histogram's top-maxDetailBins (Histogram.scala:79): every group
+ * whose count is at least the n-th largest count -- all ties at the cut included, so the caller
+ * can apply its own tie order (Spark's rdd.top breaks ties arbitrarily) -- sorted by count
+ * descending, then encoded key ascending.  *n_out / *key_bytes_out receive the sizes; when they
+ * exceed max_groups / key_cap nothing is written and DQ_ERR_SPACE is returned. */
+dq_status dq_freq_top(dq_freq* f, int n, dq_freq_group* groups, int64_t max_groups, uint8_t* key_bytes,
+                      int64_t key_cap, int64_t* n_out, int64_t* key_bytes_out);
+/* dst += src on the device (FrequenciesAndNumRows.sum, GroupingAnalyzers.scala:128-148): both
+ * tables on one device, grouping the same key types; src is unchanged. */
+dq_status dq_freq_merge(dq_freq* dst, dq_freq* src);
+/* Merge groups (and `num_rows`) into the table: FrequenciesAndNumRows.sum. */
+dq_status dq_freq_import(dq_freq* f, const dq_freq_group* groups, int64_t n, const uint8_t* key_bytes,
+                         int64_t num_rows);
 
 #ifdef __cplusplus
 }

@@ -944,12 +944,13 @@ def frequencies_state(table: OTable, columns: Sequence[str]) -> FrequenciesAndNu
 
 
 def _group_key(v, dtype):
-    if dtype in _FRACTIONAL:
-        v = float(v)
-        if v != v:
-            return "NaN"  # Spark groups all NaNs together
-        if v == 0.0:
-            return 0.0  # -0.0 and 0.0 group together
+    """Spark 2.2.2 groups by the UnsafeRow bytes of the key: floating keys group by their raw
+    bits (-0.0 and 0.0 are different groups; float normalisation only arrived in Spark 3.0,
+    SPARK-26021).  Python floats carry the bits, so the bit pattern is the group key."""
+    if dtype == "float64":
+        return ("f64bits", struct.unpack("<Q", struct.pack("<d", float(v)))[0])
+    if dtype == "float32":
+        return ("f32bits", struct.unpack("<I", struct.pack("<f", float(v)))[0])
     return v
 
 
@@ -970,8 +971,33 @@ def count_distinct_metric(state: FrequenciesAndNumRows) -> float:
 
 
 def unique_value_ratio_metric(state: FrequenciesAndNumRows) -> float:
+    """`UniqueValueRatio.scala:28-37`: with no groups the numerator sum is NULL and
+    `Row.getDouble` throws -- a failure metric, signalled here by ValueError."""
+    if not state.frequencies:
+        raise ValueError("Value at index 0 is null")
     uniq = sum(1.0 for c in state.frequencies.values() if c == 1)
-    return uniq / float(len(state.frequencies)) if state.frequencies else float("nan")
+    return uniq / float(len(state.frequencies))
+
+
+def mutual_information_metric(state: FrequenciesAndNumRows, columns: Sequence[str],
+                              grouping: Sequence[str]) -> Optional[float]:
+    """`MutualInformation.scala:34-84`: joint counts joined with both marginals, summing
+    (pxy/N)·ln((pxy/N)/((px/N)(py/N))).  None (empty state) when there are no groups.
+    `grouping` is the state's key column order."""
+    if not state.frequencies:
+        return None
+    i1, i2 = grouping.index(columns[0]), grouping.index(columns[1])
+    m1: Dict = {}
+    m2: Dict = {}
+    for k, c in state.frequencies.items():
+        m1[k[i1]] = m1.get(k[i1], 0) + c
+        m2[k[i2]] = m2.get(k[i2], 0) + c
+    total = state.num_rows
+    out = 0.0
+    for k, c in state.frequencies.items():
+        px, py, pxy = float(m1[k[i1]]), float(m2[k[i2]]), float(c)
+        out += (pxy / total) * math.log((pxy / total) / ((px / total) * (py / total)))
+    return out
 
 
 def entropy_metric(state: FrequenciesAndNumRows, ordered_counts: Optional[Sequence[int]] = None):
@@ -994,10 +1020,12 @@ def entropy_exact(state: FrequenciesAndNumRows) -> Optional[float]:
     return math.fsum(-(c / n) * math.log(c / n) for c in state.frequencies.values())
 
 
-def java_double_to_string(d: float) -> str:
-    """Java `Double.toString` (shortest-repr digits; the JDK 19+ rule, identical to JDK 8
-    for the values in the reference tests)."""
-    from decimal import Decimal
+def java_double_to_string(d: float, single: bool = False) -> str:
+    """Java `Double.toString` / `Float.toString` (`single`): the shortest decimal that
+    rounds back to the value (when that has one digit, the closest decimal of at most two
+    digits, e.g. 4.9E-324), plain for 1e-3 <= |d| < 1e7, else `d.dddE±n`.  The JDK 19+
+    rule; older JDKs agree on the values the reference tests use."""
+    import numpy as np
     if d != d:
         return "NaN"
     if d == math.inf:
@@ -1007,9 +1035,21 @@ def java_double_to_string(d: float) -> str:
     if d == 0.0:
         return "-0.0" if math.copysign(1.0, d) < 0 else "0.0"
     a = abs(d)
-    t = Decimal(repr(a)).normalize().as_tuple()
-    digits = "".join(map(str, t.digits))
-    point = len(digits) + t.exponent  # digits before the decimal point
+    to_bin = (lambda x: float(np.float32(x))) if single else float
+    # shortest round-trip digit string, searched by precision (independent of repr())
+    for prec in range(1, 18):
+        cand = "%.*e" % (prec - 1, a) if not single else \
+            np.format_float_scientific(np.float32(a), precision=prec - 1, unique=False)
+        if to_bin(float(cand)) == a:
+            break
+    mant, exp = cand.lower().split("e")
+    digits = mant.replace(".", "").rstrip("0") or "0"
+    e10 = int(exp)
+    if len(digits) == 1:
+        two = "%.1e" % a if not single else np.format_float_scientific(np.float32(a), precision=1, unique=False)
+        m2, x2 = two.lower().split("e")
+        digits, e10 = m2.replace(".", "").rstrip("0") or "0", int(x2)  # closest 2-digit decimal
+    point = e10 + 1
     sign = "-" if d < 0 else ""
     if 1e-3 <= a < 1e7:
         if point <= 0:
@@ -1019,7 +1059,7 @@ def java_double_to_string(d: float) -> str:
         else:
             body = digits[:point] + "." + digits[point:]
         return sign + body
-    return sign + digits[0] + "." + (digits[1:] or "0") + "E" + str(point - 1)
+    return sign + digits[0] + "." + (digits[1:] or "0") + "E" + str(e10)
 
 
 def histogram_state(table: OTable, column: str) -> FrequenciesAndNumRows:
@@ -1037,7 +1077,7 @@ def _spark_cast_string(v, dtype):
     if dtype in _INTEGRAL:
         return str(int(v))
     if dtype in _FRACTIONAL:
-        return java_double_to_string(float(v)) if dtype == "float64" else java_double_to_string(float(v))
+        return java_double_to_string(float(v), single=(dtype == "float32"))
     if dtype == "bool":
         return "true" if v else "false"
     return str(v)

@@ -84,12 +84,20 @@ TABLES = {
         "priority": ["string", ["low", "high"]],
         "numViews": ["int64", [10, 12]],
     },
+    # getDfWithConditionallyUninformativeColumns (:226-233)
+    "dfUninformative": {
+        "att1": ["int32", [1, 2, 3]],
+        "att2": ["int32", [0, 0, 0]],
+    },
     # getDfEmpty (:26-33)
     "dfEmpty": {"column1": ["string", []], "column2": ["string", []]},
 }
 
 A = "analyzers/AnalyzerTests.scala"
 EMPTY = "empty"  # the metric is a Failure(EmptyStateException)
+H_FULL = -(0.75 * math.log(0.75) + 0.25 * math.log(0.25))  # AnalyzerTests.scala:135-136
+NH = T + "analyzers/NullHandlingTests.scala"
+INC = T + "analyzers/IncrementalAnalyzerTest.scala"
 
 CASES = [
     # (id, table, analyzer, args, expected, source)
@@ -133,6 +141,38 @@ CASES = [
     ("incr_completeness_delta", "incrDelta", "Completeness", ["att1"], 0.5, T + "analyzers/IncrementalAnalyzerTest.scala:93"),
     ("empty_size", "dfEmpty", "Size", [], 0.0, T + "analyzers/runners/AnalysisRunnerTests.scala (Size of an empty frame is 0)"),
     ("empty_completeness", "dfEmpty", "Completeness", ["column1"], EMPTY, T + "analyzers/NullHandlingTests.scala (sum over zero rows is NULL)"),
+    # ---- frequency family (GroupingAnalyzers.scala and the analyzers built on it)
+    ("uniq_missing_att1", "dfMissing", "Uniqueness", [["att1"]], 0.0, T + A + ":83-84"),
+    ("uniq_missing_att2", "dfMissing", "Uniqueness", [["att2"]], 0.0, T + A + ":85-86"),
+    ("uniq_full_att1", "dfFull", "Uniqueness", [["att1"]], 0.25, T + A + ":89-90"),
+    ("uniq_full_att2", "dfFull", "Uniqueness", [["att2"]], 0.25, T + A + ":91-92"),
+    ("uniq_unique", "dfUnique", "Uniqueness", [["unique"]], 1.0, T + A + ":98-99"),
+    ("uniq_unique_with_nulls", "dfUnique", "Uniqueness", [["uniqueWithNulls"]], 5 / 6.0, T + A + ":100-101"),
+    ("uniq_multi_unique_nonunique", "dfUnique", "Uniqueness", [["unique", "nonUnique"]], 1.0, T + A + ":102-103"),
+    ("uniq_multi_with_nulls", "dfUnique", "Uniqueness", [["unique", "nonUniqueWithNulls"]], 3 / 6.0, T + A + ":104-106"),
+    ("uniq_multi_only_unique", "dfUnique", "Uniqueness", [["nonUnique", "onlyUniqueWithOtherNonUnique"]], 1.0, T + A + ":107-109"),
+    ("entropy_att1", "dfFull", "Entropy", ["att1"], H_FULL, T + A + ":133-136"),
+    ("entropy_att2", "dfFull", "Entropy", ["att2"], H_FULL, T + A + ":137-139"),
+    ("mi_full", "dfFull", "MutualInformation", [["att1", "att2"]], H_FULL, T + A + ":148-152"),
+    ("mi_uninformative", "dfUninformative", "MutualInformation", [["att1", "att2"]], 0.0, T + A + ":154-157"),
+    ("mi_same_column", "dfFull", "MutualInformation", [["att1", "att1"]], H_FULL, T + A + ":159-168 (== Entropy(att1))"),
+    ("countdistinct_unique_with_nulls", "dfUnique", "CountDistinct", [["uniqueWithNulls"]], 5.0, T + A + ":560-565"),
+    ("countdistinct_att1", "dfNumeric", "CountDistinct", [["att1"]], 6.0, T + "analyzers/AnalysisTest.scala:80,93-94"),
+    ("distinctness_item", "dfFull", "Distinctness", [["item"]], 1.0, T + "analyzers/AnalysisTest.scala:38,49"),
+    ("uniq_full_multi", "dfFull", "Uniqueness", [["att1", "att2"]], 0.25, T + "analyzers/AnalysisTest.scala:40,51"),
+    ("distinctness_att1", "dfFull", "Distinctness", [["att1"]], 0.5, T + "repository/AnalysisResultSerdeTest.scala:202,229-230"),
+    ("null_countdistinct", "dfNullColumns", "CountDistinct", [["stringCol"]], 0.0, NH + ":117"),
+    ("null_entropy", "dfNullColumns", "Entropy", ["stringCol"], EMPTY, NH + ":121"),
+    ("null_mi", "dfNullColumns", "MutualInformation", [["numericCol", "numericCol2"]], EMPTY, NH + ":122"),
+    ("null_mi3", "dfNullColumns", "MutualInformation", [["numericCol", "numericCol3"]], EMPTY, NH + ":123"),
+    ("incr_uniq_initial", "incrInitial", "Uniqueness", [["att1"]], 0.6666666666666666, INC + ":121"),
+    ("incr_uniq_delta", "incrDelta", "Uniqueness", [["att1"]], 0.5, INC + ":122"),
+    ("incr_uniq_multi_initial", "incrInitial", "Uniqueness", [["att1", "count"]], 0.6666666666666666, INC + ":143"),
+    ("incr_uniq_multi_delta", "incrDelta", "Uniqueness", [["att1", "count"]], 0.5, INC + ":144"),
+    # Histogram: expected = number of bins + the reported keys (or only their number)
+    ("hist_missing", "dfMissing", "Histogram", ["att1"], {"bins": 3, "keys": ["NullValue", "a", "b"]}, T + A + ":203-215"),
+    ("hist_numeric", "dfNumeric", "Histogram", ["att2"], {"bins": 4, "n_values": 4}, T + A + ":217-227"),
+    ("hist_top2", "dfMissing", "Histogram", ["att1", None, 2], {"bins": 3, "keys": ["NullValue", "a"]}, T + A + ":249-261"),
 ]
 
 # Known answers that need the union of two tables (state merge == union):
@@ -145,6 +185,8 @@ MERGE_CASES = [
     ("incr_size_merged", "incrInitial", "incrDelta", "Size", [], 5.0, T + "analyzers/IncrementalAnalyzerTest.scala:47"),
     ("incr_compliance_merged", "incrInitial", "incrDelta", "Compliance", ["att1", "att1 = 'b'"], 0.4, T + "analyzers/IncrementalAnalyzerTest.scala:75"),
     ("incr_completeness_merged", "incrInitial", "incrDelta", "Completeness", ["att1"], 0.6, T + "analyzers/IncrementalAnalyzerTest.scala:94"),
+    ("incr_uniq_merged", "incrInitial", "incrDelta", "Uniqueness", [["att1"]], 0.2, INC + ":123"),
+    ("incr_uniq_multi_merged", "incrInitial", "incrDelta", "Uniqueness", [["att1", "count"]], 0.2, INC + ":145"),
 ]
 
 

@@ -33,7 +33,19 @@ def product_analyzer(name: str, args: List):
     return getattr(d, name)(*args)
 
 
+FREQ_ANALYZERS = ("Uniqueness", "Distinctness", "CountDistinct", "UniqueValueRatio", "Entropy",
+                  "MutualInformation")
+
+
+def _columns(args) -> List[str]:
+    return [args[0]] if isinstance(args[0], str) else list(args[0])
+
+
 def oracle_state(name: str, args: List, table: O.OTable):
+    if name in FREQ_ANALYZERS:
+        return O.frequencies_state(table, _columns(args))
+    if name == "Histogram":
+        return O.histogram_state(table, args[0])
     if name == "Size":
         return O.size_state(table, *args)
     if name == "Compliance":
@@ -44,8 +56,33 @@ def oracle_state(name: str, args: List, table: O.OTable):
     return fn(table, *args)
 
 
-def oracle_metric(state) -> object:
+def oracle_metric(state, name: str = None, args: List = None) -> object:
+    """The metric the reference would report: a float, "empty" (EmptyStateException),
+    "failure" (another failure) or, for Histogram, {"bins", "values"}."""
+    if name in FREQ_ANALYZERS:
+        try:
+            v = {"Uniqueness": O.uniqueness_metric, "Distinctness": O.distinctness_metric,
+                 "CountDistinct": O.count_distinct_metric, "UniqueValueRatio": O.unique_value_ratio_metric,
+                 "Entropy": O.entropy_metric}[name](state) if name != "MutualInformation" else \
+                O.mutual_information_metric(state, _columns(args), _columns(args))
+        except ValueError:
+            return "failure"
+        return "empty" if v is None else v
+    if name == "Histogram":
+        h = O.histogram_metric(state, *([args[2]] if len(args) > 2 else []))
+        return {"bins": h["number_of_bins"], "values": h["values"]}
     return "empty" if state is None else state.metric_value()
+
+
+def histogram_matches(got: dict, expected: dict) -> bool:
+    """Known-answer histogram expectations: bins plus the key set or the number of values."""
+    if got["bins"] != expected["bins"]:
+        return False
+    if "keys" in expected and sorted(got["values"]) != sorted(expected["keys"]):
+        return False
+    if "n_values" in expected and len(got["values"]) != expected["n_values"]:
+        return False
+    return True
 
 
 def random_table(rng: np.random.Generator, n: int, null_frac: float, dtypes=None):

@@ -7,7 +7,7 @@ import pytest
 import deequ_amd as d
 from deequ_amd.metrics import EmptyStateException, Failure, Success
 from deequ_amd.states import merge
-from helpers import known_answers, product_analyzer, product_table
+from helpers import histogram_matches, known_answers, product_analyzer, product_table
 
 pytestmark = pytest.mark.gpu
 
@@ -15,6 +15,12 @@ KA = known_answers()
 
 
 def _check(metric, expected, source):
+    if isinstance(expected, dict):  # Histogram
+        assert metric.value.isSuccess, (source, metric)
+        dist = metric.value.get()
+        got = {"bins": dist.numberOfBins, "values": dist.values}
+        assert histogram_matches(got, expected), (source, got)
+        return
     if expected == "empty":
         assert isinstance(metric.value, Failure), (source, metric)
         assert isinstance(metric.value.exception, EmptyStateException), (source, metric)
