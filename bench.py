@@ -39,6 +39,13 @@ def parse_args():
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, nproc)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4"],
+                   help="c2 = the headline scan (default); c3 = HLL on 64 columns; c4 = group-by")
+    p.add_argument("--c3-columns", type=int, default=64)
+    p.add_argument("--c3-rows", type=int, default=125_000_000, help="rows per GPU (one batch)")
+    p.add_argument("--c4-rows", type=int, default=1_000_000_000, help="rows per GPU")
+    p.add_argument("--c4-batch", type=int, default=125_000_000, help="rows per string batch")
+    p.add_argument("--c4-distinct", type=int, default=201_500_000)
     return p.parse_args()
 
 
@@ -109,6 +116,171 @@ def cpu_baseline(sample_rows: int, threads: int):
                       % (sample_rows, threads, secs)}
 
 
+# ----------------------------------------------------------------------------- secondary workloads
+def _valid_bits(m: int, gen, dev, null_frac: float):
+    import torch
+    shifts = (2 ** torch.arange(8, device=dev, dtype=torch.int32)).to(torch.int32)
+    bits = torch.rand(m, generator=gen, device=dev) >= null_frac
+    pad = (-m) % 8
+    if pad:
+        bits = torch.cat([bits, torch.zeros(pad, dtype=torch.bool, device=dev)])
+    return (bits.view(-1, 8).to(torch.int32) * shifts).sum(1).to(torch.uint8)
+
+
+def make_c3_table(rows: int, n_cols: int, rank: int, device: int):
+    """C3: int64 uniform over the 64-bit range (~all distinct), 5% NULL, HBM."""
+    import torch
+    import deequ_amd as d
+    dev = torch.device("cuda", device)
+    gen = torch.Generator(device=dev)
+    chunk = 1 << 26
+    cols = {}
+    for k in range(n_cols):
+        gen.manual_seed(7000 + 1000 * rank + k)
+        vals = torch.empty(rows, dtype=torch.int64, device=dev)
+        valid = torch.empty((rows + 7) // 8 + 64, dtype=torch.uint8, device=dev)
+        for s in range(0, rows, chunk):
+            e = min(rows, s + chunk)
+            vals[s:e].random_(-2 ** 63, 2 ** 63 - 1, generator=gen)
+            packed = _valid_bits(e - s, gen, dev, 0.05)
+            valid[s // 8: s // 8 + packed.numel()] = packed
+        cols["h%d" % k] = d.Column("int64", rows, vals, valid, device=True)
+    torch.cuda.synchronize(dev)
+    return d.Table(cols)
+
+
+def make_c4_batches(rows: int, batch: int, distinct: int, rank: int, device: int):
+    """C4: a string key = 12-digit zero-padded decimal of a uniform int in [0, distinct), 1% NULL,
+    as Arrow utf8 batches of `batch` rows (int32 offsets cap one batch at 2 GiB of chars)."""
+    import torch
+    import deequ_amd as d
+    dev = torch.device("cuda", device)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(7 + 1000 * rank)
+    pow10 = torch.tensor([10 ** (11 - i) for i in range(12)], dtype=torch.int64, device=dev)
+    parts = []
+    for b0 in range(0, rows, batch):
+        m = min(batch, rows - b0)
+        chars = torch.empty(m * 12 + 16, dtype=torch.uint8, device=dev)
+        valid = torch.empty((m + 7) // 8 + 64, dtype=torch.uint8, device=dev)
+        sub = 1 << 24
+        for s in range(0, m, sub):
+            e = min(m, s + sub)
+            keys = torch.randint(0, distinct, (e - s,), generator=gen, device=dev, dtype=torch.int64)
+            digits = (keys[:, None] // pow10[None, :]) % 10 + 48
+            chars[s * 12: e * 12] = digits.to(torch.uint8).reshape(-1)
+            packed = _valid_bits(e - s, gen, dev, 0.01)
+            valid[s // 8: s // 8 + packed.numel()] = packed
+        offsets = torch.arange(0, 12 * (m + 1), 12, dtype=torch.int32, device=dev)
+        parts.append(d.Table({"key": d.Column("string", m, chars, valid, offsets=offsets, device=True)}))
+    torch.cuda.synchronize(dev)
+    return d.PartitionedTable(parts)
+
+
+def run_c3(args, world, rank, local):
+    """HLL++ ApproxCountDistinct on C3 columns: one fused dq_plan, HIP events on its stream."""
+    import torch
+    import deequ_amd as d
+    from deequ_amd.distributed import allgather_merge
+    from deequ_amd.engine import Plan, op_spec_for
+    table = make_c3_table(args.c3_rows, args.c3_columns, rank, local)
+    analyzers = [d.ApproxCountDistinct(c) for c in table.schema]
+    plan = Plan([op_spec_for(a, table.schema) for a in analyzers], table.schema, device=local)
+    stream = torch.cuda.ExternalStream(plan.stream, device=torch.device("cuda", local))
+
+    def step(ev=None):
+        plan.reset()
+        if ev is not None:
+            ev[0].record(stream)
+        plan.consume(table)
+        if ev is not None:
+            ev[1].record(stream)
+        raw = plan.finish_raw()
+        if world > 1:
+            raw = allgather_merge(raw, len(analyzers), device=local)
+        return raw
+    elapsed, kernel_ms, raw = _timed(args, world, step)
+    est = d.ApproxCountDistinctState(list(raw[0].words)).metricValue()
+    rows_total = args.c3_rows * world * args.steps
+    bpr = args.c3_columns * (8 + 1.0 / 8)
+    achieved = bpr * args.c3_rows / (kernel_ms * 1e-3) / 1e9
+    return {
+        "metric": "rows/sec & HBM GB/s for ApproxCountDistinct HLL++ (C3)", "value": rows_total / elapsed,
+        "unit": "rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int64 (XXH64)",
+        "data": "synthetic int64 uniform over 2^64, 5% NULL, generated in HBM",
+        "config": {"workload": "C3: %d rows/GPU x %d int64 columns, one HLL plan (one batch of the "
+                               "1B-row stream)" % (args.c3_rows, args.c3_columns),
+                   "rows_per_gpu": args.c3_rows, "columns": args.c3_columns},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel_ms": kernel_ms,
+                     "algorithmic_bytes_per_launch": bpr * args.c3_rows},
+        "check": {"column0_estimate": est, "rows_column0": args.c3_rows},
+    }
+
+
+def run_c4(args, world, rank, local):
+    """Uniqueness/Distinctness/Entropy/CountDistinct (one GPU group-by) + Histogram on C4."""
+    import torch
+    import deequ_amd as d
+    if world > 1:
+        raise SystemExit("c4 runs on one GPU (the key-hash all-to-all is a separate path)")
+    data = make_c4_batches(args.c4_rows, args.c4_batch, args.c4_distinct, rank, local)
+    analyzers = [d.Uniqueness(["key"]), d.Distinctness(["key"]), d.Entropy("key"),
+                 d.CountDistinct(["key"]), d.Histogram("key")]
+
+    def step(ev=None):
+        ctx = d.AnalysisRunner.onData(data).addAnalyzers(analyzers).run()
+        return ctx
+    elapsed, _, ctx = _timed(args, world, step)
+    metrics = {str(a): ctx.metric(a).value.get() for a in analyzers[:4]}
+    hist = ctx.metric(analyzers[4]).value.get()
+    in_bytes = args.c4_rows * (4 + 12 + 1.0 / 8)
+    step_s = elapsed / args.steps
+    return {
+        "metric": "rows/sec for the frequency family (C4 group-by)", "value": args.c4_rows * args.steps / elapsed,
+        "unit": "rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "utf8 keys, int64 counts",
+        "data": "synthetic 12-digit keys uniform in [0, %d), 1%% NULL, generated in HBM" % args.c4_distinct,
+        "config": {"workload": "C4: %d rows/GPU in %d-row utf8 batches; 4 frequency analyzers (one "
+                               "group-by) + Histogram (its own group-by)" % (args.c4_rows, args.c4_batch)},
+        "input_gbs_per_pass": 2 * in_bytes / step_s / 1e9,
+        "check": dict(metrics, histogram_bins=hist.numberOfBins),
+    }
+
+
+def _timed(args, world, step):
+    """W warmup steps, then K timed steps between barriers + device syncs; max over ranks."""
+    import torch
+    import torch.distributed as dist
+    out = None
+    for _ in range(args.warmup):
+        out = step()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        out = step(events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    try:
+        kernel_ms = sum(a.elapsed_time(b) for a, b in events) / len(events)
+    except (RuntimeError, ValueError):  # the step did not record the events
+        kernel_ms = None
+    return elapsed, kernel_ms, out
+
+
 def main():
     args = parse_args()
     import torch
@@ -126,6 +298,13 @@ def main():
     d.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.workload != "c2":
+        result = (run_c3 if args.workload == "c3" else run_c4)(args, world, rank, local)
+        if rank == 0:
+            print(json.dumps(result))
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     table = make_c2_table(args.rows, rank, local)
     analyzers = c2_analyzers()

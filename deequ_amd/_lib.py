@@ -67,6 +67,10 @@ class DqFreqSummary(Structure):
                 ("grouped_rows", c_int64), ("entropy", c_double)]
 
 
+class DqFreqWire(Structure):
+    _fields_ = [("ctrl", c_uint64), ("count", c_int64), ("k0", c_uint64), ("k1", c_uint64)]
+
+
 class DqFreqGroup(Structure):
     _fields_ = [("count", c_int64), ("key_offset", c_int64), ("key_len", c_int32),
                 ("reserved", c_int32)]
@@ -106,6 +110,13 @@ SIGNATURES = {
                             POINTER(c_int64), POINTER(c_int64)]),
     "dq_freq_merge": (c_int, [c_void_p, c_void_p]),
     "dq_freq_import": (c_int, [c_void_p, POINTER(DqFreqGroup), c_int64, c_void_p, c_int64]),
+    "dq_freq_partition": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_void_p, c_int64, POINTER(c_int64),
+                                  POINTER(c_int64)]),
+    "dq_freq_import_wire": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_int64]),
+    "dq_freq_count_histogram": (c_int, [c_void_p, POINTER(c_int64), c_int64, POINTER(c_int64), c_int64,
+                                        POINTER(c_int64)]),
+    "dq_freq_summary_from_histogram": (c_int, [POINTER(c_int64), c_int64, POINTER(c_int64), c_int64, c_int64,
+                                               POINTER(DqFreqSummary)]),
 }
 
 _lib = None

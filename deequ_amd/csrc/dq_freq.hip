@@ -420,18 +420,66 @@ __global__ __launch_bounds__(kBlock) void dq_freq_export_kernel(FreqTable T, uns
 __global__ __launch_bounds__(kBlock) void dq_freq_import_kernel(FreqTable T, FreqIn in) {
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < in.n; i += (uint64_t)gridDim.x * kBlock) {
     Key k;
-    k.len = (uint32_t)(in.ctrl[i] & kLenMask);
-    if (in.ctrl[i] & kHeapKey) {
-      k.ptr = in.heap + in.k0[i];
+    const uint64_t j = i * in.stride;
+    k.len = (uint32_t)(in.ctrl[j] & kLenMask);
+    if (in.ctrl[j] & kHeapKey) {
+      k.ptr = in.heap + in.k0[j];
       k.k0 = k.k1 = 0;
       k.hash = xxh64_any(k.ptr, k.len, 42);
     } else {
       k.ptr = nullptr;
-      k.k0 = in.k0[i];
-      k.k1 = in.k1[i];
+      k.k0 = in.k0[j];
+      k.k1 = in.k1[j];
       k.hash = hash_inline(k.k0, k.k1, k.len);
     }
-    if (!global_insert(T, k, in.count[i])) return;
+    if (!global_insert(T, k, in.count[j])) return;
+  }
+}
+
+// ---- multi-GPU key-hash partitioning (owner = a function of hash bits the table does not use
+// for its slot index, so every owner's keys still spread over its whole table)
+__device__ inline uint32_t freq_owner(uint64_t h, uint32_t n_parts) {
+  return (uint32_t)(((uint64_t)(uint32_t)(h >> 16) * n_parts) >> 32);
+}
+
+__device__ inline uint64_t slot_hash(const FreqTable& T, const FreqSlot& e, uint32_t len) {
+  return (e.ctrl & kHeapKey) ? xxh64_any(T.heap + e.k0, len, 42) : hash_inline(e.k0, e.k1, len);
+}
+
+__global__ __launch_bounds__(kBlock) void dq_freq_part_count_kernel(FreqTable T, int n_parts,
+                                                                    unsigned long long* cnt) {
+  const uint64_t n = T.mask + 1;
+  for (uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x; s < n; s += (uint64_t)gridDim.x * kBlock) {
+    const FreqSlot e = T.slots[s];  // launch boundary: every insert is visible
+    if (!(e.ctrl & kReady)) continue;
+    const uint32_t len = (uint32_t)(e.ctrl & kLenMask);
+    const uint32_t p = freq_owner(slot_hash(T, e, len), (uint32_t)n_parts);
+    atomicAdd(&cnt[2 * p], 1ull);
+    if (e.ctrl & kHeapKey) atomicAdd(&cnt[2 * p + 1], ((unsigned long long)len + 7ull) & ~7ull);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void dq_freq_part_scatter_kernel(FreqTable T, int n_parts,
+                                                                      const unsigned long long* base,
+                                                                      unsigned long long* cursor,
+                                                                      FreqSlot* out, uint8_t* keys) {
+  const uint64_t n = T.mask + 1;
+  for (uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x; s < n; s += (uint64_t)gridDim.x * kBlock) {
+    FreqSlot e = T.slots[s];
+    if (!(e.ctrl & kReady)) continue;
+    const uint32_t len = (uint32_t)(e.ctrl & kLenMask);
+    const uint32_t p = freq_owner(slot_hash(T, e, len), (uint32_t)n_parts);
+    const unsigned long long i = atomicAdd(&cursor[2 * p], 1ull);
+    if (e.ctrl & kHeapKey) {
+      const unsigned long long bytes = ((unsigned long long)len + 7ull) & ~7ull;
+      const unsigned long long off = atomicAdd(&cursor[2 * p + 1], bytes);  // within part p's region
+      const uint64_t* src = reinterpret_cast<const uint64_t*>(T.heap + e.k0);
+      uint64_t* dst = reinterpret_cast<uint64_t*>(keys + base[2 * p + 1] + off);
+      for (unsigned long long w = 0; w < bytes / 8; ++w) dst[w] = src[w];
+      e.k0 = off;
+    }
+    e.ctrl &= ~kReady;  // wire form: READY is a table-internal flag
+    out[base[2 * p] + i] = e;
   }
 }
 
@@ -455,6 +503,27 @@ __global__ __launch_bounds__(kBlock) void dq_freq_rehash_kernel(const FreqSlot* 
       slot = (slot + 1) & T.mask;
     }
   }
+}
+
+static unsigned slot_blocks(const FreqTable& T) {
+  const uint64_t n = T.mask + 1;
+  uint64_t blocks = (n + kBlock * 16 - 1) / (kBlock * 16);
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  return (unsigned)blocks;
+}
+
+hipError_t launch_freq_part_count(const FreqTable& T, int n_parts, unsigned long long* d_cnt, hipStream_t stream) {
+  hipLaunchKernelGGL(dq_freq_part_count_kernel, dim3(slot_blocks(T)), dim3(kBlock), 0, stream, T, n_parts, d_cnt);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_part_scatter(const FreqTable& T, int n_parts, const unsigned long long* d_base,
+                                    unsigned long long* d_cursor, FreqSlot* out_groups, uint8_t* out_keys,
+                                    hipStream_t stream) {
+  hipLaunchKernelGGL(dq_freq_part_scatter_kernel, dim3(slot_blocks(T)), dim3(kBlock), 0, stream, T, n_parts,
+                     d_base, d_cursor, out_groups, out_keys);
+  return hipGetLastError();
 }
 
 hipError_t launch_freq_rehash(const FreqSlot* d_old, uint64_t old_n, const FreqTable& T, hipStream_t stream) {

@@ -165,6 +165,7 @@ struct FreqIn {  // groups to merge in; heap offsets in k0 refer to `heap`
   const unsigned long long* k1;
   const uint8_t* heap;
   uint64_t n;
+  uint64_t stride;  // elements between consecutive groups: 1 = separate arrays, 4 = FreqSlot records
 };
 
 hipError_t launch_freq_insert(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
@@ -176,6 +177,13 @@ hipError_t launch_freq_export(const FreqTable& T, unsigned long long min_count, 
 hipError_t launch_freq_import(const FreqTable& T, const FreqIn& in, hipStream_t stream);
 hipError_t launch_freq_heap_need(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
                                  unsigned long long* d_need, hipStream_t stream);
+// Multi-GPU key-hash exchange: owner rank of a group = freq_owner(hash, n_parts).  `d_cnt` gets
+// per part {groups, long-key bytes}; the scatter writes part p's groups (FreqSlot records, k0 of
+// a long key = offset in the part's key region) from d_base[2p] / d_base[2p+1] on.
+hipError_t launch_freq_part_count(const FreqTable& T, int n_parts, unsigned long long* d_cnt, hipStream_t stream);
+hipError_t launch_freq_part_scatter(const FreqTable& T, int n_parts, const unsigned long long* d_base,
+                                    unsigned long long* d_cursor, FreqSlot* out_groups, uint8_t* out_keys,
+                                    hipStream_t stream);
 hipError_t launch_freq_rehash(const FreqSlot* d_old, uint64_t old_n, const FreqTable& T, hipStream_t stream);
 
 // ---------------------------------------------------------------- launchers (.hip files)

@@ -48,3 +48,161 @@ def allgather_merge(states, n_ops: int, group=None, device: Optional[int] = None
             acc = merge_raw(acc, L.DqState.from_buffer_copy(blobs[r], i * STATE_BYTES))
         out[i] = acc
     return out
+
+
+# ---------------------------------------------------------------- frequency family
+# The one real exchange step of the path.  Spark shuffles partial group counts by
+# key hash into `spark.sql.shuffle.partitions` and finishes the aggregate per partition
+# (GroupingAnalyzers.scala:67-72).  Here every rank groups its own row shard on its GPU, then:
+#   1. partitions its table by owner rank (dq_freq_partition, a device scatter),
+#   2. exchanges the partitions with ONE all-to-all of 32-B wire groups (+ one for long-key
+#      bytes) -- RCCL over xGMI with the nccl backend, gloo on host copies otherwise,
+#   3. merges what it received into the table of the keys it owns (dq_freq_import_wire).
+# Owners then hold disjoint keys: the metrics need only an all-reduce of the count-of-counts
+# histograms (integers, exact), and Histogram's top-N an all-gather of per-owner top-N.
+
+def _comm_device(group):
+    import torch
+    import torch.distributed as dist
+    return "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+
+
+def _to(t, device):
+    return t if t.device.type == device.type else t.to(device)
+
+
+def exchange_frequencies(table, group=None):
+    """Key-hash all-to-all of a local FrequencyTable; returns the table of the keys this rank
+    owns (numRows 0: the global numRows is the all-reduce of the local ones)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    dev = table.torch_device
+    comm = dev if _comm_device(group) == "cuda" else torch.device("cpu")
+    W = table.WIRE_BYTES
+    part_g, part_k = table.partition_sizes(world)
+    send_g = torch.empty(max(1, sum(part_g)) * W, dtype=torch.uint8, device=dev)
+    send_k = torch.empty(max(8, sum(part_k)), dtype=torch.uint8, device=dev)
+    if sum(part_g):
+        table.partition_into(world, send_g, send_k)
+    sizes = torch.tensor([[g, k] for g, k in zip(part_g, part_k)], dtype=torch.int64).reshape(-1).to(comm)
+    recv_sizes = torch.empty_like(sizes)
+    dist.all_to_all_single(recv_sizes, sizes, group=group)
+    recv = recv_sizes.cpu().reshape(world, 2).tolist()
+    in_g, out_g = [g * W for g in part_g], [r[0] * W for r in recv]
+    in_k, out_k = list(part_k), [r[1] for r in recv]
+    recv_g = torch.empty(max(W, sum(out_g)), dtype=torch.uint8, device=comm)
+    recv_k = torch.empty(max(8, sum(out_k)), dtype=torch.uint8, device=comm)
+    sg = _to(send_g, comm)
+    sk = _to(send_k, comm)
+    dist.all_to_all_single(recv_g[:sum(out_g)], sg[:sum(in_g)], out_g, in_g, group=group)
+    dist.all_to_all_single(recv_k[:sum(out_k)], sk[:sum(in_k)], out_k, in_k, group=group)
+    if comm.type == "cuda":
+        torch.cuda.current_stream(dev).synchronize()  # the library reads them on its own stream
+    recv_g, recv_k = _to(recv_g, dev), _to(recv_k, dev)
+    owned = type(table).like(table)
+    og = ok = 0
+    for s in range(world):
+        n = recv[s][0]
+        if n:
+            owned.import_wire(recv_g[og:og + n * W], n, recv_k[ok:ok + max(1, recv[s][1])], recv[s][1], 0)
+        og += n * W
+        ok += recv[s][1]
+    return owned
+
+
+class DistributedFrequencies:
+    """FrequenciesAndNumRows of the union of every rank's rows (GroupingAnalyzers.scala:124-157),
+    held as the keys each rank owns after the exchange.  Collective: every rank calls the same
+    methods in the same order."""
+
+    def __init__(self, owned, num_rows: int, group=None):
+        self.owned = owned
+        self.group = group
+        self._num_rows = int(num_rows)
+        self._summary = None
+        self.table = _DistributedTableView(self)
+
+    @property
+    def columns(self):
+        return self.owned.key_columns
+
+    @property
+    def numRows(self) -> int:
+        return self._num_rows
+
+    def summary(self):
+        if self._summary is None:
+            import torch
+            import torch.distributed as dist
+            from .frequencies import summary_from_histogram
+            hist, big = self.owned.count_histogram()
+            comm = _comm_device(self.group)
+            h = torch.from_numpy(hist).to(self.owned.torch_device if comm == "cuda" else "cpu")
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
+            bigs = [None] * dist.get_world_size(self.group)
+            dist.all_gather_object(bigs, big.tolist(), group=self.group)
+            all_big = np.array(sorted(c for b in bigs for c in b), dtype=np.int64)
+            self._summary = summary_from_histogram(h.cpu().numpy(), all_big, self._num_rows)
+        return self._summary
+
+    def frequencies(self, raw: bool = False):
+        """Every group (gathered on every rank; for small tables / tests)."""
+        import torch.distributed as dist
+        from .frequencies import decode_key
+        counts, keys = self.owned.export()
+        parts = [None] * dist.get_world_size(self.group)
+        dist.all_gather_object(parts, (counts.tolist(), keys), group=self.group)
+        out = {}
+        for cs, ks in parts:
+            for c, k in zip(cs, ks):
+                out[k if raw else decode_key(k, self.owned.dtypes, self.owned.histogram)] = c
+        return out
+
+
+class _DistributedTableView:
+    """What Histogram.computeMetricFrom reads from `state.table`: dtypes and top(n)."""
+
+    def __init__(self, state: DistributedFrequencies):
+        self._s = state
+        self.dtypes = state.owned.dtypes
+        self.key_columns = state.owned.key_columns
+        self.histogram = state.owned.histogram
+
+    def top(self, n: int):
+        """Union of every owner's top-n (owners hold disjoint keys), cut at the n-th largest
+        count with the ties kept -- the contract of FrequencyTable.top."""
+        import torch.distributed as dist
+        counts, keys = self._s.owned.top(n)
+        parts = [None] * dist.get_world_size(self._s.group)
+        dist.all_gather_object(parts, (counts.tolist(), keys), group=self._s.group)
+        items = sorted(((c, k) for cs, ks in parts for c, k in zip(cs, ks)), key=lambda ck: (-ck[0], ck[1]))
+        if len(items) > n:
+            cut = items[n - 1][0]
+            items = [ck for ck in items if ck[0] >= cut]
+        return np.array([c for c, _ in items], dtype=np.int64), [k for _, k in items]
+
+    def export(self):
+        fr = self._s.frequencies(raw=True)
+        return np.array(list(fr.values()), dtype=np.int64), list(fr.keys())
+
+
+def compute_frequencies_distributed(data, grouping_columns, histogram: bool = False, group=None,
+                                    table_factory=None):
+    """FrequencyBasedAnalyzer.computeFrequencies over the union of every rank's shard `data`."""
+    import torch
+    import torch.distributed as dist
+    from .frequencies import FrequencyTable
+    make = table_factory or FrequencyTable
+    schema = data.schema
+    local = make(grouping_columns, {c: schema[c] for c in schema}, histogram)
+    for batch in data.batches():
+        local.consume(batch)
+    n_local = local.summary().num_rows
+    owned = exchange_frequencies(local, group)
+    local.close()
+    n = torch.tensor([n_local], dtype=torch.int64)
+    if _comm_device(group) == "cuda":
+        n = n.to(owned.torch_device)
+    dist.all_reduce(n, op=dist.ReduceOp.SUM, group=group)
+    return DistributedFrequencies(owned, int(n.item()), group)

@@ -160,6 +160,51 @@ class FrequencyTable:
         buf = ctypes.create_string_buffer(blob, max(1, len(blob)))
         L.check(L.lib().dq_freq_import(self.handle, groups, n, buf, int(num_rows)))
 
+    # ---- multi-GPU key-hash exchange (deequ_amd/distributed.py)
+    WIRE_BYTES = 32  # sizeof(dq_freq_wire)
+
+    def partition_sizes(self, n_parts: int) -> Tuple[List[int], List[int]]:
+        """Groups and long-key bytes per owner part (dq_freq_partition sizing call)."""
+        pg, pk = (ctypes.c_int64 * n_parts)(), (ctypes.c_int64 * n_parts)()
+        st = L.lib().dq_freq_partition(self.handle, n_parts, None, 0, None, 0, pg, pk)
+        if st not in (L.DQ_OK, L.DQ_ERR_SPACE):
+            L.check(st)
+        return list(pg), list(pk)
+
+    def partition_into(self, n_parts: int, groups, keys) -> Tuple[List[int], List[int]]:
+        """Scatter the groups by owner into device byte tensors `groups` (32 B per group) and
+        `keys` (long-key bytes), both on this table's GPU."""
+        pg, pk = (ctypes.c_int64 * n_parts)(), (ctypes.c_int64 * n_parts)()
+        L.check(L.lib().dq_freq_partition(self.handle, n_parts, groups.data_ptr(), groups.numel() // self.WIRE_BYTES,
+                                          keys.data_ptr(), keys.numel(), pg, pk))
+        return list(pg), list(pk)
+
+    def import_wire(self, groups, n: int, keys, key_bytes: int, num_rows: int = 0) -> None:
+        """Merge `n` wire groups held in device tensors (one sender's part) into this table."""
+        L.check(L.lib().dq_freq_import_wire(self.handle, groups.data_ptr(), n, keys.data_ptr(), key_bytes,
+                                            int(num_rows)))
+
+    def count_histogram(self, n_bins: int = 1 << 16) -> Tuple[np.ndarray, np.ndarray]:
+        """(hist[c] = #groups with count c for c < n_bins, sorted counts >= n_bins)."""
+        hist = np.zeros(n_bins, dtype=np.int64)
+        cap = 16
+        while True:
+            big = np.zeros(cap, dtype=np.int64)
+            n_big = ctypes.c_int64()
+            st = L.lib().dq_freq_count_histogram(
+                self.handle, hist.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), n_bins,
+                big.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap, ctypes.byref(n_big))
+            if st == L.DQ_ERR_SPACE:
+                cap = max(cap * 2, n_big.value)
+                continue
+            L.check(st)
+            return hist, big[:n_big.value].copy()
+
+    @property
+    def torch_device(self):
+        import torch
+        return torch.device("cuda", self.device)
+
     def merge_from(self, other: "FrequencyTable") -> None:
         """self += other, device to device."""
         L.check(L.lib().dq_freq_merge(self.handle, other.handle))
@@ -192,6 +237,19 @@ def compute_frequencies(data, grouping_columns: Sequence[str], histogram: bool =
     for batch in data.batches():
         table.consume(batch)
     return FrequenciesAndNumRows(table)
+
+
+def summary_from_histogram(hist: np.ndarray, big: np.ndarray, num_rows: int) -> L.DqFreqSummary:
+    """dq_freq_summary of a (summed) count-of-counts histogram: the same fixed-order arithmetic
+    as a single table's summary, so sharded and whole-table metrics agree bit for bit."""
+    hist = np.ascontiguousarray(hist, dtype=np.int64)
+    big = np.ascontiguousarray(np.sort(np.asarray(big, dtype=np.int64)))
+    out = L.DqFreqSummary()
+    L.check(L.lib().dq_freq_summary_from_histogram(
+        hist.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), len(hist),
+        big.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)) if len(big) else None, len(big), int(num_rows),
+        ctypes.byref(out)))
+    return out
 
 
 # ---------------------------------------------------------------- the state

@@ -275,6 +275,39 @@ dq_status dq_freq_merge(dq_freq* dst, dq_freq* src);
 dq_status dq_freq_import(dq_freq* f, const dq_freq_group* groups, int64_t n, const uint8_t* key_bytes,
                          int64_t num_rows);
 
+/* ---------------------------------------------------------------- multi-GPU key-hash exchange
+ * The frequency family's one real exchange step: Spark shuffles the partial
+ * group counts by key hash into spark.sql.shuffle.partitions before the final aggregate
+ * (GroupingAnalyzers.scala:67-72).  Here every rank partitions its local table by owner rank
+ * (a hash of the encoded key), the ranks exchange the partitions with one all-to-all (RCCL over
+ * xGMI), and every owner merges what it receives with dq_freq_import_wire -- after which the
+ * owners hold disjoint keys, and their count-of-counts histograms add up to the global one. */
+typedef struct dq_freq_wire {  /* one group in device memory (32 B)                         */
+  uint64_t ctrl;               /* key length (low 24 bits) | 1 << 30 if the key is in key bytes */
+  int64_t count;
+  uint64_t k0, k1;             /* key bytes (<= 16 B, little-endian), or k0 = key-byte offset  */
+} dq_freq_wire;
+
+/* Write every group of `f`, partitioned by owner (0 .. n_parts-1), into DEVICE buffers on f's
+ * GPU: part p's groups follow parts 0..p-1 in d_groups, its long keys (8-byte padded) follow
+ * theirs in d_key_bytes, with k0 relative to the start of part p's key region.  part_groups /
+ * part_key_bytes (host, n_parts each) receive the sizes; if the buffers are too small nothing is
+ * written and DQ_ERR_SPACE is returned (call once with max_groups = 0 to size them). */
+dq_status dq_freq_partition(dq_freq* f, int n_parts, dq_freq_wire* d_groups, int64_t max_groups,
+                            uint8_t* d_key_bytes, int64_t key_cap, int64_t* part_groups,
+                            int64_t* part_key_bytes);
+/* Merge groups held in DEVICE memory (one sender's part) into f; num_rows is added to numRows. */
+dq_status dq_freq_import_wire(dq_freq* f, const dq_freq_wire* d_groups, int64_t n,
+                              const uint8_t* d_key_bytes, int64_t key_bytes, int64_t num_rows);
+/* Count-of-counts of f: hist[c] = number of groups with count c (1 <= c < n_bins, hist[0] = 0);
+ * counts >= n_bins go to big[] ascending (*n_big; DQ_ERR_SPACE if big_cap is too small). */
+dq_status dq_freq_count_histogram(dq_freq* f, int64_t* hist, int64_t n_bins, int64_t* big,
+                                  int64_t big_cap, int64_t* n_big);
+/* The dq_freq_summary of a (summed) count-of-counts histogram and numRows, with the same fixed
+ * summation order as dq_freq_get_summary. */
+dq_status dq_freq_summary_from_histogram(const int64_t* hist, int64_t n_bins, const int64_t* big,
+                                         int64_t n_big, int64_t num_rows, dq_freq_summary* out);
+
 #ifdef __cplusplus
 }
 #endif

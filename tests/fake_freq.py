@@ -1,0 +1,117 @@
+"""Host stand-in for deequ_amd.frequencies.FrequencyTable, used ONLY by the CPU (gloo) tests of
+the multi-rank exchange orchestration (deequ_amd/distributed.py): same methods, same 32-B wire
+format, groups kept in a dict.  The GPU tests run the same orchestration on the real table."""
+import struct
+from typing import Dict, List, Tuple
+
+import numpy as np
+import torch
+
+from deequ_amd.frequencies import encode_key
+
+HEAP = 1 << 30
+
+
+class FakeFrequencyTable:
+    WIRE_BYTES = 32
+
+    def __init__(self, key_columns, schema, histogram=False, device=None):
+        self.key_columns = list(key_columns)
+        self.schema = dict(schema)
+        self.dtypes = [self.schema[c] for c in self.key_columns]
+        self.histogram = histogram
+        self.groups: Dict[bytes, int] = {}
+        self.num_rows = 0
+
+    @classmethod
+    def like(cls, other):
+        return cls(other.key_columns, {c: t for c, t in zip(other.key_columns, other.dtypes)}, other.histogram)
+
+    @property
+    def torch_device(self):
+        return torch.device("cpu")
+
+    def consume(self, batch):
+        cols = [batch.columns[c].to_pylist() for c in self.key_columns]
+        for row in zip(*cols):
+            self.num_rows += 1
+            if not self.histogram and any(v is None for v in row):
+                continue
+            k = encode_key(row, self.dtypes, self.histogram)
+            self.groups[k] = self.groups.get(k, 0) + 1
+
+    def summary(self):
+        class S:
+            pass
+        s = S()
+        s.num_rows = self.num_rows
+        return s
+
+    @staticmethod
+    def _owner(key: bytes, n: int) -> int:
+        return (sum(key) * 2654435761 + len(key)) % n
+
+    def _parts(self, n):
+        parts = [[] for _ in range(n)]
+        for k in sorted(self.groups):
+            parts[self._owner(k, n)].append(k)
+        return parts
+
+    def partition_sizes(self, n) -> Tuple[List[int], List[int]]:
+        parts = self._parts(n)
+        return [len(p) for p in parts], [sum((len(k) + 7) // 8 * 8 for k in p if len(k) > 16) for p in parts]
+
+    def partition_into(self, n, groups, keys):
+        g = groups.numpy()
+        kb = keys.numpy()
+        gi, ko = 0, 0
+        for p in self._parts(n):
+            base = ko
+            for k in p:
+                if len(k) <= 16:
+                    pad = k + b"\0" * (16 - len(k))
+                    rec = struct.pack("<Qq", len(k), self.groups[k]) + pad
+                else:
+                    off = ko - base
+                    kb[ko:ko + len(k)] = np.frombuffer(k, dtype=np.uint8)
+                    ko += (len(k) + 7) // 8 * 8
+                    rec = struct.pack("<QqQQ", HEAP | len(k), self.groups[k], off, 0)
+                g[gi * 32:(gi + 1) * 32] = np.frombuffer(rec, dtype=np.uint8)
+                gi += 1
+        return self.partition_sizes(n)
+
+    def import_wire(self, groups, n, keys, key_bytes, num_rows=0):
+        g = bytes(groups.numpy()[:n * 32])
+        kb = bytes(keys.numpy()[:key_bytes])
+        self.num_rows += num_rows
+        for i in range(n):
+            ctrl, cnt, k0, k1 = struct.unpack_from("<QqQQ", g, i * 32)
+            ln = ctrl & ((1 << 24) - 1)
+            if ctrl & HEAP:
+                k = kb[k0:k0 + ln]
+            else:
+                k = (struct.pack("<QQ", k0, k1))[:ln]
+            self.groups[k] = self.groups.get(k, 0) + cnt
+
+    def count_histogram(self, n_bins=1 << 16):
+        hist = np.zeros(n_bins, dtype=np.int64)
+        big = []
+        for c in self.groups.values():
+            if c < n_bins:
+                hist[c] += 1
+            else:
+                big.append(c)
+        return hist, np.array(sorted(big), dtype=np.int64)
+
+    def top(self, n):
+        items = sorted(self.groups.items(), key=lambda kv: (-kv[1], kv[0]))
+        if len(items) > n:
+            cut = items[n - 1][1]
+            items = [kv for kv in items if kv[1] >= cut]
+        return np.array([c for _, c in items], dtype=np.int64), [k for k, _ in items]
+
+    def export(self):
+        return np.array(list(self.groups.values()), dtype=np.int64), list(self.groups.keys())
+
+    def close(self):
+        pass
