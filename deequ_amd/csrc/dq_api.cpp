@@ -340,7 +340,7 @@ static int fast_form(const Program& prog, const int32_t* types, FastPred* fp) {
 }
 
 // ------------------------------------------------------------------------------ plan
-enum Target { TGT_HOST_SIZE = 0, TGT_SCAN = 1, TGT_HLL = 2 };
+enum Target { TGT_HOST_SIZE = 0, TGT_SCAN = 1, TGT_HLL = 2, TGT_DTYPE = 3 };
 
 struct OpSlot {
   int kind;
@@ -382,10 +382,11 @@ struct dq_plan : Stager {
   std::vector<ScanTask> scan_tasks;
   std::vector<ScanGroup> groups;
   std::vector<HllTask> hll_tasks;
+  std::vector<HllTask> dtype_tasks;  // DataType: {column, type, where}
   std::vector<Program> programs;  // generic predicate programs -> batch masks
   // device state
   DevBuf d_tasks, d_groups, d_ranges, d_hll, d_progs, d_insns, d_pool, d_acc, d_partials, d_regs,
-      d_cols, d_masks, d_mask_words;
+      d_cols, d_masks, d_mask_words, d_dtype, d_dtype_counts;
   int64_t mask_words = 0;
   // pinned descriptor staging (DevColumn + DevMask arrays) guarded by an event
   void* h_desc = nullptr;
@@ -423,6 +424,7 @@ static dq_status check_op(const dq_op& op, const int32_t* types, int n_cols) {
       DQ_TRY(need_col(true));
       break;
     case DQ_OP_APPROX_COUNT_DISTINCT: DQ_TRY(need_col(false)); break;
+    case DQ_OP_DATATYPE: DQ_TRY(need_col(false)); break;
     default: return fail(DQ_ERR_UNSUPPORTED, "unknown op kind " + std::to_string(op.kind));
   }
   if (op.where.code && op.where.n_insns > 0)
@@ -561,6 +563,20 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
         slot.task = t;
         break;
       }
+      case DQ_OP_DATATYPE: {
+        plan->col_used[op.column] = true;
+        slot.target = TGT_DTYPE;
+        int t = -1;
+        for (size_t k = 0; k < plan->dtype_tasks.size(); ++k)
+          if (plan->dtype_tasks[k].column == op.column && plan->dtype_tasks[k].where_mask == where_prog)
+            t = (int)k;
+        if (t < 0) {
+          plan->dtype_tasks.push_back(HllTask{op.column, column_types[op.column], where_prog, 0});
+          t = (int)plan->dtype_tasks.size() - 1;
+        }
+        slot.task = t;
+        break;
+      }
       default: st = fail(DQ_ERR_UNSUPPORTED, "unknown op kind");
     }
     plan->slots.push_back(slot);
@@ -618,6 +634,8 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
       (s = upload(plan->d_groups, group_ids.data(), group_ids.size() * sizeof(int32_t))) != DQ_OK ||
       (s = plan->d_ranges.ensure(std::max<size_t>(1, plan->scan_tasks.size()) * sizeof(PartRange))) != DQ_OK ||
       (s = upload(plan->d_hll, plan->hll_tasks.data(), plan->hll_tasks.size() * sizeof(HllTask))) != DQ_OK ||
+      (s = upload(plan->d_dtype, plan->dtype_tasks.data(), plan->dtype_tasks.size() * sizeof(HllTask))) != DQ_OK ||
+      (s = plan->d_dtype_counts.ensure(std::max<size_t>(1, plan->dtype_tasks.size()) * 5 * sizeof(uint64_t))) != DQ_OK ||
       (s = upload(plan->d_progs, progs.data(), progs.size() * sizeof(PredProgram))) != DQ_OK ||
       (s = upload(plan->d_insns, insns.data(), insns.size() * sizeof(PredInsn))) != DQ_OK ||
       (s = upload(plan->d_pool, pool.data(), pool.size())) != DQ_OK ||
@@ -665,6 +683,8 @@ extern "C" dq_status dq_plan_reset(dq_plan* plan) {
   DQ_HIP(launch_init_acc(static_cast<ScanAcc*>(plan->d_acc.ptr), (int)plan->scan_tasks.size(), plan->stream));
   if (!plan->hll_tasks.empty())
     DQ_HIP(hipMemsetAsync(plan->d_regs.ptr, 0, plan->hll_tasks.size() * kHllM * sizeof(uint32_t), plan->stream));
+  if (!plan->dtype_tasks.empty())
+    DQ_HIP(hipMemsetAsync(plan->d_dtype_counts.ptr, 0, plan->dtype_tasks.size() * 5 * sizeof(uint64_t), plan->stream));
   DQ_HIP(hipStreamSynchronize(plan->stream));
   plan->total_rows = 0;
   return DQ_OK;
@@ -872,6 +892,13 @@ extern "C" dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, in
     DQ_HIP(launch_hll(static_cast<const HllTask*>(plan->d_hll.ptr), n_hll, d_cols, d_masks, n_rows, (int)bpt,
                       static_cast<uint32_t*>(plan->d_regs.ptr), plan->stream));
   }
+  const int n_dt = (int)plan->dtype_tasks.size();
+  if (n_dt > 0) {
+    int64_t bpt = std::max<int64_t>(1, plan->target_blocks / n_dt);
+    bpt = std::min<int64_t>(bpt, (n_rows + kBlock - 1) / kBlock);
+    DQ_HIP(launch_datatype(static_cast<const HllTask*>(plan->d_dtype.ptr), n_dt, d_cols, d_masks, n_rows, (int)bpt,
+                           static_cast<unsigned long long*>(plan->d_dtype_counts.ptr), plan->stream));
+  }
   plan->total_rows += n_rows;
   if (any_host) {  // caller's host buffers may be released once we return
     DQ_HIP(hipStreamSynchronize(plan->stream));
@@ -904,6 +931,10 @@ extern "C" dq_status dq_plan_finish(dq_plan* plan, dq_state* out, int n_out) {
   DQ_HIP(hipSetDevice(plan->ctx->device));
   std::vector<ScanAcc> acc(plan->scan_tasks.size());
   std::vector<uint32_t> regs(plan->hll_tasks.size() * kHllM);
+  std::vector<uint64_t> dtc(plan->dtype_tasks.size() * 5);
+  if (!dtc.empty())
+    DQ_HIP(hipMemcpyAsync(dtc.data(), plan->d_dtype_counts.ptr, dtc.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                          plan->stream));
   if (!acc.empty())
     DQ_HIP(hipMemcpyAsync(acc.data(), plan->d_acc.ptr, acc.size() * sizeof(ScanAcc), hipMemcpyDeviceToHost, plan->stream));
   if (!regs.empty())
@@ -921,6 +952,11 @@ extern "C" dq_status dq_plan_finish(dq_plan* plan, dq_state* out, int n_out) {
     if (s.target == TGT_HOST_SIZE) {  // count(*) is never NULL
       o.has_value = 1;
       o.num_matches = rows;
+      continue;
+    }
+    if (s.target == TGT_DTYPE) {  // the StatefulDataType UDAF never returns NULL
+      o.has_value = 1;
+      for (int k = 0; k < 5; ++k) o.words[k] = (int64_t)dtc[(size_t)s.task * 5 + k];
       continue;
     }
     if (s.target == TGT_HLL) {  // never NULL (StatefulHyperloglogPlus.nullable = false)
@@ -1163,6 +1199,9 @@ extern "C" dq_status dq_state_merge(const dq_state* a, const dq_state* b, dq_sta
     case DQ_OP_MINIMUM: r.value = java_min(a->value, b->value); break;  // Minimum.scala:27-29
     case DQ_OP_MAXIMUM: r.value = java_max(a->value, b->value); break;  // Maximum.scala:27-29
     case DQ_OP_APPROX_COUNT_DISTINCT: dq_hll_merge(a->words, b->words, r.words); break;
+    case DQ_OP_DATATYPE:  // DataTypeHistogram.sum (DataType.scala:48-51)
+      for (int k = 0; k < 5; ++k) r.words[k] = (int64_t)((uint64_t)a->words[k] + (uint64_t)b->words[k]);
+      break;
     default: return fail(DQ_ERR_INVALID, "unknown state kind");
   }
   *out = r;
@@ -1186,6 +1225,43 @@ extern "C" dq_status dq_state_metric(const dq_state* s, double* out) {
     case DQ_OP_APPROX_COUNT_DISTINCT: *out = dq_hll_count(s->words); break;
     default: return fail(DQ_ERR_INVALID, "unknown state kind");
   }
+  return DQ_OK;
+}
+
+// ------------------------------------------------------------------------------ casts
+extern "C" dq_status dq_cast_utf8(dq_ctx* ctx, const dq_column* src, int64_t n_rows, int32_t to_type,
+                                  void* d_values, uint8_t* d_validity, int64_t* n_unsupported) {
+  if (!ctx || !src || !n_unsupported || (n_rows > 0 && (!d_values || !d_validity)))
+    return fail(DQ_ERR_INVALID, "NULL argument");
+  if (src->type != DQ_T_UTF8) return fail(DQ_ERR_INVALID, "dq_cast_utf8 needs a utf8 column");
+  if (to_type != DQ_T_INT64 && to_type != DQ_T_FLOAT64) return fail(DQ_ERR_UNSUPPORTED, "cast target must be int64 or float64");
+  if (n_rows < 0 || src->length < n_rows) return fail(DQ_ERR_INVALID, "bad n_rows");
+  *n_unsupported = 0;
+  if (n_rows == 0) return DQ_OK;
+  DQ_HIP(hipSetDevice(ctx->device));
+  Stager st;
+  DQ_HIP(hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking));
+  st.col_types.assign(1, DQ_T_UTF8);
+  st.stage_values.resize(1);
+  st.stage_validity.resize(1);
+  st.stage_offsets.resize(1);
+  DevColumn dc;
+  DevBuf d_unsup;
+  dq_status s = prepare_column(&st, 0, *src, n_rows, &dc);
+  if (s == DQ_OK) s = d_unsup.ensure(sizeof(unsigned long long));
+  unsigned long long h_unsup = 0;
+  hipError_t e = hipSuccess;
+  if (s == DQ_OK) e = hipMemsetAsync(d_unsup.ptr, 0, sizeof(unsigned long long), st.stream);
+  if (s == DQ_OK && e == hipSuccess)
+    e = launch_cast_utf8(dc, n_rows, to_type, d_values, d_validity, static_cast<unsigned long long*>(d_unsup.ptr), st.stream);
+  if (s == DQ_OK && e == hipSuccess)
+    e = hipMemcpyAsync(&h_unsup, d_unsup.ptr, sizeof(h_unsup), hipMemcpyDeviceToHost, st.stream);
+  if (s == DQ_OK && e == hipSuccess) e = hipStreamSynchronize(st.stream);
+  (void)hipStreamSynchronize(st.stream);
+  (void)hipStreamDestroy(st.stream);
+  if (s != DQ_OK) return s;
+  if (e != hipSuccess) return fail(DQ_ERR_DEVICE, std::string("dq_cast_utf8: ") + hipGetErrorString(e));
+  *n_unsupported = (int64_t)h_unsup;
   return DQ_OK;
 }
 

@@ -207,6 +207,11 @@ hipError_t launch_predicates(const PredProgram* d_progs, int n_progs, const Pred
 hipError_t launch_realign_bitmap(const uint8_t* src, int64_t bit_offset, int64_t n_bits,
                                  uint8_t* dst, hipStream_t stream);
 hipError_t launch_init_acc(ScanAcc* d_acc, int n, hipStream_t stream);
+// DataType (dq_profile.hip): tasks reuse HllTask {column, type, where}; 5 u64 counts per task.
+hipError_t launch_datatype(const HllTask* d_tasks, int n_tasks, const DevColumn* d_cols, const DevMask* d_masks,
+                           int64_t n_rows, int blocks_per_task, unsigned long long* d_counts, hipStream_t stream);
+hipError_t launch_cast_utf8(const DevColumn& src, int64_t n_rows, int to_type, void* d_values, uint8_t* d_validity,
+                            unsigned long long* d_unsupported, hipStream_t stream);
 
 // ---------------------------------------------------------------- XXH64 (host + device)
 constexpr uint64_t kP1 = 0x9E3779B185EBCA87ull;

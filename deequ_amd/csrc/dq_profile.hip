@@ -1,0 +1,290 @@
+// dq_profile.hip -- kernels for the ColumnProfiler path (ColumnProfiler.scala:220-251, 427-445).
+//
+// 1. DataType (DataType.scala:152-183, catalyst/StatefulDataType.scala:26-83): per row of the
+//    column cast to string, classify it as NULL / Fractional / Integral / Boolean / String with
+//    the reference's anchored regexes, tested in this order:
+//        FRACTIONAL  ^(-|\+)? ?\d*\.\d*$        INTEGRAL  ^(-|\+)? ?\d*$        BOOLEAN  ^(true|false)$
+//    (Java `\d` = [0-9]; Scala's `case R(_)` is a whole-string match.)  On utf8 bytes this is a
+//    five-state DFA; numeric columns are classified from their value, as the string Spark's
+//    Cast would produce (integers -> Integral; a float/double prints plain -- Fractional --
+//    only for 0 and 1e-3 <= |x| < 1e7 and is "NaN"/"Infinity"/scientific -- String --
+//    otherwise; booleans -> Boolean).  The five counts are integers: order independent.
+// 2. Cast(StringType -> LongType / DoubleType) of the columns pass 1 typed as Integral /
+//    Fractional (ColumnProfiler.castNumericStringColumns, :427-445), Spark 2.2.2 semantics:
+//    long = UTF8String.toLong (optional sign, digits, optional '.' + digits truncated, no
+//    whitespace, overflow -> NULL); double = java.lang.Double.parseDouble (whitespace trimmed,
+//    sign, digits, '.', exponent, f/d suffix, NaN/Infinity).  Doubles are produced exactly
+//    (correctly rounded) on the Clinger fast path -- <= 19 significant digits, value < 2^53,
+//    |10-exponent| <= 22 -- and any other well-formed number is counted as "unsupported" so
+//    the caller routes the column to Spark instead of returning an inexact value.
+#include "dq_internal.h"
+
+namespace dq {
+
+namespace {
+
+enum DtPos { DT_NULL = 0, DT_FRACTIONAL = 1, DT_INTEGRAL = 2, DT_BOOLEAN = 3, DT_STRING = 4 };
+
+__device__ inline bool bit_at(const uint8_t* bm, int64_t row) { return (bm[row >> 3] >> (row & 7)) & 1u; }
+
+__device__ int classify_utf8(const uint8_t* p, int32_t n) {
+  // DFA: 0 start, 1 after sign, 2 after the optional space, 3 integer digits, 4 after '.', 5 fail
+  int st = 0;
+  for (int32_t i = 0; i < n && st != 5; ++i) {
+    const uint32_t c = p[i];
+    const bool digit = c - '0' < 10u;
+    switch (st) {
+      case 0: st = (c == '-' || c == '+') ? 1 : c == ' ' ? 2 : digit ? 3 : c == '.' ? 4 : 5; break;
+      case 1: st = c == ' ' ? 2 : digit ? 3 : c == '.' ? 4 : 5; break;
+      case 2: case 3: st = digit ? 3 : c == '.' ? 4 : 5; break;
+      default: st = digit ? 4 : 5; break;
+    }
+  }
+  if (st == 4) return DT_FRACTIONAL;
+  if (st != 5) return DT_INTEGRAL;
+  if (n == 4 && p[0] == 't' && p[1] == 'r' && p[2] == 'u' && p[3] == 'e') return DT_BOOLEAN;
+  if (n == 5 && p[0] == 'f' && p[1] == 'a' && p[2] == 'l' && p[3] == 's' && p[4] == 'e') return DT_BOOLEAN;
+  return DT_STRING;
+}
+
+template <typename F>
+__device__ inline int classify_float(F x) {
+  // Double.toString / Float.toString: plain notation for 1e-3 <= |x| < 1e7 (and 0)
+  if (!(x - x == x - x)) return DT_STRING;  // NaN, +-Infinity
+  const F a = x < 0 ? -x : x;
+  if (a == (F)0 || (a >= (F)1e-3 && a < (F)1e7)) return DT_FRACTIONAL;
+  return DT_STRING;
+}
+
+__device__ int classify_row(const DevColumn& c, int64_t row) {
+  switch (c.type) {
+    case DQ_T_UTF8: {
+      const int32_t b = c.offsets[row], e = c.offsets[row + 1];
+      return classify_utf8(static_cast<const uint8_t*>(c.values) + b, e - b);
+    }
+    case DQ_T_BOOL: return DT_BOOLEAN;
+    case DQ_T_FLOAT32: return classify_float(static_cast<const float*>(c.values)[row]);
+    case DQ_T_FLOAT64: return classify_float(static_cast<const double*>(c.values)[row]);
+    default: return DT_INTEGRAL;  // int8..int64 print as [-]digits
+  }
+}
+
+__device__ inline uint64_t wave_sum(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += (uint64_t)__shfl_down((unsigned long long)v, d, 64);
+  return v;
+}
+
+}  // namespace
+
+// blockIdx.y = task (column, where), blockIdx.x = row chunk; 5 counts per task, atomically
+// added (integers: the result does not depend on the schedule).
+__global__ __launch_bounds__(kBlock) void dq_datatype_kernel(const HllTask* __restrict__ tasks,
+                                                             const DevColumn* __restrict__ cols,
+                                                             const DevMask* __restrict__ masks,
+                                                             int64_t n_rows, unsigned long long* counts) {
+  const HllTask task = tasks[blockIdx.y];
+  const DevColumn& col = cols[task.column];
+  const uint8_t* wt = task.where_mask >= 0 ? reinterpret_cast<const uint8_t*>(masks[task.where_mask].t) : nullptr;
+  const int64_t per_block = (n_rows + gridDim.x - 1) / gridDim.x;
+  const int64_t r0 = (int64_t)blockIdx.x * per_block;
+  const int64_t r1 = min(r0 + per_block, n_rows);
+  uint64_t c[5] = {0, 0, 0, 0, 0};
+  for (int64_t row = r0 + threadIdx.x; row < r1; row += kBlock) {
+    // conditionalSelection: a row whose filter is not TRUE is a NULL input (Analyzer.scala:409-420)
+    const bool valid = (col.validity == nullptr || bit_at(col.validity, row)) && (wt == nullptr || bit_at(wt, row));
+    const int k = valid ? classify_row(col, row) : DT_NULL;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) c[i] += (k == i) ? 1u : 0u;
+  }
+  __shared__ uint64_t part[kBlock / 64][5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const uint64_t s = wave_sum(c[i]);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6][i] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < 5) {
+    uint64_t s = 0;
+    for (int w = 0; w < kBlock / 64; ++w) s += part[w][threadIdx.x];
+    if (s) atomicAdd(&counts[(int64_t)blockIdx.y * 5 + threadIdx.x], (unsigned long long)s);
+  }
+}
+
+namespace {
+
+__device__ inline bool is_java_ws(uint32_t c) { return c <= 0x20u; }  // String.trim()
+
+// UTF8String.toLong (Spark 2.2): [+-]digits[.digits]; the fraction is validated and dropped.
+__device__ bool parse_long(const uint8_t* p, int32_t n, int64_t* out) {
+  if (n == 0) return false;
+  int32_t i = 0;
+  const bool neg = p[0] == '-';
+  if (neg || p[0] == '+') {
+    if (n == 1) return false;
+    i = 1;
+  }
+  const int64_t stop = INT64_MIN / 10;
+  int64_t r = 0;  // accumulated negatively, as the reference does, so INT64_MIN parses
+  for (; i < n; ++i) {
+    const uint32_t b = p[i];
+    if (b == '.') {
+      ++i;
+      break;
+    }
+    if (b - '0' >= 10u) return false;
+    if (r < stop) return false;
+    r = r * 10 - (int64_t)(b - '0');
+    if (r > 0) return false;
+  }
+  for (; i < n; ++i)
+    if ((uint32_t)p[i] - '0' >= 10u) return false;
+  if (!neg) {
+    r = -r;
+    if (r < 0) return false;
+  }
+  *out = r;
+  return true;
+}
+
+// 0 = NULL (NumberFormatException), 1 = value, 2 = well formed but off the exact fast path
+__device__ int parse_double(const uint8_t* p, int32_t n, double* out) {
+  int32_t i = 0, e = n;
+  while (i < e && is_java_ws(p[i])) ++i;
+  while (e > i && is_java_ws(p[e - 1])) --e;
+  if (i == e) return 0;
+  bool neg = false;
+  if (p[i] == '+' || p[i] == '-') {
+    neg = p[i] == '-';
+    ++i;
+  }
+  const int32_t rest = e - i;
+  auto is = [&](const char* w, int32_t len) {
+    if (rest != len) return false;
+    for (int32_t k = 0; k < len; ++k)
+      if (p[i + k] != (uint8_t)w[k]) return false;
+    return true;
+  };
+  if (is("NaN", 3)) {
+    *out = __builtin_nan("");
+    return 1;
+  }
+  if (is("Infinity", 8)) {
+    *out = neg ? -__builtin_huge_val() : __builtin_huge_val();
+    return 1;
+  }
+  if (rest >= 2 && p[i] == '0' && (p[i + 1] == 'x' || p[i + 1] == 'X')) return 2;  // hex float
+  // optional f/F/d/D type suffix
+  if (e > i && (p[e - 1] == 'f' || p[e - 1] == 'F' || p[e - 1] == 'd' || p[e - 1] == 'D')) --e;
+  uint64_t m = 0;
+  int sig = 0, exp10 = 0, ndig = 0;
+  bool dropped = false, dot = false;
+  for (; i < e; ++i) {
+    const uint32_t c = p[i];
+    if (c == '.') {
+      if (dot) return 0;
+      dot = true;
+      continue;
+    }
+    if (c - '0' >= 10u) break;
+    ++ndig;
+    if (m == 0 && c == '0') {  // leading zeros carry no significance
+      if (dot) --exp10;
+      continue;
+    }
+    if (sig < 19) {
+      m = m * 10 + (c - '0');
+      ++sig;
+      if (dot) --exp10;
+    } else {
+      if (c != '0') dropped = true;
+      if (!dot) ++exp10;
+    }
+  }
+  if (ndig == 0) return 0;
+  if (i < e) {  // exponent
+    if (p[i] != 'e' && p[i] != 'E') return 0;
+    ++i;
+    bool eneg = false;
+    if (i < e && (p[i] == '+' || p[i] == '-')) {
+      eneg = p[i] == '-';
+      ++i;
+    }
+    if (i == e) return 0;
+    int64_t x = 0;
+    for (; i < e; ++i) {
+      const uint32_t c = p[i];
+      if (c - '0' >= 10u) return 0;
+      if (x < 100000) x = x * 10 + (c - '0');
+    }
+    exp10 += (int)(eneg ? -x : x);
+  }
+  if (m == 0) {
+    *out = neg ? -0.0 : 0.0;
+    return 1;
+  }
+  if (dropped || m > (1ull << 53) || exp10 < -22 || exp10 > 22) return 2;
+  const double pow10[23] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11,
+                            1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+  double v = (double)m;  // exact: m <= 2^53
+  v = exp10 >= 0 ? v * pow10[exp10] : v / pow10[-exp10];  // one correctly rounded operation
+  *out = neg ? -v : v;
+  return 1;
+}
+
+}  // namespace
+
+// One thread per 8 rows: writes one validity byte and 8 values.
+__global__ __launch_bounds__(kBlock) void dq_cast_utf8_kernel(DevColumn src, int64_t n_rows, int to_type,
+                                                              void* values, uint8_t* validity,
+                                                              unsigned long long* n_unsupported) {
+  const int64_t n_bytes = (n_rows + 7) >> 3;
+  for (int64_t byte = (int64_t)blockIdx.x * kBlock + threadIdx.x; byte < n_bytes;
+       byte += (int64_t)gridDim.x * kBlock) {
+    uint32_t vbits = 0u, unsup = 0u;
+    for (int k = 0; k < 8; ++k) {
+      const int64_t row = byte * 8 + k;
+      if (row >= n_rows) break;
+      int64_t lv = 0;
+      double dv = 0.0;
+      bool ok = false;
+      if (src.validity == nullptr || bit_at(src.validity, row)) {
+        const int32_t b = src.offsets[row], e = src.offsets[row + 1];
+        const uint8_t* p = static_cast<const uint8_t*>(src.values) + b;
+        if (to_type == DQ_T_INT64) {
+          ok = parse_long(p, e - b, &lv);
+        } else {
+          const int r = parse_double(p, e - b, &dv);
+          ok = r == 1;
+          unsup += r == 2;
+        }
+      }
+      vbits |= (ok ? 1u : 0u) << k;
+      if (to_type == DQ_T_INT64) static_cast<int64_t*>(values)[row] = ok ? lv : 0;
+      else static_cast<double*>(values)[row] = ok ? dv : 0.0;
+    }
+    validity[byte] = (uint8_t)vbits;
+    if (unsup) atomicAdd(n_unsupported, (unsigned long long)unsup);
+  }
+}
+
+hipError_t launch_datatype(const HllTask* d_tasks, int n_tasks, const DevColumn* d_cols, const DevMask* d_masks,
+                           int64_t n_rows, int blocks_per_task, unsigned long long* d_counts, hipStream_t stream) {
+  if (n_tasks <= 0 || n_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(dq_datatype_kernel, dim3(blocks_per_task, n_tasks), dim3(kBlock), 0, stream, d_tasks, d_cols,
+                     d_masks, n_rows, d_counts);
+  return hipGetLastError();
+}
+
+hipError_t launch_cast_utf8(const DevColumn& src, int64_t n_rows, int to_type, void* d_values, uint8_t* d_validity,
+                            unsigned long long* d_unsupported, hipStream_t stream) {
+  if (n_rows <= 0) return hipSuccess;
+  const int64_t n_bytes = (n_rows + 7) >> 3;
+  int64_t blocks = (n_bytes + kBlock - 1) / kBlock;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(dq_cast_utf8_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, src, n_rows, to_type,
+                     d_values, d_validity, d_unsupported);
+  return hipGetLastError();
+}
+
+}  // namespace dq

@@ -81,7 +81,8 @@ typedef enum dq_op_kind {
   DQ_OP_STDDEV = 6,                /* StandardDeviation(column, where)  StandardDeviation.scala:47-73 */
   DQ_OP_MINIMUM = 7,               /* Minimum(column, where)            Minimum.scala:35-53     */
   DQ_OP_MAXIMUM = 8,               /* Maximum(column, where)            Maximum.scala:35-53     */
-  DQ_OP_APPROX_COUNT_DISTINCT = 9  /* ApproxCountDistinct(column, where) ApproxCountDistinct.scala:47-64 */
+  DQ_OP_APPROX_COUNT_DISTINCT = 9, /* ApproxCountDistinct(column, where) ApproxCountDistinct.scala:47-64 */
+  DQ_OP_DATATYPE = 10              /* DataType(column, where)           DataType.scala:152-183  */
 } dq_op_kind;
 
 /*
@@ -148,6 +149,9 @@ typedef struct dq_op {
  *   STDDEV                       StandardDeviationState(n, avg, m2)
  *   MINIMUM / MAXIMUM            MinState(value) / MaxState(value)
  *   APPROX_COUNT_DISTINCT        ApproxCountDistinctState(words)  (always has_value = 1)
+ *   DATATYPE                     DataTypeHistogram(words[0..4] = numNull, numFractional,
+ *                                numIntegral, numBoolean, numString)  (always has_value = 1:
+ *                                the StatefulDataType UDAF never returns NULL)
  */
 typedef struct dq_state {
   int32_t kind;
@@ -218,6 +222,15 @@ void dq_hll_words_from_bytes(const uint8_t in[416], int64_t words[DQ_HLL_NUM_WOR
 
 /* Spark 2.2.2 XxHash64Function with seed 42 for one value (host reference, used by tests). */
 uint64_t dq_xxh64(const void* data, size_t len, uint64_t seed);
+
+/* Spark 2.2.2 Cast(StringType -> LongType | DoubleType) of one utf8 column, as
+ * ColumnProfiler.castNumericStringColumns does before pass 2 (ColumnProfiler.scala:346-355,
+ * 427-445).  Writes n_rows values and a validity bitmap (LSB-first, NULL = unparsable) into
+ * DEVICE buffers on ctx's GPU.  Doubles are exact (correctly rounded); a well-formed number
+ * outside the exact fast path (> 19 significant digits, |exponent| > 22, hex) is counted in
+ * *n_unsupported and its row left NULL -- the caller routes the column to Spark when > 0. */
+dq_status dq_cast_utf8(dq_ctx* ctx, const dq_column* src, int64_t n_rows, int32_t to_type,
+                       void* d_values, uint8_t* d_validity, int64_t* n_unsupported);
 
 /* ---------------------------------------------------------------- frequency group-by
  * Replaces FrequencyBasedAnalyzer.computeFrequencies (GroupingAnalyzers.scala:53-80) and the

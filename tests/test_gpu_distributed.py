@@ -76,7 +76,7 @@ def test_two_rank_exchange_matches_oracle(gpu):
         dtypes = ["string" if c == "key" else "int64" for c in cols]
         if hist:
             ostate = O.histogram_state(otable, cols[0])
-            want = {encode_key([k if k != "NullValue" else None], dtypes, True): c
+            want = {encode_key([k[0] if k[0] != "NullValue" else None], dtypes, True): c
                     for k, c in ostate.frequencies.items()}
         else:
             ostate = O.frequencies_state(otable, list(cols))
