@@ -5,7 +5,8 @@ The public names mirror the reference's Scala API (`com.amazon.deequ.analyzers`,
 goes through the C-ABI library `libdeequ_amd.so` (hand-written gfx950 HIP kernels); there is
 no CPU fallback.
 """
-from .analyzers import (Analyzer, ApproxCountDistinct, Completeness, Compliance, CountDistinct,
+from .analyzers import (Analyzer, ApproxCountDistinct, Completeness, Compliance, CountDistinct, DataType,
+                        DataTypeInstances,
                         Distinctness, Entropy, FrequencyBasedAnalyzer, GroupingAnalyzer, Histogram,
                         Maximum, Mean, Minimum, MutualInformation, Preconditions,
                         ScanShareableAnalyzer, ScanShareableFrequencyBasedAnalyzer, Size,
@@ -20,7 +21,7 @@ from .metrics import (Distribution, DistributionValue, DoubleMetric, EmptyStateE
                       WrongColumnTypeException)
 from .runner import (Analysis, AnalysisRunBuilder, AnalysisRunner, AnalyzerContext,
                      InMemoryStateProvider)
-from .states import (ApproxCountDistinctState, MaxState, MeanState, MinState, NumMatches,
+from .states import (ApproxCountDistinctState, DataTypeHistogram, MaxState, MeanState, MinState, NumMatches,
                      NumMatchesAndCount, StandardDeviationState, State, SumState)
 from .table import Column, PartitionedTable, Table
 

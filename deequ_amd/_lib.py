@@ -20,7 +20,7 @@ DQ_T_BOOL, DQ_T_INT8, DQ_T_INT16, DQ_T_INT32, DQ_T_INT64, DQ_T_FLOAT32, DQ_T_FLO
 DQ_COL_DEVICE = 0x1
 
 (DQ_OP_SIZE, DQ_OP_COMPLETENESS, DQ_OP_COMPLIANCE, DQ_OP_SUM, DQ_OP_MEAN, DQ_OP_STDDEV,
- DQ_OP_MINIMUM, DQ_OP_MAXIMUM, DQ_OP_APPROX_COUNT_DISTINCT) = range(1, 10)
+ DQ_OP_MINIMUM, DQ_OP_MAXIMUM, DQ_OP_APPROX_COUNT_DISTINCT, DQ_OP_DATATYPE) = range(1, 11)
 
 DQ_P_COLUMN, DQ_P_LIT_INT, DQ_P_LIT_FLOAT, DQ_P_LIT_NULL, DQ_P_COALESCE, DQ_P_LIT_STRING = 1, 2, 3, 4, 5, 6
 DQ_P_EQ, DQ_P_NE, DQ_P_LT, DQ_P_LE, DQ_P_GT, DQ_P_GE, DQ_P_EQ_NULLSAFE = 10, 11, 12, 13, 14, 15, 16
@@ -110,6 +110,7 @@ SIGNATURES = {
                             POINTER(c_int64), POINTER(c_int64)]),
     "dq_freq_merge": (c_int, [c_void_p, c_void_p]),
     "dq_freq_import": (c_int, [c_void_p, POINTER(DqFreqGroup), c_int64, c_void_p, c_int64]),
+    "dq_cast_utf8": (c_int, [c_void_p, POINTER(DqColumn), c_int64, c_int32, c_void_p, c_void_p, POINTER(c_int64)]),
     "dq_freq_partition": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_void_p, c_int64, POINTER(c_int64),
                                   POINTER(c_int64)]),
     "dq_freq_import_wire": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_int64]),

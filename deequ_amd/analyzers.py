@@ -273,6 +273,72 @@ class ApproxCountDistinct(StandardScanShareableAnalyzer):
         return "ApproxCountDistinct(%s,%s)" % (self.column, _opt(self.where))
 
 
+class DataTypeInstances:
+    """DataTypeInstances enumeration (DataType.scala:32-38): value ids and names."""
+    Unknown, Fractional, Integral, Boolean, String = 0, 1, 2, 3, 4
+    NAMES = ("Unknown", "Fractional", "Integral", "Boolean", "String")
+
+    @classmethod
+    def name_of(cls, v: int) -> str:
+        return cls.NAMES[v]
+
+
+def data_type_distribution(h):
+    """DataTypeHistogram.toDistribution (DataType.scala:98-114)."""
+    from .metrics import Distribution, DistributionValue
+    total = h.numNull + h.numString + h.numBoolean + h.numIntegral + h.numFractional
+    vals = {"Unknown": h.numNull, "Fractional": h.numFractional, "Integral": h.numIntegral,
+            "Boolean": h.numBoolean, "String": h.numString}
+    return Distribution({k: DistributionValue(c, (c / total) if total else float("nan"))
+                         for k, c in vals.items()}, 5)
+
+
+def determine_type(dist) -> int:
+    """DataTypeHistogram.determineType (DataType.scala:116-143)."""
+    def ratio(name):
+        v = dist.values.get(name)
+        return 0.0 if v is None else v.ratio
+    if ratio("Unknown") == 1.0:
+        return DataTypeInstances.Unknown
+    if ratio("String") > 0.0 or (ratio("Boolean") > 0.0 and (ratio("Integral") > 0.0 or ratio("Fractional") > 0.0)):
+        return DataTypeInstances.String
+    if ratio("Boolean") > 0.0:
+        return DataTypeInstances.Boolean
+    if ratio("Fractional") > 0.0:
+        return DataTypeInstances.Fractional
+    return DataTypeInstances.Integral
+
+
+@dataclass(frozen=True)
+class DataType(ScanShareableAnalyzer):
+    """DataType(column, where) (DataType.scala:152-183): the StatefulDataType UDAF's regex type
+    classification of the column cast to string, as the GPU op DQ_OP_DATATYPE (dq_profile.hip).
+    The metric is a HistogramMetric over the five type names."""
+    column: str
+    where: Optional[str] = None
+    name = "DataType"
+    DQ_KIND = L.DQ_OP_DATATYPE
+
+    def instance(self):
+        return self.column
+
+    def preconditions(self):
+        return [Preconditions.hasColumn(self.column)]
+
+    def computeMetricFrom(self, state):
+        from .metrics import HistogramMetric, Success as _S
+        if state is None:
+            return HistogramMetric(self.column, Failure(wrap_if_necessary(empty_state_exception(self))))
+        return HistogramMetric(self.column, _S(data_type_distribution(state)))
+
+    def toFailureMetric(self, error):
+        from .metrics import HistogramMetric
+        return HistogramMetric(self.column, Failure(wrap_if_necessary(error)))
+
+    def __str__(self):
+        return "DataType(%s,%s)" % (self.column, _opt(self.where))
+
+
 # ---------------------------------------------------------------- frequency-based analyzers
 def _columns_tuple(columns) -> tuple:
     return (columns,) if isinstance(columns, str) else tuple(columns)

@@ -133,15 +133,16 @@ __device__ bool parse_long(const uint8_t* p, int32_t n, int64_t* out) {
       break;
     }
     if (b - '0' >= 10u) return false;
-    if (r < stop) return false;
+    // the reference detects overflow after a wrapping step; here it is checked before the
+    // step (no signed overflow): r * 10 - digit >= INT64_MIN
+    if (r < stop || (r == stop && (int64_t)(b - '0') > -(INT64_MIN % 10))) return false;
     r = r * 10 - (int64_t)(b - '0');
-    if (r > 0) return false;
   }
   for (; i < n; ++i)
     if ((uint32_t)p[i] - '0' >= 10u) return false;
   if (!neg) {
+    if (r == INT64_MIN) return false;  // 9223372036854775808 does not fit
     r = -r;
-    if (r < 0) return false;
   }
   *out = r;
   return true;

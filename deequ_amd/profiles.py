@@ -1,0 +1,353 @@
+"""ColumnProfilerRunner / ColumnProfiler -- the reference's three-pass profiler on the GPU path.
+
+Follows `src/main/scala/com/amazon/deequ/profiles/ColumnProfiler.scala` (profile :91-208):
+
+* pass 1 (:115-145, analyzers :220-238): Completeness + ApproxCountDistinct for every column,
+  + DataType for string columns without a predefined type, + Size -- ONE AnalysisRunner run,
+  i.e. one fused GPU plan (scan, HLL and DataType kernels over each column once).
+* pass 2 (:147-173, :240-251): string columns typed Integral / Fractional are cast to
+  LongType / DoubleType on the GPU (dq_cast_utf8, Spark 2.2.2 Cast semantics, :346-355,
+  :427-445); then Minimum, Maximum, Mean, StandardDeviation and Sum of every numeric column in one
+  fused plan.  The reference's KLLSketch (a randomized sketch, :249) is out of scope, so `kll`
+  and `approxPercentiles` are None.
+* pass 3 (:175-205, :535-606): exact histograms of the low-cardinality columns with the GPU
+  group-by (NULL -> "NullValue", values as Java toString), ratio = count / rows (:598-601).
+
+Profiles, `GenericColumnStatistics.typeOf` and the JSON writer follow ColumnProfile.scala and
+ColumnProfiler.scala:18-57, 357-424, 658-710.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+from collections import OrderedDict
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+from . import _lib as L
+from .analyzers import (ApproxCountDistinct, Completeness, DataType, DataTypeInstances, Maximum, Mean,
+                        Minimum, Size, StandardDeviation, Sum, determine_type)
+from .metrics import Distribution, DistributionValue
+
+DEFAULT_CARDINALITY_THRESHOLD = 120  # ColumnProfiler.DEFAULT_CARDINALITY_THRESHOLD (:71)
+NULL_FIELD_REPLACEMENT = "NullValue"
+_HISTOGRAM_TYPES = ("string", "bool", "float64", "float32", "int32", "int64", "int16")  # :541-543
+
+
+@dataclass
+class StandardColumnProfile:
+    """StandardColumnProfile (ColumnProfile.scala:34-42)."""
+    column: str
+    completeness: float
+    approximateNumDistinctValues: int
+    dataType: int
+    isDataTypeInferred: bool
+    typeCounts: Dict[str, int]
+    histogram: Optional[Distribution]
+
+
+@dataclass
+class NumericColumnProfile:
+    """NumericColumnProfile (ColumnProfile.scala:44-59)."""
+    column: str
+    completeness: float
+    approximateNumDistinctValues: int
+    dataType: int
+    isDataTypeInferred: bool
+    typeCounts: Dict[str, int]
+    histogram: Optional[Distribution]
+    kll: Optional[object] = None
+    mean: Optional[float] = None
+    maximum: Optional[float] = None
+    minimum: Optional[float] = None
+    sum: Optional[float] = None
+    stdDev: Optional[float] = None
+    approxPercentiles: Optional[List[float]] = None
+
+
+@dataclass
+class ColumnProfiles:
+    """ColumnProfiles(profiles, numRecords) (ColumnProfile.scala:61-63)."""
+    profiles: Dict[str, object]
+    numRecords: int
+
+    @staticmethod
+    def toJson(columnProfiles: Sequence[object]) -> str:
+        """ColumnProfiles.toJson (ColumnProfile.scala:68-177), including its quirk that the
+        built typeCounts object is never attached."""
+        cols = []
+        for p in columnProfiles:
+            j = OrderedDict()
+            j["column"] = p.column
+            j["dataType"] = DataTypeInstances.name_of(p.dataType)
+            j["isDataTypeInferred"] = "true" if p.isDataTypeInferred else "false"
+            j["completeness"] = p.completeness
+            j["approximateNumDistinctValues"] = p.approximateNumDistinctValues
+            if p.histogram is not None:
+                j["histogram"] = [OrderedDict([("value", k), ("count", v.absolute), ("ratio", v.ratio)])
+                                  for k, v in p.histogram.values.items()]
+            if isinstance(p, NumericColumnProfile):
+                for name in ("mean", "maximum", "minimum", "sum", "stdDev"):
+                    v = getattr(p, name)
+                    if v is not None:
+                        j[name] = v
+                j["approxPercentiles"] = list(p.approxPercentiles or [])
+            cols.append(j)
+        return json.dumps({"columns": cols}, indent=2)
+
+
+@dataclass
+class GenericColumnStatistics:
+    """GenericColumnStatistics (ColumnProfiler.scala:31-46)."""
+    numRecords: int
+    inferredTypes: Dict[str, int]
+    knownTypes: Dict[str, int]
+    typeDetectionHistograms: Dict[str, Dict[str, int]]
+    approximateNumDistincts: Dict[str, int]
+    completenesses: Dict[str, float]
+    predefinedTypes: Dict[str, int] = field(default_factory=dict)
+
+    def typeOf(self, column: str) -> int:
+        merged = dict(self.inferredTypes)
+        merged.update(self.knownTypes)
+        merged.update(self.predefinedTypes)
+        return merged[column]
+
+
+def _known_type(dtype: str) -> int:
+    """The schema-type mapping of extractGenericStatistics (:401-420); ByteType is not in the
+    reference's match and maps to Unknown."""
+    if dtype in ("int16", "int32", "int64"):
+        return DataTypeInstances.Integral
+    if dtype in ("float32", "float64"):
+        return DataTypeInstances.Fractional
+    if dtype == "bool":
+        return DataTypeInstances.Boolean
+    return DataTypeInstances.Unknown
+
+
+def _java_long(x: float) -> int:
+    return int(x)  # Double.toLong truncates toward zero
+
+
+class ColumnProfiler:
+    DEFAULT_CARDINALITY_THRESHOLD = DEFAULT_CARDINALITY_THRESHOLD
+
+    @staticmethod
+    def profile(data, restrictToColumns: Optional[Sequence[str]] = None, printStatusUpdates: bool = False,
+                lowCardinalityHistogramThreshold: int = DEFAULT_CARDINALITY_THRESHOLD,
+                kllParameters=None, predefinedTypes: Optional[Dict[str, int]] = None) -> ColumnProfiles:
+        from .runner import AnalysisRunner
+        predefined = dict(predefinedTypes or {})
+        schema = data.schema
+        if restrictToColumns is not None:
+            for c in restrictToColumns:
+                if c not in schema:
+                    raise ValueError("requirement failed: Unable to find column %s" % c)
+        relevant = [c for c in schema if restrictToColumns is None or c in restrictToColumns]
+
+        if printStatusUpdates:
+            print("### PROFILING: Computing generic column statistics in pass (1/3)...")
+        first = []
+        for c in relevant:
+            first += [Completeness(c), ApproxCountDistinct(c)]
+            if schema[c] == "string" and c not in predefined:
+                first.append(DataType(c))
+        ctx1 = AnalysisRunner.onData(data).addAnalyzers(first).addAnalyzer(Size()).run()
+        generic = _extract_generic_statistics(relevant, schema, ctx1, predefined)
+
+        if printStatusUpdates:
+            print("### PROFILING: Computing numeric column statistics in pass (2/3)...")
+        casted = _cast_numeric_string_columns(relevant, data, generic)
+        second = []
+        for c in relevant:
+            if generic.typeOf(c) in (DataTypeInstances.Integral, DataTypeInstances.Fractional):
+                second += [Minimum(c), Maximum(c), Mean(c), StandardDeviation(c), Sum(c)]
+        ctx2 = AnalysisRunner.onData(casted).addAnalyzers(second).run()
+        numeric = _extract_numeric_statistics(ctx2)
+
+        if printStatusUpdates:
+            print("### PROFILING: Computing histograms of low-cardinality columns in pass (3/3)...")
+        targets = _find_target_columns_for_histograms(schema, generic, lowCardinalityHistogramThreshold)
+        histograms = compute_histograms(data, targets)
+        return _create_profiles(relevant, generic, numeric, histograms)
+
+
+def _extract_generic_statistics(columns, schema, ctx, predefined) -> GenericColumnStatistics:
+    """extractGenericStatistics (:357-424)."""
+    num_records = None
+    inferred, type_counts, approx, completeness = {}, {}, {}, {}
+    for a, m in ctx.metricMap.items():
+        if isinstance(a, Size):
+            num_records = _java_long(m.value.get())
+        elif isinstance(a, DataType):
+            if a.column in predefined:
+                continue
+            dist = m.value.get()
+            inferred[a.column] = determine_type(dist)
+            type_counts[a.column] = {k: v.absolute for k, v in dist.values.items()}
+        elif isinstance(a, ApproxCountDistinct):
+            approx[a.column] = _java_long(m.value.get())
+        elif isinstance(a, Completeness):
+            completeness[a.column] = m.value.get()
+    known = {c: _known_type(schema[c]) for c in columns if c not in predefined and schema[c] != "string"}
+    return GenericColumnStatistics(num_records, inferred, known, type_counts, approx, completeness, predefined)
+
+
+def cast_string_column(col, to_dtype: str, device: Optional[int] = None):
+    """Spark 2.2.2 Cast(StringType -> LongType | DoubleType) of one utf8 column on the GPU
+    (dq_cast_utf8); the result is a device-resident column.  Raises UnsupportedOnGpu when a value
+    needs the exact slow-path double parse (the reference would run that column on Spark)."""
+    import torch
+    from .engine import current_device
+    from .table import Column
+    dev_idx = current_device() if device is None else device
+    dev = torch.device("cuda", dev_idx)
+    n = col.length
+    vals = torch.empty(max(1, n), dtype=torch.int64 if to_dtype == "int64" else torch.float64, device=dev)
+    valid = torch.empty((n + 7) // 8 + 8, dtype=torch.uint8, device=dev)
+    unsupported = ctypes.c_int64()
+    src = col.to_dq()
+    L.check(L.lib().dq_cast_utf8(L.Context.get(dev_idx).handle, ctypes.byref(src), n, L.TYPE_CODES[to_dtype],
+                                 vals.data_ptr(), valid.data_ptr(), ctypes.byref(unsupported)))
+    if unsupported.value:
+        raise L.UnsupportedOnGpu(L.DQ_ERR_UNSUPPORTED, "%d values need Spark's exact (slow-path) string to "
+                                 "double parse" % unsupported.value)
+    return Column(to_dtype, n, vals, valid, device=True)
+
+
+def _cast_numeric_string_columns(columns, data, generic):
+    """castNumericStringColumns (:427-445): string columns typed Integral -> LongType, Fractional
+    -> DoubleType.  (Numeric columns keep their type: the reference's cast of them is value
+    preserving and the GPU aggregates every numeric width with Spark's semantics.)"""
+    from .table import PartitionedTable, Table
+    targets = {}
+    for c in columns:
+        if data.schema[c] != "string":
+            continue
+        t = generic.typeOf(c)
+        if t == DataTypeInstances.Integral:
+            targets[c] = "int64"
+        elif t == DataTypeInstances.Fractional:
+            targets[c] = "float64"
+    if not targets:
+        return data
+    parts = []
+    for batch in data.batches():
+        cols = OrderedDict()
+        for name, col in batch.columns.items():
+            cols[name] = cast_string_column(col, targets[name]) if name in targets else col
+        parts.append(Table(cols))
+    return parts[0] if len(parts) == 1 else PartitionedTable(parts)
+
+
+def _extract_numeric_statistics(ctx):
+    """extractNumericStatistics (:448-528): successful metrics only."""
+    out = {"mean": {}, "stdDev": {}, "maximum": {}, "minimum": {}, "sum": {}}
+    key = {Mean: "mean", StandardDeviation: "stdDev", Maximum: "maximum", Minimum: "minimum", Sum: "sum"}
+    for a, m in ctx.metricMap.items():
+        k = key.get(type(a))
+        if k is not None and m.value.isSuccess:
+            out[k][a.column] = m.value.get()
+    return out
+
+
+def _find_target_columns_for_histograms(schema, generic, threshold) -> List[str]:
+    """findTargetColumnsForHistograms (:535-557)."""
+    ok_types = (DataTypeInstances.String, DataTypeInstances.Boolean, DataTypeInstances.Integral,
+                DataTypeInstances.Fractional)
+    return [c for c, count in generic.approximateNumDistincts.items()
+            if schema[c] in _HISTOGRAM_TYPES and generic.typeOf(c) in ok_types and count <= threshold]
+
+
+def compute_histograms(data, target_columns: Sequence[str]) -> Dict[str, Distribution]:
+    """computeHistograms (:564-606): exact (column, value.toString) counts, NULL -> "NullValue",
+    one GPU group-by per target column; ratio = count / (sum of the column's counts)."""
+    from .frequencies import FrequencyTable, decode_key
+    from .javafmt import spark_cast_to_string
+    schema = data.schema
+    out = {}
+    for c in target_columns:
+        dtype = schema[c]
+        table = FrequencyTable([c], dict(schema), histogram=True)
+        try:
+            for batch in data.batches():
+                table.consume(batch)
+            counts, keys = table.export()
+        finally:
+            table.close()
+        per_value: Dict[str, int] = {}
+        for k, n in zip(keys, counts.tolist()):
+            v = decode_key(k, [dtype], histogram=True)[0]
+            s = NULL_FIELD_REPLACEMENT if v is None else spark_cast_to_string(v, dtype)
+            per_value[s] = per_value.get(s, 0) + int(n)
+        total = sum(per_value.values())
+        values = {s: DistributionValue(n, n / total) for s, n in sorted(per_value.items())}
+        out[c] = Distribution(values, len(values))
+    return out
+
+
+def _create_profiles(columns, generic, numeric, histograms) -> ColumnProfiles:
+    """createProfiles (:658-710)."""
+    profiles = OrderedDict()
+    for name in columns:
+        t = generic.typeOf(name)
+        common = dict(column=name, completeness=generic.completenesses[name],
+                      approximateNumDistinctValues=generic.approximateNumDistincts[name], dataType=t,
+                      isDataTypeInferred=name in generic.inferredTypes,
+                      typeCounts=generic.typeDetectionHistograms.get(name, {}),
+                      histogram=histograms.get(name))
+        if t in (DataTypeInstances.Integral, DataTypeInstances.Fractional):
+            profiles[name] = NumericColumnProfile(
+                **common, kll=None, mean=numeric["mean"].get(name), maximum=numeric["maximum"].get(name),
+                minimum=numeric["minimum"].get(name), sum=numeric["sum"].get(name),
+                stdDev=numeric["stdDev"].get(name), approxPercentiles=None)
+        else:
+            profiles[name] = StandardColumnProfile(**common)
+    return ColumnProfiles(profiles, generic.numRecords)
+
+
+class ColumnProfilerRunner:
+    """ColumnProfilerRunner (ColumnProfilerRunner.scala:38-84)."""
+
+    def onData(self, data) -> "ColumnProfilerRunBuilder":
+        return ColumnProfilerRunBuilder(data)
+
+
+class ColumnProfilerRunBuilder:
+    """ColumnProfilerRunBuilder (ColumnProfilerRunBuilder.scala:24-157)."""
+
+    def __init__(self, data):
+        self.data = data
+        self._print = False
+        self._threshold = DEFAULT_CARDINALITY_THRESHOLD
+        self._restrict = None
+        self._kll = None
+        self._predefined = {}
+
+    def printStatusUpdates(self, flag: bool) -> "ColumnProfilerRunBuilder":
+        self._print = flag
+        return self
+
+    def cacheInputs(self, flag: bool) -> "ColumnProfilerRunBuilder":
+        return self  # inputs already live in HBM or host memory; nothing to cache
+
+    def withLowCardinalityHistogramThreshold(self, threshold: int) -> "ColumnProfilerRunBuilder":
+        self._threshold = threshold
+        return self
+
+    def restrictToColumns(self, columns: Sequence[str]) -> "ColumnProfilerRunBuilder":
+        self._restrict = list(columns)
+        return self
+
+    def setKLLParameters(self, params) -> "ColumnProfilerRunBuilder":
+        self._kll = params
+        return self
+
+    def setPredefinedTypes(self, types: Dict[str, int]) -> "ColumnProfilerRunBuilder":
+        self._predefined = dict(types)
+        return self
+
+    def run(self) -> ColumnProfiles:
+        return ColumnProfiler.profile(self.data, self._restrict, self._print, self._threshold, self._kll,
+                                      self._predefined)

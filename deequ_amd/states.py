@@ -11,6 +11,7 @@ partial states do.
 * StandardDeviationState -- StandardDeviation.scala:25-45
 * MinState / MaxState -- Minimum.scala:25-33 / Maximum.scala:25-33
 * ApproxCountDistinctState -- ApproxCountDistinct.scala:26-40
+* DataTypeHistogram -- DataType.scala:40-52
 """
 from __future__ import annotations
 
@@ -263,6 +264,54 @@ class ApproxCountDistinctState(State):
         return "ApproxCountDistinctState(%s)" % ",".join(str(w) for w in self.words)
 
 
+class DataTypeHistogram(State):
+    """DataTypeHistogram(numNull, numFractional, numIntegral, numBoolean, numString)
+    (DataType.scala:40-52); sum adds the counts.  Not a DoubleValuedState."""
+    KIND = L.DQ_OP_DATATYPE
+    SIZE_IN_BYTES = 40
+
+    def __init__(self, numNull: int, numFractional: int, numIntegral: int, numBoolean: int, numString: int):
+        self.numNull, self.numFractional, self.numIntegral = int(numNull), int(numFractional), int(numIntegral)
+        self.numBoolean, self.numString = int(numBoolean), int(numString)
+
+    def counts(self) -> Tuple[int, int, int, int, int]:
+        return (self.numNull, self.numFractional, self.numIntegral, self.numBoolean, self.numString)
+
+    def to_dq(self):
+        s = self._dq()
+        for i, c in enumerate(self.counts()):
+            s.words[i] = c
+        return s
+
+    @classmethod
+    def from_dq(cls, s):
+        return cls(*[s.words[i] for i in range(5)])
+
+    def metricValue(self):
+        raise TypeError("DataTypeHistogram is not a DoubleValuedState")
+
+    def toBytes(self) -> bytes:
+        """DataTypeHistogram.toBytes (DataType.scala:75-96): five big-endian longs."""
+        import struct
+        return struct.pack(">5q", *self.counts())
+
+    @classmethod
+    def fromBytes(cls, b: bytes) -> "DataTypeHistogram":
+        import struct
+        if len(b) != cls.SIZE_IN_BYTES:
+            raise ValueError("requirement failed")
+        return cls(*struct.unpack(">5q", b))
+
+    def __eq__(self, o):
+        return isinstance(o, DataTypeHistogram) and o.counts() == self.counts()
+
+    def __hash__(self):
+        return hash(("DataTypeHistogram",) + self.counts())
+
+    def __repr__(self):
+        return "DataTypeHistogram(%d,%d,%d,%d,%d)" % self.counts()
+
+
 _BY_KIND = {
     L.DQ_OP_SIZE: NumMatches,
     L.DQ_OP_COMPLETENESS: NumMatchesAndCount,
@@ -273,6 +322,7 @@ _BY_KIND = {
     L.DQ_OP_MINIMUM: MinState,
     L.DQ_OP_MAXIMUM: MaxState,
     L.DQ_OP_APPROX_COUNT_DISTINCT: ApproxCountDistinctState,
+    L.DQ_OP_DATATYPE: DataTypeHistogram,
 }
 
 

@@ -25,6 +25,8 @@ What is restated (reference = /root/reference, deequ 1.0.3-SNAPSHOT on Spark 2.2
   XXH64 itself is the third-party algorithm (Spark `XXH64` port of Yann Collet's
   xxHash64, not vendored); it is restated here from the published spec and pinned
   against the `xxhash` 3.8.1 Python binding.
+* DataType: `StatefulDataType.scala:36-38,58-69` (regex classification of the value cast
+  to string), `DataType.scala:98-143` (distribution, determineType).
 * Frequency family: `GroupingAnalyzers.scala:53-80` (group-by, NULL rows dropped,
   numRows = all rows), Uniqueness `Uniqueness.scala:29-31`, Distinctness
   `Distinctness.scala:32-34`, Entropy `Entropy.scala:31-41`, CountDistinct
@@ -38,6 +40,7 @@ module by `tests/test_oracle_golden.py`.
 from __future__ import annotations
 
 import math
+import re
 import struct
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -928,6 +931,39 @@ def approx_count_distinct_state(table: OTable, column: str, where: Optional[str]
     col = table[column]
     vals = _selected_values(table, column, where)
     return ApproxCountDistinctState(tuple(hll_pack(hll_registers(vals, col.dtype))))
+
+
+# ---------------------------------------------------------------------------- DataType
+# `StatefulDataType.update` (catalyst/StatefulDataType.scala:36-38, 58-69): the value cast to
+# string (Spark 2.2 Cast: Java toString for numbers/booleans) is matched, in this order, against
+# FRACTIONAL / INTEGRAL / BOOLEAN with whole-string matching; Java `\d` is [0-9].
+_DT_FRACTIONAL = re.compile(r"(-|\+)? ?[0-9]*\.[0-9]*")
+_DT_INTEGRAL = re.compile(r"(-|\+)? ?[0-9]*")
+_DT_BOOLEAN = re.compile(r"(true|false)")
+
+
+def _datatype_class(v, dtype: str) -> int:
+    """0 null, 1 fractional, 2 integral, 3 boolean, 4 string (DataTypeHistogram positions)."""
+    if v is None:
+        return 0
+    s = v if dtype == "string" else _spark_cast_string(v, dtype)
+    if _DT_FRACTIONAL.fullmatch(s):
+        return 1
+    if _DT_INTEGRAL.fullmatch(s):
+        return 2
+    if _DT_BOOLEAN.fullmatch(s):
+        return 3
+    return 4
+
+
+def datatype_state(table: OTable, column: str, where: Optional[str] = None):
+    """`DataType.computeStateFrom` (`DataType.scala:157-165`): never None (the UDAF always
+    returns its buffer); where-filtered rows are NULL inputs (conditionalSelection)."""
+    col = table[column]
+    counts = [0, 0, 0, 0, 0]
+    for v in _selected_values(table, column, where):
+        counts[_datatype_class(v, col.dtype)] += 1
+    return tuple(counts)
 
 
 def frequencies_state(table: OTable, columns: Sequence[str]) -> FrequenciesAndNumRows:

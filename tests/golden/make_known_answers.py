@@ -91,6 +91,38 @@ TABLES = {
     },
     # getDfEmpty (:26-33)
     "dfEmpty": {"column1": ["string", []], "column2": ["string", []]},
+    # ---- DataType fixtures (AnalyzerTests.scala:294-420)
+    "dfNegative": {  # getDfWithNegativeNumbers (:75-84)
+        "item": ["string", ["1", "2", "3", "4"]],
+        "att1": ["string", ["-1", "-2", "-3", "-4"]],
+        "att2": ["string", ["-1.0", "-2.0", "-3.0", "-4.0"]],
+    },
+    "dfFracInt": {"item": ["string", ["1", "2"]], "att1": ["string", ["1.0", "1"]]},  # :110-117
+    "dfFracStr": {"item": ["string", ["1", "2"]], "att1": ["string", ["1.0", "a"]]},  # :119-126
+    "dfIntStr": {"item": ["string", ["1", "2"]], "att1": ["string", ["1", "a"]]},  # :128-135
+    # getDfWithNumericValues.att1 cast to FloatType / StringType (AnalyzerTests.scala:321-334)
+    "dfNumericCasts": {
+        "att1_float": ["float32", [1.0, 2.0, 3.0, 4.0, 5.0, 6.0]],
+        "att1_str": ["string", ["1", "2", "3", "4", "5", "6"]],
+    },
+    # getDfWithNumericFractionalValues.att1 cast to StringType (:336-343)
+    "dfFractionalStr": {"att1_str": ["string", ["1.0", "2.0", "3.0", "4.0", "5.0", "6.0"]]},
+    "dfBool": {"item": ["string", ["1", "2"]], "att1": ["string", ["true", "false"]]},  # :392-402
+    "dfBoolNull": {"item": ["string", ["1", "2", "3", "4"]],  # :404-420
+                   "att1": ["string", ["true", "false", None, "2.0"]]},
+    # ---- ColumnProfiler fixtures (profiles/ColumnProfilerTest.scala)
+    # getDfCompleteAndInCompleteColumns (utils/FixtureSupport.scala:86-97)
+    "dfCompleteIncomplete": {
+        "item": ["string", ["1", "2", "3", "4", "5", "6"]],
+        "att1": ["string", ["a", "b", "a", "a", "b", "a"]],
+        "att2": ["string", ["f", "d", None, "f", None, "f"]],
+    },
+    "profBool": {"attribute": ["bool", [True, True, True, False, False, None]]},  # :228-253
+    "profInt": {"attribute": ["int32", [2147483647, 2147483647, 2147483647, 2, 2, None]]},  # :255-280
+    "profLong": {"attribute": ["int64", [1, 1, 1, 2, 2, None]]},  # :282-307
+    "profDouble": {"attribute": ["float64", [1.0, 1.0, 1.0, 2.0, 2.0, None]]},  # :309-334
+    "profFloat": {"attribute": ["float32", [1.0, 1.0, 1.0, 2.0, 2.0, None]]},  # :336-361
+    "profShort": {"attribute": ["int16", [1, 1, 1, 2, 2, None]]},  # :363-400
 }
 
 A = "analyzers/AnalyzerTests.scala"
@@ -190,6 +222,67 @@ MERGE_CASES = [
 ]
 
 
+# DataType known answers: expected DataTypeHistogram (numNull, numFractional, numIntegral,
+# numBoolean, numString) -- the distribution's absolute counts
+DT = "analyzers/AnalyzerTests.scala"
+DATATYPE_CASES = [
+    ("dt_string_fallback", "dfFull", "att1", [0, 0, 0, 0, 4], T + DT + ":294-299"),
+    ("dt_integral", "dfNumeric", "att1", [0, 0, 6, 0, 0], T + DT + ":301-305"),
+    ("dt_integral_negative", "dfNegative", "att1", [0, 0, 4, 0, 0], T + DT + ":307-311"),
+    ("dt_fractional_negative", "dfNegative", "att2", [0, 4, 0, 0, 0], T + DT + ":313-318"),
+    ("dt_fractional_float", "dfNumericCasts", "att1_float", [0, 6, 0, 0, 0], T + DT + ":321-327"),
+    ("dt_integral_string", "dfNumericCasts", "att1_str", [0, 0, 6, 0, 0], T + DT + ":329-334"),
+    ("dt_fractional_string", "dfFractionalStr", "att1_str", [0, 6, 0, 0, 0], T + DT + ":336-343"),
+    ("dt_frac_and_int", "dfFracInt", "att1", [0, 1, 1, 0, 0], T + DT + ":352-360"),
+    ("dt_frac_and_string", "dfFracStr", "att1", [0, 1, 0, 0, 1], T + DT + ":362-370"),
+    ("dt_int_and_string", "dfIntStr", "att1", [0, 0, 1, 0, 1], T + DT + ":372-380"),
+    ("dt_numeric_and_null", "dfUnique", "uniqueWithNulls", [1, 0, 5, 0, 0], T + DT + ":382-390"),
+    ("dt_boolean", "dfBool", "att1", [0, 0, 0, 2, 0], T + DT + ":392-402"),
+    ("dt_boolean_null_frac", "dfBoolNull", "att1", [1, 1, 0, 2, 0], T + DT + ":404-420"),
+    ("dt_all_null", "dfNullColumns", "stringCol", [8, 0, 0, 0, 0], NH + ":72-73,112-113"),
+]
+
+# ColumnProfiler known answers (profiles/ColumnProfilerTest.scala).  `expect` holds only the
+# fields the reference test asserts; dataType ids: 0 Unknown 1 Fractional 2 Integral 3 Boolean 4 String.
+PT = T + "profiles/ColumnProfilerTest.scala"
+_ATT2_COUNTS = {"Boolean": 0, "Fractional": 0, "Integral": 0, "Unknown": 2, "String": 4}
+PROFILE_CASES = [
+    ("prof_standard", "dfCompleteIncomplete", ["att2"], 1, {}, "att2",
+     dict(kind="standard", completeness=2.0 / 3.0, approx=2, dataType=4, inferred=True,
+          typeCounts=_ATT2_COUNTS, histogram=None), PT + ":52-76"),
+    ("prof_predefined_type", "dfCompleteIncomplete", ["item"], 1, {"item": 4}, "item",
+     dict(kind="standard", completeness=1.0, approx=6, dataType=4, inferred=False, typeCounts={},
+          histogram=None), PT + ":78-97"),
+    ("prof_other_predefined", "dfCompleteIncomplete", ["att2"], 1, {"item": 4}, "att2",
+     dict(kind="standard", completeness=2.0 / 3.0, approx=2, dataType=4, inferred=True,
+          typeCounts=_ATT2_COUNTS, histogram=None), PT + ":99-121"),
+    ("prof_numeric_string", "dfCompleteIncomplete", ["item"], 1, {}, "item",
+     dict(kind="numeric", completeness=1.0, approx=6, dataType=2, inferred=True,
+          typeCounts={"Boolean": 0, "Fractional": 0, "Integral": 6, "Unknown": 0, "String": 0},
+          histogram=None, mean=3.5, maximum=6.0, minimum=1.0, sum=21.0, stdDev=1.707825127659933),
+     PT + ":124-159"),
+    ("prof_numeric", "dfFractional", ["att1"], 1, {}, "att1",
+     dict(kind="numeric", completeness=1.0, approx=6, dataType=1, inferred=False, typeCounts={},
+          histogram=None, mean=3.5, maximum=6.0, minimum=1.0, sum=21.0, stdDev=1.707825127659933),
+     PT + ":162-196"),
+    ("prof_string_histogram", "dfCompleteIncomplete", ["att2"], 10, {}, "att2",
+     dict(kind="standard", completeness=2.0 / 3.0, approx=2, dataType=4, inferred=True,
+          typeCounts=_ATT2_COUNTS,
+          histogram={"bins": 3, "values": {"d": [1, 0.16666666666666666], "f": [3, 0.5],
+                                           "NullValue": [2, 0.3333333333333333]}}), PT + ":200-226"),
+] + [
+    ("prof_hist_" + name, table, None, 120, {}, "attribute",
+     dict(histogram_values={k: [c, c / 6.0] for k, c in vals.items()}), PT + lines)
+    for name, table, vals, lines in (
+        ("boolean", "profBool", {"true": 3, "false": 2, "NullValue": 1}, ":228-253"),
+        ("int", "profInt", {"2147483647": 3, "2": 2, "NullValue": 1}, ":255-280"),
+        ("long", "profLong", {"1": 3, "2": 2, "NullValue": 1}, ":282-307"),
+        ("double", "profDouble", {"1.0": 3, "2.0": 2, "NullValue": 1}, ":309-334"),
+        ("float", "profFloat", {"1.0": 3, "2.0": 2, "NullValue": 1}, ":336-361"),
+        ("short", "profShort", {"1": 3, "2": 2, "NullValue": 1}, ":363-400"))
+]
+
+
 def main():
     # the Completeness(att2) initial case is the reference's own 4/6 computed on att2
     out = {
@@ -198,6 +291,10 @@ def main():
                   for c in CASES],
         "merge_cases": [dict(id=c[0], table_a=c[1], table_b=c[2], analyzer=c[3], args=c[4],
                              expected=c[5], source=c[6]) for c in MERGE_CASES],
+        "datatype_cases": [dict(id=c[0], table=c[1], column=c[2], expected=c[3], source=c[4])
+                           for c in DATATYPE_CASES],
+        "profile_cases": [dict(id=c[0], table=c[1], restrict=c[2], threshold=c[3], predefined=c[4],
+                               column=c[5], expect=c[6], source=c[7]) for c in PROFILE_CASES],
     }
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_known_answers.json")
     with open(path, "w") as f:

@@ -1,0 +1,216 @@
+"""DataType, the Spark string casts and the ColumnProfiler on the GPU.
+
+* DataType (DataType.scala:152-183): the reference's known answers (AnalyzerTests.scala:294-420,
+  NullHandlingTests.scala:72) and bit-exact parity with the oracle's regex restatement on
+  randomized strings and numeric columns (including the Double.toString plain/scientific cut).
+* dq_cast_utf8: Spark 2.2.2 Cast(StringType -> LongType | DoubleType) against the restatements
+  below (UTF8String.toLong; java.lang.Double.parseDouble for the forms the exact path covers).
+* ColumnProfiler (ColumnProfiler.scala:91-208): every known answer of ColumnProfilerTest.scala.
+"""
+import math
+import struct
+
+import numpy as np
+import pytest
+
+import deequ_amd as d
+import pyoracle as O
+from deequ_amd.profiles import ColumnProfiler, ColumnProfilerRunner, NumericColumnProfile, cast_string_column
+from helpers import known_answers, oracle_table, product_table
+
+pytestmark = pytest.mark.gpu
+KA = known_answers()
+
+
+@pytest.mark.parametrize("case", KA["datatype_cases"], ids=[c["id"] for c in KA["datatype_cases"]])
+def test_datatype_known_answers(gpu, case):
+    table = product_table(KA["tables"][case["table"]])
+    a = d.DataType(case["column"])
+    state = a.computeStateFrom(table)
+    assert list(state.counts()) == case["expected"], case["source"]
+    m = a.calculate(table)
+    total = sum(case["expected"])
+    for name, c in zip(d.DataTypeInstances.NAMES, case["expected"]):
+        assert m.value.get()[name] == d.DistributionValue(c, c / total), (case["source"], name)
+
+
+def test_datatype_fused_with_other_analyzers(gpu):
+    spec = KA["tables"]["dfBoolNull"]
+    table = product_table(spec)
+    analyzers = [d.DataType("att1"), d.Completeness("att1"), d.ApproxCountDistinct("att1"), d.Size(),
+                 d.DataType("item"), d.DataType("att1", "item != '4'")]
+    ctx = d.AnalysisRunner.onData(table).addAnalyzers(analyzers).run()
+    assert ctx.metric(analyzers[0]).value.get()["Boolean"].absolute == 2
+    assert ctx.metric(analyzers[4]).value.get()["Integral"].absolute == 4
+    # where-filtered rows are NULL inputs: "2.0" (item 4) becomes Unknown
+    dist = ctx.metric(analyzers[5]).value.get()
+    assert (dist["Unknown"].absolute, dist["Fractional"].absolute) == (2, 0)
+
+
+_ALPHABET = ["0", "1", "7", "9", ".", "-", "+", " ", "a", "e", "E", "true", "false", "\n", "é", "x"]
+
+
+def _random_strings(rng, n):
+    out = []
+    for _ in range(n):
+        r = rng.random()
+        if r < 0.08:
+            out.append(None)
+        elif r < 0.14:
+            out.append(["true", "false", "True", "", ".", "-", "+", " ", "-.", "+ .5", "- 12"][rng.integers(0, 11)])
+        else:
+            k = int(rng.integers(0, 9))
+            out.append("".join(_ALPHABET[int(rng.integers(0, len(_ALPHABET)))] if rng.random() < 0.25
+                               else str(int(rng.integers(0, 10))) for _ in range(k)))
+    return out
+
+
+@pytest.mark.parametrize("n", [1, 63, 2049, 20000])
+def test_datatype_random_strings_match_oracle(gpu, n):
+    rng = np.random.default_rng(n)
+    spec = {"s": ["string", _random_strings(rng, n)], "w": ["int32", [int(x) for x in rng.integers(0, 3, n)]]}
+    table, ot = product_table(spec), oracle_table(spec)
+    for where in (None, "w > 0"):
+        got = d.DataType("s", where).computeStateFrom(table)
+        assert got.counts() == O.datatype_state(ot, "s", where), where
+
+
+def test_datatype_numeric_columns_match_oracle(gpu):
+    rng = np.random.default_rng(3)
+    n = 5000
+    f64 = [float(x) for x in rng.choice([0.0, -0.0, 1e-3, 9.999999999999998e-4, 1e7, 9999999.999999998,
+                                         float("nan"), float("inf"), -float("inf"), 2.5, -123.25, 1e-5, 3e9],
+                                        n)]
+    f32 = [float(np.float32(x)) for x in rng.choice([0.0, 1e-3, 9.99e-4, 1e7, 9999999.0, 1.5, float("nan"),
+                                                     -2.25, 1e-8], n)]
+    spec = {"f64": ["float64", [None if i % 9 == 0 else v for i, v in enumerate(f64)]],
+            "f32": ["float32", f32],
+            "i8": ["int8", [int(x) for x in rng.integers(-128, 127, n)]],
+            "i64": ["int64", [int(x) for x in rng.integers(-2 ** 62, 2 ** 62, n)]],
+            "b": ["bool", [bool(x) for x in rng.integers(0, 2, n)]]}
+    table, ot = product_table(spec), oracle_table(spec)
+    for c in spec:
+        assert d.DataType(c).computeStateFrom(table).counts() == O.datatype_state(ot, c), c
+
+
+# ---- string casts: restatements of Spark 2.2.2's two parsers (test-local)
+def _spark_to_long(s):
+    """UTF8String.toLong (Spark 2.2): sign, digits, optional '.' + digits (truncated)."""
+    b = s.encode()
+    if not b:
+        return None
+    neg = b[0:1] == b"-"
+    i = 1 if (neg or b[0:1] == b"+") else 0
+    if i and len(b) == 1:
+        return None
+    r = 0
+    while i < len(b):
+        c = b[i]
+        i += 1
+        if c == ord("."):
+            break
+        if not 48 <= c <= 57:
+            return None
+        r = r * 10 + (c - 48)
+    if any(not 48 <= c <= 57 for c in b[i:]):
+        return None
+    r = -r if neg else r
+    return r if -2 ** 63 <= r < 2 ** 63 else None
+
+
+def _java_parse_double(s):
+    """java.lang.Double.parseDouble for decimal forms (trim, sign, digits, '.', exponent,
+    f/d suffix, NaN, Infinity); Python float() rounds correctly as Java does."""
+    i, j = 0, len(s)
+    while i < j and ord(s[i]) <= 32:  # String.trim()
+        i += 1
+    while j > i and ord(s[j - 1]) <= 32:
+        j -= 1
+    t = s[i:j]
+    if not t:
+        return None
+    import re
+    body = t[1:] if t[0] in "+-" else t
+    if body in ("NaN", "Infinity"):
+        return float(t.replace("Infinity", "inf").replace("NaN", "nan"))
+    if not re.fullmatch(r"[+-]?([0-9]+\.?[0-9]*|\.[0-9]+)([eE][+-]?[0-9]+)?[fFdD]?", t):
+        return None
+    return float(t.rstrip("fFdD"))
+
+
+def test_cast_to_long_matches_spark(gpu):
+    vals = ["1", "-1", "+7", "", "-", "+", "12.5", "12.", "1.2.3", " 5", "5 ", "- 5", "007",
+            "9223372036854775807", "9223372036854775808", "-9223372036854775808", "-9223372036854775809",
+            "1e3", "abc", None, "0", "-0", "123456789012", "3.x"]
+    col = d.Column.from_pylist(vals, "string")
+    out = cast_string_column(col, "int64")
+    got = out.to_pylist()
+    assert got == [None if v is None else _spark_to_long(v) for v in vals]
+
+
+def test_cast_to_double_matches_java(gpu):
+    rng = np.random.default_rng(9)
+    vals = ["1.5", "-0.25", ".5", "5.", ".", "-.", "", "  2.0  ", "- 1.5", "+3", "1e3", "1E-3", "2.5f", "7d",
+            "NaN", "-Infinity", "Infinity", "1234567890123456", "0.1", "0", "-0.0", None, "1.0e22",
+            "4.35", "123.456e-5", "abc", "1,5"]
+    vals += ["%d.%0*d" % (int(rng.integers(0, 10 ** 6)), int(k), int(rng.integers(0, 10 ** int(k))))
+             for k in rng.integers(1, 9, 400)]
+    col = d.Column.from_pylist(vals, "string")
+    got = cast_string_column(col, "float64").to_pylist()
+    for v, g in zip(vals, got):
+        want = None if v is None else _java_parse_double(v)
+        if want is None:
+            assert g is None, (v, g)
+        elif math.isnan(want):
+            assert g is not None and math.isnan(g), v
+        else:
+            assert g is not None and struct.pack("<d", g) == struct.pack("<d", want), (v, g, want)
+
+
+def test_cast_off_fast_path_is_unsupported(gpu):
+    col = d.Column.from_pylist(["1.25", "3.14159265358979323846264"], "string")
+    from deequ_amd._lib import UnsupportedOnGpu
+    with pytest.raises(UnsupportedOnGpu):
+        cast_string_column(col, "float64")
+
+
+# ---- ColumnProfiler known answers
+@pytest.mark.parametrize("case", KA["profile_cases"], ids=[c["id"] for c in KA["profile_cases"]])
+def test_profiler_known_answers(gpu, case):
+    table = product_table(KA["tables"][case["table"]])
+    profiles = ColumnProfiler.profile(table, case["restrict"], False, case["threshold"],
+                                      predefinedTypes=case["predefined"])
+    p = profiles.profiles[case["column"]]
+    e = case["expect"]
+    if "histogram_values" in e:
+        assert p.histogram is not None
+        for k, (c, r) in e["histogram_values"].items():
+            assert p.histogram[k] == d.DistributionValue(c, r), (case["source"], k)
+        return
+    assert isinstance(p, NumericColumnProfile) == (e["kind"] == "numeric"), case["source"]
+    assert p.completeness == e["completeness"]
+    assert p.approximateNumDistinctValues == e["approx"]
+    assert p.dataType == e["dataType"]
+    assert p.isDataTypeInferred == e["inferred"]
+    assert p.typeCounts == e["typeCounts"]
+    if e["histogram"] is None:
+        assert p.histogram is None
+    else:
+        assert p.histogram.numberOfBins == e["histogram"]["bins"]
+        assert {k: [v.absolute, v.ratio] for k, v in p.histogram.values.items()} == e["histogram"]["values"]
+    if e["kind"] == "numeric":
+        for f in ("mean", "maximum", "minimum", "sum", "stdDev"):
+            assert getattr(p, f) == e[f], (case["source"], f)
+
+
+def test_profiler_runner_and_json(gpu):
+    table = product_table(KA["tables"]["dfCompleteIncomplete"])
+    profiles = ColumnProfilerRunner().onData(table).withLowCardinalityHistogramThreshold(10).run()
+    assert profiles.numRecords == 6
+    assert set(profiles.profiles) == {"item", "att1", "att2"}
+    assert profiles.profiles["att1"].histogram["a"] == d.DistributionValue(4, 4 / 6.0)
+    import json
+    from deequ_amd.profiles import ColumnProfiles
+    j = json.loads(ColumnProfiles.toJson(list(profiles.profiles.values())))
+    assert [c["column"] for c in j["columns"]] == ["item", "att1", "att2"]
+    assert j["columns"][0]["dataType"] == "Integral" and j["columns"][0]["mean"] == 3.5

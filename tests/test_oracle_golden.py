@@ -100,3 +100,29 @@ def test_predicate_three_valued_logic():
     assert O.eval_predicate("a IN (1, 3)", t) == [True, None, True]
     assert O.eval_predicate("a > 1.5", t) == [False, None, True]
     assert O.eval_predicate("a IS NULL", t) == [False, True, False]
+
+
+@pytest.mark.parametrize("case", KA["datatype_cases"], ids=[c["id"] for c in KA["datatype_cases"]])
+def test_oracle_datatype_known_answers(case):
+    table = oracle_table(KA["tables"][case["table"]])
+    assert list(O.datatype_state(table, case["column"])) == case["expected"], case["source"]
+
+
+def test_datatype_host_logic():
+    """DataTypeHistogram.toDistribution / determineType (DataType.scala:98-143) on the host."""
+    import deequ_amd as d
+    from deequ_amd.analyzers import data_type_distribution, determine_type
+    h = d.DataTypeHistogram(1, 0, 5, 0, 0)
+    dist = data_type_distribution(h)
+    assert dist.numberOfBins == 5
+    assert dist["Unknown"] == d.DistributionValue(1, 1.0 / 6.0)
+    assert dist["Integral"] == d.DistributionValue(5, 5.0 / 6.0)
+    I = d.DataTypeInstances
+    assert determine_type(dist) == I.Integral
+    assert determine_type(data_type_distribution(d.DataTypeHistogram(3, 0, 0, 0, 0))) == I.Unknown
+    assert determine_type(data_type_distribution(d.DataTypeHistogram(0, 1, 1, 0, 0))) == I.Fractional
+    assert determine_type(data_type_distribution(d.DataTypeHistogram(0, 0, 1, 1, 0))) == I.String
+    assert determine_type(data_type_distribution(d.DataTypeHistogram(1, 0, 0, 2, 0))) == I.Boolean
+    assert determine_type(data_type_distribution(d.DataTypeHistogram(0, 1, 0, 0, 1))) == I.String
+    assert h.sum(d.DataTypeHistogram(1, 2, 3, 4, 5)) == d.DataTypeHistogram(2, 2, 8, 4, 5)
+    assert d.DataTypeHistogram.fromBytes(h.toBytes()) == h and len(h.toBytes()) == 40
