@@ -66,8 +66,28 @@ static bool valid_type(int t) { return t >= DQ_T_BOOL && t <= DQ_T_UTF8; }
 struct DevBuf {
   void* ptr = nullptr;
   size_t cap = 0;
-  ~DevBuf() {
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : ptr(o.ptr), cap(o.cap) {
+    o.ptr = nullptr;
+    o.cap = 0;
+  }
+  DevBuf& operator=(DevBuf&& o) noexcept {
+    if (this != &o) {
+      release();
+      ptr = o.ptr;
+      cap = o.cap;
+      o.ptr = nullptr;
+      o.cap = 0;
+    }
+    return *this;
+  }
+  ~DevBuf() { release(); }
+  void release() {
     if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    cap = 0;
   }
   dq_status ensure(size_t bytes) {
     if (bytes <= cap) return DQ_OK;

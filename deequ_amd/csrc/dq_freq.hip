@@ -210,9 +210,19 @@ __device__ bool make_key(const FreqKeySpec& ks, const DevColumn* cols, int64_t r
   return true;
 }
 
+// Hash bit use: the top bucket_bits select the slice, the low kFreqSliceLog bits the first
+// probe, bits 12..43 the 32-bit tag kept in ctrl (independent of both).
 __device__ inline uint32_t tag_of(uint64_t h) {
-  const uint32_t t = (uint32_t)(h >> 32);
+  const uint32_t t = (uint32_t)(h >> 12);
   return t ? t : 1u;
+}
+
+__device__ inline uint64_t slice_of(const FreqTable& T, uint64_t h) {
+  return T.bucket_bits ? (h >> (64 - T.bucket_bits)) : 0ull;
+}
+
+__device__ inline uint64_t probe_slot(const FreqTable& T, uint64_t h, uint64_t i) {
+  return (slice_of(T, h) << kFreqSliceLog) | ((h + i) & (kFreqSliceSlots - 1));
 }
 
 // Compare a long key with heap bytes (heap words written by atomic exchange: read coherently).
@@ -230,9 +240,10 @@ __device__ bool global_insert(const FreqTable& T, const Key& k, unsigned long lo
   const uint32_t tag = tag_of(k.hash);
   const bool inl = k.len <= 16;
   const unsigned long long want = ((unsigned long long)tag << 32) | (inl ? 0ull : kHeapKey) | k.len;
-  uint64_t slot = k.hash & T.mask;
+  uint64_t probes = 0;
+  uint64_t slot = probe_slot(T, k.hash, 0);
   uint32_t waits = 0;
-  for (uint64_t probes = 0; probes <= T.mask;) {
+  while (probes < kFreqSliceSlots) {
     FreqSlot* e = &T.slots[slot];
     unsigned long long c = atomicCAS(&e->ctrl, 0ull, want);
     if (c == 0ull) {  // claimed: publish key, count, then READY
@@ -279,8 +290,7 @@ __device__ bool global_insert(const FreqTable& T, const Key& k, unsigned long lo
         return true;
       }
     }
-    slot = (slot + 1) & T.mask;
-    ++probes;
+    slot = probe_slot(T, k.hash, ++probes);
   }
   atomicOr(T.overflow, 1u);
   return false;
@@ -483,6 +493,188 @@ __global__ __launch_bounds__(kBlock) void dq_freq_part_scatter_kernel(FreqTable 
   }
 }
 
+// ---- sorted-bucket path ---------------------------------------------------------------------
+// High-cardinality group-by without device-scope atomics per row: rows are staged as 16-B
+// records (one streaming pass), bucketed by the slice their hash selects, sorted by bucket
+// (rocprim radix sort, dq_sort.hip), and every slice is then aggregated by ONE workgroup in LDS
+// and written back with plain stores (the workgroup owns its slice).  Keys of up to 15 bytes.
+constexpr unsigned long long kRecLenShift = 56;
+constexpr unsigned long long kRecKeyMask = (1ull << kRecLenShift) - 1;
+
+__device__ inline void rec_unpack(const FreqRec& r, unsigned long long* k1, uint32_t* len) {
+  *len = (uint32_t)(r.k1 >> kRecLenShift);
+  *k1 = r.k1 & kRecKeyMask;
+}
+
+// HLL++-style sketch of the staged hashes (p = 9, as deequ's): an estimate of the number of
+// distinct keys, used only to size the table before aggregation.
+__device__ inline void sketch_update(uint32_t* regs, uint64_t h) {
+  uint32_t idx, pw;
+  hll_idx_rank(h, &idx, &pw);
+  if (pw > regs[idx]) atomicMax(&regs[idx], pw);
+}
+
+__global__ __launch_bounds__(kBlock) void dq_freq_stage_kernel(FreqKeySpec ks, const DevColumn* __restrict__ cols,
+                                                               int64_t n_rows, FreqRec* out,
+                                                               unsigned long long* cursor, uint32_t* hll) {
+  __shared__ uint32_t regs[kHllM];
+  for (int i = threadIdx.x; i < kHllM; i += kBlock) regs[i] = 0u;
+  __syncthreads();
+  alignas(8) uint8_t scratch[kMaxLocalKey];
+  const uint32_t lane = threadIdx.x & 63u;
+  for (int64_t base = (int64_t)blockIdx.x * kBlock; base < n_rows; base += (int64_t)gridDim.x * kBlock) {
+    const int64_t row = base + threadIdx.x;
+    Key k;
+    bool ok = false;
+    if (row < n_rows) {
+      bool too_long;
+      ok = make_key(ks, cols, row, k, scratch, too_long) && k.len <= 15 && k.ptr == nullptr;
+    }
+    const uint64_t m = __ballot(ok);
+    unsigned long long w = 0;
+    if (lane == 0 && m) w = atomicAdd(cursor, (unsigned long long)__builtin_popcountll(m));
+    w = __shfl(w, 0, 64);
+    if (ok) {
+      const unsigned long long pos = w + __builtin_popcountll(m & ((1ull << lane) - 1ull));
+      FreqRec r;
+      r.k0 = k.k0;
+      r.k1 = k.k1 | ((unsigned long long)k.len << kRecLenShift);
+      out[pos] = r;
+      sketch_update(regs, k.hash);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kHllM; i += kBlock)
+    if (regs[i]) atomicMax(&hll[i], regs[i]);
+}
+
+__global__ __launch_bounds__(kBlock) void dq_freq_bucket_kernel(const FreqRec* __restrict__ recs, uint64_t n,
+                                                                int bucket_bits, uint32_t* keys) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    const FreqRec r = recs[i];
+    unsigned long long k1;
+    uint32_t len;
+    rec_unpack(r, &k1, &len);
+    const uint64_t h = hash_inline(r.k0, k1, len);
+    keys[i] = bucket_bits ? (uint32_t)(h >> (64 - bucket_bits)) : 0u;
+  }
+}
+
+// off[b] = first sorted position with key >= b (b = 0 .. n_buckets).
+__global__ __launch_bounds__(kBlock) void dq_freq_bounds_kernel(const uint32_t* __restrict__ keys, uint64_t n,
+                                                                uint64_t n_buckets, uint64_t* off) {
+  for (uint64_t b = (uint64_t)blockIdx.x * kBlock + threadIdx.x; b <= n_buckets; b += (uint64_t)gridDim.x * kBlock) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if ((uint64_t)keys[mid] < b) lo = mid + 1;
+      else hi = mid;
+    }
+    off[b] = lo;
+  }
+}
+
+// One workgroup per slice: the slice's groups and its bucket's records meet in LDS.  LDS slot
+// words: K1 = EMPTY / BUSY (being published) / FOREIGN (a group this path cannot hold: a long
+// or 16-byte key) / the record's k1 (length in the top byte); K0 = low key bytes; C = new rows.
+constexpr unsigned long long kLdsEmpty = ~0ull;
+constexpr unsigned long long kLdsBusy = ~0ull - 1ull;
+constexpr unsigned long long kLdsForeign = 0xFEull << kRecLenShift;
+
+__global__ __launch_bounds__(kBlock) void dq_freq_agg_kernel(FreqTable T, const FreqRec* __restrict__ recs,
+                                                             const uint64_t* __restrict__ off, uint64_t n_buckets,
+                                                             FreqRec* retry, unsigned long long* n_retry,
+                                                             unsigned long long* new_groups) {
+  constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
+  __shared__ unsigned long long K0[S], K1[S];
+  __shared__ uint32_t C[S];
+  __shared__ int overflow;
+  __shared__ uint32_t fresh;
+  __shared__ unsigned long long retry_base;
+  for (uint64_t b = blockIdx.x; b < n_buckets; b += gridDim.x) {
+    const uint64_t r0 = off[b], r1 = off[b + 1];
+    if (r0 == r1) continue;  // uniform: every thread reads the same bounds
+    FreqSlot* slice = T.slots + (b << kFreqSliceLog);
+    for (uint32_t s = threadIdx.x; s < S; s += kBlock) {
+      const FreqSlot e = slice[s];
+      const uint32_t len = (uint32_t)(e.ctrl & kLenMask);
+      if (!(e.ctrl & kReady)) {
+        K1[s] = kLdsEmpty;
+      } else if ((e.ctrl & kHeapKey) || len > 15) {
+        K1[s] = kLdsForeign;
+      } else {
+        K0[s] = e.k0;
+        K1[s] = e.k1 | ((unsigned long long)len << kRecLenShift);
+      }
+      C[s] = 0u;
+    }
+    if (threadIdx.x == 0) {
+      overflow = 0;
+      fresh = 0u;
+    }
+    __syncthreads();
+    for (uint64_t i = r0 + threadIdx.x; i < r1; i += kBlock) {
+      const FreqRec r = recs[i];
+      unsigned long long k1;
+      uint32_t len;
+      rec_unpack(r, &k1, &len);
+      const uint64_t h = hash_inline(r.k0, k1, len);
+      uint32_t s = (uint32_t)(h & (S - 1));
+      bool done = false;
+      for (uint32_t probe = 0; probe < S && !done;) {
+        const unsigned long long c = atomicCAS(&K1[s], kLdsEmpty, kLdsBusy);
+        if (c == kLdsEmpty) {  // claimed: publish the key, then count
+          K0[s] = r.k0;
+          __threadfence_block();
+          atomicExch(&K1[s], r.k1);
+          atomicAdd(&C[s], 1u);
+          done = true;
+        } else if (c == kLdsBusy) {
+          // another lane is publishing this slot: look at it again
+        } else if (c == r.k1 &&
+                   __hip_atomic_load(&K0[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == r.k0) {
+          atomicAdd(&C[s], 1u);
+          done = true;
+        } else {
+          s = (s + 1) & (S - 1);
+          ++probe;
+        }
+      }
+      if (!done) overflow = 1;
+    }
+    __syncthreads();
+    if (overflow) {  // the slice is full: leave it untouched, hand the bucket's rows back
+      if (threadIdx.x == 0) retry_base = atomicAdd(n_retry, (unsigned long long)(r1 - r0));
+      __syncthreads();
+      for (uint64_t i = r0 + threadIdx.x; i < r1; i += kBlock) retry[retry_base + (i - r0)] = recs[i];
+    } else {
+      for (uint32_t s = threadIdx.x; s < S; s += kBlock) {
+        const uint32_t c = C[s];
+        if (!c) continue;
+        FreqSlot& e = slice[s];
+        if (e.ctrl & kReady) {
+          e.count += c;
+        } else {
+          const unsigned long long k1 = K1[s];
+          const uint32_t len = (uint32_t)(k1 >> kRecLenShift);
+          const unsigned long long key1 = k1 & kRecKeyMask;
+          const uint64_t h = hash_inline(K0[s], key1, len);
+          FreqSlot n;
+          n.ctrl = ((unsigned long long)tag_of(h) << 32) | kReady | len;
+          n.count = c;
+          n.k0 = K0[s];
+          n.k1 = key1;
+          e = n;
+          atomicAdd(&fresh, 1u);
+        }
+      }
+      __syncthreads();
+      if (threadIdx.x == 0 && fresh) atomicAdd(new_groups, (unsigned long long)fresh);
+    }
+    __syncthreads();  // LDS is reused by the next slice
+  }
+}
+
 // Table growth: move every group of `old_slots` into the (empty, larger) table T.  All keys
 // are distinct, so a slot is claimed with its final ctrl word and nobody compares keys.
 __global__ __launch_bounds__(kBlock) void dq_freq_rehash_kernel(const FreqSlot* __restrict__ old_slots,
@@ -492,16 +684,17 @@ __global__ __launch_bounds__(kBlock) void dq_freq_rehash_kernel(const FreqSlot* 
     if (!(e.ctrl & kReady)) continue;
     const uint32_t len = (uint32_t)(e.ctrl & kLenMask);
     const uint64_t h = (e.ctrl & kHeapKey) ? xxh64_any(T.heap + e.k0, len, 42) : hash_inline(e.k0, e.k1, len);
-    uint64_t slot = h & T.mask;
-    for (uint64_t it = 0; it <= T.mask; ++it) {
+    uint64_t it = 0;
+    for (; it < kFreqSliceSlots; ++it) {
+      const uint64_t slot = probe_slot(T, h, it);
       if (atomicCAS(&T.slots[slot].ctrl, 0ull, e.ctrl) == 0ull) {
         T.slots[slot].count = e.count;
         T.slots[slot].k0 = e.k0;
         T.slots[slot].k1 = e.k1;
         break;
       }
-      slot = (slot + 1) & T.mask;
     }
+    if (it == kFreqSliceSlots) atomicOr(T.overflow, 1u);
   }
 }
 
@@ -526,6 +719,45 @@ hipError_t launch_freq_part_scatter(const FreqTable& T, int n_parts, const unsig
   return hipGetLastError();
 }
 
+hipError_t launch_freq_stage(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, FreqRec* d_out,
+                             unsigned long long* d_cursor, uint32_t* d_hll, hipStream_t stream) {
+  if (n_rows <= 0) return hipSuccess;
+  int64_t blocks = (n_rows + kBlock * 8 - 1) / (kBlock * 8);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(dq_freq_stage_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, ks, d_cols, n_rows, d_out,
+                     d_cursor, d_hll);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_bucket(const FreqRec* d_recs, uint64_t n, int bucket_bits, uint32_t* d_keys,
+                              hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  uint64_t blocks = (n + kBlock * 8 - 1) / (kBlock * 8);
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(dq_freq_bucket_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, d_recs, n, bucket_bits,
+                     d_keys);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_bounds(const uint32_t* d_sorted_keys, uint64_t n, uint64_t n_buckets, uint64_t* d_off,
+                              hipStream_t stream) {
+  uint64_t blocks = (n_buckets + 1 + kBlock - 1) / kBlock;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(dq_freq_bounds_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, d_sorted_keys, n,
+                     n_buckets, d_off);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_agg(const FreqTable& T, const FreqRec* d_recs, const uint64_t* d_off, uint64_t n_buckets,
+                           FreqRec* d_retry, unsigned long long* d_n_retry, unsigned long long* d_new_groups,
+                           hipStream_t stream) {
+  uint64_t blocks = n_buckets < 65536 ? n_buckets : 65536;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(dq_freq_agg_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, d_recs, d_off, n_buckets,
+                     d_retry, d_n_retry, d_new_groups);
+  return hipGetLastError();
+}
+
 hipError_t launch_freq_rehash(const FreqSlot* d_old, uint64_t old_n, const FreqTable& T, hipStream_t stream) {
   uint64_t blocks = (old_n + kBlock * 8 - 1) / (kBlock * 8);
   if (blocks > 8192) blocks = 8192;
@@ -536,8 +768,10 @@ hipError_t launch_freq_rehash(const FreqSlot* d_old, uint64_t old_n, const FreqT
 
 // Bytes of long (> 16 B) single-string keys in a batch: the key heap is grown to fit first.
 __global__ __launch_bounds__(kBlock) void dq_freq_heap_need_kernel(FreqKeySpec ks, const DevColumn* __restrict__ cols,
-                                                                   int64_t n_rows, unsigned long long* need) {
+                                                                   int64_t n_rows, unsigned long long* need,
+                                                                   unsigned long long* max_len) {
   unsigned long long local = 0;
+  unsigned int longest = 0;
   for (int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x; row < n_rows; row += (int64_t)gridDim.x * kBlock) {
     uint32_t n = 0;
     bool any_null = false;
@@ -551,10 +785,17 @@ __global__ __launch_bounds__(kBlock) void dq_freq_heap_need_kernel(FreqKeySpec k
       else n += (uint32_t)width_of(c.type);
     }
     if (any_null && !(ks.null_as_key && ks.n_keys == 1)) n = 0;
+    if (any_null && ks.null_as_key && ks.n_keys == 1 && cols[ks.key_cols[0]].type == DQ_T_UTF8) n = 9;  // "NullValue"
     if (n > 16) local += (n + 7u) & ~7u;
+    longest = n > longest ? n : longest;
   }
-  for (int d = 32; d >= 1; d >>= 1) local += __shfl_down(local, d, 64);
+  for (int d = 32; d >= 1; d >>= 1) {
+    local += __shfl_down(local, d, 64);
+    const unsigned int o = __shfl_down(longest, d, 64);
+    longest = o > longest ? o : longest;
+  }
   if ((threadIdx.x & 63) == 0 && local) atomicAdd(need, local);
+  if ((threadIdx.x & 63) == 0 && longest) atomicMax(max_len, (unsigned long long)longest);
 }
 
 hipError_t launch_freq_insert(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
@@ -597,12 +838,12 @@ hipError_t launch_freq_import(const FreqTable& T, const FreqIn& in, hipStream_t 
 }
 
 hipError_t launch_freq_heap_need(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
-                                 unsigned long long* d_need, hipStream_t stream) {
+                                 unsigned long long* d_need, unsigned long long* d_max_len, hipStream_t stream) {
   if (n_rows <= 0) return hipSuccess;
   int64_t blocks = (n_rows + kBlock * 16 - 1) / (kBlock * 16);
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(dq_freq_heap_need_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, ks, d_cols,
-                     n_rows, d_need);
+                     n_rows, d_need, d_max_len);
   return hipGetLastError();
 }
 

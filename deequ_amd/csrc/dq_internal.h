@@ -133,9 +133,23 @@ struct FreqSlot {  // 32 B; see dq_freq.hip for the ctrl word
   unsigned long long ctrl, count, k0, k1;
 };
 
+// The table is an array of 2^bucket_bits slices of kFreqSliceSlots slots; a key lives in the
+// slice selected by the top bucket_bits bits of its hash and probes linearly inside it.  A
+// slice (64 KiB of slots) is what one workgroup aggregates in LDS (dq_freq_agg_kernel).
+constexpr int kFreqSliceLog = 11;
+constexpr uint64_t kFreqSliceSlots = 1ull << kFreqSliceLog;
+
+// A staged row of the sorted-bucket path: key bytes 0..14 (zero padded) in k0 and the low 7
+// bytes of k1, the key length (<= 15) in the top byte of k1.
+struct alignas(16) FreqRec {
+  unsigned long long k0, k1;
+};
+
 struct FreqTable {
   FreqSlot* slots;
-  uint64_t mask;                   // capacity - 1 (capacity is a power of two)
+  uint64_t mask;                   // capacity - 1 (capacity: a power of two >= kFreqSliceSlots)
+  int32_t bucket_bits;             // log2(capacity / kFreqSliceSlots)
+  int32_t pad_;
   unsigned long long* n_groups;    // device counter of claimed slots
   uint8_t* heap;                   // key bytes of keys longer than 16 B
   unsigned long long* heap_used;
@@ -176,7 +190,7 @@ hipError_t launch_freq_export(const FreqTable& T, unsigned long long min_count, 
                               hipStream_t stream);
 hipError_t launch_freq_import(const FreqTable& T, const FreqIn& in, hipStream_t stream);
 hipError_t launch_freq_heap_need(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
-                                 unsigned long long* d_need, hipStream_t stream);
+                                 unsigned long long* d_need, unsigned long long* d_max_len, hipStream_t stream);
 // Multi-GPU key-hash exchange: owner rank of a group = freq_owner(hash, n_parts).  `d_cnt` gets
 // per part {groups, long-key bytes}; the scatter writes part p's groups (FreqSlot records, k0 of
 // a long key = offset in the part's key region) from d_base[2p] / d_base[2p+1] on.
@@ -184,6 +198,19 @@ hipError_t launch_freq_part_count(const FreqTable& T, int n_parts, unsigned long
 hipError_t launch_freq_part_scatter(const FreqTable& T, int n_parts, const unsigned long long* d_base,
                                     unsigned long long* d_cursor, FreqSlot* out_groups, uint8_t* out_keys,
                                     hipStream_t stream);
+// Sorted-bucket path (dq_freq.hip, dq_sort.hip): stage rows as FreqRec (+ an HLL sketch of
+// their hashes, to size the table), bucket them, sort by bucket, aggregate each slice in LDS.
+hipError_t launch_freq_stage(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, FreqRec* d_out,
+                             unsigned long long* d_cursor, uint32_t* d_hll, hipStream_t stream);
+hipError_t launch_freq_bucket(const FreqRec* d_recs, uint64_t n, int bucket_bits, uint32_t* d_keys,
+                              hipStream_t stream);
+hipError_t sort_freq_records(void* d_tmp, size_t& tmp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
+                             const FreqRec* recs_in, FreqRec* recs_out, uint64_t n, int bits, hipStream_t stream);
+hipError_t launch_freq_bounds(const uint32_t* d_sorted_keys, uint64_t n, uint64_t n_buckets, uint64_t* d_off,
+                              hipStream_t stream);
+hipError_t launch_freq_agg(const FreqTable& T, const FreqRec* d_recs, const uint64_t* d_off, uint64_t n_buckets,
+                           FreqRec* d_retry, unsigned long long* d_n_retry, unsigned long long* d_new_groups,
+                           hipStream_t stream);
 hipError_t launch_freq_rehash(const FreqSlot* d_old, uint64_t old_n, const FreqTable& T, hipStream_t stream);
 
 // ---------------------------------------------------------------- launchers (.hip files)

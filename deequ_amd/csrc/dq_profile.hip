@@ -148,6 +148,16 @@ __device__ bool parse_long(const uint8_t* p, int32_t n, int64_t* out) {
   return true;
 }
 
+__device__ const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                      1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+__device__ inline bool bytes_are(const uint8_t* p, int32_t n, const char* w, int32_t len) {
+  if (n != len) return false;
+  for (int32_t k = 0; k < len; ++k)
+    if (p[k] != (uint8_t)w[k]) return false;
+  return true;
+}
+
 // 0 = NULL (NumberFormatException), 1 = value, 2 = well formed but off the exact fast path
 __device__ int parse_double(const uint8_t* p, int32_t n, double* out) {
   int32_t i = 0, e = n;
@@ -159,52 +169,47 @@ __device__ int parse_double(const uint8_t* p, int32_t n, double* out) {
     neg = p[i] == '-';
     ++i;
   }
-  const int32_t rest = e - i;
-  auto is = [&](const char* w, int32_t len) {
-    if (rest != len) return false;
-    for (int32_t k = 0; k < len; ++k)
-      if (p[i + k] != (uint8_t)w[k]) return false;
-    return true;
-  };
-  if (is("NaN", 3)) {
+  if (bytes_are(p + i, e - i, "NaN", 3)) {
     *out = __builtin_nan("");
     return 1;
   }
-  if (is("Infinity", 8)) {
+  if (bytes_are(p + i, e - i, "Infinity", 8)) {
     *out = neg ? -__builtin_huge_val() : __builtin_huge_val();
     return 1;
   }
-  if (rest >= 2 && p[i] == '0' && (p[i + 1] == 'x' || p[i + 1] == 'X')) return 2;  // hex float
-  // optional f/F/d/D type suffix
-  if (e > i && (p[e - 1] == 'f' || p[e - 1] == 'F' || p[e - 1] == 'd' || p[e - 1] == 'D')) --e;
+  if (e - i >= 2 && p[i] == '0' && (p[i + 1] == 'x' || p[i + 1] == 'X')) return 2;  // hex float
+  const uint32_t last = p[e - 1];  // optional f/F/d/D type suffix
+  if (last == 'f' || last == 'F' || last == 'd' || last == 'D') --e;
   uint64_t m = 0;
-  int sig = 0, exp10 = 0, ndig = 0;
+  int32_t sig = 0, exp10 = 0, ndig = 0;
   bool dropped = false, dot = false;
-  for (; i < e; ++i) {
+  while (i < e) {
     const uint32_t c = p[i];
     if (c == '.') {
       if (dot) return 0;
       dot = true;
+      ++i;
       continue;
     }
-    if (c - '0' >= 10u) break;
+    const uint32_t dg = c - 48u;
+    if (dg > 9u) break;
     ++ndig;
-    if (m == 0 && c == '0') {  // leading zeros carry no significance
+    ++i;
+    if (m == 0 && dg == 0) {  // leading zeros carry no significance
       if (dot) --exp10;
-      continue;
-    }
-    if (sig < 19) {
-      m = m * 10 + (c - '0');
+    } else if (sig < 19) {
+      m = m * 10u + dg;
       ++sig;
       if (dot) --exp10;
     } else {
-      if (c != '0') dropped = true;
+      dropped = dropped || dg != 0;
       if (!dot) ++exp10;
     }
   }
   if (ndig == 0) return 0;
   if (i < e) {  // exponent
-    if (p[i] != 'e' && p[i] != 'E') return 0;
+    const uint32_t c = p[i];
+    if (c != 'e' && c != 'E') return 0;
     ++i;
     bool eneg = false;
     if (i < e && (p[i] == '+' || p[i] == '-')) {
@@ -212,23 +217,22 @@ __device__ int parse_double(const uint8_t* p, int32_t n, double* out) {
       ++i;
     }
     if (i == e) return 0;
-    int64_t x = 0;
-    for (; i < e; ++i) {
-      const uint32_t c = p[i];
-      if (c - '0' >= 10u) return 0;
-      if (x < 100000) x = x * 10 + (c - '0');
+    int32_t x = 0;
+    while (i < e) {
+      const uint32_t dg = (uint32_t)p[i] - 48u;
+      if (dg > 9u) return 0;
+      if (x < 100000) x = x * 10 + (int32_t)dg;
+      ++i;
     }
-    exp10 += (int)(eneg ? -x : x);
+    exp10 += eneg ? -x : x;
   }
   if (m == 0) {
     *out = neg ? -0.0 : 0.0;
     return 1;
   }
   if (dropped || m > (1ull << 53) || exp10 < -22 || exp10 > 22) return 2;
-  const double pow10[23] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11,
-                            1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
   double v = (double)m;  // exact: m <= 2^53
-  v = exp10 >= 0 ? v * pow10[exp10] : v / pow10[-exp10];  // one correctly rounded operation
+  v = exp10 >= 0 ? v * kPow10[exp10] : v / kPow10[-exp10];  // one correctly rounded operation
   *out = neg ? -v : v;
   return 1;
 }

@@ -1,0 +1,82 @@
+"""Both group-by paths of dq_freq against the oracle, and against each other.
+
+* sorted-bucket path (default for keys of <= 15 bytes): rows staged as 16-B records, sorted by
+  slice, aggregated per slice in LDS;
+* atomic path (keys > 15 bytes, or DQ_FREQ_PATH=atomic): per-row inserts with device atomics;
+* a tiny staging budget (DQ_FREQ_STAGE_BUDGET) forces aggregation in the middle of a batch
+  sequence, and a table mixing short and long keys exercises both paths on one table.
+Bit-exact: every group and count; #groups, #unique, top-N."""
+import os
+
+import numpy as np
+import pytest
+
+import deequ_amd as d
+import pyoracle as O
+from deequ_amd.frequencies import FrequencyTable, encode_key
+from helpers import oracle_table, product_table
+
+pytestmark = pytest.mark.gpu
+
+
+def _spec(n, seed, long_frac=0.0):
+    rng = np.random.default_rng(seed)
+    a = rng.integers(0, n // 3 + 1, n)
+    keys = [None if i % 19 == 0 else ("a-much-longer-grouping-key-%d" % a[i] if rng.random() < long_frac
+                                      else "k%d" % a[i]) for i in range(n)]
+    ints = [None if i % 23 == 0 else int(a[i] % 1000) for i in range(n)]
+    return {"key": ["string", keys], "i": ["int64", ints]}
+
+
+def _freqs(table, cols, batches=1):
+    schema = dict(table.schema)
+    t = FrequencyTable(cols, schema)
+    n = table.num_rows
+    step = (n + batches - 1) // batches
+    for s in range(0, n, step):
+        part = d.Table.from_pydict({c: (schema[c], table.columns[c].to_pylist()[s:s + step]) for c in schema})
+        t.consume(part)
+    counts, keys = t.export()
+    s = t.summary()
+    return dict(zip(keys, counts.tolist())), s
+
+
+def _want(spec, cols):
+    st = O.frequencies_state(oracle_table(spec), cols)
+    dtypes = [spec[c][0] for c in cols]
+    return {encode_key(list(k), dtypes): c for k, c in st.frequencies.items()}
+
+
+@pytest.mark.parametrize("path", ["sorted", "atomic"])
+@pytest.mark.parametrize("budget", [None, "700"])
+@pytest.mark.parametrize("long_frac", [0.0, 0.2])
+def test_paths_match_oracle(gpu, monkeypatch, path, budget, long_frac):
+    monkeypatch.setenv("DQ_FREQ_PATH", path)
+    if budget:
+        monkeypatch.setenv("DQ_FREQ_STAGE_BUDGET", budget)
+    spec = _spec(20000, 1, long_frac)
+    table = product_table(spec)
+    for cols in (["key"], ["i"], ["key", "i"]):
+        got, s = _freqs(table, cols, batches=4)
+        want = _want(spec, cols)
+        assert got == want, (cols, path)
+        assert s.num_groups == len(want) and s.num_unique == sum(1 for c in want.values() if c == 1)
+        assert s.num_rows == 20000
+
+
+def test_high_cardinality_grows_table(gpu):
+    """~1.5M distinct int64 keys: the table grows through many slice doublings; the sketch
+    sizes it before aggregation."""
+    rng = np.random.default_rng(2)
+    n = 3_000_000
+    vals = rng.integers(0, 1_500_000, n)
+    table = d.Table({"v": d.Column.from_numpy(vals, None, "int64")})
+    t = FrequencyTable(["v"], {"v": "int64"})
+    t.consume(table)
+    s = t.summary()
+    u, c = np.unique(vals, return_counts=True)
+    assert s.num_groups == len(u)
+    assert s.num_unique == int((c == 1).sum())
+    assert s.grouped_rows == n
+    counts, keys = t.top(5)
+    assert sorted(counts.tolist())[-1] == int(c.max())
