@@ -81,6 +81,7 @@ SIGNATURES = {
     "dq_last_error": (c_char_p, []),
     "dq_abi_version": (c_int, []),
     "dq_device_count": (c_int, [POINTER(c_int)]),
+    "dq_release_cached_memory": (c_int, [c_int]),
     "dq_ctx_create": (c_int, [c_int, c_int, POINTER(c_void_p)]),
     "dq_ctx_destroy": (c_int, [c_void_p]),
     "dq_plan_create": (c_int, [c_void_p, POINTER(DqOp), c_int, POINTER(c_int32), c_int, POINTER(c_void_p)]),

@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -63,51 +64,140 @@ static bool is_numeric(int t) { return t >= DQ_T_INT8 && t <= DQ_T_FLOAT64; }
 static bool is_integral(int t) { return t >= DQ_T_INT8 && t <= DQ_T_INT64; }
 static bool valid_type(int t) { return t >= DQ_T_BOOL && t <= DQ_T_UTF8; }
 
+// Device block pool.  hipMalloc / hipFree of multi-GB buffers cost milliseconds to seconds (and
+// hipFree synchronises the device); the frequency path sizes its staging and sort buffers by the
+// batch, for every table.  Freed blocks of at least kPoolMin bytes are therefore kept per device
+// and handed out again (best fit within 2x of the request).  A block may still be in use by a
+// stream when it is freed: it is reused only after a device synchronisation.  On an allocation
+// failure the device's cached blocks are released and the allocation retried.
+class BlockPool {
+ public:
+  static constexpr size_t kPoolMin = (size_t)16 << 20;
+  static constexpr size_t kPoolMaxCached = (size_t)64 << 30;
+
+  static BlockPool& get() {
+    static BlockPool* pool = new BlockPool();  // never destroyed: no hipFree after runtime teardown
+    return *pool;
+  }
+
+  hipError_t alloc(int dev, size_t bytes, void** out) {
+    if (bytes >= kPoolMin) {
+      std::lock_guard<std::mutex> g(mu_);
+      int best = -1;
+      for (size_t i = 0; i < blocks_.size(); ++i) {
+        const Blk& b = blocks_[i];
+        if (b.dev == dev && b.bytes >= bytes && b.bytes <= 2 * bytes &&
+            (best < 0 || b.bytes < blocks_[best].bytes))
+          best = (int)i;
+      }
+      if (best >= 0) {
+        if (!blocks_[best].fenced) {
+          hipError_t e = hipDeviceSynchronize();
+          if (e != hipSuccess) return e;
+          for (Blk& b : blocks_)
+            if (b.dev == dev) b.fenced = true;
+        }
+        *out = blocks_[best].ptr;
+        cached_ -= blocks_[best].bytes;
+        blocks_.erase(blocks_.begin() + best);
+        return hipSuccess;
+      }
+    }
+    hipError_t e = hipMalloc(out, bytes);
+    if (e == hipErrorOutOfMemory) {
+      (void)hipGetLastError();
+      trim(dev);
+      e = hipMalloc(out, bytes);
+    }
+    return e;
+  }
+
+  void release(int dev, void* ptr, size_t bytes) {
+    if (bytes < kPoolMin) {
+      (void)hipFree(ptr);
+      return;
+    }
+    std::lock_guard<std::mutex> g(mu_);
+    blocks_.push_back(Blk{ptr, bytes, dev, false});
+    cached_ += bytes;
+    while (cached_ > kPoolMaxCached && !blocks_.empty()) {  // drop the oldest
+      cached_ -= blocks_.front().bytes;
+      (void)hipFree(blocks_.front().ptr);
+      blocks_.erase(blocks_.begin());
+    }
+  }
+
+  void trim(int dev) {
+    std::lock_guard<std::mutex> g(mu_);
+    for (size_t i = 0; i < blocks_.size();) {
+      if (blocks_[i].dev == dev) {
+        cached_ -= blocks_[i].bytes;
+        (void)hipFree(blocks_[i].ptr);
+        blocks_.erase(blocks_.begin() + i);
+      } else {
+        ++i;
+      }
+    }
+  }
+
+ private:
+  struct Blk {
+    void* ptr;
+    size_t bytes;
+    int dev;
+    bool fenced;
+  };
+  std::mutex mu_;
+  std::vector<Blk> blocks_;
+  size_t cached_ = 0;
+};
+
 struct DevBuf {
   void* ptr = nullptr;
   size_t cap = 0;
+  int dev = 0;
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
-  DevBuf(DevBuf&& o) noexcept : ptr(o.ptr), cap(o.cap) {
-    o.ptr = nullptr;
-    o.cap = 0;
-  }
+  DevBuf(DevBuf&& o) noexcept { swap(o); }
   DevBuf& operator=(DevBuf&& o) noexcept {
     if (this != &o) {
       release();
-      ptr = o.ptr;
-      cap = o.cap;
-      o.ptr = nullptr;
-      o.cap = 0;
+      swap(o);
     }
     return *this;
   }
   ~DevBuf() { release(); }
+  void swap(DevBuf& o) noexcept {
+    std::swap(ptr, o.ptr);
+    std::swap(cap, o.cap);
+    std::swap(dev, o.dev);
+  }
   void release() {
-    if (ptr) (void)hipFree(ptr);
+    if (ptr) BlockPool::get().release(dev, ptr, cap);
     ptr = nullptr;
     cap = 0;
   }
   dq_status ensure(size_t bytes) {
     if (bytes <= cap) return DQ_OK;
-    if (ptr) {
-      (void)hipFree(ptr);
-      ptr = nullptr;
-      cap = 0;
-    }
+    release();
     size_t want = std::max<size_t>(bytes, 256);
     want = (want + 255) & ~(size_t)255;  // padded: kernels may read whole aligned words
-    DQ_HIP(hipMalloc(&ptr, want));
+    DQ_HIP(hipGetDevice(&dev));
+    DQ_HIP(BlockPool::get().alloc(dev, want, &ptr));
     cap = want;
     return DQ_OK;
   }
 };
 
-// ------------------------------------------------------------------------------ context
 struct dq_ctx {
   int device = 0;
 };
+
+extern "C" dq_status dq_release_cached_memory(int device) {
+  BlockPool::get().trim(device);
+  return DQ_OK;
+}
 
 extern "C" dq_status dq_device_count(int* out) {
   if (!out) return fail(DQ_ERR_INVALID, "out is NULL");

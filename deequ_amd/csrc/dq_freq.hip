@@ -236,6 +236,9 @@ __device__ bool heap_equal(const FreqTable& T, uint64_t off, const uint8_t* p, u
 }
 
 // Insert `cnt` rows of key k into the global table.  Returns false on table/heap overflow.
+// kFlagOverflow = false: a full slice is reported only by the return value (the sorted path
+// hands such rows back for a retry after the table grows).
+template <bool kFlagOverflow = true>
 __device__ bool global_insert(const FreqTable& T, const Key& k, unsigned long long cnt) {
   const uint32_t tag = tag_of(k.hash);
   const bool inl = k.len <= 16;
@@ -292,7 +295,7 @@ __device__ bool global_insert(const FreqTable& T, const Key& k, unsigned long lo
     }
     slot = probe_slot(T, k.hash, ++probes);
   }
-  atomicOr(T.overflow, 1u);
+  if (kFlagOverflow) atomicOr(T.overflow, 1u);
   return false;
 }
 
@@ -494,96 +497,178 @@ __global__ __launch_bounds__(kBlock) void dq_freq_part_scatter_kernel(FreqTable 
 }
 
 // ---- sorted-bucket path ---------------------------------------------------------------------
-// High-cardinality group-by without device-scope atomics per row: rows are staged as 16-B
-// records (one streaming pass), bucketed by the slice their hash selects, sorted by bucket
-// (rocprim radix sort, dq_sort.hip), and every slice is then aggregated by ONE workgroup in LDS
-// and written back with plain stores (the workgroup owns its slice).  Keys of up to 15 bytes.
+// High-cardinality group-by without a device-scope atomic per row:
+//  1. stage (one streaming pass): every selected row becomes a 16-B record plus a 32-bit sort
+//     key (the top hash bits), and feeds an HLL sketch of the hashes that sizes the table.  A
+//     workgroup owns a contiguous row range and reserves its output with ONE atomic (its rows
+//     are counted from the validity bitmaps first), so no address takes an atomic per wave;
+//  2. sort: rocPRIM radix sort of (key, record) on the top log2(#slices) key bits (dq_sort.hip);
+//  3. agg: one work item per slice's bucket.  A bucket of at most kFreqAggPiece records is one work
+//     item: its slice is loaded into LDS, the records are counted there and the slice is written
+//     back with plain stores (the workgroup owns it).  A larger bucket (a hot key, or Histogram's
+//     NULL group) is cut into pieces of kFreqAggPiece records; each piece is pre-aggregated in LDS and
+//     merged into the slice with device-scope atomics, so a skewed key spreads over many CUs
+//     instead of serialising one workgroup.
+// Keys of up to 15 bytes (the length lives in the top byte of the record's second word).
 constexpr unsigned long long kRecLenShift = 56;
 constexpr unsigned long long kRecKeyMask = (1ull << kRecLenShift) - 1;
+constexpr uint32_t kRecHole = 0xFFu;  // length byte of a record that holds no row
 
 __device__ inline void rec_unpack(const FreqRec& r, unsigned long long* k1, uint32_t* len) {
   *len = (uint32_t)(r.k1 >> kRecLenShift);
   *k1 = r.k1 & kRecKeyMask;
 }
 
-// HLL++-style sketch of the staged hashes (p = 9, as deequ's): an estimate of the number of
-// distinct keys, used only to size the table before aggregation.
+// HLL sketch of the staged hashes (p = 9): an estimate of the number of distinct keys, used
+// only to size the table before aggregation.
 __device__ inline void sketch_update(uint32_t* regs, uint64_t h) {
   uint32_t idx, pw;
   hll_idx_rank(h, &idx, &pw);
   if (pw > regs[idx]) atomicMax(&regs[idx], pw);
 }
 
+// The rows make_key accepts, from the validity bitmaps alone (the host routes a batch here only
+// when every accepted key is at most 15 bytes long).
+__device__ inline bool row_selected(const FreqKeySpec& ks, const DevColumn* cols, int64_t row) {
+  if (ks.n_keys == 1) return ks.null_as_key || col_valid(cols[ks.key_cols[0]], row);
+  for (int i = 0; i < ks.n_keys; ++i)
+    if (!col_valid(cols[ks.key_cols[i]], row)) return false;
+  return true;
+}
+
+__device__ inline uint32_t block_sum(uint32_t v, uint32_t* wsum) {
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t t = 0;
+  for (int w = 0; w < kBlock / 64; ++w) t += wsum[w];
+  __syncthreads();
+  return t;
+}
+
 __global__ __launch_bounds__(kBlock) void dq_freq_stage_kernel(FreqKeySpec ks, const DevColumn* __restrict__ cols,
-                                                               int64_t n_rows, FreqRec* out,
+                                                               int64_t n_rows, FreqRec* out, uint32_t* sort_keys,
                                                                unsigned long long* cursor, uint32_t* hll) {
   __shared__ uint32_t regs[kHllM];
+  __shared__ uint32_t wsum[kBlock / 64];
+  __shared__ unsigned long long base_s;
   for (int i = threadIdx.x; i < kHllM; i += kBlock) regs[i] = 0u;
+  const int64_t per = (((n_rows + gridDim.x - 1) / gridDim.x) + 63) & ~(int64_t)63;
+  const int64_t r0 = min((int64_t)blockIdx.x * per, n_rows);
+  const int64_t r1 = min(r0 + per, n_rows);
+  uint32_t mine = 0;
+  for (int64_t row = r0 + threadIdx.x; row < r1; row += kBlock) mine += row_selected(ks, cols, row) ? 1u : 0u;
+  const uint32_t total = block_sum(mine, wsum);
+  if (threadIdx.x == 0) base_s = total ? atomicAdd(cursor, (unsigned long long)total) : 0ull;
   __syncthreads();
+  unsigned long long w = base_s;
   alignas(8) uint8_t scratch[kMaxLocalKey];
-  const uint32_t lane = threadIdx.x & 63u;
-  for (int64_t base = (int64_t)blockIdx.x * kBlock; base < n_rows; base += (int64_t)gridDim.x * kBlock) {
-    const int64_t row = base + threadIdx.x;
-    Key k;
-    bool ok = false;
-    if (row < n_rows) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  for (int64_t b0 = r0; b0 < r1; b0 += kBlock) {
+    const int64_t row = b0 + threadIdx.x;
+    const bool sel = row < r1 && row_selected(ks, cols, row);
+    const uint64_t m = __ballot(sel);
+    if (lane == 0) wsum[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+    for (uint32_t v = 0; v < (uint32_t)(kBlock / 64); ++v) {
+      const uint32_t c = wsum[v];
+      before += v < wave ? c : 0u;
+      all += c;
+    }
+    if (sel) {
+      const unsigned long long pos = w + before + (unsigned long long)__popcll(m & ((1ull << lane) - 1ull));
+      Key k;
       bool too_long;
-      ok = make_key(ks, cols, row, k, scratch, too_long) && k.len <= 15 && k.ptr == nullptr;
-    }
-    const uint64_t m = __ballot(ok);
-    unsigned long long w = 0;
-    if (lane == 0 && m) w = atomicAdd(cursor, (unsigned long long)__builtin_popcountll(m));
-    w = __shfl(w, 0, 64);
-    if (ok) {
-      const unsigned long long pos = w + __builtin_popcountll(m & ((1ull << lane) - 1ull));
       FreqRec r;
-      r.k0 = k.k0;
-      r.k1 = k.k1 | ((unsigned long long)k.len << kRecLenShift);
+      uint32_t key32 = 0xFFFFFFFFu;
+      if (make_key(ks, cols, row, k, scratch, too_long) && k.len <= 15 && k.ptr == nullptr) {
+        r.k0 = k.k0;
+        r.k1 = k.k1 | ((unsigned long long)k.len << kRecLenShift);
+        key32 = (uint32_t)(k.hash >> 32);
+        sketch_update(regs, k.hash);
+      } else {  // cannot happen on a batch the host routed here; keep the reserved slot inert
+        r.k0 = 0;
+        r.k1 = (unsigned long long)kRecHole << kRecLenShift;
+      }
       out[pos] = r;
-      sketch_update(regs, k.hash);
+      sort_keys[pos] = key32;
     }
+    w += all;
+    __syncthreads();
   }
   __syncthreads();
   for (int i = threadIdx.x; i < kHllM; i += kBlock)
     if (regs[i]) atomicMax(&hll[i], regs[i]);
 }
 
-__global__ __launch_bounds__(kBlock) void dq_freq_bucket_kernel(const FreqRec* __restrict__ recs, uint64_t n,
-                                                                int bucket_bits, uint32_t* keys) {
+// Slice ids to sort by.  Round 0: the staged keys (top 32 hash bits) shifted down to the slice
+// id in place; retry rounds: recomputed from the records a full slice handed back.  (The sort
+// then runs on bits [0, bits): rocPRIM's radix sort with begin_bit > 0 left small inputs
+// unsorted on gfx950 / ROCm 7.2, measured.)
+__global__ __launch_bounds__(kBlock) void dq_freq_slice_keys_kernel(const FreqRec* __restrict__ recs, uint64_t n,
+                                                                    int bits, int from_records, uint32_t* keys) {
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
-    const FreqRec r = recs[i];
-    unsigned long long k1;
-    uint32_t len;
-    rec_unpack(r, &k1, &len);
-    const uint64_t h = hash_inline(r.k0, k1, len);
-    keys[i] = bucket_bits ? (uint32_t)(h >> (64 - bucket_bits)) : 0u;
-  }
-}
-
-// off[b] = first sorted position with key >= b (b = 0 .. n_buckets).
-__global__ __launch_bounds__(kBlock) void dq_freq_bounds_kernel(const uint32_t* __restrict__ keys, uint64_t n,
-                                                                uint64_t n_buckets, uint64_t* off) {
-  for (uint64_t b = (uint64_t)blockIdx.x * kBlock + threadIdx.x; b <= n_buckets; b += (uint64_t)gridDim.x * kBlock) {
-    uint64_t lo = 0, hi = n;
-    while (lo < hi) {
-      const uint64_t mid = (lo + hi) >> 1;
-      if ((uint64_t)keys[mid] < b) lo = mid + 1;
-      else hi = mid;
+    uint32_t key;
+    if (from_records) {
+      const FreqRec r = recs[i];
+      unsigned long long k1;
+      uint32_t len;
+      rec_unpack(r, &k1, &len);
+      key = len == kRecHole ? 0xFFFFFFFFu : (uint32_t)(hash_inline(r.k0, k1, len) >> 32);
+    } else {
+      key = keys[i];
     }
-    off[b] = lo;
+    keys[i] = bits ? key >> (32 - bits) : 0u;
   }
 }
 
-// One workgroup per slice: the slice's groups and its bucket's records meet in LDS.  LDS slot
-// words: K1 = EMPTY / BUSY (being published) / FOREIGN (a group this path cannot hold: a long
-// or 16-byte key) / the record's k1 (length in the top byte); K0 = low key bytes; C = new rows.
+__device__ inline uint64_t key_slice(uint32_t key, int /*bits*/) { return key; }  // keys hold slice ids
+
+__device__ inline uint64_t first_at_or_above(const uint32_t* keys, uint64_t n, int bits, uint64_t b) {
+  uint64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (key_slice(keys[mid], bits) < b) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// off[b] = first sorted position of slice b (b = 0 .. n_buckets); pieces[b] = work items of b.
+__global__ __launch_bounds__(kBlock) void dq_freq_bounds_kernel(const uint32_t* __restrict__ keys, uint64_t n,
+                                                                int bits, uint64_t n_buckets, uint64_t* off,
+                                                                uint32_t* pieces) {
+  for (uint64_t b = (uint64_t)blockIdx.x * kBlock + threadIdx.x; b <= n_buckets; b += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t lo = first_at_or_above(keys, n, bits, b);
+    off[b] = lo;
+    if (b < n_buckets) {
+      const uint64_t hi = first_at_or_above(keys, n, bits, b + 1);
+      pieces[b] = (uint32_t)((hi - lo + kFreqAggPiece - 1) / kFreqAggPiece);
+    } else {
+      pieces[b] = 0u;
+    }
+  }
+}
+
+// LDS slot words: K1 = EMPTY / BUSY (being published) / FOREIGN (a group this path cannot hold:
+// a long or 16-byte key) / the record's k1 (length in the top byte); K0 = low key bytes;
+// C = rows counted in this work item.
 constexpr unsigned long long kLdsEmpty = ~0ull;
 constexpr unsigned long long kLdsBusy = ~0ull - 1ull;
 constexpr unsigned long long kLdsForeign = 0xFEull << kRecLenShift;
 
+__device__ inline void emit_retry(FreqRec* retry, unsigned long long* n_retry, const FreqRec& r,
+                                  unsigned long long copies) {
+  const unsigned long long at = atomicAdd(n_retry, copies);
+  for (unsigned long long j = 0; j < copies; ++j) retry[at + j] = r;
+}
+
 __global__ __launch_bounds__(kBlock) void dq_freq_agg_kernel(FreqTable T, const FreqRec* __restrict__ recs,
-                                                             const uint64_t* __restrict__ off, uint64_t n_buckets,
-                                                             FreqRec* retry, unsigned long long* n_retry,
+                                                             const uint64_t* __restrict__ off,
+                                                             const uint32_t* __restrict__ piece_start,
+                                                             uint64_t n_buckets, int table_empty, FreqRec* retry,
+                                                             unsigned long long* n_retry,
                                                              unsigned long long* new_groups) {
   constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
   __shared__ unsigned long long K0[S], K1[S];
@@ -591,20 +676,34 @@ __global__ __launch_bounds__(kBlock) void dq_freq_agg_kernel(FreqTable T, const 
   __shared__ int overflow;
   __shared__ uint32_t fresh;
   __shared__ unsigned long long retry_base;
-  for (uint64_t b = blockIdx.x; b < n_buckets; b += gridDim.x) {
-    const uint64_t r0 = off[b], r1 = off[b + 1];
-    if (r0 == r1) continue;  // uniform: every thread reads the same bounds
+  const uint32_t n_items = piece_start[n_buckets];
+  for (uint32_t w = blockIdx.x; w < n_items; w += gridDim.x) {
+    // the bucket of work item w: piece_start[b] <= w < piece_start[b + 1]
+    uint64_t lo = 0, hi = n_buckets;
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (piece_start[mid] <= w) lo = mid;
+      else hi = mid;
+    }
+    const uint64_t b = lo;
+    const bool owner = piece_start[b + 1] - piece_start[b] == 1u;
+    const uint64_t r0 = off[b] + (uint64_t)(w - piece_start[b]) * kFreqAggPiece;
+    const uint64_t r1 = min(off[b + 1], r0 + kFreqAggPiece);
     FreqSlot* slice = T.slots + (b << kFreqSliceLog);
     for (uint32_t s = threadIdx.x; s < S; s += kBlock) {
-      const FreqSlot e = slice[s];
-      const uint32_t len = (uint32_t)(e.ctrl & kLenMask);
-      if (!(e.ctrl & kReady)) {
-        K1[s] = kLdsEmpty;
-      } else if ((e.ctrl & kHeapKey) || len > 15) {
-        K1[s] = kLdsForeign;
+      if (owner && !table_empty) {
+        const FreqSlot e = slice[s];
+        const uint32_t len = (uint32_t)(e.ctrl & kLenMask);
+        if (!(e.ctrl & kReady)) {
+          K1[s] = kLdsEmpty;
+        } else if ((e.ctrl & kHeapKey) || len > 15) {
+          K1[s] = kLdsForeign;
+        } else {
+          K0[s] = e.k0;
+          K1[s] = e.k1 | ((unsigned long long)len << kRecLenShift);
+        }
       } else {
-        K0[s] = e.k0;
-        K1[s] = e.k1 | ((unsigned long long)len << kRecLenShift);
+        K1[s] = kLdsEmpty;
       }
       C[s] = 0u;
     }
@@ -618,6 +717,7 @@ __global__ __launch_bounds__(kBlock) void dq_freq_agg_kernel(FreqTable T, const 
       unsigned long long k1;
       uint32_t len;
       rec_unpack(r, &k1, &len);
+      if (len == kRecHole) continue;
       const uint64_t h = hash_inline(r.k0, k1, len);
       uint32_t s = (uint32_t)(h & (S - 1));
       bool done = false;
@@ -640,10 +740,40 @@ __global__ __launch_bounds__(kBlock) void dq_freq_agg_kernel(FreqTable T, const 
           ++probe;
         }
       }
-      if (!done) overflow = 1;
+      if (!done) {
+        if (owner) {
+          overflow = 1;
+        } else {  // the piece holds more keys than LDS: this row goes straight to the slice
+          Key k;
+          k.k0 = r.k0;
+          k.k1 = k1;
+          k.len = len;
+          k.ptr = nullptr;
+          k.hash = h;
+          if (!global_insert<false>(T, k, 1ull)) emit_retry(retry, n_retry, r, 1ull);
+        }
+      }
     }
     __syncthreads();
-    if (overflow) {  // the slice is full: leave it untouched, hand the bucket's rows back
+    if (!owner) {  // merge the piece's counts into the shared slice
+      for (uint32_t s = threadIdx.x; s < S; s += kBlock) {
+        const uint32_t c = C[s];
+        if (!c) continue;
+        const unsigned long long kk1 = K1[s];
+        Key k;
+        k.k0 = K0[s];
+        k.k1 = kk1 & kRecKeyMask;
+        k.len = (uint32_t)(kk1 >> kRecLenShift);
+        k.ptr = nullptr;
+        k.hash = hash_inline(k.k0, k.k1, k.len);
+        if (!global_insert<false>(T, k, (unsigned long long)c)) {
+          FreqRec r;
+          r.k0 = k.k0;
+          r.k1 = kk1;
+          emit_retry(retry, n_retry, r, (unsigned long long)c);
+        }
+      }
+    } else if (overflow) {  // the slice is full: leave it untouched, hand the bucket's rows back
       if (threadIdx.x == 0) retry_base = atomicAdd(n_retry, (unsigned long long)(r1 - r0));
       __syncthreads();
       for (uint64_t i = r0 + threadIdx.x; i < r1; i += kBlock) retry[retry_base + (i - r0)] = recs[i];
@@ -652,7 +782,7 @@ __global__ __launch_bounds__(kBlock) void dq_freq_agg_kernel(FreqTable T, const 
         const uint32_t c = C[s];
         if (!c) continue;
         FreqSlot& e = slice[s];
-        if (e.ctrl & kReady) {
+        if (!table_empty && (e.ctrl & kReady)) {
           e.count += c;
         } else {
           const unsigned long long k1 = K1[s];
@@ -671,7 +801,7 @@ __global__ __launch_bounds__(kBlock) void dq_freq_agg_kernel(FreqTable T, const 
       __syncthreads();
       if (threadIdx.x == 0 && fresh) atomicAdd(new_groups, (unsigned long long)fresh);
     }
-    __syncthreads();  // LDS is reused by the next slice
+    __syncthreads();  // LDS is reused by the next work item
   }
 }
 
@@ -720,41 +850,43 @@ hipError_t launch_freq_part_scatter(const FreqTable& T, int n_parts, const unsig
 }
 
 hipError_t launch_freq_stage(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, FreqRec* d_out,
-                             unsigned long long* d_cursor, uint32_t* d_hll, hipStream_t stream) {
+                             uint32_t* d_sort_keys, unsigned long long* d_cursor, uint32_t* d_hll,
+                             hipStream_t stream) {
   if (n_rows <= 0) return hipSuccess;
-  int64_t blocks = (n_rows + kBlock * 8 - 1) / (kBlock * 8);
+  int64_t blocks = (n_rows + kBlock * 16 - 1) / (kBlock * 16);
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(dq_freq_stage_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, ks, d_cols, n_rows, d_out,
-                     d_cursor, d_hll);
+                     d_sort_keys, d_cursor, d_hll);
   return hipGetLastError();
 }
 
-hipError_t launch_freq_bucket(const FreqRec* d_recs, uint64_t n, int bucket_bits, uint32_t* d_keys,
-                              hipStream_t stream) {
+hipError_t launch_freq_slice_keys(const FreqRec* d_recs, uint64_t n, int bits, int from_records, uint32_t* d_keys,
+                                  hipStream_t stream) {
   if (n == 0) return hipSuccess;
   uint64_t blocks = (n + kBlock * 8 - 1) / (kBlock * 8);
   if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(dq_freq_bucket_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, d_recs, n, bucket_bits,
-                     d_keys);
+  hipLaunchKernelGGL(dq_freq_slice_keys_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, d_recs, n, bits,
+                     from_records, d_keys);
   return hipGetLastError();
 }
 
-hipError_t launch_freq_bounds(const uint32_t* d_sorted_keys, uint64_t n, uint64_t n_buckets, uint64_t* d_off,
-                              hipStream_t stream) {
+hipError_t launch_freq_bounds(const uint32_t* d_sorted_keys, uint64_t n, int bits, uint64_t n_buckets,
+                              uint64_t* d_off, uint32_t* d_pieces, hipStream_t stream) {
   uint64_t blocks = (n_buckets + 1 + kBlock - 1) / kBlock;
   if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(dq_freq_bounds_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, d_sorted_keys, n,
-                     n_buckets, d_off);
+  hipLaunchKernelGGL(dq_freq_bounds_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, d_sorted_keys, n, bits,
+                     n_buckets, d_off, d_pieces);
   return hipGetLastError();
 }
 
-hipError_t launch_freq_agg(const FreqTable& T, const FreqRec* d_recs, const uint64_t* d_off, uint64_t n_buckets,
+hipError_t launch_freq_agg(const FreqTable& T, const FreqRec* d_recs, const uint64_t* d_off,
+                           const uint32_t* d_piece_start, uint64_t n_buckets, uint64_t max_items, int table_empty,
                            FreqRec* d_retry, unsigned long long* d_n_retry, unsigned long long* d_new_groups,
                            hipStream_t stream) {
-  uint64_t blocks = n_buckets < 65536 ? n_buckets : 65536;
+  uint64_t blocks = max_items < 65536 ? max_items : 65536;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(dq_freq_agg_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, d_recs, d_off, n_buckets,
-                     d_retry, d_n_retry, d_new_groups);
+  hipLaunchKernelGGL(dq_freq_agg_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, d_recs, d_off,
+                     d_piece_start, n_buckets, table_empty, d_retry, d_n_retry, d_new_groups);
   return hipGetLastError();
 }
 

@@ -138,6 +138,8 @@ struct FreqSlot {  // 32 B; see dq_freq.hip for the ctrl word
 // slice (64 KiB of slots) is what one workgroup aggregates in LDS (dq_freq_agg_kernel).
 constexpr int kFreqSliceLog = 11;
 constexpr uint64_t kFreqSliceSlots = 1ull << kFreqSliceLog;
+// Records per aggregation work item of a split (hot) bucket in the sorted-bucket path.
+constexpr uint64_t kFreqAggPiece = 32768;
 
 // A staged row of the sorted-bucket path: key bytes 0..14 (zero padded) in k0 and the low 7
 // bytes of k1, the key length (<= 15) in the top byte of k1.
@@ -198,17 +200,22 @@ hipError_t launch_freq_part_count(const FreqTable& T, int n_parts, unsigned long
 hipError_t launch_freq_part_scatter(const FreqTable& T, int n_parts, const unsigned long long* d_base,
                                     unsigned long long* d_cursor, FreqSlot* out_groups, uint8_t* out_keys,
                                     hipStream_t stream);
-// Sorted-bucket path (dq_freq.hip, dq_sort.hip): stage rows as FreqRec (+ an HLL sketch of
-// their hashes, to size the table), bucket them, sort by bucket, aggregate each slice in LDS.
+// Sorted-bucket path (dq_freq.hip, dq_sort.hip): stage rows as FreqRec + a 32-bit sort key (top
+// hash bits) + an HLL sketch of their hashes (to size the table), sort by the key's top `bits`
+// bits (the slice), then aggregate every slice's bucket in LDS (split buckets merge atomically).
 hipError_t launch_freq_stage(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, FreqRec* d_out,
-                             unsigned long long* d_cursor, uint32_t* d_hll, hipStream_t stream);
-hipError_t launch_freq_bucket(const FreqRec* d_recs, uint64_t n, int bucket_bits, uint32_t* d_keys,
-                              hipStream_t stream);
+                             uint32_t* d_sort_keys, unsigned long long* d_cursor, uint32_t* d_hll,
+                             hipStream_t stream);
+hipError_t launch_freq_slice_keys(const FreqRec* d_recs, uint64_t n, int bits, int from_records, uint32_t* d_keys,
+                                  hipStream_t stream);
 hipError_t sort_freq_records(void* d_tmp, size_t& tmp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
                              const FreqRec* recs_in, FreqRec* recs_out, uint64_t n, int bits, hipStream_t stream);
-hipError_t launch_freq_bounds(const uint32_t* d_sorted_keys, uint64_t n, uint64_t n_buckets, uint64_t* d_off,
-                              hipStream_t stream);
-hipError_t launch_freq_agg(const FreqTable& T, const FreqRec* d_recs, const uint64_t* d_off, uint64_t n_buckets,
+hipError_t scan_freq_pieces(void* d_tmp, size_t& tmp_bytes, const uint32_t* pieces, uint32_t* piece_start,
+                            uint64_t n, hipStream_t stream);
+hipError_t launch_freq_bounds(const uint32_t* d_sorted_keys, uint64_t n, int bits, uint64_t n_buckets,
+                              uint64_t* d_off, uint32_t* d_pieces, hipStream_t stream);
+hipError_t launch_freq_agg(const FreqTable& T, const FreqRec* d_recs, const uint64_t* d_off,
+                           const uint32_t* d_piece_start, uint64_t n_buckets, uint64_t max_items, int table_empty,
                            FreqRec* d_retry, unsigned long long* d_n_retry, unsigned long long* d_new_groups,
                            hipStream_t stream);
 hipError_t launch_freq_rehash(const FreqSlot* d_old, uint64_t old_n, const FreqTable& T, hipStream_t stream);

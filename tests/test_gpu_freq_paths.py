@@ -80,3 +80,42 @@ def test_high_cardinality_grows_table(gpu):
     assert s.grouped_rows == n
     counts, keys = t.top(5)
     assert sorted(counts.tolist())[-1] == int(c.max())
+
+
+@pytest.mark.parametrize("hot_frac", [0.5, 0.02])
+def test_hot_key_buckets_split_across_workgroups(gpu, hot_frac):
+    """A key holding a large share of the rows fills one slice's bucket far beyond one work
+    item (kFreqAggPiece records): its pieces are pre-aggregated in LDS and merged atomically.
+    Exact counts, also for the cold keys sharing that slice."""
+    rng = np.random.default_rng(3)
+    n = 4_000_000
+    vals = rng.integers(0, 200_000, n)
+    hot = rng.random(n) < hot_frac
+    vals[hot] = 123_456_789
+    valid = rng.random(n) > 0.01
+    table = d.Table({"v": d.Column.from_numpy(vals, valid, "int64")})
+    for hist in (False, True):
+        t = FrequencyTable(["v"], {"v": "int64"}, histogram=hist)
+        t.consume(table)
+        s = t.summary()
+        u, c = np.unique(vals[valid], return_counts=True)
+        extra = 1 if hist and (~valid).any() else 0
+        assert s.num_groups == len(u) + extra
+        assert s.num_unique == int((c == 1).sum()) + (1 if extra and (~valid).sum() == 1 else 0)
+        counts, keys = t.top(3)
+        want = sorted(c.tolist() + ([int((~valid).sum())] if extra else []), reverse=True)[:3]
+        assert sorted(counts.tolist(), reverse=True)[:3] == want  # top() keeps ties at the threshold
+
+
+def test_low_cardinality_many_rows(gpu):
+    """16 distinct keys over 3M rows: every bucket is split into pieces (the table is tiny)."""
+    rng = np.random.default_rng(4)
+    n = 3_000_000
+    vals = rng.integers(0, 16, n).astype(np.int32)
+    table = d.Table({"v": d.Column.from_numpy(vals, None, "int32")})
+    t = FrequencyTable(["v"], {"v": "int32"})
+    t.consume(table)
+    counts, keys = t.export()
+    got = {int.from_bytes(k, "little", signed=True): int(c) for k, c in zip(keys, counts.tolist())}
+    u, c = np.unique(vals, return_counts=True)
+    assert got == dict(zip(u.tolist(), c.tolist()))
