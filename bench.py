@@ -257,6 +257,7 @@ def _timed(args, world, step):
     import torch.distributed as dist
     out = None
     for _ in range(args.warmup):
+        out = None  # a step's result (e.g. HBM-resident frequency tables) is dropped before the next
         out = step()
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
@@ -265,6 +266,7 @@ def _timed(args, world, step):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
+        out = None
         out = step(events[k])
     torch.cuda.synchronize()
     if world > 1:

@@ -73,7 +73,7 @@ static bool valid_type(int t) { return t >= DQ_T_BOOL && t <= DQ_T_UTF8; }
 class BlockPool {
  public:
   static constexpr size_t kPoolMin = (size_t)16 << 20;
-  static constexpr size_t kPoolMaxCached = (size_t)64 << 30;
+  static constexpr size_t kPoolMaxCached = (size_t)128 << 30;
 
   static BlockPool& get() {
     static BlockPool* pool = new BlockPool();  // never destroyed: no hipFree after runtime teardown

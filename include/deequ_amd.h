@@ -175,7 +175,7 @@ int dq_abi_version(void);
 dq_status dq_device_count(int* out);
 
 /* Give the device blocks the library keeps cached for reuse (staging / sort buffers of the
- * frequency group-by, >= 16 MiB each, at most 64 GiB) back to the HIP runtime.  No reference
+ * frequency group-by, >= 16 MiB each, at most 128 GiB) back to the HIP runtime.  No reference
  * counterpart: Spark's executors free their memory through the JVM. */
 dq_status dq_release_cached_memory(int device);
 
