@@ -449,6 +449,39 @@ __global__ __launch_bounds__(kBlock) void dq_freq_import_kernel(FreqTable T, Fre
   }
 }
 
+// Count of one encoded key (0 if absent): a single-thread probe of the key's slice.
+__global__ void dq_freq_lookup_kernel(FreqTable T, const uint8_t* key, uint32_t len, unsigned long long* out) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  Key k;
+  k.len = len;
+  k.k0 = k.k1 = 0;
+  k.ptr = nullptr;
+  if (len <= 16) {
+    k.k0 = ld_partial(key, len < 8 ? len : 8);
+    k.k1 = len > 8 ? ld_partial(key + 8, len - 8) : 0;
+    k.hash = hash_inline(k.k0, k.k1, len);
+  } else {
+    k.ptr = key;
+    k.hash = xxh64_any(key, len, 42);
+  }
+  const uint32_t tag = tag_of(k.hash);
+  *out = 0ull;
+  for (uint64_t i = 0; i < kFreqSliceSlots; ++i) {
+    const FreqSlot& e = T.slots[probe_slot(T, k.hash, i)];
+    if (e.ctrl == 0ull) return;  // launch boundary: the table is complete and visible
+    if ((uint32_t)(e.ctrl >> 32) != tag || (uint32_t)(e.ctrl & kLenMask) != len) continue;
+    if (len <= 16 && !(e.ctrl & kHeapKey)) {
+      if (e.k0 != k.k0 || e.k1 != k.k1) continue;
+    } else {
+      bool eq = (e.ctrl & kHeapKey) != 0;
+      for (uint32_t j = 0; eq && j < len; ++j) eq = T.heap[e.k0 + j] == key[j];
+      if (!eq) continue;
+    }
+    *out = e.count;
+    return;
+  }
+}
+
 // ---- multi-GPU key-hash partitioning (owner = a function of hash bits the table does not use
 // for its slot index, so every owner's keys still spread over its whole table)
 __device__ inline uint32_t freq_owner(uint64_t h, uint32_t n_parts) {
@@ -958,6 +991,12 @@ hipError_t launch_freq_export(const FreqTable& T, unsigned long long min_count, 
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(dq_freq_export_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, min_count, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_lookup(const FreqTable& T, const uint8_t* d_key, uint32_t len, unsigned long long* d_out,
+                              hipStream_t stream) {
+  hipLaunchKernelGGL(dq_freq_lookup_kernel, dim3(1), dim3(64), 0, stream, T, d_key, len, d_out);
   return hipGetLastError();
 }
 

@@ -191,6 +191,8 @@ hipError_t launch_freq_hist(const FreqTable& T, unsigned long long* d_hist, unsi
 hipError_t launch_freq_export(const FreqTable& T, unsigned long long min_count, const FreqOut& out,
                               hipStream_t stream);
 hipError_t launch_freq_import(const FreqTable& T, const FreqIn& in, hipStream_t stream);
+hipError_t launch_freq_lookup(const FreqTable& T, const uint8_t* d_key, uint32_t len, unsigned long long* d_out,
+                              hipStream_t stream);
 hipError_t launch_freq_heap_need(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
                                  unsigned long long* d_need, unsigned long long* d_max_len, hipStream_t stream);
 // Multi-GPU key-hash exchange: owner rank of a group = freq_owner(hash, n_parts).  `d_cnt` gets

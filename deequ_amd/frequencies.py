@@ -146,6 +146,13 @@ class FrequencyTable:
             L.check(st)
             return _unpack_groups(groups, got.value, keys.raw)
 
+    def lookup(self, key: bytes) -> int:
+        """Count of the group with this encoded key (0 if there is none)."""
+        out = ctypes.c_int64()
+        buf = ctypes.create_string_buffer(key, max(1, len(key)))
+        L.check(L.lib().dq_freq_lookup(self.handle, buf, len(key), ctypes.byref(out)))
+        return int(out.value)
+
     def import_groups(self, counts: Sequence[int], keys: Sequence[bytes], num_rows: int) -> None:
         """FrequenciesAndNumRows.sum for the given groups (GroupingAnalyzers.scala:128-148)."""
         n = len(keys)

@@ -111,7 +111,7 @@ class AnalysisRunner:
         return AnalyzerContext(OrderedDict((a, ctx.metricMap[a]) for a in analyzers if a in ctx.metricMap))
 
     @staticmethod
-    def _runGroupingAnalyzers(data, analyzers, aggregateWith, saveStatesWith) -> AnalyzerContext:
+    def _runGroupingAnalyzers(data, analyzers, aggregateWith, saveStatesWith, states_out=None) -> AnalyzerContext:
         """One GPU group-by per sorted grouping-column set (AnalysisRunner.scala:172-186,
         259-287), metrics of all analyzers of that grouping from the one table (:480-548)."""
         from .frequencies import compute_frequencies
@@ -136,6 +136,8 @@ class AnalysisRunner:
                     results[a] = a.toFailureMetric(e)
             if saveStatesWith is not None:
                 saveStatesWith.persist(group[0], state)
+            if states_out is not None:
+                states_out[cols] = state
         return AnalyzerContext(results)
 
     @staticmethod
@@ -166,12 +168,31 @@ class AnalysisRunner:
             except Exception as e:  # noqa: BLE001 - the whole pass fails (:320-323)
                 for a in eligible:
                     results[a] = a.toFailureMetric(e)
+        tables = OrderedDict()
         if grouping:
             results.update(AnalysisRunner._runGroupingAnalyzers(
-                data, grouping, aggregateWith, saveStatesWith).metricMap)
+                data, grouping, aggregateWith, saveStatesWith, tables).metricMap)
         for a in others:
-            results[a] = a.calculate(data, aggregateWith, saveStatesWith)
+            shared = AnalysisRunner._sharedFrequencies(a, data.schema, tables, aggregateWith, saveStatesWith)
+            if shared is not None:
+                results[a] = a.metricFromFrequencies(shared)
+            else:
+                results[a] = a.calculate(data, aggregateWith, saveStatesWith)
         return AnalyzerContext(results)
+
+    @staticmethod
+    def _sharedFrequencies(analyzer, schema, tables, aggregateWith, saveStatesWith):
+        """A Histogram (no binning UDF, no state loading/saving: its persisted state has its own
+        form) whose column was just grouped by a frequency analyzer reuses that table instead of
+        running a second group-by over the data (the reference runs a separate Spark job)."""
+        from .analyzers import Histogram
+        if not isinstance(analyzer, Histogram) or analyzer.binningUdf is not None:
+            return None
+        if aggregateWith is not None or saveStatesWith is not None:
+            return None
+        if schema.get(analyzer.column) not in Histogram.SHARES_FREQUENCIES:
+            return None
+        return tables.get((analyzer.column,))
 
     @staticmethod
     def runOnAggregatedStates(schema: Dict[str, str], analysis: "Analysis", stateLoaders,

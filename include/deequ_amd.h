@@ -290,6 +290,10 @@ dq_status dq_freq_top(dq_freq* f, int n, dq_freq_group* groups, int64_t max_grou
  * tables on one device, grouping the same key types; src is unchanged. */
 dq_status dq_freq_merge(dq_freq* dst, dq_freq* src);
 /* Merge groups (and `num_rows`) into the table: FrequenciesAndNumRows.sum. */
+/* Count of one group (0 if the key is absent), key in the encoded form above.  Used to fold a
+ * literal "NullValue" string into Histogram's NULL bin when Histogram shares the frequency
+ * table of its column (Histogram.scala:63-64: NULL is replaced by that literal before grouping). */
+dq_status dq_freq_lookup(dq_freq* f, const uint8_t* key, int64_t key_len, int64_t* count);
 dq_status dq_freq_import(dq_freq* f, const dq_freq_group* groups, int64_t n, const uint8_t* key_bytes,
                          int64_t num_rows);
 

@@ -295,3 +295,27 @@ def test_grouping_runner_shares_one_table_and_persists(gpu):
     ctx2 = d.AnalysisRunner.onData(table).addAnalyzers(analyzers[:2]).aggregateWith(provider).run()
     assert ctx2.metric(analyzers[0]).value == Success(0.0)
     assert ctx2.metric(analyzers[1]).value == Success(0.25)
+
+
+@pytest.mark.parametrize("t", ["string", "int64", "bool"])
+def test_histogram_shares_the_frequency_table(gpu, t):
+    """Histogram run beside a frequency analyzer of its column takes its metric from that
+    table (one group-by); the result equals the oracle and Histogram run alone, including a
+    literal "NullValue" string merging with the NULL bin (Histogram.scala:63-64)."""
+    rng = np.random.default_rng(62)
+    spec = random_table(rng, 4000, 0.1, [t])
+    col = "c_" + t
+    if t == "int64":
+        spec[col][1] = [None if v is None else v % 50 for v in spec[col][1]]
+    if t == "string":
+        spec[col][1] = [("NullValue" if i % 97 == 0 else v) for i, v in enumerate(spec[col][1])]
+    data = product_table(spec)
+    for bins in (1000, 7, 1):
+        hist = d.Histogram(col, maxDetailBins=bins)
+        ctx = d.AnalysisRunner.onData(data).addAnalyzers([d.Uniqueness([col]), hist]).run()
+        shared = ctx.metric(hist).value.get()
+        alone = hist.calculate(data).value.get()
+        exp = O.histogram_metric(O.histogram_state(oracle_table(spec), col), bins)
+        for h in (shared, alone):
+            assert h.numberOfBins == exp["number_of_bins"]
+            assert {k: (v.absolute, v.ratio) for k, v in h.values.items()} == exp["values"]
