@@ -106,6 +106,10 @@ class FrequencyTable:
         return cls(other.key_columns, {c: t for c, t in zip(other.key_columns, other.dtypes)},
                    other.histogram, other.device)
 
+    def reserve(self, rows: int) -> None:
+        """Size the staging for `rows` rows about to be consumed (optional)."""
+        L.check(L.lib().dq_freq_reserve(self.handle, int(rows)))
+
     def consume(self, batch) -> None:
         from .table import dq_columns
         cols = dq_columns(batch, self.names)
@@ -241,6 +245,7 @@ def compute_frequencies(data, grouping_columns: Sequence[str], histogram: bool =
     """FrequencyBasedAnalyzer.computeFrequencies over every batch of `data` (one pass)."""
     schema = data.schema
     table = FrequencyTable(grouping_columns, {c: schema[c] for c in schema}, histogram)
+    table.reserve(data.count())
     for batch in data.batches():
         table.consume(batch)
     return FrequenciesAndNumRows(table)

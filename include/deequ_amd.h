@@ -271,6 +271,9 @@ typedef struct dq_freq_group {
 dq_status dq_freq_create(dq_ctx* ctx, const int32_t* key_columns, int n_keys,
                          const int32_t* column_types, int n_columns, int flags, dq_freq** out);
 dq_status dq_freq_destroy(dq_freq* f);
+/* Optional: size the table's staging for `rows` more rows before consuming them (e.g. the row
+ * count of every partition about to be consumed), so staging is not regrown batch by batch. */
+dq_status dq_freq_reserve(dq_freq* f, int64_t rows);
 dq_status dq_freq_reset(dq_freq* f);
 dq_status dq_freq_consume(dq_freq* f, const dq_column* columns, int n_columns, int64_t n_rows);
 dq_status dq_freq_get_summary(dq_freq* f, dq_freq_summary* out);
