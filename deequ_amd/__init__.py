@@ -8,7 +8,8 @@ no CPU fallback.
 from .analyzers import (Analyzer, ApproxCountDistinct, Completeness, Compliance, CountDistinct, DataType,
                         DataTypeInstances,
                         Distinctness, Entropy, FrequencyBasedAnalyzer, GroupingAnalyzer, Histogram,
-                        Maximum, Mean, Minimum, MutualInformation, Preconditions,
+                        Correlation, MaxLength, Maximum, Mean, MinLength, Minimum, MutualInformation,
+                        Preconditions,
                         ScanShareableAnalyzer, ScanShareableFrequencyBasedAnalyzer, Size,
                         StandardDeviation, StandardScanShareableAnalyzer, Sum, Uniqueness,
                         UniqueValueRatio)
@@ -21,7 +22,8 @@ from .metrics import (Distribution, DistributionValue, DoubleMetric, EmptyStateE
                       WrongColumnTypeException)
 from .runner import (Analysis, AnalysisRunBuilder, AnalysisRunner, AnalyzerContext,
                      InMemoryStateProvider)
-from .states import (ApproxCountDistinctState, DataTypeHistogram, MaxState, MeanState, MinState, NumMatches,
+from .states import (ApproxCountDistinctState, CorrelationState, DataTypeHistogram, MaxState, MeanState, MinState,
+                     NumMatches,
                      NumMatchesAndCount, StandardDeviationState, State, SumState)
 from .table import Column, PartitionedTable, Table
 

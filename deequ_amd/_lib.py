@@ -20,7 +20,8 @@ DQ_T_BOOL, DQ_T_INT8, DQ_T_INT16, DQ_T_INT32, DQ_T_INT64, DQ_T_FLOAT32, DQ_T_FLO
 DQ_COL_DEVICE = 0x1
 
 (DQ_OP_SIZE, DQ_OP_COMPLETENESS, DQ_OP_COMPLIANCE, DQ_OP_SUM, DQ_OP_MEAN, DQ_OP_STDDEV,
- DQ_OP_MINIMUM, DQ_OP_MAXIMUM, DQ_OP_APPROX_COUNT_DISTINCT, DQ_OP_DATATYPE) = range(1, 11)
+ DQ_OP_MINIMUM, DQ_OP_MAXIMUM, DQ_OP_APPROX_COUNT_DISTINCT, DQ_OP_DATATYPE, DQ_OP_MIN_LENGTH,
+ DQ_OP_MAX_LENGTH, DQ_OP_CORRELATION) = range(1, 14)
 
 DQ_P_COLUMN, DQ_P_LIT_INT, DQ_P_LIT_FLOAT, DQ_P_LIT_NULL, DQ_P_COALESCE, DQ_P_LIT_STRING = 1, 2, 3, 4, 5, 6
 DQ_P_EQ, DQ_P_NE, DQ_P_LT, DQ_P_LE, DQ_P_GT, DQ_P_GE, DQ_P_EQ_NULLSAFE = 10, 11, 12, 13, 14, 15, 16
@@ -52,14 +53,15 @@ class DqPredicate(Structure):
 
 
 class DqOp(Structure):
-    _fields_ = [("kind", c_int32), ("column", c_int32), ("predicate", DqPredicate),
-                ("where", DqPredicate)]
+    _fields_ = [("kind", c_int32), ("column", c_int32), ("column2", c_int32), ("reserved", c_int32),
+                ("predicate", DqPredicate), ("where", DqPredicate)]
 
 
 class DqState(Structure):
     _fields_ = [("kind", c_int32), ("has_value", c_int32), ("num_matches", c_int64),
                 ("count", c_int64), ("sum", c_double), ("n", c_double), ("avg", c_double),
-                ("m2", c_double), ("value", c_double), ("words", c_int64 * DQ_HLL_NUM_WORDS)]
+                ("m2", c_double), ("value", c_double), ("words", c_int64 * DQ_HLL_NUM_WORDS),
+                ("y_avg", c_double), ("ck", c_double), ("x_mk", c_double), ("y_mk", c_double)]
 
 
 class DqFreqSummary(Structure):

@@ -50,6 +50,15 @@ class Preconditions:
         return check
 
     @staticmethod
+    def isString(column: str) -> Callable[[Dict[str, str]], None]:
+        def check(schema):
+            t = schema[column]
+            if t != "string":
+                raise WrongColumnTypeException(
+                    "Expected type of column %s to be StringType, but found %s instead!" % (column, t))
+        return check
+
+    @staticmethod
     def atLeastOne(columns) -> Callable[[Dict[str, str]], None]:
         def check(_schema):
             if len(columns) == 0:
@@ -271,6 +280,64 @@ class ApproxCountDistinct(StandardScanShareableAnalyzer):
 
     def __str__(self):
         return "ApproxCountDistinct(%s,%s)" % (self.column, _opt(self.where))
+
+
+@dataclass(frozen=True)
+class MinLength(StandardScanShareableAnalyzer):
+    """min(length(sel)).cast(double) over a string column (MinLength.scala:25-41)."""
+    column: str
+    where: Optional[str] = None
+    name = "MinLength"
+    DQ_KIND = L.DQ_OP_MIN_LENGTH
+
+    def instance(self):
+        return self.column
+
+    def additionalPreconditions(self):
+        return [Preconditions.hasColumn(self.column), Preconditions.isString(self.column)]
+
+    def __str__(self):
+        return "MinLength(%s,%s)" % (self.column, _opt(self.where))
+
+
+@dataclass(frozen=True)
+class MaxLength(StandardScanShareableAnalyzer):
+    """max(length(sel)).cast(double) over a string column (MaxLength.scala:25-41)."""
+    column: str
+    where: Optional[str] = None
+    name = "MaxLength"
+    DQ_KIND = L.DQ_OP_MAX_LENGTH
+
+    def instance(self):
+        return self.column
+
+    def additionalPreconditions(self):
+        return [Preconditions.hasColumn(self.column), Preconditions.isString(self.column)]
+
+    def __str__(self):
+        return "MaxLength(%s,%s)" % (self.column, _opt(self.where))
+
+
+@dataclass(frozen=True)
+class Correlation(StandardScanShareableAnalyzer):
+    """Pearson correlation of two numeric columns (Correlation.scala:65-105); state
+    CorrelationState, metric ck / sqrt(xMk * yMk)."""
+    firstColumn: str
+    secondColumn: str
+    where: Optional[str] = None
+    name = "Correlation"
+    entity = Entity.Mutlicolumn
+    DQ_KIND = L.DQ_OP_CORRELATION
+
+    def instance(self):
+        return "%s,%s" % (self.firstColumn, self.secondColumn)
+
+    def additionalPreconditions(self):
+        return [Preconditions.hasColumn(self.firstColumn), Preconditions.isNumeric(self.firstColumn),
+                Preconditions.hasColumn(self.secondColumn), Preconditions.isNumeric(self.secondColumn)]
+
+    def __str__(self):
+        return "Correlation(%s,%s,%s)" % (self.firstColumn, self.secondColumn, _opt(self.where))
 
 
 class DataTypeInstances:

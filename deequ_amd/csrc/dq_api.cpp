@@ -264,7 +264,7 @@ static dq_status validate_predicate(const dq_predicate& p, const int32_t* types,
         break;
       }
       case DQ_P_LIT_STRING: {
-        if (in.i64 < 0 || in.arg < 0 || !p.strings || in.i64 + in.arg > (int64_t)p.strings_len)
+        if (in.i64 < 0 || in.arg < 0 || (in.arg > 0 && !p.strings) || in.i64 + in.arg > (int64_t)p.strings_len)
           return fail(DQ_ERR_INVALID, "string literal outside the predicate's string pool");
         st.push_back(V_STR);
         break;
@@ -450,7 +450,7 @@ static int fast_form(const Program& prog, const int32_t* types, FastPred* fp) {
 }
 
 // ------------------------------------------------------------------------------ plan
-enum Target { TGT_HOST_SIZE = 0, TGT_SCAN = 1, TGT_HLL = 2, TGT_DTYPE = 3 };
+enum Target { TGT_HOST_SIZE = 0, TGT_SCAN = 1, TGT_HLL = 2, TGT_DTYPE = 3, TGT_STRLEN = 4, TGT_CORR = 5 };
 
 struct OpSlot {
   int kind;
@@ -493,10 +493,12 @@ struct dq_plan : Stager {
   std::vector<ScanGroup> groups;
   std::vector<HllTask> hll_tasks;
   std::vector<HllTask> dtype_tasks;  // DataType: {column, type, where}
+  std::vector<HllTask> len_tasks;    // MinLength / MaxLength: {column, type, where}
+  std::vector<CorrTask> corr_tasks;  // Correlation: {x, y, where}
   std::vector<Program> programs;  // generic predicate programs -> batch masks
   // device state
   DevBuf d_tasks, d_groups, d_ranges, d_hll, d_progs, d_insns, d_pool, d_acc, d_partials, d_regs,
-      d_cols, d_masks, d_mask_words, d_dtype, d_dtype_counts;
+      d_cols, d_masks, d_mask_words, d_dtype, d_dtype_counts, d_len, d_len_out, d_corr, d_corr_part, d_corr_acc;
   int64_t mask_words = 0;
   // pinned descriptor staging (DevColumn + DevMask arrays) guarded by an event
   void* h_desc = nullptr;
@@ -535,6 +537,17 @@ static dq_status check_op(const dq_op& op, const int32_t* types, int n_cols) {
       break;
     case DQ_OP_APPROX_COUNT_DISTINCT: DQ_TRY(need_col(false)); break;
     case DQ_OP_DATATYPE: DQ_TRY(need_col(false)); break;
+    case DQ_OP_MIN_LENGTH: case DQ_OP_MAX_LENGTH:
+      DQ_TRY(need_col(false));
+      if (types[op.column] != DQ_T_UTF8)
+        return fail(DQ_ERR_UNSUPPORTED, "analyzer needs a string column (Preconditions.isString)");
+      break;
+    case DQ_OP_CORRELATION:
+      DQ_TRY(need_col(true));
+      if (op.column2 < 0 || op.column2 >= n_cols) return fail(DQ_ERR_INVALID, "op column2 out of range");
+      if (!is_numeric(types[op.column2]))
+        return fail(DQ_ERR_UNSUPPORTED, "analyzer needs a numeric column (Preconditions.isNumeric)");
+      break;
     default: return fail(DQ_ERR_UNSUPPORTED, "unknown op kind " + std::to_string(op.kind));
   }
   if (op.where.code && op.where.n_insns > 0)
@@ -687,6 +700,35 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
         slot.task = t;
         break;
       }
+      case DQ_OP_MIN_LENGTH: case DQ_OP_MAX_LENGTH: {
+        plan->col_used[op.column] = true;
+        slot.target = TGT_STRLEN;
+        int t = -1;
+        for (size_t k = 0; k < plan->len_tasks.size(); ++k)
+          if (plan->len_tasks[k].column == op.column && plan->len_tasks[k].where_mask == where_prog) t = (int)k;
+        if (t < 0) {
+          plan->len_tasks.push_back(HllTask{op.column, column_types[op.column], where_prog, 0});
+          t = (int)plan->len_tasks.size() - 1;
+        }
+        slot.task = t;
+        break;
+      }
+      case DQ_OP_CORRELATION: {
+        plan->col_used[op.column] = true;
+        plan->col_used[op.column2] = true;
+        slot.target = TGT_CORR;
+        int t = -1;
+        for (size_t k = 0; k < plan->corr_tasks.size(); ++k)
+          if (plan->corr_tasks[k].x == op.column && plan->corr_tasks[k].y == op.column2 &&
+              plan->corr_tasks[k].where_mask == where_prog)
+            t = (int)k;
+        if (t < 0) {
+          plan->corr_tasks.push_back(CorrTask{op.column, op.column2, where_prog, 0});
+          t = (int)plan->corr_tasks.size() - 1;
+        }
+        slot.task = t;
+        break;
+      }
       default: st = fail(DQ_ERR_UNSUPPORTED, "unknown op kind");
     }
     plan->slots.push_back(slot);
@@ -746,6 +788,10 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
       (s = upload(plan->d_hll, plan->hll_tasks.data(), plan->hll_tasks.size() * sizeof(HllTask))) != DQ_OK ||
       (s = upload(plan->d_dtype, plan->dtype_tasks.data(), plan->dtype_tasks.size() * sizeof(HllTask))) != DQ_OK ||
       (s = plan->d_dtype_counts.ensure(std::max<size_t>(1, plan->dtype_tasks.size()) * 5 * sizeof(uint64_t))) != DQ_OK ||
+      (s = upload(plan->d_len, plan->len_tasks.data(), plan->len_tasks.size() * sizeof(HllTask))) != DQ_OK ||
+      (s = plan->d_len_out.ensure(std::max<size_t>(1, plan->len_tasks.size()) * 3 * sizeof(uint64_t))) != DQ_OK ||
+      (s = upload(plan->d_corr, plan->corr_tasks.data(), plan->corr_tasks.size() * sizeof(CorrTask))) != DQ_OK ||
+      (s = plan->d_corr_acc.ensure(std::max<size_t>(1, plan->corr_tasks.size()) * sizeof(CorrAcc))) != DQ_OK ||
       (s = upload(plan->d_progs, progs.data(), progs.size() * sizeof(PredProgram))) != DQ_OK ||
       (s = upload(plan->d_insns, insns.data(), insns.size() * sizeof(PredInsn))) != DQ_OK ||
       (s = upload(plan->d_pool, pool.data(), pool.size())) != DQ_OK ||
@@ -795,6 +841,10 @@ extern "C" dq_status dq_plan_reset(dq_plan* plan) {
     DQ_HIP(hipMemsetAsync(plan->d_regs.ptr, 0, plan->hll_tasks.size() * kHllM * sizeof(uint32_t), plan->stream));
   if (!plan->dtype_tasks.empty())
     DQ_HIP(hipMemsetAsync(plan->d_dtype_counts.ptr, 0, plan->dtype_tasks.size() * 5 * sizeof(uint64_t), plan->stream));
+  if (!plan->len_tasks.empty())
+    DQ_HIP(hipMemsetAsync(plan->d_len_out.ptr, 0, plan->len_tasks.size() * 3 * sizeof(uint64_t), plan->stream));
+  if (!plan->corr_tasks.empty())  // all-zero CorrAcc = the empty state (n = 0)
+    DQ_HIP(hipMemsetAsync(plan->d_corr_acc.ptr, 0, plan->corr_tasks.size() * sizeof(CorrAcc), plan->stream));
   DQ_HIP(hipStreamSynchronize(plan->stream));
   plan->total_rows = 0;
   return DQ_OK;
@@ -1009,6 +1059,22 @@ extern "C" dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, in
     DQ_HIP(launch_datatype(static_cast<const HllTask*>(plan->d_dtype.ptr), n_dt, d_cols, d_masks, n_rows, (int)bpt,
                            static_cast<unsigned long long*>(plan->d_dtype_counts.ptr), plan->stream));
   }
+  const int n_len = (int)plan->len_tasks.size();
+  if (n_len > 0) {
+    int64_t bpt = std::max<int64_t>(1, plan->target_blocks / n_len);
+    bpt = std::min<int64_t>(bpt, (n_rows + kBlock - 1) / kBlock);
+    DQ_HIP(launch_strlen(static_cast<const HllTask*>(plan->d_len.ptr), n_len, d_cols, d_masks, n_rows, (int)bpt,
+                         static_cast<unsigned long long*>(plan->d_len_out.ptr), plan->stream));
+  }
+  const int n_corr = (int)plan->corr_tasks.size();
+  if (n_corr > 0) {
+    int64_t bpt = std::max<int64_t>(1, plan->target_blocks / n_corr);
+    bpt = std::min<int64_t>(bpt, (n_rows + kBlock - 1) / kBlock);
+    DQ_TRY(plan->d_corr_part.ensure((size_t)n_corr * (size_t)bpt * sizeof(CorrAcc)));
+    DQ_HIP(launch_corr(static_cast<const CorrTask*>(plan->d_corr.ptr), n_corr, d_cols, d_masks, n_rows, (int)bpt,
+                       static_cast<CorrAcc*>(plan->d_corr_part.ptr), static_cast<CorrAcc*>(plan->d_corr_acc.ptr),
+                       plan->stream));
+  }
   plan->total_rows += n_rows;
   if (any_host) {  // caller's host buffers may be released once we return
     DQ_HIP(hipStreamSynchronize(plan->stream));
@@ -1042,6 +1108,14 @@ extern "C" dq_status dq_plan_finish(dq_plan* plan, dq_state* out, int n_out) {
   std::vector<ScanAcc> acc(plan->scan_tasks.size());
   std::vector<uint32_t> regs(plan->hll_tasks.size() * kHllM);
   std::vector<uint64_t> dtc(plan->dtype_tasks.size() * 5);
+  std::vector<uint64_t> lens(plan->len_tasks.size() * 3);
+  std::vector<CorrAcc> corr(plan->corr_tasks.size());
+  if (!lens.empty())
+    DQ_HIP(hipMemcpyAsync(lens.data(), plan->d_len_out.ptr, lens.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                          plan->stream));
+  if (!corr.empty())
+    DQ_HIP(hipMemcpyAsync(corr.data(), plan->d_corr_acc.ptr, corr.size() * sizeof(CorrAcc), hipMemcpyDeviceToHost,
+                          plan->stream));
   if (!dtc.empty())
     DQ_HIP(hipMemcpyAsync(dtc.data(), plan->d_dtype_counts.ptr, dtc.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
                           plan->stream));
@@ -1067,6 +1141,23 @@ extern "C" dq_status dq_plan_finish(dq_plan* plan, dq_state* out, int n_out) {
     if (s.target == TGT_DTYPE) {  // the StatefulDataType UDAF never returns NULL
       o.has_value = 1;
       for (int k = 0; k < 5; ++k) o.words[k] = (int64_t)dtc[(size_t)s.task * 5 + k];
+      continue;
+    }
+    if (s.target == TGT_STRLEN) {  // min/max(length(...)) is NULL without a selected row
+      const uint64_t* l = &lens[(size_t)s.task * 3];
+      o.has_value = l[0] > 0;
+      o.value = s.kind == DQ_OP_MIN_LENGTH ? (double)(~l[1]) : (double)l[2];
+      continue;
+    }
+    if (s.target == TGT_CORR) {  // Correlation.fromAggregationResult: None unless n > 0 (:85-96)
+      const CorrAcc& c = corr[s.task];
+      o.has_value = c.n > 0.0;
+      o.n = c.n;
+      o.avg = c.xavg;
+      o.y_avg = c.yavg;
+      o.ck = c.ck;
+      o.x_mk = c.xmk;
+      o.y_mk = c.ymk;
       continue;
     }
     if (s.target == TGT_HLL) {  // never NULL (StatefulHyperloglogPlus.nullable = false)
@@ -1306,8 +1397,24 @@ extern "C" dq_status dq_state_merge(const dq_state* a, const dq_state* b, dq_sta
       r.m2 = a->m2 + b->m2 + delta * delta_n * a->n * b->n;
       break;
     }
-    case DQ_OP_MINIMUM: r.value = java_min(a->value, b->value); break;  // Minimum.scala:27-29
-    case DQ_OP_MAXIMUM: r.value = java_max(a->value, b->value); break;  // Maximum.scala:27-29
+    case DQ_OP_MINIMUM: case DQ_OP_MIN_LENGTH:  // MinState.sum (Minimum.scala:27-29)
+      r.value = java_min(a->value, b->value);
+      break;
+    case DQ_OP_MAXIMUM: case DQ_OP_MAX_LENGTH:  // MaxState.sum (Maximum.scala:27-29)
+      r.value = java_max(a->value, b->value);
+      break;
+    case DQ_OP_CORRELATION: {  // CorrelationState.sum (Correlation.scala:37-52)
+      const double n1 = a->n, n2 = b->n, new_n = n1 + n2;
+      const double dx = b->avg - a->avg, dx_n = new_n == 0.0 ? 0.0 : dx / new_n;
+      const double dy = b->y_avg - a->y_avg, dy_n = new_n == 0.0 ? 0.0 : dy / new_n;
+      r.n = new_n;
+      r.avg = a->avg + dx_n * n2;
+      r.y_avg = a->y_avg + dy_n * n2;
+      r.ck = a->ck + b->ck + dx * dy_n * n1 * n2;
+      r.x_mk = a->x_mk + b->x_mk + dx * dx_n * n1 * n2;
+      r.y_mk = a->y_mk + b->y_mk + dy * dy_n * n1 * n2;
+      break;
+    }
     case DQ_OP_APPROX_COUNT_DISTINCT: dq_hll_merge(a->words, b->words, r.words); break;
     case DQ_OP_DATATYPE:  // DataTypeHistogram.sum (DataType.scala:48-51)
       for (int k = 0; k < 5; ++k) r.words[k] = (int64_t)((uint64_t)a->words[k] + (uint64_t)b->words[k]);
@@ -1331,7 +1438,8 @@ extern "C" dq_status dq_state_metric(const dq_state* s, double* out) {
       *out = s->count == 0 ? std::numeric_limits<double>::quiet_NaN() : s->sum / (double)s->count;
       break;
     case DQ_OP_STDDEV: *out = std::sqrt(s->m2 / s->n); break;
-    case DQ_OP_MINIMUM: case DQ_OP_MAXIMUM: *out = s->value; break;
+    case DQ_OP_MINIMUM: case DQ_OP_MAXIMUM: case DQ_OP_MIN_LENGTH: case DQ_OP_MAX_LENGTH: *out = s->value; break;
+    case DQ_OP_CORRELATION: *out = s->ck / std::sqrt(s->x_mk * s->y_mk); break;  // Correlation.scala:54-56
     case DQ_OP_APPROX_COUNT_DISTINCT: *out = dq_hll_count(s->words); break;
     default: return fail(DQ_ERR_INVALID, "unknown state kind");
   }

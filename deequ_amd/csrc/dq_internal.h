@@ -111,6 +111,16 @@ struct HllTask {
   int32_t pad;
 };
 
+// Correlation task (dq_pair.hip) and its running state CorrelationState(n, xAvg, yAvg, ck, xMk, yMk).
+struct CorrTask {
+  int32_t x, y;
+  int32_t where_mask;  // -1 = none
+  int32_t pad;
+};
+struct CorrAcc {
+  double n, xavg, yavg, ck, xmk, ymk;
+};
+
 // One instruction of the generic predicate interpreter (dq_pred_insn after validation).
 struct PredInsn {
   int32_t opcode;
@@ -246,6 +256,14 @@ hipError_t launch_init_acc(ScanAcc* d_acc, int n, hipStream_t stream);
 // DataType (dq_profile.hip): tasks reuse HllTask {column, type, where}; 5 u64 counts per task.
 hipError_t launch_datatype(const HllTask* d_tasks, int n_tasks, const DevColumn* d_cols, const DevMask* d_masks,
                            int64_t n_rows, int blocks_per_task, unsigned long long* d_counts, hipStream_t stream);
+// MinLength / MaxLength (dq_pair.hip): tasks {column, type, where}; 3 u64 per task
+// {selected rows, max of ~length, max of length}.
+hipError_t launch_strlen(const HllTask* d_tasks, int n_tasks, const DevColumn* d_cols, const DevMask* d_masks,
+                         int64_t n_rows, int blocks_per_task, unsigned long long* d_out, hipStream_t stream);
+// Correlation (dq_pair.hip): per-block partials (n_tasks x blocks_per_task), then merged into d_acc.
+hipError_t launch_corr(const CorrTask* d_tasks, int n_tasks, const DevColumn* d_cols, const DevMask* d_masks,
+                       int64_t n_rows, int blocks_per_task, CorrAcc* d_partials, CorrAcc* d_acc,
+                       hipStream_t stream);
 hipError_t launch_cast_utf8(const DevColumn& src, int64_t n_rows, int to_type, void* d_values, uint8_t* d_validity,
                             unsigned long long* d_unsupported, hipStream_t stream);
 

@@ -53,15 +53,17 @@ def _fill_pred(dst: L.DqPredicate, packed) -> None:
 class OpSpec:
     """One dq_op: kind, column index, compiled predicate / where programs."""
 
-    def __init__(self, kind: int, column: int = -1, predicate=None, where=None):
+    def __init__(self, kind: int, column: int = -1, predicate=None, where=None, column2: int = -1):
         self.kind = kind
         self.column = column
+        self.column2 = column2
         self.predicate = _pred_array(predicate)
         self.where = _pred_array(where)
 
     def fill(self, op: L.DqOp) -> None:
         op.kind = self.kind
         op.column = self.column
+        op.column2 = self.column2
         if self.predicate is not None:
             _fill_pred(op.predicate, self.predicate)
         if self.where is not None:
@@ -80,6 +82,8 @@ def op_spec_for(analyzer, schema: Dict[str, str]) -> OpSpec:
         return OpSpec(kind, -1, None, where)
     if kind == L.DQ_OP_COMPLIANCE:
         return OpSpec(kind, -1, compile_predicate(analyzer.predicate, idx), where)
+    if kind == L.DQ_OP_CORRELATION:
+        return OpSpec(kind, idx[analyzer.firstColumn][0], None, where, idx[analyzer.secondColumn][0])
     return OpSpec(kind, idx[analyzer.column][0], None, where)
 
 

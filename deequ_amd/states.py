@@ -12,6 +12,7 @@ partial states do.
 * MinState / MaxState -- Minimum.scala:25-33 / Maximum.scala:25-33
 * ApproxCountDistinctState -- ApproxCountDistinct.scala:26-40
 * DataTypeHistogram -- DataType.scala:40-52
+* CorrelationState -- Correlation.scala:26-57
 """
 from __future__ import annotations
 
@@ -312,6 +313,36 @@ class DataTypeHistogram(State):
         return "DataTypeHistogram(%d,%d,%d,%d,%d)" % self.counts()
 
 
+class CorrelationState(State):
+    """CorrelationState(n, xAvg, yAvg, ck, xMk, yMk) (Correlation.scala:26-57)."""
+    KIND = L.DQ_OP_CORRELATION
+
+    def __init__(self, n: float, xAvg: float, yAvg: float, ck: float, xMk: float, yMk: float):
+        if not n > 0.0:  # Correlation.scala:35
+            raise ValueError("requirement failed: Correlation undefined for n = 0.")
+        self.n, self.xAvg, self.yAvg = float(n), float(xAvg), float(yAvg)
+        self.ck, self.xMk, self.yMk = float(ck), float(xMk), float(yMk)
+
+    def fields(self) -> Tuple[float, ...]:
+        return (self.n, self.xAvg, self.yAvg, self.ck, self.xMk, self.yMk)
+
+    def to_dq(self):
+        return self._dq(n=self.n, avg=self.xAvg, y_avg=self.yAvg, ck=self.ck, x_mk=self.xMk, y_mk=self.yMk)
+
+    @classmethod
+    def from_dq(cls, s):
+        return cls(s.n, s.avg, s.y_avg, s.ck, s.x_mk, s.y_mk)
+
+    def __eq__(self, o):
+        return isinstance(o, CorrelationState) and o.fields() == self.fields()
+
+    def __hash__(self):
+        return hash(("CorrelationState",) + self.fields())
+
+    def __repr__(self):
+        return "CorrelationState(%r,%r,%r,%r,%r,%r)" % self.fields()
+
+
 _BY_KIND = {
     L.DQ_OP_SIZE: NumMatches,
     L.DQ_OP_COMPLETENESS: NumMatchesAndCount,
@@ -323,6 +354,9 @@ _BY_KIND = {
     L.DQ_OP_MAXIMUM: MaxState,
     L.DQ_OP_APPROX_COUNT_DISTINCT: ApproxCountDistinctState,
     L.DQ_OP_DATATYPE: DataTypeHistogram,
+    L.DQ_OP_MIN_LENGTH: MinState,  # MinLength's state is a MinState (MinLength.scala:26)
+    L.DQ_OP_MAX_LENGTH: MaxState,
+    L.DQ_OP_CORRELATION: CorrelationState,
 }
 
 

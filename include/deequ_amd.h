@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define DQ_ABI_VERSION 1
+#define DQ_ABI_VERSION 2
 
 /* ---------------------------------------------------------------- status codes */
 typedef enum dq_status {
@@ -82,7 +82,10 @@ typedef enum dq_op_kind {
   DQ_OP_MINIMUM = 7,               /* Minimum(column, where)            Minimum.scala:35-53     */
   DQ_OP_MAXIMUM = 8,               /* Maximum(column, where)            Maximum.scala:35-53     */
   DQ_OP_APPROX_COUNT_DISTINCT = 9, /* ApproxCountDistinct(column, where) ApproxCountDistinct.scala:47-64 */
-  DQ_OP_DATATYPE = 10              /* DataType(column, where)           DataType.scala:152-183  */
+  DQ_OP_DATATYPE = 10,             /* DataType(column, where)           DataType.scala:152-183  */
+  DQ_OP_MIN_LENGTH = 11,           /* MinLength(column, where)          MinLength.scala:25-41   */
+  DQ_OP_MAX_LENGTH = 12,           /* MaxLength(column, where)          MaxLength.scala:25-41   */
+  DQ_OP_CORRELATION = 13           /* Correlation(column, column2, where) Correlation.scala:77-105 */
 } dq_op_kind;
 
 /*
@@ -131,6 +134,8 @@ typedef struct dq_predicate {
 typedef struct dq_op {
   int32_t kind;              /* dq_op_kind                                     */
   int32_t column;            /* batch column index; ignored for SIZE/COMPLIANCE */
+  int32_t column2;           /* CORRELATION: the second column (secondColumn)    */
+  int32_t reserved;          /* 0                                                */
   dq_predicate predicate;    /* COMPLIANCE only                                */
   dq_predicate where;        /* optional filter (Analyzers.conditionalSelection) */
 } dq_op;
@@ -152,6 +157,8 @@ typedef struct dq_op {
  *   DATATYPE                     DataTypeHistogram(words[0..4] = numNull, numFractional,
  *                                numIntegral, numBoolean, numString)  (always has_value = 1:
  *                                the StatefulDataType UDAF never returns NULL)
+ *   MIN_LENGTH / MAX_LENGTH      MinState(value) / MaxState(value) of the string lengths
+ *   CORRELATION                  CorrelationState(n, avg = xAvg, y_avg, ck, x_mk, y_mk)
  */
 typedef struct dq_state {
   int32_t kind;
@@ -162,6 +169,7 @@ typedef struct dq_state {
   double n, avg, m2;
   double value;
   int64_t words[DQ_HLL_NUM_WORDS];
+  double y_avg, ck, x_mk, y_mk;  /* CORRELATION (with n, avg) */
 } dq_state;
 
 /* ---------------------------------------------------------------- context / plan */

@@ -25,6 +25,13 @@ What is restated (reference = /root/reference, deequ 1.0.3-SNAPSHOT on Spark 2.2
   XXH64 itself is the third-party algorithm (Spark `XXH64` port of Yann Collet's
   xxHash64, not vendored); it is restated here from the published spec and pinned
   against the `xxhash` 3.8.1 Python binding.
+* MinLength / MaxLength `MinLength.scala:25-41`, `MaxLength.scala:25-41`:
+  min/max(length(sel)).cast(double), `length` = Spark 2.2.2 `UTF8String.numChars` (a walk
+  over first bytes: 0xC0-0xDF skip 2, 0xE0-0xEF 3, 0xF0-0xF7 4, 0xF8-0xFB 5, 0xFC-0xFD 6,
+  anything else 1).
+* Correlation `Correlation.scala:26-105` + `catalyst/StatefulCorrelation.scala:24-49`
+  (Spark 2.2.2 `Corr`: per-row update when both inputs are non-NULL, state
+  (n, xAvg, yAvg, ck, xMk, yMk), merge `Correlation.scala:37-52`, metric ck/sqrt(xMk*yMk)).
 * DataType: `StatefulDataType.scala:36-38,58-69` (regex classification of the value cast
   to string), `DataType.scala:98-143` (distribution, determineType).
 * Frequency family: `GroupingAnalyzers.scala:53-80` (group-by, NULL rows dropped,
@@ -375,6 +382,45 @@ class StandardDeviationState:
 
     def metric_value(self):
         return math.sqrt(self.m2 / self.n)
+
+
+def java_div(a: float, b: float) -> float:
+    """Java double division (a / 0.0 is +-Infinity or NaN instead of an exception)."""
+    if b != 0.0 or a != a or b != b:
+        return a / b if b == b else float("nan")
+    if a == 0.0:
+        return float("nan")
+    return math.copysign(math.inf, a) * math.copysign(1.0, b)
+
+
+@dataclass
+class CorrelationState:
+    n: float
+    xAvg: float
+    yAvg: float
+    ck: float
+    xMk: float
+    yMk: float
+
+    def __post_init__(self):
+        if not self.n > 0.0:
+            raise ValueError("Correlation undefined for n = 0.")
+
+    def sum(self, o):  # Correlation.scala:37-52
+        n1, n2 = self.n, o.n
+        new_n = n1 + n2
+        dx = o.xAvg - self.xAvg
+        dx_n = 0.0 if new_n == 0.0 else dx / new_n
+        dy = o.yAvg - self.yAvg
+        dy_n = 0.0 if new_n == 0.0 else dy / new_n
+        return CorrelationState(new_n, self.xAvg + dx_n * n2, self.yAvg + dy_n * n2,
+                                self.ck + o.ck + dx * dy_n * n1 * n2,
+                                self.xMk + o.xMk + dx * dx_n * n1 * n2,
+                                self.yMk + o.yMk + dy * dy_n * n1 * n2)
+
+    def metric_value(self):  # ck / math.sqrt(xMk * yMk), Java arithmetic
+        d = self.xMk * self.yMk
+        return java_div(self.ck, math.sqrt(d) if d >= 0.0 else float("nan"))
 
 
 def _java_min(a: float, b: float) -> float:
@@ -924,6 +970,56 @@ def max_state(table: OTable, column: str, where: Optional[str] = None):
         if _spark_double_lt(best, float(v)):
             best = float(v)
     return MaxState(best)
+
+
+def utf8_num_chars(b: bytes) -> int:
+    """Spark 2.2.2 `UTF8String.numChars`: count the first bytes visited by the walk
+    `i += numBytesForFirstByte(b[i])` (0xFE/0xFF, an index error in 2.2.2, step 1 here)."""
+    n = i = 0
+    while i < len(b):
+        c = b[i]
+        i += 2 if 0xC0 <= c <= 0xDF else 3 if 0xE0 <= c <= 0xEF else 4 if 0xF0 <= c <= 0xF7 else \
+            5 if 0xF8 <= c <= 0xFB else 6 if 0xFC <= c <= 0xFD else 1
+        n += 1
+    return n
+
+
+def _lengths_selected(table, column, where):
+    return [utf8_num_chars(v.encode("utf-8")) for v in _selected_values(table, column, where) if v is not None]
+
+
+def min_length_state(table: OTable, column: str, where: Optional[str] = None):
+    lens = _lengths_selected(table, column, where)
+    return MinState(float(min(lens))) if lens else None
+
+
+def max_length_state(table: OTable, column: str, where: Optional[str] = None):
+    lens = _lengths_selected(table, column, where)
+    return MaxState(float(max(lens))) if lens else None
+
+
+def correlation_state(table: OTable, first: str, second: str, where: Optional[str] = None):
+    """Spark 2.2.2 `Corr` update per row with both inputs non-NULL (cast to double), one
+    partition; None when no row qualifies (Correlation.scala:77-96)."""
+    xs = _selected_values(table, first, where)
+    ys = _selected_values(table, second, where)
+    n = xa = ya = ck = xmk = ymk = 0.0
+    for xv, yv in zip(xs, ys):
+        if xv is None or yv is None:
+            continue
+        x, y = float(xv), float(yv)
+        new_n = n + 1.0
+        dx = x - xa
+        dx_n = dx / new_n
+        dy = y - ya
+        dy_n = dy / new_n
+        new_xa = xa + dx_n
+        new_ya = ya + dy_n
+        ck += dx * (y - new_ya)
+        xmk += dx * (x - new_xa)
+        ymk += dy * (y - new_ya)
+        n, xa, ya = new_n, new_xa, new_ya
+    return CorrelationState(n, xa, ya, ck, xmk, ymk) if n > 0.0 else None
 
 
 def approx_count_distinct_state(table: OTable, column: str, where: Optional[str] = None):

@@ -89,6 +89,13 @@ TABLES = {
         "att1": ["int32", [1, 2, 3]],
         "att2": ["int32", [0, 0, 0]],
     },
+    # getDfWithConditionallyInformativeColumns (:235-242)
+    "dfInformative": {
+        "att1": ["int32", [1, 2, 3]],
+        "att2": ["int32", [4, 5, 6]],
+    },
+    # getDfWithVariableStringLengthValues (:259-268)
+    "dfStringLengths": {"att1": ["string", ["", "a", "bb", "ccc", "dddd"]]},
     # getDfEmpty (:26-33)
     "dfEmpty": {"column1": ["string", []], "column2": ["string", []]},
     # ---- DataType fixtures (AnalyzerTests.scala:294-420)
@@ -205,6 +212,19 @@ CASES = [
     ("hist_missing", "dfMissing", "Histogram", ["att1"], {"bins": 3, "keys": ["NullValue", "a", "b"]}, T + A + ":203-215"),
     ("hist_numeric", "dfNumeric", "Histogram", ["att2"], {"bins": 4, "n_values": 4}, T + A + ":217-227"),
     ("hist_top2", "dfMissing", "Histogram", ["att1", None, 2], {"bins": 3, "keys": ["NullValue", "a"]}, T + A + ":249-261"),
+    # MinLength / MaxLength (AnalyzerTests.scala:506-540, CheckTest.scala:443-452)
+    ("minlength_att1", "dfStringLengths", "MinLength", ["att1"], 0.0, T + A + ":506-510"),
+    ("minlength_where", "dfStringLengths", "MinLength", ["att1", "att1 != ''"], 1.0, T + A + ":512-517"),
+    ("maxlength_att1", "dfStringLengths", "MaxLength", ["att1"], 4.0, T + A + ":524-528"),
+    ("maxlength_where", "dfStringLengths", "MaxLength", ["att1", "att1 != 'dddd'"], 3.0, T + A + ":530-535"),
+    ("null_minlength", "dfNullColumns", "MinLength", ["stringCol"], EMPTY, NH + ":69,109"),
+    ("null_maxlength", "dfNullColumns", "MaxLength", ["stringCol"], EMPTY, NH + ":70,110"),
+    # Correlation (AnalyzerTests.scala:637-655, CheckTest.scala:433-440): "nan" = Double.NaN
+    ("corr_uninformative", "dfUninformative", "Correlation", ["att1", "att2"], "nan", T + A + ":637-642"),
+    ("corr_informative", "dfInformative", "Correlation", ["att1", "att2"], 1.0, T + A + ":643-650"),
+    ("corr_commutative", "dfInformative", "Correlation", ["att2", "att1"], 1.0, T + A + ":651-654"),
+    ("null_corr", "dfNullColumns", "Correlation", ["numericCol", "numericCol2"], EMPTY, NH + ":93,124"),
+    ("null_corr3", "dfNullColumns", "Correlation", ["numericCol", "numericCol3"], EMPTY, NH + ":125"),
 ]
 
 # Known answers that need the union of two tables (state merge == union):

@@ -52,7 +52,8 @@ def oracle_state(name: str, args: List, table: O.OTable):
         return O.compliance_state(table, args[1], *args[2:])
     fn = {"Completeness": O.completeness_state, "Sum": O.sum_state, "Mean": O.mean_state,
           "StandardDeviation": O.stddev_state, "Minimum": O.min_state, "Maximum": O.max_state,
-          "ApproxCountDistinct": O.approx_count_distinct_state}[name]
+          "ApproxCountDistinct": O.approx_count_distinct_state, "MinLength": O.min_length_state,
+          "MaxLength": O.max_length_state, "Correlation": O.correlation_state}[name]
     return fn(table, *args)
 
 
@@ -71,7 +72,10 @@ def oracle_metric(state, name: str = None, args: List = None) -> object:
     if name == "Histogram":
         h = O.histogram_metric(state, *([args[2]] if len(args) > 2 else []))
         return {"bins": h["number_of_bins"], "values": h["values"]}
-    return "empty" if state is None else state.metric_value()
+    if state is None:
+        return "empty"
+    v = state.metric_value()
+    return "nan" if v != v else v
 
 
 def histogram_matches(got: dict, expected: dict) -> bool:

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
     # the ctypes signature table covers the whole header too
     assert declared == set(_lib.SIGNATURES), declared ^ set(_lib.SIGNATURES)
-    assert _lib.lib().dq_abi_version() == 1
+    assert _lib.lib().dq_abi_version() == 2
 
 
 def test_library_reports_no_device_without_gpu_cleanly():
@@ -97,6 +97,42 @@ def test_state_algebra_matches_oracle():
     assert d.NumMatchesAndCount(0, 0).metricValue() != d.NumMatchesAndCount(0, 0).metricValue()  # NaN
     with pytest.raises(ValueError):
         d.StandardDeviationState(0.0, 0.0, 0.0)
+
+
+def test_correlation_state_algebra_matches_oracle():
+    """CorrelationState.sum / metricValue through dq_state_merge / dq_state_metric, bit-exact
+    with the oracle's restatement of Correlation.scala:37-56."""
+    import deequ_amd as d
+    rnd = random.Random(10)
+    for _ in range(200):
+        a = (float(rnd.randint(1, 10 ** 6)),) + tuple(rnd.uniform(-1e3, 1e3) for _ in range(3)) + \
+            (rnd.uniform(0, 1e9), rnd.uniform(0, 1e9))
+        b = (float(rnd.randint(1, 10 ** 6)),) + tuple(rnd.uniform(-1e3, 1e3) for _ in range(3)) + \
+            (rnd.uniform(0, 1e9), rnd.uniform(0, 1e9))
+        got = d.CorrelationState(*a).sum(d.CorrelationState(*b))
+        want = O.CorrelationState(*a).sum(O.CorrelationState(*b))
+        assert got.fields() == (want.n, want.xAvg, want.yAvg, want.ck, want.xMk, want.yMk)
+        assert got.metricValue() == want.metric_value()
+    assert math.isnan(d.CorrelationState(3.0, 2.0, 0.0, 0.0, 2.0, 0.0).metricValue())  # 0 / 0
+    with pytest.raises(ValueError):
+        d.CorrelationState(0.0, 0.0, 0.0, 0.0, 0.0, 0.0)
+
+
+def test_new_ops_are_supported_and_typed():
+    """MinLength/MaxLength need a utf8 column, Correlation two numeric ones; an empty string
+    literal in a `where` filter (AnalyzerTests.scala:515) is a valid predicate."""
+    import ctypes
+    from deequ_amd import _lib as L
+    from deequ_amd.engine import op_spec_for, op_supported
+    from deequ_amd.metrics import MetricCalculationException  # noqa: F401
+    import deequ_amd as d
+    schema = {"s": "string", "i": "int64", "f": "float64"}
+    for a in (d.MinLength("s"), d.MaxLength("s", "s != ''"), d.Correlation("i", "f", "s != 'x'")):
+        op_supported(op_spec_for(a, schema), schema)
+    for a in (d.MinLength("i"), d.Correlation("s", "f")):
+        with pytest.raises(L.DeequAmdError):
+            op_supported(op_spec_for(a, schema), schema)
+    assert ctypes.sizeof(L.DqOp) == 4 * 4 + 2 * ctypes.sizeof(L.DqPredicate)
 
 
 def test_merge_option_semantics():
@@ -223,6 +259,8 @@ def test_known_answer_predicates_compile():
             texts = []
         elif case["analyzer"] == "Compliance":
             texts = args[1:]
+        elif case["analyzer"] == "Correlation":
+            texts = args[2:]
         elif len(args) > 1 or (case["analyzer"] == "Size" and args):
             texts = args[-1:]
         for t in texts:

@@ -24,6 +24,8 @@ def _check(metric, expected, source):
     if expected == "empty":
         assert isinstance(metric.value, Failure), (source, metric)
         assert isinstance(metric.value.exception, EmptyStateException), (source, metric)
+    elif expected == "nan":
+        assert metric.value.isSuccess and metric.value.get() != metric.value.get(), (source, metric)
     else:
         assert metric.value == Success(expected), (source, metric)
 
@@ -71,6 +73,12 @@ def test_precondition_failures(gpu):
     assert isinstance(d.Completeness("someMissingColumn").calculate(table).value.exception,
                       d.NoSuchColumnException)
     assert d.Completeness("someMissingColumn").calculate(table).value.isFailure
+    # MinLength / MaxLength need a string column (AnalyzerTests.scala:519-522, 537-540)
+    numeric = product_table(KA["tables"]["dfNumeric"])
+    for a in (d.MinLength("att1"), d.MaxLength("att1")):
+        assert isinstance(a.calculate(numeric).value.exception, d.WrongColumnTypeException)
+    assert isinstance(d.Correlation("item", "att1").calculate(numeric).value.exception,
+                      d.WrongColumnTypeException)
 
 
 def test_incremental_with_state_provider(gpu):

@@ -27,6 +27,10 @@ PREDICATES = ["c_int64 >= 0", "COALESCE(c_float64, 0.0) > 1000", "c_int8 IS NULL
               "c_int8 = 7", "TRUE"]
 
 
+CORR_PAIRS = [("c_int64", "c_float64"), ("c_int32", "c_float32"), ("c_float64", "c_int8"),
+              ("c_int16", "c_int16")]
+
+
 def _analyzers():
     out = []
     for w in WHERES:
@@ -38,6 +42,9 @@ def _analyzers():
                 d.ApproxCountDistinct("c_string", w), d.ApproxCountDistinct("c_bool", w)]
         for k, p in enumerate(PREDICATES):
             out.append(d.Compliance("p%d" % k, p, w))
+        out += [d.MinLength("c_string", w), d.MaxLength("c_string", w)]
+        for x, y in CORR_PAIRS:
+            out.append(d.Correlation(x, y, w))
     return out
 
 
@@ -68,6 +75,16 @@ def _check_state(a, got, ot):
         else:
             assert got == d.NumMatchesAndCount(exp.num_matches, exp.count), (a, got, exp)
         return
+    if name in ("MinLength", "MaxLength"):
+        exp = (O.min_length_state if name == "MinLength" else O.max_length_state)(ot, a.column, where)
+        if exp is None:
+            assert got is None, (a, got)
+        else:
+            assert got == (d.MinState(exp.min_value) if name == "MinLength" else d.MaxState(exp.max_value)), (a, got)
+        return
+    if name == "Correlation":
+        _check_correlation(a, got, ot)
+        return
     if name == "ApproxCountDistinct":
         exp = O.approx_count_distinct_state(ot, a.column, where)
         assert got is not None and list(got.words) == list(exp.words), a
@@ -96,6 +113,29 @@ def _check_state(a, got, ot):
         assert got == d.MinState(O.min_state(ot, a.column, where).min_value), a
     elif name == "Maximum":
         assert got == d.MaxState(O.max_state(ot, a.column, where).max_value), a
+
+
+def _check_correlation(a, got, ot):
+    """Bit-exact n; xAvg, yAvg, ck, xMk, yMk within 1e-12 of the exact (rational) values, ck on
+    the scale sqrt(xMk * yMk) (it may cancel to ~0)."""
+    w = O._where_mask(ot, a.where)
+    pairs = [(Fraction(float(x)), Fraction(float(y))) for x, y, keep in
+             zip(ot[a.firstColumn].values, ot[a.secondColumn].values, w)
+             if keep is True and x is not None and y is not None]
+    if not pairs:
+        assert got is None, (a, got)
+        return
+    n = len(pairs)
+    sx = sum(p[0] for p in pairs)
+    sy = sum(p[1] for p in pairs)
+    xmk = sum(p[0] * p[0] for p in pairs) - sx * sx / n
+    ymk = sum(p[1] * p[1] for p in pairs) - sy * sy / n
+    ck = sum(p[0] * p[1] for p in pairs) - sx * sy / n
+    assert got.n == float(n), a
+    for g, e in ((got.xAvg, sx / n), (got.yAvg, sy / n), (got.xMk, xmk), (got.yMk, ymk)):
+        assert abs(g - float(e)) <= REL_TOL * abs(float(e)) + 1e-9, (a, g, float(e))
+    scale = math.sqrt(float(xmk) * float(ymk))
+    assert abs(got.ck - float(ck)) <= REL_TOL * scale + 1e-9, (a, got.ck, float(ck))
 
 
 @pytest.mark.parametrize("n", [0, 1, 5, 17, 2047, 2048, 2049, 9000])
@@ -222,3 +262,37 @@ def test_large_batch_properties(gpu):
             assert st2[a] == st[a], a
     del tdev
     torch.cuda.empty_cache()
+
+
+def test_string_lengths_unicode(gpu):
+    """MinLength/MaxLength count characters the way Spark 2.2.2's UTF8String.numChars does
+    (multi-byte sequences are one character each), against the oracle."""
+    vals = ["", "a", "é", "€uro", "日本語テキスト", "😀😀", "x" * 300, None, "mixé€😀", "ab"]
+    spec = {"s": ["string", vals * 37], "i": ["int32", list(range(len(vals) * 37))]}
+    ot, pt = oracle_table(spec), product_table(spec)
+    for w in (None, "i > 100", "i < 0"):
+        for a in (d.MinLength("s", w), d.MaxLength("s", w)):
+            _check_state(a, d.run_scan([a], pt)[a], ot)
+    ctx = d.AnalysisRunner.onData(pt).addAnalyzers([d.MaxLength("s"), d.MinLength("s")]).run()
+    assert ctx.metric(d.MaxLength("s")).value.get() == 300.0
+    assert ctx.metric(d.MinLength("s")).value.get() == 0.0
+
+
+def test_correlation_state_merge_equals_union(gpu):
+    """CorrelationState.sum of two batches' states equals the state of their union (within the
+    fp64 bar), and batch-split invariance of the plan."""
+    rng = np.random.default_rng(77)
+    spec = random_table(rng, 20000, 0.1, ["int64", "float64"])
+    pt = product_table(spec)
+    a = d.Correlation("c_int64", "c_float64")
+    whole = d.run_scan([a], pt)[a]
+    half = 20000 // 2
+    parts = [d.Table.from_pydict({k: (v[0], v[1][s:e]) for k, v in spec.items()}) for s, e in ((0, half), (half, 20000))]
+    merged = d.run_scan([a], parts[0])[a].sum(d.run_scan([a], parts[1])[a])
+    for g, e in zip(merged.fields(), whole.fields()):
+        assert abs(g - e) <= 1e-12 * max(1.0, abs(e)), (merged, whole)
+    batched = d.run_scan([a], d.PartitionedTable(parts))[a]
+    for g, e in zip(batched.fields(), whole.fields()):
+        assert abs(g - e) <= 1e-12 * max(1.0, abs(e)), (batched, whole)
+    r = a.computeMetricFrom(whole).value.get()
+    assert -1.0 <= r <= 1.0
