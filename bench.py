@@ -39,13 +39,14 @@ def parse_args():
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, nproc)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4"],
+    p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
                    help="c2 = the headline scan (default); c3 = HLL on 64 columns; c4 = group-by")
     p.add_argument("--c3-columns", type=int, default=64)
     p.add_argument("--c3-rows", type=int, default=125_000_000, help="rows per GPU (one batch)")
     p.add_argument("--c4-rows", type=int, default=1_000_000_000, help="rows per GPU")
     p.add_argument("--c4-batch", type=int, default=125_000_000, help="rows per string batch")
     p.add_argument("--c4-distinct", type=int, default=201_500_000)
+    p.add_argument("--c5-rows", type=int, default=100_000_000, help="rows per GPU")
     return p.parse_args()
 
 
@@ -252,6 +253,88 @@ def run_c4(args, world, rank, local):
     }
 
 
+def _strings_from_ints(ids, width: int, prefix: bytes, dev):
+    """utf8 column pieces: `prefix` + the zero-padded decimal digits of `ids` (fixed width)."""
+    import torch
+    n = ids.numel()
+    pw = torch.tensor([10 ** (width - 1 - i) for i in range(width)], dtype=torch.int64, device=dev)
+    digits = ((ids[:, None] // pw[None, :]) % 10 + 48).to(torch.uint8)
+    if prefix:
+        pre = torch.tensor(list(prefix), dtype=torch.uint8, device=dev).expand(n, len(prefix))
+        digits = torch.cat([pre, digits], dim=1)
+    return digits.reshape(-1)
+
+
+def make_c5_table(rows: int, rank: int, device: int):
+    """C5: 100 columns, 5% NULL each, seed 5: 40 int64, 30 fp64, 10 low-cardinality
+    strings (<= 100 categories, "cat_NN"), 10 high-cardinality strings (16 digits), 10 bool."""
+    import torch
+    import deequ_amd as d
+    dev = torch.device("cuda", device)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(5 + 1000 * rank)
+    cols = {}
+
+    def valid():
+        return _valid_bits(rows, gen, dev, 0.05)
+
+    for k in range(40):
+        v = torch.randint(-10 ** 6, 10 ** 9, (rows,), generator=gen, device=dev, dtype=torch.int64)
+        cols["l%02d" % k] = d.Column("int64", rows, v, valid(), device=True)
+    for k in range(30):
+        v = torch.randn(rows, generator=gen, device=dev, dtype=torch.float64) * 100.0 + 1000.0
+        cols["d%02d" % k] = d.Column("float64", rows, v, valid(), device=True)
+    for k in range(20):
+        low = k < 10
+        width = 2 if low else 16
+        prefix = b"cat_" if low else b""
+        n_cat = 100 if low else 10 ** 15
+        step = len(prefix) + width
+        chars = torch.empty(rows * step + 16, dtype=torch.uint8, device=dev)
+        sub = 1 << 24
+        for s0 in range(0, rows, sub):
+            e0 = min(rows, s0 + sub)
+            ids = torch.randint(0, n_cat, (e0 - s0,), generator=gen, device=dev, dtype=torch.int64)
+            chars[s0 * step: e0 * step] = _strings_from_ints(ids, width, prefix, dev)
+        offsets = torch.arange(0, step * (rows + 1), step, dtype=torch.int32, device=dev)
+        cols[("s%02d" if low else "u%02d") % k] = d.Column("string", rows, chars, valid(), offsets=offsets,
+                                                        device=True)
+    for k in range(10):
+        bits = _valid_bits(rows, gen, dev, 0.5)  # uniform booleans, packed like a bitmap
+        cols["b%02d" % k] = d.Column("bool", rows, bits, valid(), device=True)
+    torch.cuda.synchronize(dev)
+    return d.Table(cols)
+
+
+def run_c5(args, world, rank, local):
+    """ColumnProfilerRunner over the C5 table: 3 passes (generic stats + HLL + DataType; numeric
+    stats; exact histograms of the low-cardinality columns)."""
+    import deequ_amd as d
+    from deequ_amd.profiles import ColumnProfilerRunner
+    if world > 1:
+        raise SystemExit("c5 runs on one GPU")
+    data = make_c5_table(args.c5_rows, rank, local)
+
+    def step(ev=None):
+        return ColumnProfilerRunner().onData(data).run()
+    elapsed, _, profiles = _timed(args, world, step)
+    p = profiles.profiles
+    n_hist = sum(1 for c in p.values() if c.histogram is not None)
+    step_s = elapsed / args.steps
+    return {
+        "metric": "rows/sec for ColumnProfilerRunner (C5)", "value": args.c5_rows * args.steps / elapsed,
+        "unit": "rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "int64/fp64/utf8/bool", "data": "synthetic C5 table generated in HBM (seed 5, 5% NULL)",
+        "config": {"workload": "C5: %d rows x 100 columns (40 int64, 30 fp64, 10 low- and 10 high-cardinality "
+                               "utf8, 10 bool); ColumnProfilerRunner, 3 passes, KLL off (reference default)"
+                               % args.c5_rows},
+        "check": {"columns": len(p), "histograms": n_hist,
+                  "s00_distinct": p["s00"].approximateNumDistinctValues,
+                  "l00_completeness": p["l00"].completeness},
+    }
+
+
 def _timed(args, world, step):
     """W warmup steps, then K timed steps between barriers + device syncs; max over ranks."""
     import torch
@@ -302,7 +385,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     if args.workload != "c2":
-        result = (run_c3 if args.workload == "c3" else run_c4)(args, world, rank, local)
+        result = {"c3": run_c3, "c4": run_c4, "c5": run_c5}[args.workload](args, world, rank, local)
         if rank == 0:
             print(json.dumps(result))
         if world > 1:

@@ -25,6 +25,7 @@ from .runner import (Analysis, AnalysisRunBuilder, AnalysisRunner, AnalyzerConte
 from .states import (ApproxCountDistinctState, CorrelationState, DataTypeHistogram, MaxState, MeanState, MinState,
                      NumMatches,
                      NumMatchesAndCount, StandardDeviationState, State, SumState)
+from .state_provider import HdfsStateProvider
 from .table import Column, PartitionedTable, Table
 
 __all__ = [n for n in dir() if not n.startswith("_")]

@@ -110,6 +110,7 @@ SIGNATURES = {
     "dq_freq_export": (c_int, [c_void_p, POINTER(DqFreqGroup), c_int64, c_void_p, c_int64,
                                POINTER(c_int64)]),
     "dq_freq_reserve": (c_int, [c_void_p, c_int64]),
+    "dq_freq_expect_groups": (c_int, [c_void_p, c_int64]),
     "dq_freq_lookup": (c_int, [c_void_p, c_void_p, c_int64, POINTER(c_int64)]),
     "dq_freq_top": (c_int, [c_void_p, c_int, POINTER(DqFreqGroup), c_int64, c_void_p, c_int64,
                             POINTER(c_int64), POINTER(c_int64)]),

@@ -25,9 +25,38 @@ namespace {
 
 enum DtPos { DT_NULL = 0, DT_FRACTIONAL = 1, DT_INTEGRAL = 2, DT_BOOLEAN = 3, DT_STRING = 4 };
 
+// Byte sources for the parsers: a plain pointer, or (strings of <= 24 bytes) the aligned 8-byte
+// words covering the string, loaded once -- 4 vector loads instead of one per byte.  Only words
+// holding at least one byte of the string are read (never beyond the page of a valid byte).
+struct PtrSrc {
+  const uint8_t* p;
+  __device__ uint32_t operator[](int32_t i) const { return p[i]; }
+};
+struct WordSrc {
+  uint64_t w0, w1, w2, w3;
+  uint32_t sh;
+  __device__ WordSrc(const uint8_t* p, int32_t n) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(a & ~(uintptr_t)7);
+    sh = (uint32_t)(a & 7);
+    const int32_t last = n > 0 ? (int32_t)(sh + n - 1) >> 3 : -1;
+    w0 = last >= 0 ? w[0] : 0;
+    w1 = last >= 1 ? w[1] : 0;
+    w2 = last >= 2 ? w[2] : 0;
+    w3 = last >= 3 ? w[3] : 0;
+  }
+  __device__ uint32_t operator[](int32_t i) const {
+    const uint32_t j = sh + (uint32_t)i;
+    const uint64_t w = (j >> 3) == 0 ? w0 : (j >> 3) == 1 ? w1 : (j >> 3) == 2 ? w2 : w3;
+    return (uint32_t)(w >> ((j & 7u) * 8u)) & 0xffu;
+  }
+};
+
+
 __device__ inline bool bit_at(const uint8_t* bm, int64_t row) { return (bm[row >> 3] >> (row & 7)) & 1u; }
 
-__device__ int classify_utf8(const uint8_t* p, int32_t n) {
+template <typename Src>
+__device__ int classify_utf8(const Src& p, int32_t n) {
   // DFA: 0 start, 1 after sign, 2 after the optional space, 3 integer digits, 4 after '.', 5 fail
   int st = 0;
   for (int32_t i = 0; i < n && st != 5; ++i) {
@@ -60,7 +89,8 @@ __device__ int classify_row(const DevColumn& c, int64_t row) {
   switch (c.type) {
     case DQ_T_UTF8: {
       const int32_t b = c.offsets[row], e = c.offsets[row + 1];
-      return classify_utf8(static_cast<const uint8_t*>(c.values) + b, e - b);
+      const uint8_t* p = static_cast<const uint8_t*>(c.values) + b;
+      return e - b <= 24 ? classify_utf8(WordSrc(p, e - b), e - b) : classify_utf8(PtrSrc{p}, e - b);
     }
     case DQ_T_BOOL: return DT_BOOLEAN;
     case DQ_T_FLOAT32: return classify_float(static_cast<const float*>(c.values)[row]);
@@ -116,7 +146,8 @@ namespace {
 __device__ inline bool is_java_ws(uint32_t c) { return c <= 0x20u; }  // String.trim()
 
 // UTF8String.toLong (Spark 2.2): [+-]digits[.digits]; the fraction is validated and dropped.
-__device__ bool parse_long(const uint8_t* p, int32_t n, int64_t* out) {
+template <typename Src>
+__device__ bool parse_long(const Src& p, int32_t n, int64_t* out) {
   if (n == 0) return false;
   int32_t i = 0;
   const bool neg = p[0] == '-';
@@ -151,15 +182,17 @@ __device__ bool parse_long(const uint8_t* p, int32_t n, int64_t* out) {
 __device__ const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
                                       1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
 
-__device__ inline bool bytes_are(const uint8_t* p, int32_t n, const char* w, int32_t len) {
+template <typename Src>
+__device__ inline bool bytes_are(const Src& p, int32_t at, int32_t n, const char* w, int32_t len) {
   if (n != len) return false;
   for (int32_t k = 0; k < len; ++k)
-    if (p[k] != (uint8_t)w[k]) return false;
+    if (p[at + k] != (uint32_t)(uint8_t)w[k]) return false;
   return true;
 }
 
 // 0 = NULL (NumberFormatException), 1 = value, 2 = well formed but off the exact fast path
-__device__ int parse_double(const uint8_t* p, int32_t n, double* out) {
+template <typename Src>
+__device__ int parse_double(const Src& p, int32_t n, double* out) {
   int32_t i = 0, e = n;
   while (i < e && is_java_ws(p[i])) ++i;
   while (e > i && is_java_ws(p[e - 1])) --e;
@@ -169,11 +202,11 @@ __device__ int parse_double(const uint8_t* p, int32_t n, double* out) {
     neg = p[i] == '-';
     ++i;
   }
-  if (bytes_are(p + i, e - i, "NaN", 3)) {
+  if (bytes_are(p, i, e - i, "NaN", 3)) {
     *out = __builtin_nan("");
     return 1;
   }
-  if (bytes_are(p + i, e - i, "Infinity", 8)) {
+  if (bytes_are(p, i, e - i, "Infinity", 8)) {
     *out = neg ? -__builtin_huge_val() : __builtin_huge_val();
     return 1;
   }
@@ -219,7 +252,7 @@ __device__ int parse_double(const uint8_t* p, int32_t n, double* out) {
     if (i == e) return 0;
     int32_t x = 0;
     while (i < e) {
-      const uint32_t dg = (uint32_t)p[i] - 48u;
+      const uint32_t dg = p[i] - 48u;
       if (dg > 9u) return 0;
       if (x < 100000) x = x * 10 + (int32_t)dg;
       ++i;
@@ -237,40 +270,50 @@ __device__ int parse_double(const uint8_t* p, int32_t n, double* out) {
   return 1;
 }
 
+template <typename Src>
+__device__ inline bool cast_one(const Src& p, int32_t n, int to_type, int64_t* lv, double* dv, uint32_t* unsup) {
+  if (to_type == DQ_T_INT64) return parse_long(p, n, lv);
+  const int r = parse_double(p, n, dv);
+  *unsup += r == 2;
+  return r == 1;
+}
+
 }  // namespace
 
-// One thread per 8 rows: writes one validity byte and 8 values.
+// One row per lane: values are written coalesced, and each wave's 64 validity bits (a ballot)
+// are stored by its first lane -- one 8-byte word when the wave's rows are all in range.
 __global__ __launch_bounds__(kBlock) void dq_cast_utf8_kernel(DevColumn src, int64_t n_rows, int to_type,
                                                               void* values, uint8_t* validity,
                                                               unsigned long long* n_unsupported) {
-  const int64_t n_bytes = (n_rows + 7) >> 3;
-  for (int64_t byte = (int64_t)blockIdx.x * kBlock + threadIdx.x; byte < n_bytes;
-       byte += (int64_t)gridDim.x * kBlock) {
-    uint32_t vbits = 0u, unsup = 0u;
-    for (int k = 0; k < 8; ++k) {
-      const int64_t row = byte * 8 + k;
-      if (row >= n_rows) break;
-      int64_t lv = 0;
-      double dv = 0.0;
-      bool ok = false;
-      if (src.validity == nullptr || bit_at(src.validity, row)) {
-        const int32_t b = src.offsets[row], e = src.offsets[row + 1];
-        const uint8_t* p = static_cast<const uint8_t*>(src.values) + b;
-        if (to_type == DQ_T_INT64) {
-          ok = parse_long(p, e - b, &lv);
-        } else {
-          const int r = parse_double(p, e - b, &dv);
-          ok = r == 1;
-          unsup += r == 2;
-        }
-      }
-      vbits |= (ok ? 1u : 0u) << k;
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t unsup = 0u;
+  for (int64_t base = (int64_t)blockIdx.x * kBlock; base < n_rows; base += (int64_t)gridDim.x * kBlock) {
+    const int64_t row = base + threadIdx.x;
+    int64_t lv = 0;
+    double dv = 0.0;
+    bool ok = false;
+    if (row < n_rows && (src.validity == nullptr || bit_at(src.validity, row))) {
+      const int32_t b = src.offsets[row], e = src.offsets[row + 1];
+      const uint8_t* p = static_cast<const uint8_t*>(src.values) + b;
+      if (e - b <= 24) ok = cast_one(WordSrc(p, e - b), e - b, to_type, &lv, &dv, &unsup);
+      else ok = cast_one(PtrSrc{p}, e - b, to_type, &lv, &dv, &unsup);
+    }
+    if (row < n_rows) {
       if (to_type == DQ_T_INT64) static_cast<int64_t*>(values)[row] = ok ? lv : 0;
       else static_cast<double*>(values)[row] = ok ? dv : 0.0;
     }
-    validity[byte] = (uint8_t)vbits;
-    if (unsup) atomicAdd(n_unsupported, (unsigned long long)unsup);
+    const uint64_t m = __ballot(ok);
+    const int64_t row0 = row - (int64_t)lane;  // first row of the wave: a multiple of 64
+    if (lane == 0 && row0 < n_rows) {
+      if (row0 + 64 <= n_rows) {
+        *reinterpret_cast<uint64_t*>(validity + (row0 >> 3)) = m;
+      } else {
+        const int64_t nb = ((n_rows - row0) + 7) >> 3;
+        for (int64_t k = 0; k < nb; ++k) validity[(row0 >> 3) + k] = (uint8_t)(m >> (8 * k));
+      }
+    }
   }
+  if (unsup) atomicAdd(n_unsupported, (unsigned long long)unsup);
 }
 
 hipError_t launch_datatype(const HllTask* d_tasks, int n_tasks, const DevColumn* d_cols, const DevMask* d_masks,
@@ -284,8 +327,7 @@ hipError_t launch_datatype(const HllTask* d_tasks, int n_tasks, const DevColumn*
 hipError_t launch_cast_utf8(const DevColumn& src, int64_t n_rows, int to_type, void* d_values, uint8_t* d_validity,
                             unsigned long long* d_unsupported, hipStream_t stream) {
   if (n_rows <= 0) return hipSuccess;
-  const int64_t n_bytes = (n_rows + 7) >> 3;
-  int64_t blocks = (n_bytes + kBlock - 1) / kBlock;
+  int64_t blocks = (n_rows + kBlock - 1) / kBlock;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(dq_cast_utf8_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, src, n_rows, to_type,
                      d_values, d_validity, d_unsupported);

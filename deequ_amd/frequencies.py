@@ -110,6 +110,10 @@ class FrequencyTable:
         """Size the staging for `rows` rows about to be consumed (optional)."""
         L.check(L.lib().dq_freq_reserve(self.handle, int(rows)))
 
+    def expect_groups(self, groups: int) -> None:
+        """Hint: at most about `groups` groups (optional; picks the LDS-aggregating path)."""
+        L.check(L.lib().dq_freq_expect_groups(self.handle, int(groups)))
+
     def consume(self, batch) -> None:
         from .table import dq_columns
         cols = dq_columns(batch, self.names)

@@ -169,7 +169,7 @@ class ColumnProfiler:
         if printStatusUpdates:
             print("### PROFILING: Computing histograms of low-cardinality columns in pass (3/3)...")
         targets = _find_target_columns_for_histograms(schema, generic, lowCardinalityHistogramThreshold)
-        histograms = compute_histograms(data, targets)
+        histograms = compute_histograms(data, targets, generic.approximateNumDistincts)
         return _create_profiles(relevant, generic, numeric, histograms)
 
 
@@ -260,7 +260,8 @@ def _find_target_columns_for_histograms(schema, generic, threshold) -> List[str]
             if schema[c] in _HISTOGRAM_TYPES and generic.typeOf(c) in ok_types and count <= threshold]
 
 
-def compute_histograms(data, target_columns: Sequence[str]) -> Dict[str, Distribution]:
+def compute_histograms(data, target_columns: Sequence[str],
+                       expected_groups: Optional[Dict[str, int]] = None) -> Dict[str, Distribution]:
     """computeHistograms (:564-606): exact (column, value.toString) counts, NULL -> "NullValue",
     one GPU group-by per target column; ratio = count / (sum of the column's counts)."""
     from .frequencies import FrequencyTable, decode_key
@@ -270,6 +271,8 @@ def compute_histograms(data, target_columns: Sequence[str]) -> Dict[str, Distrib
     for c in target_columns:
         dtype = schema[c]
         table = FrequencyTable([c], dict(schema), histogram=True)
+        if expected_groups and c in expected_groups:  # the pass-1 estimate (<= the threshold)
+            table.expect_groups(int(expected_groups[c]) + 1)
         try:
             for batch in data.batches():
                 table.consume(batch)

@@ -282,6 +282,10 @@ dq_status dq_freq_destroy(dq_freq* f);
 /* Optional: size the table's staging for `rows` more rows before consuming them (e.g. the row
  * count of every partition about to be consumed), so staging is not regrown batch by batch. */
 dq_status dq_freq_reserve(dq_freq* f, int64_t rows);
+/* Optional: the caller expects at most `groups` groups (e.g. ColumnProfiler's approximate
+ * distinct count before its histogram pass, ColumnProfiler.scala:535-557).  A handful of groups
+ * is aggregated in LDS per workgroup instead of being staged and sorted. */
+dq_status dq_freq_expect_groups(dq_freq* f, int64_t groups);
 dq_status dq_freq_reset(dq_freq* f);
 dq_status dq_freq_consume(dq_freq* f, const dq_column* columns, int n_columns, int64_t n_rows);
 dq_status dq_freq_get_summary(dq_freq* f, dq_freq_summary* out);
