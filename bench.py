@@ -2,12 +2,13 @@
 
 Workload: per rank 1e9 rows x 8 columns, Bernoulli(0.05) NULLs per
 column; i0..i3 int64 uniform in [-2^30, 2^32), f0,f1 fp64 uniform in [0, 1e6), f2,f3 fp64
-N(1e3, 1e2).  Analyzers (57): Size + per column Completeness, Compliance (c >= 0 for ints,
-c > 5e5 / c > 1e3 for floats), Sum, Mean, StandardDeviation, Minimum, Maximum -- all in ONE
-fused pass per step, exactly as AnalysisRunner.runScanningAnalyzers fuses them.
+N(1e3, 1e2).  Analyzers (65, the north star's "full scan-shareable + HLL suite"): Size + per
+column Completeness, Compliance (c >= 0 for ints, c > 5e5 / c > 1e3 for floats), Sum, Mean,
+StandardDeviation, Minimum, Maximum, ApproxCountDistinct -- all in ONE fused pass per step
+(every column is read once), as AnalysisRunner.runScanningAnalyzers fuses them.
 
 A step = reset the plan, scan the device-resident batch (the fused gfx950 kernels), pull the
-57 states to the host and -- on N > 1 GPUs -- all-gather them over RCCL and merge them in rank
+65 states to the host and -- on N > 1 GPUs -- all-gather them over RCCL and merge them in rank
 order (State.sum), i.e. the whole job including the final merge.  Inputs are resident in HBM
 before timing starts.  Weak scaling: every rank owns its own 1e9-row shard.
 
@@ -97,7 +98,7 @@ def c2_analyzers():
              "f0": "f0 > 5e5", "f1": "f1 > 5e5", "f2": "f2 > 1e3", "f3": "f3 > 1e3"}
     for c in ["i0", "i1", "i2", "i3", "f0", "f1", "f2", "f3"]:
         out += [d.Completeness(c), d.Compliance("%s_rule" % c, preds[c]), d.Sum(c), d.Mean(c),
-                d.StandardDeviation(c), d.Minimum(c), d.Maximum(c)]
+                d.StandardDeviation(c), d.Minimum(c), d.Maximum(c), d.ApproxCountDistinct(c)]
     return out
 
 
@@ -112,7 +113,7 @@ def cpu_baseline(sample_rows: int, threads: int):
                 "sample": "unavailable: %s" % e}
     secs = cdq_oracle.time_c2_scan(sample_rows, threads)
     return {"value": sample_rows / secs, "unit": "rows/s", "cores": threads, "kind": "port",
-            "sample": "%d rows x 8 cols (C2 distributions, 5%% NULL), 57 analyzers, C restatement "
+            "sample": "%d rows x 8 cols (C2 distributions, 5%% NULL), 65 analyzers (8 HLL), C restatement "
                       "of Spark 2.2.2 aggregation (oracle/dq_oracle.c), %d threads, %.2f s"
                       % (sample_rows, threads, secs)}
 
@@ -461,8 +462,8 @@ def main():
         "vs_baseline": None,
         "dtype": "int64+f64",
         "data": "synthetic (C2 distributions generated in HBM, 5% NULL per column)",
-        "config": {"workload": "C2: %d rows/GPU x 8 cols (4 int64 + 4 fp64), 57 scan-shareable "
-                               "analyzers fused in one pass" % args.rows,
+        "config": {"workload": "C2: %d rows/GPU x 8 cols (4 int64 + 4 fp64), 65 scan-shareable "
+                               "analyzers (incl. 8 ApproxCountDistinct) fused in one pass" % args.rows,
                    "rows_per_gpu": args.rows, "columns": 8, "analyzers": n_ops,
                    "parallelism": "dp%d (row shards, states all-gathered over RCCL)" % world},
         "hbm_gbs": achieved,

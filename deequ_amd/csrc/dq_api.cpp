@@ -491,7 +491,8 @@ struct dq_plan : Stager {
   std::vector<OpSlot> slots;
   std::vector<ScanTask> scan_tasks;
   std::vector<ScanGroup> groups;
-  std::vector<HllTask> hll_tasks;
+  std::vector<HllTask> hll_tasks;    // ApproxCountDistinct not fused into the value scan
+  std::vector<std::pair<int, int>> hll_sets;  // (column, where program) of each register set
   std::vector<HllTask> dtype_tasks;  // DataType: {column, type, where}
   std::vector<HllTask> len_tasks;    // MinLength / MaxLength: {column, type, where}
   std::vector<CorrTask> corr_tasks;  // Correlation: {x, y, where}
@@ -662,7 +663,7 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
           // task full: open a sibling task on the same column/filter
           TaskBuild tb = tasks[t];
           tb.t.n_preds = 0;
-          tb.t.flags &= ~TF_STATS;
+          tb.t.flags &= ~(TF_STATS | TF_HLL);
           tasks.push_back(tb);
           t = (int)tasks.size() - 1;
         }
@@ -675,13 +676,19 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
       case DQ_OP_APPROX_COUNT_DISTINCT: {
         plan->col_used[op.column] = true;
         slot.target = TGT_HLL;
-        int t = -1;
-        for (size_t k = 0; k < plan->hll_tasks.size(); ++k)
-          if (plan->hll_tasks[k].column == op.column && plan->hll_tasks[k].where_mask == where_prog)
-            t = (int)k;
+        int t = -1;  // one register set per (column, where)
+        for (size_t k = 0; k < plan->hll_sets.size(); ++k)
+          if (plan->hll_sets[k] == std::make_pair(op.column, where_prog)) t = (int)k;
         if (t < 0) {
-          plan->hll_tasks.push_back(HllTask{op.column, column_types[op.column], where_prog, 0});
-          t = (int)plan->hll_tasks.size() - 1;
+          t = (int)plan->hll_sets.size();
+          plan->hll_sets.emplace_back(op.column, where_prog);
+          if (is_numeric(column_types[op.column])) {  // hashed in the column's value scan
+            const int st_ = find_or_add_task(op.column, where_prog);
+            tasks[st_].t.flags |= TF_VALUES | TF_HLL;
+            tasks[st_].t.hll = t;
+          } else {  // strings / booleans: the HLL kernel
+            plan->hll_tasks.push_back(HllTask{op.column, column_types[op.column], where_prog, t});
+          }
         }
         slot.task = t;
         break;
@@ -796,7 +803,7 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
       (s = upload(plan->d_insns, insns.data(), insns.size() * sizeof(PredInsn))) != DQ_OK ||
       (s = upload(plan->d_pool, pool.data(), pool.size())) != DQ_OK ||
       (s = plan->d_acc.ensure(std::max<size_t>(1, plan->scan_tasks.size()) * sizeof(ScanAcc))) != DQ_OK ||
-      (s = plan->d_regs.ensure(std::max<size_t>(1, plan->hll_tasks.size()) * kHllM * sizeof(uint32_t))) != DQ_OK ||
+      (s = plan->d_regs.ensure(std::max<size_t>(1, plan->hll_sets.size()) * kHllM * sizeof(uint32_t))) != DQ_OK ||
       (s = plan->d_cols.ensure(std::max(1, n_columns) * sizeof(DevColumn))) != DQ_OK ||
       (s = plan->d_masks.ensure(std::max<size_t>(1, plan->programs.size()) * sizeof(DevMask))) != DQ_OK) {
     delete plan;
@@ -837,8 +844,8 @@ extern "C" dq_status dq_plan_reset(dq_plan* plan) {
   if (!plan) return fail(DQ_ERR_INVALID, "plan is NULL");
   DQ_HIP(hipSetDevice(plan->ctx->device));
   DQ_HIP(launch_init_acc(static_cast<ScanAcc*>(plan->d_acc.ptr), (int)plan->scan_tasks.size(), plan->stream));
-  if (!plan->hll_tasks.empty())
-    DQ_HIP(hipMemsetAsync(plan->d_regs.ptr, 0, plan->hll_tasks.size() * kHllM * sizeof(uint32_t), plan->stream));
+  if (!plan->hll_sets.empty())
+    DQ_HIP(hipMemsetAsync(plan->d_regs.ptr, 0, plan->hll_sets.size() * kHllM * sizeof(uint32_t), plan->stream));
   if (!plan->dtype_tasks.empty())
     DQ_HIP(hipMemsetAsync(plan->d_dtype_counts.ptr, 0, plan->dtype_tasks.size() * 5 * sizeof(uint64_t), plan->stream));
   if (!plan->len_tasks.empty())
@@ -1040,7 +1047,8 @@ extern "C" dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, in
     for (size_t g = 0; g < plan->groups.size(); ++g) {
       const ScanGroup& G = plan->groups[g];
       DQ_HIP(launch_scan_group(G.kind, G.ptype, G.np, d_tasks, d_groups + G.dev_offset, (int)G.tasks.size(),
-                               d_cols, d_masks, n_rows, (int)group_bpt[g], parts + group_base[g], plan->stream));
+                               d_cols, d_masks, n_rows, (int)group_bpt[g], parts + group_base[g],
+                               static_cast<uint32_t*>(plan->d_regs.ptr), plan->stream));
     }
     DQ_HIP(launch_scan_reduce(parts, static_cast<const PartRange*>(plan->d_ranges.ptr), n_scan,
                               static_cast<ScanAcc*>(plan->d_acc.ptr), plan->stream));
@@ -1106,7 +1114,7 @@ extern "C" dq_status dq_plan_finish(dq_plan* plan, dq_state* out, int n_out) {
     return fail(DQ_ERR_INVALID, "output array too small");
   DQ_HIP(hipSetDevice(plan->ctx->device));
   std::vector<ScanAcc> acc(plan->scan_tasks.size());
-  std::vector<uint32_t> regs(plan->hll_tasks.size() * kHllM);
+  std::vector<uint32_t> regs(plan->hll_sets.size() * kHllM);
   std::vector<uint64_t> dtc(plan->dtype_tasks.size() * 5);
   std::vector<uint64_t> lens(plan->len_tasks.size() * 3);
   std::vector<CorrAcc> corr(plan->corr_tasks.size());

@@ -24,28 +24,7 @@ struct alignas(16) Vec16 {
   uint32_t w[4];
 };
 
-__device__ inline void hll_update(uint32_t* regs, uint64_t x) {
-  uint32_t idx, pw;
-  hll_idx_rank(x, &idx, &pw);
-  if (pw > regs[idx]) atomicMax(&regs[idx], pw);
-}
-
-// Spark 2.2.2 hash by type (InterpretedHashFunction / XxHash64Function).
-template <typename T> __device__ inline uint64_t spark_hash(T v);
-template <> __device__ inline uint64_t spark_hash<int8_t>(int8_t v) { return xxh64_u32((uint32_t)(int32_t)v, 42); }
-template <> __device__ inline uint64_t spark_hash<int16_t>(int16_t v) { return xxh64_u32((uint32_t)(int32_t)v, 42); }
-template <> __device__ inline uint64_t spark_hash<int32_t>(int32_t v) { return xxh64_u32((uint32_t)v, 42); }
-template <> __device__ inline uint64_t spark_hash<int64_t>(int64_t v) { return xxh64_u64((uint64_t)v, 42); }
-template <> __device__ inline uint64_t spark_hash<float>(float v) {
-  uint32_t bits = __float_as_uint(v);
-  if (v != v) bits = 0x7fc00000u;  // Float.floatToIntBits canonical NaN
-  return xxh64_u32(bits, 42);
-}
-template <> __device__ inline uint64_t spark_hash<double>(double v) {
-  uint64_t bits = (uint64_t)__double_as_longlong(v);
-  if (v != v) bits = 0x7ff8000000000000ull;  // Double.doubleToLongBits canonical NaN
-  return xxh64_u64(bits, 42);
-}
+__device__ inline void hll_update(uint32_t* regs, uint64_t x) { hll_update_lds(regs, x); }
 
 template <int RPL>
 __device__ inline uint32_t load_bits(const uint8_t* bm, int64_t row0, int64_t left) {
@@ -202,7 +181,7 @@ __global__ __launch_bounds__(kBlock) void dq_hll_kernel(const HllTask* __restric
     default: break;
   }
   __syncthreads();
-  uint32_t* out = registers + (int64_t)blockIdx.y * kHllM;
+  uint32_t* out = registers + (int64_t)task.reg_set * kHllM;
   for (int r = threadIdx.x; r < kHllM; r += kBlock) {
     const uint32_t v = regs[r];
     if (v) atomicMax(&out[r], v);

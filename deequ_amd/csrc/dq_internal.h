@@ -68,7 +68,8 @@ enum ScanTaskFlags : int32_t {
   TF_VALUES = 1,      // the task must read the primary column's values
   TF_STATS = 2,       // sum/mean/stddev/min/max wanted
   TF_WHERE = 4,       // filter rows by batch mask `where_mask`
-  TF_VALIDITY = 8     // primary column is read for validity (completeness / null tests)
+  TF_VALIDITY = 8,    // primary column is read for validity (completeness / null tests)
+  TF_HLL = 16         // ApproxCountDistinct of the primary column, fused into the value scan
 };
 
 struct ScanTask {
@@ -77,7 +78,7 @@ struct ScanTask {
   int32_t flags;       // ScanTaskFlags
   int32_t where_mask;  // batch mask index when TF_WHERE
   int32_t n_preds;
-  int32_t pad;
+  int32_t hll;         // TF_HLL: the task's HLL register set (registers + hll * kHllM)
   FastPred preds[kMaxPreds];
 };
 
@@ -108,7 +109,7 @@ struct HllTask {
   int32_t column;
   int32_t ctype;
   int32_t where_mask;  // -1 = none
-  int32_t pad;
+  int32_t reg_set;     // HLL: register set (registers + reg_set * kHllM); unused elsewhere
 };
 
 // Correlation task (dq_pair.hip) and its running state CorrelationState(n, xAvg, yAvg, ck, xMk, yMk).
@@ -240,7 +241,7 @@ hipError_t launch_freq_rehash(const FreqSlot* d_old, uint64_t old_n, const FreqT
 hipError_t launch_scan_group(int kind, int ptype, int np, const ScanTask* d_tasks,
                              const int32_t* d_group, int n_group, const DevColumn* d_cols,
                              const DevMask* d_masks, int64_t n_rows, int blocks_per_task,
-                             ScanAcc* d_partials, hipStream_t stream);
+                             ScanAcc* d_partials, uint32_t* d_hll_regs, hipStream_t stream);
 hipError_t launch_scan_reduce(const ScanAcc* d_partials, const PartRange* d_ranges, int n_tasks,
                               ScanAcc* d_acc, hipStream_t stream);
 hipError_t launch_hll(const HllTask* d_tasks, int n_tasks, const DevColumn* d_cols,
@@ -314,6 +315,35 @@ __host__ __device__ inline void hll_idx_rank(uint64_t x, uint32_t* idx, uint32_t
 #else
   *pw = (uint32_t)__builtin_clzll(w) + 1u;
 #endif
+}
+
+// Spark 2.2.2 XxHash64Function (seed 42) of one value by type (InterpretedHashFunction):
+// the int family hashes as a 4-byte int, long as 8 bytes, float / double through
+// floatToIntBits / doubleToLongBits (one canonical NaN, no -0.0 normalisation in 2.2).
+template <typename T> __host__ __device__ inline uint64_t spark_hash(T v);
+template <> __host__ __device__ inline uint64_t spark_hash<int8_t>(int8_t v) { return xxh64_u32((uint32_t)(int32_t)v, 42); }
+template <> __host__ __device__ inline uint64_t spark_hash<int16_t>(int16_t v) { return xxh64_u32((uint32_t)(int32_t)v, 42); }
+template <> __host__ __device__ inline uint64_t spark_hash<int32_t>(int32_t v) { return xxh64_u32((uint32_t)v, 42); }
+template <> __host__ __device__ inline uint64_t spark_hash<int64_t>(int64_t v) { return xxh64_u64((uint64_t)v, 42); }
+template <> __host__ __device__ inline uint64_t spark_hash<float>(float v) {
+  uint32_t bits;
+  __builtin_memcpy(&bits, &v, 4);
+  if (v != v) bits = 0x7fc00000u;  // Float.floatToIntBits canonical NaN
+  return xxh64_u32(bits, 42);
+}
+template <> __host__ __device__ inline uint64_t spark_hash<double>(double v) {
+  uint64_t bits;
+  __builtin_memcpy(&bits, &v, 8);
+  if (v != v) bits = 0x7ff8000000000000ull;  // Double.doubleToLongBits canonical NaN
+  return xxh64_u64(bits, 42);
+}
+
+// M[idx] = max(M[idx], pw) on a workgroup's LDS register copy; the atomic is skipped when the
+// register already holds >= pw (after a few thousand rows almost every update is a no-op).
+__device__ inline void hll_update_lds(uint32_t* regs, uint64_t x) {
+  uint32_t idx, pw;
+  hll_idx_rank(x, &idx, &pw);
+  if (pw > regs[idx]) atomicMax(&regs[idx], pw);
 }
 
 }  // namespace dq

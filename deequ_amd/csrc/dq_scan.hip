@@ -25,6 +25,10 @@
 //                    (StandardDeviation.scala:37-44); no per-element fp64 divide
 //   pm / pn        : per predicate Σ TRUE / Σ NOT NULL among where-TRUE rows
 //                    (Compliance: sum(cast(when(where, pred) as int)), Compliance.scala:49)
+//   HLL registers  : ApproxCountDistinct of a numeric column rides on the same pass (TF_HLL):
+//                    each selected row is hashed (Spark XXH64, seed 42) into a workgroup copy of
+//                    the 512 registers in LDS, folded into the task's set with atomicMax at the
+//                    end (StatefulHyperloglogPlus.scala:89-139) -- the column is read once
 #include "dq_internal.h"
 
 namespace dq {
@@ -433,6 +437,17 @@ __device__ inline uint32_t cmp_bits(const V* x, V lit, const FastPred& fp) {
   return r;
 }
 
+// HLL updates of R rows (selection bits `sel`): every row is hashed (branch-free), only the
+// selected ones touch the LDS registers.
+template <typename T, int R>
+__device__ inline void hll_rows(uint32_t* lregs, const T* vals, uint32_t sel) {
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const uint64_t x = spark_hash<T>(vals[k]);
+    if ((sel >> k) & 1u) hll_update_lds(lregs, x);
+  }
+}
+
 // Inline predicates over R rows: counts TRUE and NOT NULL among where-TRUE rows.
 template <typename T, int NP, int R>
 __device__ inline void predicate_rows(ThreadAcc<NP>& a, const FastPred* fps, const T* vals,
@@ -480,7 +495,7 @@ template <typename T, int NP, bool EXT>
 __global__ __launch_bounds__(kBlock) void dq_scan_values_kernel(
     const ScanTask* __restrict__ tasks, const int32_t* __restrict__ group,
     const DevColumn* __restrict__ cols, const DevMask* __restrict__ masks, int64_t n_rows,
-    ScanAcc* partials) {
+    ScanAcc* partials, uint32_t* __restrict__ hll_regs) {
   constexpr int RPL = 16 / (int)sizeof(T);
   constexpr int UNROLL = sizeof(T) >= 8 ? 4 : (sizeof(T) == 4 ? 2 : 1);
   constexpr uint32_t ROWS_PER_ITER = (uint32_t)kBlock * RPL * UNROLL;
@@ -492,6 +507,13 @@ __global__ __launch_bounds__(kBlock) void dq_scan_values_kernel(
   int64_t row_begin, row_end;
   chunk_of_block(n_rows, row_begin, row_end);
   const uint32_t span = (uint32_t)(row_end - row_begin);  // host keeps span * 8 < 4 GiB
+  // fused ApproxCountDistinct: the workgroup's copy of the 512 registers (uniform per block)
+  __shared__ uint32_t lregs[kHllM];
+  const bool hll_on = (task.flags & TF_HLL) != 0;
+  if (hll_on) {
+    for (int r = threadIdx.x; r < kHllM; r += kBlock) lregs[r] = 0u;
+    __syncthreads();
+  }
 
   const DevColumn& col = cols[task.primary];
   const __amdgpu_buffer_rsrc_t rv =
@@ -585,6 +607,7 @@ __global__ __launch_bounds__(kBlock) void dq_scan_values_kernel(
       a.n_wnn += __builtin_popcount(wnb[u]);
       accumulate_rows<T, NP, RPL>(a, vals, sel, shift, psum);
       predicate_rows<T, NP, RPL>(a, fps, vals, vb[u], wtb[u], mtb[u], mnb[u]);
+      if (hll_on) hll_rows<T, RPL>(lregs, vals, sel);
     }
     if constexpr (!IsIntegral<T>::value) neumaier_add(a.fs, a.fc, psum);
   }
@@ -605,8 +628,17 @@ __global__ __launch_bounds__(kBlock) void dq_scan_values_kernel(
     a.n_wnn += wn;
     accumulate_rows<T, NP, 1>(a, &v, valid & wt, shift, psum);
     predicate_rows<T, NP, 1>(a, fps, &v, valid, wt, mt, mn);
+    if (hll_on) hll_rows<T, 1>(lregs, &v, valid & wt);
   }
   if constexpr (!IsIntegral<T>::value) neumaier_add(a.fs, a.fc, psum);
+  if (hll_on) {  // fold the workgroup's registers into the task's set (max: order independent)
+    __syncthreads();
+    uint32_t* out = hll_regs + (int64_t)task.hll * kHllM;
+    for (int r = threadIdx.x; r < kHllM; r += kBlock) {
+      const uint32_t v = lregs[r];
+      if (v) atomicMax(&out[r], v);
+    }
+  }
   a.shift = shift;
   thread_finish<NP>(a, NP, &partials[(int64_t)blockIdx.y * gridDim.x + blockIdx.x]);
 }
@@ -721,18 +753,18 @@ __global__ void dq_init_acc_kernel(ScanAcc* acc, int n) {
 template <typename T>
 static hipError_t launch_values_np(int np, dim3 grid, hipStream_t s, const ScanTask* t,
                                    const int32_t* g, const DevColumn* c, const DevMask* m,
-                                   int64_t n, ScanAcc* part) {
+                                   int64_t n, ScanAcc* part, uint32_t* hr) {
   if (np < 0) {  // EXT: where masks / mask predicates, all predicate slots
-    hipLaunchKernelGGL((dq_scan_values_kernel<T, kMaxPreds, true>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part);
+    hipLaunchKernelGGL((dq_scan_values_kernel<T, kMaxPreds, true>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part, hr);
     return hipGetLastError();
   }
   switch (np) {
-    case 0: hipLaunchKernelGGL((dq_scan_values_kernel<T, 0, false>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part); break;
-    case 1: hipLaunchKernelGGL((dq_scan_values_kernel<T, 1, false>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part); break;
-    case 2: hipLaunchKernelGGL((dq_scan_values_kernel<T, 2, false>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part); break;
-    case 3: hipLaunchKernelGGL((dq_scan_values_kernel<T, 3, false>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part); break;
-    case 4: hipLaunchKernelGGL((dq_scan_values_kernel<T, 4, false>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part); break;
-    default: hipLaunchKernelGGL((dq_scan_values_kernel<T, kMaxPreds, false>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part); break;
+    case 0: hipLaunchKernelGGL((dq_scan_values_kernel<T, 0, false>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part, hr); break;
+    case 1: hipLaunchKernelGGL((dq_scan_values_kernel<T, 1, false>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part, hr); break;
+    case 2: hipLaunchKernelGGL((dq_scan_values_kernel<T, 2, false>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part, hr); break;
+    case 3: hipLaunchKernelGGL((dq_scan_values_kernel<T, 3, false>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part, hr); break;
+    case 4: hipLaunchKernelGGL((dq_scan_values_kernel<T, 4, false>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part, hr); break;
+    default: hipLaunchKernelGGL((dq_scan_values_kernel<T, kMaxPreds, false>), grid, dim3(kBlock), 0, s, t, g, c, m, n, part, hr); break;
   }
   return hipGetLastError();
 }
@@ -740,7 +772,7 @@ static hipError_t launch_values_np(int np, dim3 grid, hipStream_t s, const ScanT
 hipError_t launch_scan_group(int kind, int ptype, int np, const ScanTask* d_tasks,
                              const int32_t* d_group, int n_group, const DevColumn* d_cols,
                              const DevMask* d_masks, int64_t n_rows, int blocks_per_task,
-                             ScanAcc* d_partials, hipStream_t stream) {
+                             ScanAcc* d_partials, uint32_t* d_hll_regs, hipStream_t stream) {
   if (n_group <= 0) return hipSuccess;
   dim3 grid(blocks_per_task, n_group);
   if (kind == 0) {
@@ -749,12 +781,17 @@ hipError_t launch_scan_group(int kind, int ptype, int np, const ScanTask* d_task
     return hipGetLastError();
   }
   switch (ptype) {
-    case DQ_T_INT8: return launch_values_np<int8_t>(np, grid, stream, d_tasks, d_group, d_cols, d_masks, n_rows, d_partials);
-    case DQ_T_INT16: return launch_values_np<int16_t>(np, grid, stream, d_tasks, d_group, d_cols, d_masks, n_rows, d_partials);
-    case DQ_T_INT32: return launch_values_np<int32_t>(np, grid, stream, d_tasks, d_group, d_cols, d_masks, n_rows, d_partials);
-    case DQ_T_INT64: return launch_values_np<int64_t>(np, grid, stream, d_tasks, d_group, d_cols, d_masks, n_rows, d_partials);
-    case DQ_T_FLOAT32: return launch_values_np<float>(np, grid, stream, d_tasks, d_group, d_cols, d_masks, n_rows, d_partials);
-    default: return launch_values_np<double>(np, grid, stream, d_tasks, d_group, d_cols, d_masks, n_rows, d_partials);
+    case DQ_T_INT8: return launch_values_np<int8_t>(np, grid, stream, d_tasks, d_group, d_cols, d_masks, n_rows, d_partials, d_hll_regs);
+    case DQ_T_INT16: return launch_values_np<int16_t>(np, grid, stream, d_tasks, d_group, d_cols, d_masks, n_rows, d_partials,
+                                                        d_hll_regs);
+    case DQ_T_INT32: return launch_values_np<int32_t>(np, grid, stream, d_tasks, d_group, d_cols, d_masks, n_rows, d_partials,
+                                                        d_hll_regs);
+    case DQ_T_INT64: return launch_values_np<int64_t>(np, grid, stream, d_tasks, d_group, d_cols, d_masks, n_rows, d_partials,
+                                                        d_hll_regs);
+    case DQ_T_FLOAT32: return launch_values_np<float>(np, grid, stream, d_tasks, d_group, d_cols, d_masks, n_rows, d_partials,
+                                                        d_hll_regs);
+    default: return launch_values_np<double>(np, grid, stream, d_tasks, d_group, d_cols, d_masks, n_rows, d_partials,
+                                                        d_hll_regs);
   }
 }
 

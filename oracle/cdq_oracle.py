@@ -37,6 +37,8 @@ def lib():
                                ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double),
                                ctypes.c_int, ctypes.POINTER(ColState)]
+        l.dqo_time_c2_hll.restype = ctypes.c_double
+        l.dqo_time_c2_hll.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         l.dqo_gen_c2.restype = None
         l.dqo_gen_c2.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int,
                                  ctypes.c_void_p, ctypes.c_void_p]
@@ -49,11 +51,12 @@ def lib():
     return _lib
 
 
-def time_c2_scan(rows: int, threads: int) -> float:
+def time_c2_scan(rows: int, threads: int, hll: bool = True) -> float:
     """Seconds for the Spark-semantics scan of a C2 sample of `rows` rows on `threads` threads
-    (data generation excluded)."""
+    (data generation excluded); with `hll`, the 8 columns' HLL registers in the timed region."""
     out = (ColState * 8)()
-    secs = lib().dqo_time_c2(rows, threads, out)
+    regs = (ctypes.c_uint8 * (8 * 512))() if hll else None
+    secs = lib().dqo_time_c2_hll(rows, threads, out, regs)
     if secs < 0:
         raise MemoryError("oracle could not allocate the C2 sample")
     return secs

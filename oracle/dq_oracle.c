@@ -239,7 +239,33 @@ static void* gen_thread(void* arg) {
 }
 
 /* bench.py cpu_baseline: generate a C2 sample (untimed), time dqo_scan over it. */
+typedef struct {
+  int64_t b, e;
+  void** values;
+  uint8_t** validity;
+  uint8_t regs[8][512];
+} hll_job;
+
+void dqo_hll_registers(int type, int64_t n, const void* values, const int32_t* offsets,
+                       const uint8_t* validity, uint8_t* regs512);
+
+static void* hll_thread(void* arg) {
+  hll_job* j = (hll_job*)arg;
+  for (int c = 0; c < 8; ++c)
+    dqo_hll_registers(c < 4 ? 5 : 7, j->e - j->b, (const uint8_t*)j->values[c] + j->b * 8, NULL,
+                      j->validity[c] + (j->b >> 3), j->regs[c]);
+  return NULL;
+}
+
+/* C2 with ApproxCountDistinct too: the scan, then the HLL registers of the 8 columns (row
+ * partitions per thread, merged by register max = DeequHyperLogLogPlusPlusUtils.merge). */
+double dqo_time_c2_hll(int64_t rows, int threads, dqo_colstate* out8, uint8_t* regs8x512);
+
 double dqo_time_c2(int64_t rows, int threads, dqo_colstate* out8) {
+  return dqo_time_c2_hll(rows, threads, out8, NULL);
+}
+
+double dqo_time_c2_hll(int64_t rows, int threads, dqo_colstate* out8, uint8_t* regs8x512) {
   int types[8], pred_op[8], as_f64[8];
   int64_t lit_i[8];
   double lit_f[8];
@@ -272,6 +298,26 @@ double dqo_time_c2(int64_t rows, int threads, dqo_colstate* out8) {
   clock_gettime(CLOCK_MONOTONIC, &t0);
   dqo_scan(rows, 8, types, (const void* const*)values, (const uint8_t* const*)validity, pred_op,
            as_f64, lit_i, lit_f, threads, out8);
+  if (regs8x512) {
+    const int ng = threads < 1 ? 1 : (threads > 64 ? 64 : threads);
+    pthread_t th[64];
+    hll_job* jobs = (hll_job*)calloc((size_t)ng, sizeof(hll_job));
+    if (!jobs) return -1.0;
+    for (int t = 0; t < ng; ++t) {
+      jobs[t].b = (rows * t / ng) & ~7ll;
+      jobs[t].e = t == ng - 1 ? rows : ((rows * (t + 1) / ng) & ~7ll);
+      jobs[t].values = values;
+      jobs[t].validity = validity;
+      pthread_create(&th[t], NULL, hll_thread, &jobs[t]);
+    }
+    for (int t = 0; t < ng; ++t) pthread_join(th[t], NULL);
+    memset(regs8x512, 0, 8 * 512);
+    for (int t = 0; t < ng; ++t)
+      for (int c = 0; c < 8; ++c)
+        for (int r = 0; r < 512; ++r)
+          if (jobs[t].regs[c][r] > regs8x512[c * 512 + r]) regs8x512[c * 512 + r] = jobs[t].regs[c][r];
+    free(jobs);
+  }
   clock_gettime(CLOCK_MONOTONIC, &t1);
   for (int c = 0; c < 8; ++c) {
     free(values[c]);
