@@ -179,6 +179,23 @@ def make_c4_batches(rows: int, batch: int, distinct: int, rank: int, device: int
     return d.PartitionedTable(parts)
 
 
+def valu_roofline(device: int, hashes: float, kernel_ms: float):
+    """The hash-bound side of an HLL pass ("HLL is additionally checked against the
+    VALU int64-multiply rate"): `hashes` XXH64+register updates executed per launch (every row of
+    every HLL column -- the kernels hash branch-free, NULL rows included) over the launch time,
+    against the rate a register-only kernel (dq_diag_hash_rate, no HBM traffic) sustains on this
+    card right now."""
+    from deequ_amd import _lib
+    peak = ctypes.c_double(0.0)
+    if _lib.lib().dq_diag_hash_rate(device, 1, 5, ctypes.byref(peak)) != 0:
+        return None
+    achieved = hashes / (kernel_ms * 1e-3)
+    return {"bound": "valu", "achieved": achieved / 1e9, "peak": peak.value / 1e9,
+            "unit": "Ghash/s", "frac": achieved / peak.value, "hashes_per_launch": hashes,
+            "peak_source": "dq_diag_hash_rate: Spark XXH64 (5 x 64-bit multiply) + HLL LDS "
+                           "update, register-only, measured live"}
+
+
 def run_c3(args, world, rank, local):
     """HLL++ ApproxCountDistinct on C3 columns: one fused dq_plan, HIP events on its stream."""
     import torch
@@ -218,6 +235,7 @@ def run_c3(args, world, rank, local):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel_ms": kernel_ms,
                      "algorithmic_bytes_per_launch": bpr * args.c3_rows},
+        "valu_roofline": valu_roofline(local, float(args.c3_rows) * args.c3_columns, kernel_ms),
         "check": {"column0_estimate": est, "rows_column0": args.c3_rows},
     }
 
@@ -398,6 +416,7 @@ def main():
     plan = Plan([op_spec_for(a, table.schema) for a in analyzers], table.schema, device=local)
     stream = torch.cuda.ExternalStream(plan.stream, device=torch.device("cuda", local))
     n_ops = len(analyzers)
+    n_hll = sum(isinstance(a, d.ApproxCountDistinct) for a in analyzers)
 
     def step(ev_pair=None):
         plan.reset()
@@ -471,6 +490,7 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel_ms": kernel_ms,
                      "algorithmic_bytes_per_launch": BYTES_PER_ROW * args.rows},
+        "valu_roofline": valu_roofline(local, float(args.rows) * n_hll, kernel_ms) if n_hll else None,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -78,6 +78,12 @@ class DqFreqGroup(Structure):
                 ("reserved", c_int32)]
 
 
+# measurement entry points (include/deequ_amd_diag.h; not part of the drop-in boundary)
+DIAG_SIGNATURES = {
+    "dq_diag_hash_rate": (c_int, [c_int, c_int, c_int, POINTER(c_double)]),
+}
+
+
 # every symbol include/deequ_amd.h declares, with its ctypes signature
 SIGNATURES = {
     "dq_last_error": (c_char_p, []),
@@ -157,7 +163,7 @@ def lib():
         except ImportError:
             pass
         l = ctypes.CDLL(LIB_PATH)
-        for name, (res, args) in SIGNATURES.items():
+        for name, (res, args) in list(SIGNATURES.items()) + list(DIAG_SIGNATURES.items()):
             fn = getattr(l, name)
             fn.restype = res
             fn.argtypes = args

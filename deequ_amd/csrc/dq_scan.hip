@@ -386,7 +386,6 @@ __device__ inline T buf_elem(__amdgpu_buffer_rsrc_t rs, uint32_t row) {
 template <typename T, int NP, int R>
 __device__ inline void accumulate_rows(ThreadAcc<NP>& a, const T* vals, uint32_t sel, double shift,
                                        double& psum) {
-  a.n_sel += __builtin_popcount(sel);
   if constexpr (IsIntegral<T>::value) {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
@@ -437,15 +436,12 @@ __device__ inline uint32_t cmp_bits(const V* x, V lit, const FastPred& fp) {
   return r;
 }
 
-// HLL updates of R rows (selection bits `sel`): every row is hashed (branch-free), only the
-// selected ones touch the LDS registers.
+// Spark XXH64 of R rows (every row is hashed, branch-free); the register updates go through
+// hll_update_lds_batch once per iteration.
 template <typename T, int R>
-__device__ inline void hll_rows(uint32_t* lregs, const T* vals, uint32_t sel) {
+__device__ inline void hash_rows(uint64_t* h, const T* vals) {
 #pragma unroll
-  for (int k = 0; k < R; ++k) {
-    const uint64_t x = spark_hash<T>(vals[k]);
-    if ((sel >> k) & 1u) hll_update_lds(lregs, x);
-  }
+  for (int k = 0; k < R; ++k) h[k] = spark_hash<T>(vals[k]);
 }
 
 // Inline predicates over R rows: counts TRUE and NOT NULL among where-TRUE rows.
@@ -510,6 +506,8 @@ __global__ __launch_bounds__(kBlock) void dq_scan_values_kernel(
   // fused ApproxCountDistinct: the workgroup's copy of the 512 registers (uniform per block)
   __shared__ uint32_t lregs[kHllM];
   const bool hll_on = (task.flags & TF_HLL) != 0;
+  // Sum/Mean/StdDev/Min/Max of the primary column wanted (uniform per block: a scalar branch)
+  const bool stats_on = (task.flags & TF_STATS) != 0;
   if (hll_on) {
     for (int r = threadIdx.x; r < kHllM; r += kBlock) lregs[r] = 0u;
     __syncthreads();
@@ -605,11 +603,23 @@ __global__ __launch_bounds__(kBlock) void dq_scan_values_kernel(
       const uint32_t sel = vb[u] & wtb[u];
       a.n_rows += __builtin_popcount(wtb[u]);
       a.n_wnn += __builtin_popcount(wnb[u]);
-      accumulate_rows<T, NP, RPL>(a, vals, sel, shift, psum);
+      a.n_sel += __builtin_popcount(sel);
+      if (stats_on) accumulate_rows<T, NP, RPL>(a, vals, sel, shift, psum);
       predicate_rows<T, NP, RPL>(a, fps, vals, vb[u], wtb[u], mtb[u], mnb[u]);
-      if (hll_on) hll_rows<T, RPL>(lregs, vals, sel);
     }
-    if constexpr (!IsIntegral<T>::value) neumaier_add(a.fs, a.fc, psum);
+    if (hll_on) {  // all UNROLL * RPL rows of the iteration: hashes, then one batched update
+      uint64_t h[UNROLL * RPL];
+      uint32_t sel_all = 0u;
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        hash_rows<T, RPL>(h + u * RPL, reinterpret_cast<const T*>(&vec[u]));
+        sel_all |= (vb[u] & wtb[u]) << (u * RPL);
+      }
+      hll_update_lds_batch<UNROLL * RPL>(lregs, h, sel_all);
+    }
+    if constexpr (!IsIntegral<T>::value) {
+      if (stats_on) neumaier_add(a.fs, a.fc, psum);
+    }
   }
   // ---- ragged end of the chunk: one row per lane
   double psum = 0.0;
@@ -626,9 +636,13 @@ __global__ __launch_bounds__(kBlock) void dq_scan_values_kernel(
     }
     a.n_rows += wt;
     a.n_wnn += wn;
-    accumulate_rows<T, NP, 1>(a, &v, valid & wt, shift, psum);
+    a.n_sel += valid & wt;
+    if (stats_on) accumulate_rows<T, NP, 1>(a, &v, valid & wt, shift, psum);
     predicate_rows<T, NP, 1>(a, fps, &v, valid, wt, mt, mn);
-    if (hll_on) hll_rows<T, 1>(lregs, &v, valid & wt);
+    if (hll_on) {
+      const uint64_t h = spark_hash<T>(v);
+      hll_update_lds_batch<1>(lregs, &h, valid & wt);
+    }
   }
   if constexpr (!IsIntegral<T>::value) neumaier_add(a.fs, a.fc, psum);
   if (hll_on) {  // fold the workgroup's registers into the task's set (max: order independent)

@@ -1,0 +1,27 @@
+/*
+ * deequ_amd_diag.h -- measurement entry points of libdeequ_amd.so.  Not part of the drop-in
+ * boundary (deequ_amd.h): no reference call site binds these.  bench.py uses them to price
+ * the hash-bound kernels (ApproxCountDistinct, StatefulHyperloglogPlus.scala:89-115) against
+ * the VALU hash rate the card sustains, next to the HBM roofline.
+ */
+#ifndef DEEQU_AMD_DIAG_H
+#define DEEQU_AMD_DIAG_H
+
+#include <stdint.h>
+#include "deequ_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Runs `reps` launches of a register-only kernel that hashes int64 values with Spark's
+ * XXH64 (seed 42), and with `with_hll` != 0 also takes each hash's HLL index/rank and folds it
+ * into an LDS register copy, on `device`; no HBM traffic.  Writes the sustained hash rate
+ * (hashes per second, best launch) to *hashes_per_sec. */
+dq_status dq_diag_hash_rate(int device, int with_hll, int reps, double* hashes_per_sec);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DEEQU_AMD_DIAG_H */

@@ -265,3 +265,12 @@ def test_known_answer_predicates_compile():
             texts = args[-1:]
         for t in texts:
             compile_predicate(t, schema)
+
+
+def test_library_exports_every_diag_symbol():
+    from deequ_amd import _lib
+    header = open(os.path.join(ROOT, "include", "deequ_amd_diag.h")).read()
+    declared = set(re.findall(r"^(?:const\s+)?[a-z_0-9]+\s*\*?\s*(dq_[a-z0-9_]+)\s*\(", header, re.M))
+    assert declared == set(_lib.DIAG_SIGNATURES), declared ^ set(_lib.DIAG_SIGNATURES)
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    assert all(hasattr(lib, s) for s in declared)
