@@ -40,8 +40,9 @@ def parse_args():
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, nproc)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
+    p.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5"],
                    help="c2 = the headline scan (default); c3 = HLL on 64 columns; c4 = group-by")
+    p.add_argument("--c1-rows", type=int, default=10_000_000, help="rows per GPU")
     p.add_argument("--c3-columns", type=int, default=64)
     p.add_argument("--c3-rows", type=int, default=125_000_000, help="rows per GPU (one batch)")
     p.add_argument("--c4-rows", type=int, default=1_000_000_000, help="rows per GPU")
@@ -325,6 +326,79 @@ def make_c5_table(rows: int, rank: int, device: int):
     return d.Table(cols)
 
 
+def make_c1_table(rows: int, rank: int, device: int):
+    """C1 (BASELINE configs[0]): the Item table of examples/entities.scala:19-25,
+    seed 1.  id = 0..n-1; productName "Thingy <id>" and description (fixed-width utf8), priority
+    "high"/"low" (variable-length utf8), each 5% NULL; numViews uniform int64 in [-1e3, 1e6),
+    5% NULL."""
+    import torch
+    import deequ_amd as d
+    dev = torch.device("cuda", device)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1 + 1000 * rank)
+    ids = torch.arange(rows, dtype=torch.int64, device=dev) + rows * rank
+
+    def fixed(prefix: bytes, width: int, vals):
+        step = len(prefix) + width
+        chars = torch.cat([_strings_from_ints(vals, width, prefix, dev),
+                           torch.zeros(16, dtype=torch.uint8, device=dev)])
+        offs = torch.arange(0, step * (rows + 1), step, dtype=torch.int32, device=dev)
+        return chars, offs
+
+    cols = {"id": d.Column("int64", rows, ids, None, device=True)}
+    chars, offs = fixed(b"Thingy ", 10, ids)
+    cols["productName"] = d.Column("string", rows, chars, _valid_bits(rows, gen, dev, 0.05), offsets=offs, device=True)
+    chars, offs = fixed(b"item description ", 6, (ids * 7919) % 100003)
+    cols["description"] = d.Column("string", rows, chars, _valid_bits(rows, gen, dev, 0.05), offsets=offs, device=True)
+    high = torch.randint(0, 2, (rows,), generator=gen, device=dev).bool()
+    lens = torch.where(high, 4, 3).to(torch.int32)
+    offs = torch.zeros(rows + 1, dtype=torch.int32, device=dev)
+    offs[1:] = torch.cumsum(lens, 0)
+    words = torch.tensor([list(b"high"), list(b"low\0")], dtype=torch.uint8, device=dev)
+    chars = torch.zeros(int(offs[-1]) + 16, dtype=torch.uint8, device=dev)
+    j = torch.arange(4, device=dev)
+    pos = offs[:-1, None].to(torch.int64) + j[None, :]
+    keep = j[None, :] < lens[:, None]
+    chars[pos[keep]] = words[(~high).long()][keep]
+    cols["priority"] = d.Column("string", rows, chars, _valid_bits(rows, gen, dev, 0.05), offsets=offs, device=True)
+    views = torch.randint(-1000, 1_000_000, (rows,), generator=gen, device=dev, dtype=torch.int64)
+    cols["numViews"] = d.Column("int64", rows, views, _valid_bits(rows, gen, dev, 0.05), device=True)
+    torch.cuda.synchronize(dev)
+    return d.Table(cols)
+
+
+def c1_analyzers():
+    import deequ_amd as d
+    return ([d.Size()] + [d.Completeness(c) for c in ("id", "productName", "description", "priority", "numViews")]
+            + [d.Compliance("numViews non-negative", "numViews >= 0"), d.Mean("numViews"),
+               d.StandardDeviation("numViews"), d.Minimum("numViews"), d.Maximum("numViews")])
+
+
+def run_c1(args, world, rank, local):
+    """The reference's CPU-runnable case through the AnalysisRunner mirror: one whole
+    AnalysisRunner.onData(...).addAnalyzers(...).run() per step (plan, fused scan, states,
+    metrics), every rank on its own 10M-row Item shard."""
+    import deequ_amd as d
+    data = make_c1_table(args.c1_rows, rank, local)
+    analyzers = c1_analyzers()
+
+    def step(ev=None):
+        return d.AnalysisRunner.onData(data).addAnalyzers(analyzers).run()
+    elapsed, _, ctx = _timed(args, world, step)
+    metrics = {str(a): ctx.metric(a).value.get() for a in analyzers}
+    return {
+        "metric": "rows/sec for the C1 AnalysisRunner suite (Item table)",
+        "value": args.c1_rows * world * args.steps / elapsed, "unit": "rows/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64 + utf8 validity",
+        "data": "synthetic Item table generated in HBM (seed 1, 5% NULL)",
+        "config": {"workload": "C1: %d rows/GPU Item(id, productName, description, priority, numViews); "
+                               "Size, 5 x Completeness, Compliance(numViews >= 0), Mean/StdDev/Min/Max(numViews) "
+                               "through AnalysisRunner" % args.c1_rows},
+        "check": metrics,
+    }
+
+
 def run_c5(args, world, rank, local):
     """ColumnProfilerRunner over the C5 table: 3 passes (generic stats + HLL + DataType; numeric
     stats; exact histograms of the low-cardinality columns)."""
@@ -404,7 +478,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     if args.workload != "c2":
-        result = {"c3": run_c3, "c4": run_c4, "c5": run_c5}[args.workload](args, world, rank, local)
+        result = {"c1": run_c1, "c3": run_c3, "c4": run_c4, "c5": run_c5}[args.workload](args, world, rank, local)
         if rank == 0:
             print(json.dumps(result))
         if world > 1:
