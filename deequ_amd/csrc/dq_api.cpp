@@ -382,7 +382,7 @@ static void finalize_fast_pred(FastPred* fp) {
   const uint32_t ON = ~0u;
   fp->m_lt = fp->m_eq = fp->m_gt = 0;
   fp->f_cmp = fp->f_coal = fp->f_isnull = fp->f_isnotnull = fp->f_true = fp->f_mask = 0;
-  fp->f_nn_valid = fp->f_nn_one = fp->pad = 0;
+  fp->f_nn_valid = fp->f_nn_one = fp->cmp_sel = 0;
   switch (fp->kind) {
     case FP_CMP:
     case FP_COALESCE_CMP:
@@ -400,6 +400,17 @@ static void finalize_fast_pred(FastPred* fp) {
         case CMP_LE: fp->m_lt = fp->m_eq = ON; break;
         case CMP_GT: fp->m_gt = ON; break;
         default: fp->m_gt = fp->m_eq = ON; break;  // CMP_GE
+      }
+      if (!(fp->as_f64 && fp->lit_f != fp->lit_f)) {  // a NaN literal keeps the three masks
+        switch (fp->op) {
+          case CMP_EQ: fp->cmp_sel = CS_EQ; break;
+          case CMP_NE: fp->cmp_sel = CS_EQ | CS_INV; break;
+          case CMP_LT: fp->cmp_sel = CS_LT; break;
+          case CMP_LE: fp->cmp_sel = CS_LE; break;
+          case CMP_GT: fp->cmp_sel = CS_LE | CS_INV; break;
+          case CMP_GE: fp->cmp_sel = CS_LT | CS_INV; break;
+          default: break;
+        }
       }
       break;
     case FP_IS_NULL: fp->f_isnull = ON; fp->f_nn_one = ON; break;
@@ -545,6 +556,8 @@ struct dq_plan : Stager {
   bool desc_pending = false;
   int64_t total_rows = 0;
   int target_blocks = 2048;
+  int n_cu = 0;          // compute units of the device (0 = unknown)
+  int scan_rounds = 6;   // value-scan grids: whole rounds of resident workgroups (DQ_SCAN_ROUNDS)
 
   ~dq_plan() {
     if (stream) {
@@ -861,7 +874,11 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
   plan->stage_offsets.resize(n_columns);
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess)
+  {
     plan->target_blocks = std::max(256, prop.multiProcessorCount * 8);
+    plan->n_cu = prop.multiProcessorCount;
+  }
+  if (const char* r = std::getenv("DQ_SCAN_ROUNDS")) plan->scan_rounds = std::max(0, std::atoi(r));
   if ((s = dq_plan_reset(plan)) != DQ_OK) {
     delete plan;
     return s;
@@ -1049,6 +1066,13 @@ extern "C" dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, in
   for (size_t g = 0; g < plan->groups.size(); ++g) {
     const int64_t ng = (int64_t)plan->groups[g].tasks.size();
     int64_t bpt = (plan->target_blocks + ng - 1) / ng;
+    const ScanGroup& G = plan->groups[g];
+    if (G.kind != 0 && plan->n_cu > 0 && plan->scan_rounds > 0) {
+      // the value scans are VALU-bound: one (or scan_rounds) full round(s) of resident
+      // workgroups, split evenly over the group's tasks
+      const int per_cu = scan_group_blocks_per_cu(G.kind, G.ptype, G.np);
+      if (per_cu > 0) bpt = std::max<int64_t>(1, (int64_t)plan->n_cu * per_cu * plan->scan_rounds / ng);
+    }
     bpt = std::max<int64_t>(1, std::min<int64_t>(bpt, chunks));
     // a block's rows are addressed by 32-bit buffer offsets: keep its span <= 2^27 rows
     bpt = std::max<int64_t>(bpt, (chunks + (((int64_t)1 << 27) / kScanRowAlign) - 1) /
@@ -1247,7 +1271,7 @@ extern "C" dq_status dq_plan_finish(dq_plan* plan, dq_state* out, int n_out) {
       case DQ_OP_MINIMUM:
         o.has_value = a.n_sel > 0;
         if (is_integral(ptype)) o.value = (double)a.imin;
-        else o.value = (a.nnan == a.n_sel) ? std::numeric_limits<double>::quiet_NaN() : a.fmin;
+        else o.value = (a.fmin > a.fmax) ? std::numeric_limits<double>::quiet_NaN() : a.fmin;  // all NaN
         break;
       case DQ_OP_MAXIMUM:
         o.has_value = a.n_sel > 0;

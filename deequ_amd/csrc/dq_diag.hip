@@ -20,18 +20,20 @@ __global__ __launch_bounds__(kBlock) void dq_diag_hash_kernel(int iters, uint64_
     __syncthreads();
   }
   const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  uint64_t x0 = t * 4 + 1, x1 = t * 4 + 2, x2 = t * 4 + 3, x3 = t * 4 + 4;
+  uint64_t x[4] = {t * 4 + 1, t * 4 + 2, t * 4 + 3, t * 4 + 4};
   for (int i = 0; i < iters; ++i) {
-    x0 = spark_hash<int64_t>((int64_t)x0);
-    x1 = spark_hash<int64_t>((int64_t)x1);
-    x2 = spark_hash<int64_t>((int64_t)x2);
-    x3 = spark_hash<int64_t>((int64_t)x3);
-    if (WITH_HLL) {  // the scan kernel's batched register update
-      const uint64_t h[4] = {x0, x1, x2, x3};
-      hll_update_lds_batch<4>(lregs, h, 0xfu);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {  // the scan kernel's per-row hash + register update
+      const W64 h = spark_hash_dev<int64_t>((int64_t)x[c]);
+      x[c] = ((uint64_t)h.hi << 32) | h.lo;
+      if (WITH_HLL) {
+        uint32_t idx, nlz;
+        hll_slot(h, idx, nlz);
+        __hip_atomic_fetch_max(&lregs[idx], nlz + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
     }
   }
-  uint64_t acc = x0 ^ x1 ^ x2 ^ x3;
+  uint64_t acc = x[0] ^ x[1] ^ x[2] ^ x[3];
   if (WITH_HLL) {
     __syncthreads();
     acc += lregs[threadIdx.x];

@@ -61,8 +61,14 @@ struct FastPred {
   //   NOT NULL = valid & f_nn_valid | f_nn_one | mask_nn & f_mask
   // (a NaN x is neither < nor == a non-NaN literal, so it lands in "greater": Spark's order)
   uint32_t m_lt, m_eq, m_gt;
-  uint32_t f_cmp, f_coal, f_isnull, f_isnotnull, f_true, f_mask, f_nn_valid, f_nn_one, pad;
+  uint32_t f_cmp, f_coal, f_isnull, f_isnotnull, f_true, f_mask, f_nn_valid, f_nn_one;
+  // One-compare form of the same operator (0 when it does not apply): bits 0-1 pick the
+  // compare (CS_LT: x < lit, CS_LE: x <= lit, CS_EQ: x == lit), bit 2 (CS_INV) negates it:
+  // GE = !LT, GT = !LE, NE = !EQ.  An ordered fp64 compare is false for a NaN x, so NaN lands
+  // above every (non-NaN) literal, Spark's NaN-safe order; a NaN literal keeps the three masks.
+  uint32_t cmp_sel;
 };
+enum CmpSel : uint32_t { CS_MASKS = 0, CS_LT = 1, CS_LE = 2, CS_EQ = 3, CS_INV = 4 };
 
 enum ScanTaskFlags : int32_t {
   TF_VALUES = 1,      // the task must read the primary column's values
@@ -243,6 +249,7 @@ hipError_t launch_scan_group(int kind, int ptype, int np, const ScanTask* d_task
                              const DevMask* d_masks, int64_t n_rows, int blocks_per_task,
                              ScanAcc* d_partials, uint32_t* d_hll_regs, hipStream_t stream);
 hipError_t launch_diag_hash(int blocks, int iters, bool with_hll, uint64_t* sink, hipStream_t s);
+int scan_group_blocks_per_cu(int kind, int ptype, int np);  // 0 = unknown
 hipError_t launch_scan_reduce(const ScanAcc* d_partials, const PartRange* d_ranges, int n_tasks,
                               ScanAcc* d_acc, hipStream_t stream);
 hipError_t launch_hll(const HllTask* d_tasks, int n_tasks, const DevColumn* d_cols,
@@ -337,6 +344,113 @@ template <> __host__ __device__ inline uint64_t spark_hash<double>(double v) {
   __builtin_memcpy(&bits, &v, 8);
   if (v != v) bits = 0x7ff8000000000000ull;  // Double.doubleToLongBits canonical NaN
   return xxh64_u64(bits, 42);
+}
+
+// ---------------------------------------------------------------- device XXH64 on 32-bit halves
+// The same Spark XXH64 (seed 42) as xxh64_u64 / xxh64_u32 above, written for the gfx950 VALU,
+// where the per-row hash is the bound of every fused HLL pass (each instruction here is one
+// issue slot of 64 rows):
+//   * a 64x64-bit multiply by a constant is one v_mad_u64_u32 (lo x lo, with the constant
+//     addend of the next step folded in) + two v_mul_lo_u32 for the cross terms;
+//   * a 64-bit rotate is two v_alignbit_b32; rotl27(S ^ k) = rotl27(S) ^ rotl27(k) folds the
+//     seed word into one constant;
+//   * the avalanche shifts by 33 / 29 / 32 touch only the halves they move.
+// Bit-identical to xxh64_u64 / xxh64_u32 (pinned by the GPU HLL register parity tests).
+struct W64 {
+  uint32_t lo, hi;
+};
+
+template <uint64_t C, uint64_t A = 0>
+__device__ inline W64 w64_mul(W64 a) {  // a * C + A (mod 2^64)
+  const uint64_t p = (uint64_t)a.lo * (uint32_t)C + A;
+  const uint32_t hi = (uint32_t)(p >> 32) + a.lo * (uint32_t)(C >> 32) + a.hi * (uint32_t)C;
+  return {(uint32_t)p, hi};
+}
+template <int R>  // rotl64 by 0 < R < 32
+__device__ inline W64 w64_rotl(W64 x) {
+  return {__builtin_amdgcn_alignbit(x.lo, x.hi, 32 - R), __builtin_amdgcn_alignbit(x.hi, x.lo, 32 - R)};
+}
+__device__ inline W64 w64_avalanche(W64 h) {
+  h.lo ^= h.hi >> 1;                                   // h ^= h >> 33
+  h = w64_mul<kP2>(h);
+  h.lo ^= __builtin_amdgcn_alignbit(h.hi, h.lo, 29);  // h ^= h >> 29
+  h.hi ^= h.hi >> 29;
+  h = w64_mul<kP3>(h);
+  h.lo ^= h.hi;                                        // h ^= h >> 32
+  return h;
+}
+constexpr uint64_t rotl64_c(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+
+__device__ inline W64 xxh64_8_dev(uint32_t lo, uint32_t hi) {  // Spark XXH64.hashLong, seed 42
+  constexpr uint64_t RS = rotl64_c(42ull + kP5 + 8, 27);
+  W64 k = w64_mul<kP2>({lo, hi});
+  k = w64_mul<kP1>(w64_rotl<31>(k));
+  W64 h = w64_rotl<27>(k);
+  h.lo ^= (uint32_t)RS;
+  h.hi ^= (uint32_t)(RS >> 32);
+  return w64_avalanche(w64_mul<kP1, kP4>(h));
+}
+__device__ inline W64 xxh64_4_dev(uint32_t v) {  // Spark XXH64.hashInt, seed 42
+  constexpr uint64_t RS = rotl64_c(42ull + kP5 + 4, 23);
+  const uint64_t p = (uint64_t)v * (uint32_t)kP1;
+  W64 h = w64_rotl<23>({(uint32_t)p, (uint32_t)(p >> 32) + v * (uint32_t)(kP1 >> 32)});
+  h.lo ^= (uint32_t)RS;
+  h.hi ^= (uint32_t)(RS >> 32);
+  return w64_avalanche(w64_mul<kP2, kP3>(h));
+}
+
+// spark_hash<T> on the device, as halves.
+template <typename T> __device__ inline W64 spark_hash_dev(T v) {
+  return xxh64_4_dev((uint32_t)(int32_t)v);  // the int family hashes as a 4-byte int
+}
+template <> __device__ inline W64 spark_hash_dev<int64_t>(int64_t v) {
+  return xxh64_8_dev((uint32_t)(uint64_t)v, (uint32_t)((uint64_t)v >> 32));
+}
+// doubleToLongBits / floatToIntBits map every NaN to the canonical one; NaN rows are rare, so
+// the rewrite sits behind a wave-uniform branch.
+template <> __device__ inline W64 spark_hash_dev<double>(double v) {
+  uint64_t bits = __builtin_bit_cast(uint64_t, v);
+  if (__ballot(v != v)) bits = (v != v) ? 0x7ff8000000000000ull : bits;
+  return xxh64_8_dev((uint32_t)bits, (uint32_t)(bits >> 32));
+}
+template <> __device__ inline W64 spark_hash_dev<float>(float v) {
+  uint32_t bits = __builtin_bit_cast(uint32_t, v);
+  if (__ballot(v != v)) bits = (v != v) ? 0x7fc00000u : bits;
+  return xxh64_4_dev(bits);
+}
+
+// Register index and rank of a hash (StatefulHyperloglogPlus.scala:96-99) from its halves:
+// idx = x >>> 55, pw = nlz((x << 9) | W_PADDING) + 1.
+__device__ inline uint32_t ffbh_u32(uint32_t v) {  // v_ffbh_u32: leading zeros, ~0u for 0
+  uint32_t r;
+  asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+// idx and nlz = pw - 1.  The high word of w = (x << 9) | W_PADDING is zero for one hash in 2^32:
+// that case (nlz >= 32) is taken on a wave-uniform branch instead of paying a 64-bit count
+// on every row.
+__device__ inline void hll_slot(W64 x, uint32_t& idx, uint32_t& nlz) {
+  idx = x.hi >> (kHllIdxShift - 32);
+  const uint32_t w_hi = __builtin_amdgcn_alignbit(x.hi, x.lo, 23);  // (x << 9) >> 32
+  nlz = ffbh_u32(w_hi);
+  if (__ballot(nlz == ~0u)) {
+    const uint32_t w_lo = (x.lo << 9) | (uint32_t)kHllWPadding;
+    if (nlz == ~0u) nlz = 32u + ffbh_u32(w_lo);
+  }
+}
+
+// Hash one value and raise its register in the workgroup's LDS copy: a register only grows,
+// so every row issues one ds_max_u32 with no return value (nothing to wait for); a row that is
+// not selected raises nothing (rank 0).  `s` = 1 (row selected) or 0.
+template <typename T>
+__device__ inline void hll_hash_update(uint32_t* regs, T v, uint32_t s) {
+  uint32_t idx, nlz;
+  hll_slot(spark_hash_dev<T>(v), idx, nlz);
+  // rank * s = nlz * s + s: one v_mad_u32_u24 (the compiler would rebuild an add and a select
+  // from the plain expression)
+  uint32_t r;
+  asm("v_mad_u32_u24 %0, %1, %2, %2" : "=v"(r) : "v"(nlz), "v"(s));
+  __hip_atomic_fetch_max(&regs[idx], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // M[idx] = max(M[idx], pw) on a workgroup's LDS register copy; the atomic is skipped when the

@@ -19,7 +19,8 @@
 //   n_sel          : Σ valid ∧ where-TRUE              (Completeness numerator, Mean count, n)
 //   isum           : wrapping int64 sum (Spark Sum over integral types is LongType)
 //   fs + fc        : Neumaier-compensated fp64 sum     (Spark: sequential fp64 sum)
-//   imin/imax, fmin/fmax/nnan : Spark NaN-safe min/max (NaN is the largest double)
+//   imin/imax, fmin/fmax/nnan : Spark NaN-safe min/max (NaN is the largest double); nnan > 0
+//                    iff a selected value is NaN, fmin > fmax iff every selected value is NaN
 //   mean, m2       : moments about the mean, from per-lane shifted sums then Chan merges
 //                    with the exact formula of StandardDeviationState.sum
 //                    (StandardDeviation.scala:37-44); no per-element fp64 divide
@@ -45,16 +46,22 @@ struct alignas(16) Vec16 {
 
 template <int NP>
 struct ThreadAcc {
-  uint32_t n_rows, n_wnn, n_sel, nnan;
+  uint32_t n_rows, n_wnn, n_sel;
+  uint64_t nan_wave;  // fp: ballot of the wave's selected NaN rows (wave-uniform)
   int64_t isum, imin, imax;
   double fs, fc, fmin, fmax;
   double shift, s1, s2;
   uint32_t pm[NP > 0 ? NP : 1], pn[NP > 0 ? NP : 1];
+  // wave-uniform counters of the main loop (ballot + scalar popcount, no VALU): selected rows
+  // and one-compare predicate counts; lane counters above cover the diverged tail
+  uint64_t n_sel_w;
+  uint64_t pm_w[NP > 0 ? NP : 1], pn_w[NP > 0 ? NP : 1];
 };
 
 template <int NP>
 __device__ inline void thread_acc_init(ThreadAcc<NP>& a) {
-  a.n_rows = a.n_wnn = a.n_sel = a.nnan = 0;
+  a.n_rows = a.n_wnn = a.n_sel = 0;
+  a.nan_wave = 0;
   a.isum = 0;
   a.imin = INT64_MAX;
   a.imax = INT64_MIN;
@@ -64,6 +71,9 @@ __device__ inline void thread_acc_init(ThreadAcc<NP>& a) {
   a.shift = a.s1 = a.s2 = 0.0;
 #pragma unroll
   for (int p = 0; p < (NP > 0 ? NP : 1); ++p) a.pm[p] = a.pn[p] = 0;
+  a.n_sel_w = 0;
+#pragma unroll
+  for (int p = 0; p < (NP > 0 ? NP : 1); ++p) a.pm_w[p] = a.pn_w[p] = 0;
 }
 
 // Spark's NaN-safe three-way comparison (Utils.nanSafeCompareDoubles): NaN == NaN and NaN is
@@ -92,60 +102,6 @@ __device__ inline void neumaier_add(double& s, double& c, double x) {
   const double t = s + x;
   c += (fabs(s) >= fabs(x)) ? ((s - t) + x) : ((x - t) + s);
   s = t;
-}
-
-// One element of the primary column.
-template <typename T, int NP>
-__device__ inline void accumulate_element(ThreadAcc<NP>& a, T v, uint32_t sel) {
-  const bool first = sel && (a.n_sel == 0);
-  a.n_sel += sel;
-  double xd;
-  if constexpr (IsIntegral<T>::value) {
-    const int64_t xi = (int64_t)v;
-    a.isum += sel ? xi : 0;
-    a.imin = (sel && xi < a.imin) ? xi : a.imin;
-    a.imax = (sel && xi > a.imax) ? xi : a.imax;
-    xd = (double)xi;
-  } else {
-    xd = (double)v;
-    const bool isnan = xd != xd;
-    neumaier_add(a.fs, a.fc, sel ? xd : 0.0);
-    a.nnan += (sel && isnan) ? 1u : 0u;
-    a.fmin = (sel && !isnan && xd < a.fmin) ? xd : a.fmin;
-    a.fmax = (sel && !isnan && xd > a.fmax) ? xd : a.fmax;
-  }
-  a.shift = first ? xd : a.shift;
-  const double d = sel ? (xd - a.shift) : 0.0;
-  a.s1 += d;
-  a.s2 = fma(d, d, a.s2);
-}
-
-// Inline predicate over one element -> (TRUE, NOT NULL) bits.
-template <typename T>
-__device__ inline void eval_fast_pred(const FastPred& fp, T v, uint32_t valid, uint32_t mt,
-                                      uint32_t mnn, uint32_t& r, uint32_t& nn) {
-  switch (fp.kind) {
-    case FP_CMP:
-    case FP_COALESCE_CMP: {
-      const bool use_coal = (fp.kind == FP_COALESCE_CMP) && !valid;
-      int ord;
-      if (fp.as_f64) {
-        const double x = use_coal ? fp.coal_f : (double)v;
-        ord = ord_f64(x, fp.lit_f);
-      } else {
-        const int64_t x = use_coal ? fp.coal_i : (int64_t)v;
-        ord = ord_i64(x, fp.lit_i);
-      }
-      nn = (fp.kind == FP_COALESCE_CMP) ? 1u : valid;
-      r = apply_cmp(fp.op, ord) ? 1u : 0u;
-      break;
-    }
-    case FP_IS_NULL: r = valid ^ 1u; nn = 1u; break;
-    case FP_IS_NOT_NULL: r = valid; nn = 1u; break;
-    case FP_CONST: r = fp.lit_i == 1 ? 1u : 0u; nn = fp.lit_i == -1 ? 0u : 1u; break;
-    case FP_MASK: r = mt; nn = mnn; break;
-    default: r = 0u; nn = 0u; break;
-  }
 }
 
 template <int RPL>
@@ -283,7 +239,7 @@ __device__ inline void wave_moments(double& n, double& m, double& m2) {
 // Reduce one ScanAcc-shaped set of per-thread values to the block's partial, field by field
 // (short live ranges), wave results staged in LDS, waves combined in order by thread 0.
 template <int NPRED>
-__device__ void block_reduce_store(uint64_t n_rows, uint64_t n_wnn, uint64_t n_sel, uint64_t nnan,
+__device__ __attribute__((always_inline)) inline void block_reduce_store(uint64_t n_rows, uint64_t n_wnn, uint64_t n_sel, uint64_t nnan,
                                    int64_t isum, int64_t imin, int64_t imax, double fs, double fc,
                                    double fmin, double fmax, double mean, double m2,
                                    const uint64_t* pm, const uint64_t* pn, int n_preds,
@@ -325,22 +281,48 @@ __device__ void block_reduce_store(uint64_t n_rows, uint64_t n_wnn, uint64_t n_s
   }
 }
 
-template <int NP>
+// Lane statistics -> block partial.  The moments are formed per wave (the shift is
+// wave-uniform, so the lanes' Σd and Σd² simply add), from the wave-uniform main-loop counts
+// plus the lanes' tail counts.  fp columns carry (fs, fc) = compensated Σd about the shift, so
+// Σx = n * shift + Σd, the product's rounding error kept exactly by an fma.  Lane 0 carries
+// the wave's totals into the block reduction; the other lanes carry identities.
+__device__ inline double wave_sum_f64(double v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_down(v, d, 64);
+  return v;
+}
+
+template <typename T, int NP>
 __device__ inline void thread_finish(const ThreadAcc<NP>& t, int n_preds, ScanAcc* out) {
+  const bool lane0 = (threadIdx.x & 63) == 0;
+  const uint64_t n_w = wave_sum_u64((uint64_t)t.n_sel) + t.n_sel_w;  // lane 0
+  const double s1 = IsIntegral<T>::value ? t.s1 : (t.fs + t.fc);
+  const double S1 = wave_sum_f64(s1), S2 = wave_sum_f64(t.s2);     // lane 0
   double mean = 0.0, m2 = 0.0;
-  if (t.n_sel > 0) {
-    const double n = (double)t.n_sel;
-    mean = t.shift + t.s1 / n;
-    m2 = t.s2 - t.s1 * t.s1 / n;
+  double fs = t.fs, fc = t.fc;
+  uint64_t n_out = 0;
+  if (lane0 && n_w > 0) {
+    n_out = n_w;
+    const double n = (double)n_w;
+    mean = t.shift + S1 / n;
+    m2 = S2 - S1 * S1 / n;
     m2 = (m2 < 0.0) ? 0.0 : m2;  // rounding; NaN/Inf propagate
+    if constexpr (!IsIntegral<T>::value) {
+      const double p = n * t.shift;
+      const double pe = (p - p == 0.0) ? fma(n, t.shift, -p) : 0.0;
+      two_sum_merge(fs, fc, p, pe);
+    }
   }
+  // (the ragged tail runs diverged, so lanes may hold different copies of the flag: OR them)
+  const bool wave_nan = __ballot(t.nan_wave != 0) != 0;
+  const uint64_t nnan = (lane0 && wave_nan) ? 1u : 0u;
   uint64_t pm[NP > 0 ? NP : 1], pn[NP > 0 ? NP : 1];
 #pragma unroll
   for (int p = 0; p < (NP > 0 ? NP : 1); ++p) {
-    pm[p] = t.pm[p];
-    pn[p] = t.pn[p];
+    pm[p] = t.pm[p] + (lane0 ? t.pm_w[p] : 0u);
+    pn[p] = t.pn[p] + (lane0 ? t.pn_w[p] : 0u);
   }
-  block_reduce_store<NP>(t.n_rows, t.n_wnn, t.n_sel, t.nnan, t.isum, t.imin, t.imax, t.fs, t.fc,
+  block_reduce_store<NP>(t.n_rows, t.n_wnn, n_out, nnan, t.isum, t.imin, t.imax, fs, fc,
                          t.fmin, t.fmax, mean, m2, pm, pn, n_preds, out);
 }
 
@@ -382,41 +364,67 @@ __device__ inline T buf_elem(__amdgpu_buffer_rsrc_t rs, uint32_t row) {
   }
 }
 
-// Statistics over R rows of one lane (selection bits `sel`), against the wave's shift.
+// v_min_f64 / v_max_f64 as the hardware does them: a quiet-NaN operand is dropped.  (minnum /
+// maxnum through the compiler add a canonicalising op per operand.)
+__device__ inline double vmin_f64(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ inline double vmax_f64(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// Statistics over R rows of one lane (selection bits `sel`), against the wave's shift.  The pass
+// is bound by VALU issue once HLL rides on it, so each statistic is written for the fewest
+// instructions: a selected-row test is one compare reused by every statistic (the min/max
+// updates AND it into their compare mask), and int64 -> double is cvt(hi) * 2^32 + cvt(lo) as
+// one fma (the same correctly rounded value as (double)xi).
 template <typename T, int NP, int R>
 __device__ inline void accumulate_rows(ThreadAcc<NP>& a, const T* vals, uint32_t sel, double shift,
-                                       double& psum) {
+                                       double& dsum) {
   if constexpr (IsIntegral<T>::value) {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const bool s = (sel >> k) & 1u;
       const int64_t xi = (int64_t)vals[k];
       a.isum += s ? xi : 0;
-      const int64_t vmn = s ? xi : INT64_MAX;
-      const int64_t vmx = s ? xi : INT64_MIN;
-      a.imin = vmn < a.imin ? vmn : a.imin;
-      a.imax = vmx > a.imax ? vmx : a.imax;
-      const double d = s ? ((double)xi - shift) : 0.0;
+      if (s & (xi < a.imin)) a.imin = xi;
+      if (s & (xi > a.imax)) a.imax = xi;
+      double dd;
+      if constexpr (sizeof(T) == 8) {  // xi - shift: cvt(hi) * 2^32 + (cvt(lo) - shift), one fma
+        dd = fma((double)(int32_t)((uint64_t)xi >> 32), 0x1p32,
+                 (double)(uint32_t)(uint64_t)xi - shift);
+      } else {
+        dd = (double)xi - shift;
+      }
+      const double d = s ? dd : 0.0;
       a.s1 += d;
       a.s2 = fma(d, d, a.s2);
     }
   } else {
-    uint32_t nanb = 0u;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const bool s = (sel >> k) & 1u;
       const double x = (double)vals[k];
-      psum += s ? x : 0.0;
+      // the fp64 sum is n_sel * shift + Σd (compensated per iteration by the caller), so one
+      // masked d feeds both the sum and the moments
       const double d = s ? (x - shift) : 0.0;
-      a.s1 += d;
+      dsum += d;
       a.s2 = fma(d, d, a.s2);
-      // minnum/maxnum drop a NaN operand: NaN never wins min (Spark's NaN-safe order); a NaN
-      // max is restored from `nnan` when the state is built.
-      a.fmin = __builtin_fmin(a.fmin, s ? x : __builtin_huge_val());
-      a.fmax = __builtin_fmax(a.fmax, s ? x : -__builtin_huge_val());
-      nanb |= (s && x != x) ? (1u << k) : 0u;
+      // min / max through minnum / maxnum of the value, or of a quiet NaN (one select on the
+      // high word) for an unselected row: minnum / maxnum drop a NaN operand, so a NaN never
+      // wins min (Spark's NaN-safe order) and the max is restored from the NaN flag.
+      const uint64_t xb = __builtin_bit_cast(uint64_t, x);
+      const uint32_t xh = s ? (uint32_t)(xb >> 32) : 0x7ff80000u;
+      const double xn = __builtin_bit_cast(double, ((uint64_t)xh << 32) | (uint32_t)xb);
+      a.fmin = vmin_f64(a.fmin, xn);
+      a.fmax = vmax_f64(a.fmax, xn);
+      // any selected NaN: a wave ballot OR-ed on the scalar unit
+      a.nan_wave |= __ballot(s & (x != x));
     }
-    a.nnan += __builtin_popcount(nanb);
   }
 }
 
@@ -436,44 +444,109 @@ __device__ inline uint32_t cmp_bits(const V* x, V lit, const FastPred& fp) {
   return r;
 }
 
-// Spark XXH64 of R rows (every row is hashed, branch-free); the register updates go through
-// hll_update_lds_batch once per iteration.
-template <typename T, int R>
-__device__ inline void hash_rows(uint64_t* h, const T* vals) {
+// The one-compare form (FastPred::cmp_sel): one v_cmp per value, the operator's negation
+// applied once to the R bits.
+template <int CS, typename V, int R>
+__device__ inline uint32_t cmp_bits1(const V* x, V lit) {
+  uint32_t r = 0u;
 #pragma unroll
-  for (int k = 0; k < R; ++k) h[k] = spark_hash<T>(vals[k]);
+  for (int k = 0; k < R; ++k) {
+    bool b;
+    if constexpr (CS == CS_LT) b = x[k] < lit;
+    else if constexpr (CS == CS_LE) b = x[k] <= lit;
+    else b = x[k] == lit;
+    r |= b ? (1u << k) : 0u;
+  }
+  return r;
 }
 
-// Inline predicates over R rows: counts TRUE and NOT NULL among where-TRUE rows.
+template <typename V, int R>
+__device__ inline uint32_t cmp_dispatch(const V* x, V lit, const FastPred& fp) {
+  constexpr uint32_t FULL = (R == 32) ? 0xffffffffu : ((1u << R) - 1u);
+  const uint32_t inv = (fp.cmp_sel & CS_INV) ? FULL : 0u;
+  switch (fp.cmp_sel & 3u) {  // uniform
+    case CS_LT: return cmp_bits1<CS_LT, V, R>(x, lit) ^ inv;
+    case CS_LE: return cmp_bits1<CS_LE, V, R>(x, lit) ^ inv;
+    case CS_EQ: return cmp_bits1<CS_EQ, V, R>(x, lit) ^ inv;
+    default: return cmp_bits<V, R>(x, lit, fp);
+  }
+}
+
+// One inline predicate over R rows: counts TRUE and NOT NULL among where-TRUE rows (lane bits).
+template <typename T, int NP, int R>
+__device__ inline void predicate_one(ThreadAcc<NP>& a, int p, const FastPred& fp, const T* vals,
+                                     uint32_t valid, uint32_t wt, uint32_t mt, uint32_t mn) {
+  constexpr uint32_t FULL = (R == 32) ? 0xffffffffu : ((1u << R) - 1u);
+  uint32_t c = 0u;
+  if (fp.f_cmp) {  // uniform
+    if (IsIntegral<T>::value && !fp.as_f64) {
+      int64_t x[R];
+      if (fp.f_coal) {  // uniform
+#pragma unroll
+        for (int k = 0; k < R; ++k) x[k] = ((valid >> k) & 1u) ? (int64_t)vals[k] : fp.coal_i;
+      } else {
+#pragma unroll
+        for (int k = 0; k < R; ++k) x[k] = (int64_t)vals[k];
+      }
+      c = cmp_dispatch<int64_t, R>(x, fp.lit_i, fp);
+    } else {
+      double x[R];
+      if (fp.f_coal) {
+#pragma unroll
+        for (int k = 0; k < R; ++k) x[k] = ((valid >> k) & 1u) ? (double)vals[k] : fp.coal_f;
+      } else {
+#pragma unroll
+        for (int k = 0; k < R; ++k) x[k] = (double)vals[k];
+      }
+      c = cmp_dispatch<double, R>(x, fp.lit_f, fp);
+    }
+  }
+  const uint32_t r = ((c & fp.f_cmp) | (~valid & fp.f_isnull) | (valid & fp.f_isnotnull) |
+                      fp.f_true | (mt & fp.f_mask)) & FULL;
+  const uint32_t nn = ((valid & fp.f_nn_valid) | fp.f_nn_one | (mn & fp.f_mask)) & FULL;
+  a.pm[p] += __builtin_popcount(wt & nn & r);
+  a.pn[p] += __builtin_popcount(wt & nn);
+}
+
 template <typename T, int NP, int R>
 __device__ inline void predicate_rows(ThreadAcc<NP>& a, const FastPred* fps, const T* vals,
                                       uint32_t valid, uint32_t wt, const uint32_t* mt,
                                       const uint32_t* mn) {
-  constexpr uint32_t FULL = (R == 32) ? 0xffffffffu : ((1u << R) - 1u);
+#pragma unroll
+  for (int p = 0; p < NP; ++p) predicate_one<T, NP, R>(a, p, fps[p], vals, valid, wt, mt[p], mn[p]);
+}
+
+// Main-loop form of predicate_rows: a plain `column CMP literal` (kind FP_CMP with a one-compare
+// selector) is counted with one v_cmp per row and a ballot popcount on the scalar unit; other
+// kinds fall back to the lane bit path.  Uniform control flow only (wave-uniform counters).
+template <typename T, int NP, int R>
+__device__ inline void predicate_rows_wave(ThreadAcc<NP>& a, const FastPred* fps, const T* vals,
+                                           uint32_t valid, uint32_t wt, const uint32_t* mt,
+                                           const uint32_t* mn) {
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     const FastPred& fp = fps[p];
-    uint32_t c = 0u;
-    if (fp.f_cmp) {  // uniform
-      if (IsIntegral<T>::value && !fp.as_f64) {
-        int64_t x[R];
+    const uint32_t cs = fp.cmp_sel & 3u;
+    if (fp.kind == FP_CMP && cs != CS_MASKS) {  // uniform
+      const bool inv = (fp.cmp_sel & CS_INV) != 0;
+      const bool f64 = !IsIntegral<T>::value || fp.as_f64;
 #pragma unroll
-        for (int k = 0; k < R; ++k)
-          x[k] = (fp.f_coal && !((valid >> k) & 1u)) ? fp.coal_i : (int64_t)vals[k];
-        c = cmp_bits<int64_t, R>(x, fp.lit_i, fp);
-      } else {
-        double x[R];
-#pragma unroll
-        for (int k = 0; k < R; ++k)
-          x[k] = (fp.f_coal && !((valid >> k) & 1u)) ? fp.coal_f : (double)vals[k];
-        c = cmp_bits<double, R>(x, fp.lit_f, fp);
+      for (int k = 0; k < R; ++k) {
+        const bool in = ((valid & wt) >> k) & 1u;  // NOT NULL (FP_CMP: valid) and where TRUE
+        bool b;
+        if (f64) {
+          const double x = (double)vals[k];
+          b = cs == CS_LT ? x < fp.lit_f : (cs == CS_LE ? x <= fp.lit_f : x == fp.lit_f);
+        } else {
+          const int64_t x = (int64_t)vals[k];
+          b = cs == CS_LT ? x < fp.lit_i : (cs == CS_LE ? x <= fp.lit_i : x == fp.lit_i);
+        }
+        a.pm_w[p] += __builtin_popcountll(__ballot(in & (b != inv)));
+        a.pn_w[p] += __builtin_popcountll(__ballot(in));
       }
+    } else {
+      predicate_one<T, NP, R>(a, p, fp, vals, valid, wt, mt[p], mn[p]);
     }
-    const uint32_t r = ((c & fp.f_cmp) | (~valid & fp.f_isnull) | (valid & fp.f_isnotnull) |
-                        fp.f_true | (mt[p] & fp.f_mask)) & FULL;
-    const uint32_t nn = ((valid & fp.f_nn_valid) | fp.f_nn_one | (mn[p] & fp.f_mask)) & FULL;
-    a.pm[p] += __builtin_popcount(wt & nn & r);
-    a.pn[p] += __builtin_popcount(wt & nn);
   }
 }
 
@@ -488,7 +561,7 @@ __device__ inline void predicate_rows(ThreadAcc<NP>& a, const FastPred* fps, con
 // returns 0 without touching memory) and a uniform "absent" mask is OR-ed in afterwards, so
 // no load sits behind a branch (which would force a vmcnt(0) per load).
 template <typename T, int NP, bool EXT>
-__global__ __launch_bounds__(kBlock) void dq_scan_values_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu((NP <= 3 && !EXT) ? 6 : 1))) void dq_scan_values_kernel(
     const ScanTask* __restrict__ tasks, const int32_t* __restrict__ group,
     const DevColumn* __restrict__ cols, const DevMask* __restrict__ masks, int64_t n_rows,
     ScanAcc* partials, uint32_t* __restrict__ hll_regs) {
@@ -530,6 +603,7 @@ __global__ __launch_bounds__(kBlock) void dq_scan_values_kernel(
   }
   FastPred fps[NPS];
   __amdgpu_buffer_rsrc_t rmt[NPS], rmn[NPS];
+  rmt[0] = rmn[0] = make_rsrc(nullptr, 0);  // (NP == 0: the tail still reads slot 0)
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     fps[p] = task.preds[p];
@@ -565,6 +639,7 @@ __global__ __launch_bounds__(kBlock) void dq_scan_values_kernel(
   thread_acc_init(a);
   const uint32_t tid = threadIdx.x;
   const uint32_t full_iters = span / ROWS_PER_ITER;
+#pragma unroll 1
   for (uint32_t it = 0; it < full_iters; ++it) {
     dq_v4u vec[UNROLL];
     uint32_t vb[UNROLL], wtb[UNROLL], wnb[UNROLL];
@@ -596,33 +671,34 @@ __global__ __launch_bounds__(kBlock) void dq_scan_values_kernel(
       wnb[u] = (wnb[u] | no_where) & FULL;
     }
     // ---- compute phase
-    double psum = 0.0;
+    double dsum = 0.0;
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const T* vals = reinterpret_cast<const T*>(&vec[u]);
       const uint32_t sel = vb[u] & wtb[u];
       a.n_rows += __builtin_popcount(wtb[u]);
       a.n_wnn += __builtin_popcount(wnb[u]);
-      a.n_sel += __builtin_popcount(sel);
-      if (stats_on) accumulate_rows<T, NP, RPL>(a, vals, sel, shift, psum);
-      predicate_rows<T, NP, RPL>(a, fps, vals, vb[u], wtb[u], mtb[u], mnb[u]);
+#pragma unroll
+      for (int k = 0; k < RPL; ++k) a.n_sel_w += __builtin_popcountll(__ballot((sel >> k) & 1u));
+      if (stats_on) accumulate_rows<T, NP, RPL>(a, vals, sel, shift, dsum);
+      predicate_rows_wave<T, NP, RPL>(a, fps, vals, vb[u], wtb[u], mtb[u], mnb[u]);
     }
-    if (hll_on) {  // all UNROLL * RPL rows of the iteration: hashes, then one batched update
-      uint64_t h[UNROLL * RPL];
-      uint32_t sel_all = 0u;
+    if (hll_on) {  // every row is hashed (branch-free); unselected rows raise nothing
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
-        hash_rows<T, RPL>(h + u * RPL, reinterpret_cast<const T*>(&vec[u]));
-        sel_all |= (vb[u] & wtb[u]) << (u * RPL);
+        const T* vals = reinterpret_cast<const T*>(&vec[u]);
+        const uint32_t sel = vb[u] & wtb[u];
+#pragma unroll
+        for (int k = 0; k < RPL; ++k)
+          hll_hash_update<T>(lregs, vals[k], (sel >> k) & 1u);
       }
-      hll_update_lds_batch<UNROLL * RPL>(lregs, h, sel_all);
     }
     if constexpr (!IsIntegral<T>::value) {
-      if (stats_on) neumaier_add(a.fs, a.fc, psum);
+      if (stats_on) neumaier_add(a.fs, a.fc, dsum);
     }
   }
   // ---- ragged end of the chunk: one row per lane
-  double psum = 0.0;
+  double dsum = 0.0;
   for (uint32_t r = full_iters * ROWS_PER_ITER + tid; r < span; r += kBlock) {
     const T v = buf_elem<T>(rv, r);
     const uint32_t valid = (buf_bits<1>(rvalid, r) | no_valid) & 1u;
@@ -637,14 +713,11 @@ __global__ __launch_bounds__(kBlock) void dq_scan_values_kernel(
     a.n_rows += wt;
     a.n_wnn += wn;
     a.n_sel += valid & wt;
-    if (stats_on) accumulate_rows<T, NP, 1>(a, &v, valid & wt, shift, psum);
+    if (stats_on) accumulate_rows<T, NP, 1>(a, &v, valid & wt, shift, dsum);
     predicate_rows<T, NP, 1>(a, fps, &v, valid, wt, mt, mn);
-    if (hll_on) {
-      const uint64_t h = spark_hash<T>(v);
-      hll_update_lds_batch<1>(lregs, &h, valid & wt);
-    }
+    if (hll_on) hll_hash_update<T>(lregs, v, valid & wt & 1u);
   }
-  if constexpr (!IsIntegral<T>::value) neumaier_add(a.fs, a.fc, psum);
+  if constexpr (!IsIntegral<T>::value) neumaier_add(a.fs, a.fc, dsum);
   if (hll_on) {  // fold the workgroup's registers into the task's set (max: order independent)
     __syncthreads();
     uint32_t* out = hll_regs + (int64_t)task.hll * kHllM;
@@ -654,7 +727,7 @@ __global__ __launch_bounds__(kBlock) void dq_scan_values_kernel(
     }
   }
   a.shift = shift;
-  thread_finish<NP>(a, NP, &partials[(int64_t)blockIdx.y * gridDim.x + blockIdx.x]);
+  thread_finish<T, NP>(a, NP, &partials[(int64_t)blockIdx.y * gridDim.x + blockIdx.x]);
 }
 
 // Tasks that need no values (Completeness, Size(where), IS [NOT] NULL / mask / constant
@@ -807,6 +880,41 @@ hipError_t launch_scan_group(int kind, int ptype, int np, const ScanTask* d_task
     default: return launch_values_np<double>(np, grid, stream, d_tasks, d_group, d_cols, d_masks, n_rows, d_partials,
                                                         d_hll_regs);
   }
+}
+
+// Workgroups of one value-scan specialisation that fit on a CU at once (VGPR-bound), so the
+// host can size the grid to whole rounds of resident workgroups: a grid of 1.33 rounds leaves
+// the last third of the pass running at a third of the occupancy.
+template <typename T>
+static const void* values_kernel_ptr(int np) {
+  if (np < 0) return reinterpret_cast<const void*>(&dq_scan_values_kernel<T, kMaxPreds, true>);
+  switch (np) {
+    case 0: return reinterpret_cast<const void*>(&dq_scan_values_kernel<T, 0, false>);
+    case 1: return reinterpret_cast<const void*>(&dq_scan_values_kernel<T, 1, false>);
+    case 2: return reinterpret_cast<const void*>(&dq_scan_values_kernel<T, 2, false>);
+    case 3: return reinterpret_cast<const void*>(&dq_scan_values_kernel<T, 3, false>);
+    case 4: return reinterpret_cast<const void*>(&dq_scan_values_kernel<T, 4, false>);
+    default: return reinterpret_cast<const void*>(&dq_scan_values_kernel<T, kMaxPreds, false>);
+  }
+}
+
+int scan_group_blocks_per_cu(int kind, int ptype, int np) {
+  const void* fn;
+  if (kind == 0) {
+    fn = reinterpret_cast<const void*>(&dq_scan_bits_kernel);
+  } else {
+    switch (ptype) {
+      case DQ_T_INT8: fn = values_kernel_ptr<int8_t>(np); break;
+      case DQ_T_INT16: fn = values_kernel_ptr<int16_t>(np); break;
+      case DQ_T_INT32: fn = values_kernel_ptr<int32_t>(np); break;
+      case DQ_T_INT64: fn = values_kernel_ptr<int64_t>(np); break;
+      case DQ_T_FLOAT32: fn = values_kernel_ptr<float>(np); break;
+      default: fn = values_kernel_ptr<double>(np); break;
+    }
+  }
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kBlock, 0) != hipSuccess || nb < 1) return 0;
+  return nb;
 }
 
 hipError_t launch_scan_reduce(const ScanAcc* d_partials, const PartRange* d_ranges, int n_tasks,
