@@ -25,7 +25,8 @@ __global__ __launch_bounds__(kBlock) void dq_diag_hash_kernel(int iters, uint64_
 #pragma unroll
     for (int c = 0; c < 4; ++c) {  // the scan kernel's per-row hash + register update
       const W64 h = spark_hash_dev<int64_t>((int64_t)x[c]);
-      x[c] = ((uint64_t)h.hi << 32) | h.lo;
+      const W64 f = xxh64_final(h);
+      x[c] = ((uint64_t)f.hi << 32) | f.lo;
       if (WITH_HLL) {
         uint32_t idx, nlz;
         hll_slot(h, idx, nlz);

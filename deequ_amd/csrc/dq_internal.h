@@ -370,17 +370,24 @@ template <int R>  // rotl64 by 0 < R < 32
 __device__ inline W64 w64_rotl(W64 x) {
   return {__builtin_amdgcn_alignbit(x.lo, x.hi, 32 - R), __builtin_amdgcn_alignbit(x.hi, x.lo, 32 - R)};
 }
-__device__ inline W64 w64_avalanche(W64 h) {
+// The avalanche up to (not including) the final h ^= h >> 32, which only moves the high word
+// into the low one: the HLL slot reads the high word directly (hll_slot).
+__device__ inline W64 w64_avalanche_pre32(W64 h) {
   h.lo ^= h.hi >> 1;                                   // h ^= h >> 33
   h = w64_mul<kP2>(h);
   h.lo ^= __builtin_amdgcn_alignbit(h.hi, h.lo, 29);  // h ^= h >> 29
   h.hi ^= h.hi >> 29;
-  h = w64_mul<kP3>(h);
+  return w64_mul<kP3>(h);
+}
+__device__ inline W64 w64_avalanche(W64 h) {
+  h = w64_avalanche_pre32(h);
   h.lo ^= h.hi;                                        // h ^= h >> 32
   return h;
 }
 constexpr uint64_t rotl64_c(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
 
+// xxh64_*_dev return the hash BEFORE its last step (x = h ^ (h >> 32)): xxh64_final() applies it.
+__device__ inline W64 xxh64_final(W64 h) { return {h.lo ^ h.hi, h.hi}; }
 __device__ inline W64 xxh64_8_dev(uint32_t lo, uint32_t hi) {  // Spark XXH64.hashLong, seed 42
   constexpr uint64_t RS = rotl64_c(42ull + kP5 + 8, 27);
   W64 k = w64_mul<kP2>({lo, hi});
@@ -388,7 +395,7 @@ __device__ inline W64 xxh64_8_dev(uint32_t lo, uint32_t hi) {  // Spark XXH64.ha
   W64 h = w64_rotl<27>(k);
   h.lo ^= (uint32_t)RS;
   h.hi ^= (uint32_t)(RS >> 32);
-  return w64_avalanche(w64_mul<kP1, kP4>(h));
+  return w64_avalanche_pre32(w64_mul<kP1, kP4>(h));
 }
 __device__ inline W64 xxh64_4_dev(uint32_t v) {  // Spark XXH64.hashInt, seed 42
   constexpr uint64_t RS = rotl64_c(42ull + kP5 + 4, 23);
@@ -396,7 +403,7 @@ __device__ inline W64 xxh64_4_dev(uint32_t v) {  // Spark XXH64.hashInt, seed 42
   W64 h = w64_rotl<23>({(uint32_t)p, (uint32_t)(p >> 32) + v * (uint32_t)(kP1 >> 32)});
   h.lo ^= (uint32_t)RS;
   h.hi ^= (uint32_t)(RS >> 32);
-  return w64_avalanche(w64_mul<kP2, kP3>(h));
+  return w64_avalanche_pre32(w64_mul<kP2, kP3>(h));
 }
 
 // spark_hash<T> on the device, as halves.
@@ -429,13 +436,17 @@ __device__ inline uint32_t ffbh_u32(uint32_t v) {  // v_ffbh_u32: leading zeros,
 // idx and nlz = pw - 1.  The high word of w = (x << 9) | W_PADDING is zero for one hash in 2^32:
 // that case (nlz >= 32) is taken on a wave-uniform branch instead of paying a 64-bit count
 // on every row.
-__device__ inline void hll_slot(W64 x, uint32_t& idx, uint32_t& nlz) {
-  idx = x.hi >> (kHllIdxShift - 32);
-  const uint32_t w_hi = __builtin_amdgcn_alignbit(x.hi, x.lo, 23);  // (x << 9) >> 32
-  nlz = ffbh_u32(w_hi);
+// `h` is the pre-final hash (xxh64_*_dev): x = h ^ (h >> 32) has x.hi = h.hi, and the bits of
+// w below its top 23 only matter when those 23 (bits 22..0 of x.hi) are all zero, so the
+// common case counts on h.hi << 9 alone.
+__device__ inline void hll_slot(W64 h, uint32_t& idx, uint32_t& nlz) {
+  idx = h.hi >> (kHllIdxShift - 32);
+  nlz = ffbh_u32(h.hi << 9);
   if (__ballot(nlz == ~0u)) {
+    const W64 x = xxh64_final(h);
+    const uint32_t w_hi = __builtin_amdgcn_alignbit(x.hi, x.lo, 23);  // (x << 9) >> 32
     const uint32_t w_lo = (x.lo << 9) | (uint32_t)kHllWPadding;
-    if (nlz == ~0u) nlz = 32u + ffbh_u32(w_lo);
+    if (nlz == ~0u) nlz = (w_hi != 0u) ? ffbh_u32(w_hi) : 32u + ffbh_u32(w_lo);
   }
 }
 

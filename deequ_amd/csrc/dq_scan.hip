@@ -521,8 +521,8 @@ __device__ inline void predicate_rows(ThreadAcc<NP>& a, const FastPred* fps, con
 // kinds fall back to the lane bit path.  Uniform control flow only (wave-uniform counters).
 template <typename T, int NP, int R>
 __device__ inline void predicate_rows_wave(ThreadAcc<NP>& a, const FastPred* fps, const T* vals,
-                                           uint32_t valid, uint32_t wt, const uint32_t* mt,
-                                           const uint32_t* mn) {
+                                           uint32_t valid, uint32_t wt, uint32_t sel,
+                                           const uint32_t* mt, const uint32_t* mn) {
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     const FastPred& fp = fps[p];
@@ -532,7 +532,7 @@ __device__ inline void predicate_rows_wave(ThreadAcc<NP>& a, const FastPred* fps
       const bool f64 = !IsIntegral<T>::value || fp.as_f64;
 #pragma unroll
       for (int k = 0; k < R; ++k) {
-        const bool in = ((valid & wt) >> k) & 1u;  // NOT NULL (FP_CMP: valid) and where TRUE
+        const bool in = (sel >> k) & 1u;  // valid & where TRUE (FP_CMP: NOT NULL = valid)
         bool b;
         if (f64) {
           const double x = (double)vals[k];
@@ -681,7 +681,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu((NP <= 3
 #pragma unroll
       for (int k = 0; k < RPL; ++k) a.n_sel_w += __builtin_popcountll(__ballot((sel >> k) & 1u));
       if (stats_on) accumulate_rows<T, NP, RPL>(a, vals, sel, shift, dsum);
-      predicate_rows_wave<T, NP, RPL>(a, fps, vals, vb[u], wtb[u], mtb[u], mnb[u]);
+      predicate_rows_wave<T, NP, RPL>(a, fps, vals, vb[u], wtb[u], sel, mtb[u], mnb[u]);
     }
     if (hll_on) {  // every row is hashed (branch-free); unselected rows raise nothing
 #pragma unroll
