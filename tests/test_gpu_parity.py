@@ -296,3 +296,31 @@ def test_correlation_state_merge_equals_union(gpu):
         assert abs(g - e) <= 1e-12 * max(1.0, abs(e)), (batched, whole)
     r = a.computeMetricFrom(whole).value.get()
     assert -1.0 <= r <= 1.0
+
+
+def test_hll_rare_rank_branches(gpu):
+    """Hashes whose rank is not decided by the high word (1 in 2^23 rows) or exceeds 32
+    (1 in 2^32): the device's wave-uniform rare branch must give the oracle's registers."""
+    import json
+    import os
+    import struct
+    with open(os.path.join(os.path.dirname(__file__), "golden", "hll_rare_values.json")) as f:
+        fx = json.load(f)
+    i64 = [e["value"] for e in fx["int64"]]
+    i32 = [e["value"] for e in fx["int32"]]
+    f64 = [struct.unpack("<d", struct.pack("<q", v))[0] for v in i64]  # same bit patterns
+    # rare rows among ordinary ones, at several lane positions and inside the vector main loop
+    rng = np.random.default_rng(11)
+    def spread(vals, ordinary):
+        out = list(ordinary)
+        for k, v in enumerate(vals):
+            out[(k * 977 + 5) % len(out)] = v
+        return out
+    n = 5000
+    cols = {"a": ["int64", spread(i64, [int(x) for x in rng.integers(-2**62, 2**62, n)])],
+            "b": ["int32", spread(i32, [int(x) for x in rng.integers(-2**31, 2**31, n)])],
+            "c": ["float64", spread(f64, [float(x) for x in rng.normal(0, 1e6, n)])]}
+    ot = oracle_table(cols)
+    st = d.run_scan([d.ApproxCountDistinct(c) for c in cols], product_table(cols))
+    for c in cols:
+        assert list(st[d.ApproxCountDistinct(c)].words) == list(O.approx_count_distinct_state(ot, c).words), c

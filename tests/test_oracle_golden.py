@@ -126,3 +126,24 @@ def test_datatype_host_logic():
     assert determine_type(data_type_distribution(d.DataTypeHistogram(0, 1, 0, 0, 1))) == I.String
     assert h.sum(d.DataTypeHistogram(1, 2, 3, 4, 5)) == d.DataTypeHistogram(2, 2, 8, 4, 5)
     assert d.DataTypeHistogram.fromBytes(h.toBytes()) == h and len(h.toBytes()) == 40
+
+
+def _rare_fixture():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "hll_rare_values.json")) as f:
+        return json.load(f)
+
+
+def test_hll_rare_rank_fixture_is_rare():
+    """The values in hll_rare_values.json really reach the device's rare HLL branches."""
+    fx = _rare_fixture()
+    for dtype, key in (("int64", "int64"), ("int32", "int32")):
+        for e in fx[key]:
+            x = O.spark_hash(e["value"], dtype)
+            if e["kind"] == "rare2":
+                assert (x >> 23) & 0xFFFFFFFF == 0
+                assert O.hll_index_and_rank(x)[1] > 32
+            else:
+                assert (x >> 32) & 0x7FFFFF == 0 and (x >> 23) & 0xFFFFFFFF != 0
+    assert any(e["kind"] == "rare2" for e in fx["int64"])
