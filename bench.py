@@ -44,6 +44,8 @@ def parse_args():
                    help="c2 = the headline scan (default); c3 = HLL on 64 columns; c4 = group-by")
     p.add_argument("--c1-rows", type=int, default=10_000_000, help="rows per GPU")
     p.add_argument("--c3-columns", type=int, default=64)
+    p.add_argument("--c3-type", default="int64", choices=["int64", "utf8"],
+                   help="C3 main run (int64) or its string variant (16-char lowercase hex of a u64)")
     p.add_argument("--c3-rows", type=int, default=125_000_000, help="rows per GPU (one batch)")
     p.add_argument("--c4-rows", type=int, default=1_000_000_000, help="rows per GPU")
     p.add_argument("--c4-batch", type=int, default=125_000_000, help="rows per string batch")
@@ -152,6 +154,35 @@ def make_c3_table(rows: int, n_cols: int, rank: int, device: int):
     return d.Table(cols)
 
 
+def make_c3_string_table(rows: int, n_cols: int, rank: int, device: int):
+    """C3 string variant: 16-char lowercase hex of a uniform u64, 5% NULL, as
+    Arrow utf8 (int32 offsets + 16 B of chars per row)."""
+    import torch
+    import deequ_amd as d
+    dev = torch.device("cuda", device)
+    gen = torch.Generator(device=dev)
+    hexd = torch.tensor(list(b"0123456789abcdef"), dtype=torch.uint8, device=dev)
+    shifts = torch.arange(60, -4, -4, dtype=torch.int64, device=dev)
+    chunk = 1 << 24
+    cols = {}
+    for k in range(n_cols):
+        gen.manual_seed(9000 + 1000 * rank + k)
+        chars = torch.empty(rows * 16 + 16, dtype=torch.uint8, device=dev)
+        valid = torch.empty((rows + 7) // 8 + 64, dtype=torch.uint8, device=dev)
+        for s in range(0, rows, chunk):
+            e = min(rows, s + chunk)
+            ids = torch.empty(e - s, dtype=torch.int64, device=dev).random_(-2 ** 63, 2 ** 63 - 1,
+                                                                          generator=gen)
+            nib = (ids[:, None] >> shifts[None, :]) & 15
+            chars[s * 16: e * 16] = hexd[nib].reshape(-1)
+            packed = _valid_bits(e - s, gen, dev, 0.05)
+            valid[s // 8: s // 8 + packed.numel()] = packed
+        offsets = torch.arange(0, 16 * (rows + 1), 16, dtype=torch.int32, device=dev)
+        cols["x%d" % k] = d.Column("string", rows, chars, valid, offsets=offsets, device=True)
+    torch.cuda.synchronize(dev)
+    return d.Table(cols)
+
+
 def make_c4_batches(rows: int, batch: int, distinct: int, rank: int, device: int):
     """C4: a string key = 12-digit zero-padded decimal of a uniform int in [0, distinct), 1% NULL,
     as Arrow utf8 batches of `batch` rows (int32 offsets cap one batch at 2 GiB of chars)."""
@@ -203,7 +234,8 @@ def run_c3(args, world, rank, local):
     import deequ_amd as d
     from deequ_amd.distributed import allgather_merge
     from deequ_amd.engine import Plan, op_spec_for
-    table = make_c3_table(args.c3_rows, args.c3_columns, rank, local)
+    utf8 = args.c3_type == "utf8"
+    table = (make_c3_string_table if utf8 else make_c3_table)(args.c3_rows, args.c3_columns, rank, local)
     analyzers = [d.ApproxCountDistinct(c) for c in table.schema]
     plan = Plan([op_spec_for(a, table.schema) for a in analyzers], table.schema, device=local)
     stream = torch.cuda.ExternalStream(plan.stream, device=torch.device("cuda", local))
@@ -222,21 +254,24 @@ def run_c3(args, world, rank, local):
     elapsed, kernel_ms, raw = _timed(args, world, step)
     est = d.ApproxCountDistinctState(list(raw[0].words)).metricValue()
     rows_total = args.c3_rows * world * args.steps
-    bpr = args.c3_columns * (8 + 1.0 / 8)
+    bpr = args.c3_columns * ((4 + 16 + 1.0 / 8) if utf8 else (8 + 1.0 / 8))
     achieved = bpr * args.c3_rows / (kernel_ms * 1e-3) / 1e9
     return {
         "metric": "rows/sec & HBM GB/s for ApproxCountDistinct HLL++ (C3)", "value": rows_total / elapsed,
         "unit": "rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "int64 (XXH64)",
-        "data": "synthetic int64 uniform over 2^64, 5% NULL, generated in HBM",
-        "config": {"workload": "C3: %d rows/GPU x %d int64 columns, one HLL plan (one batch of the "
-                               "1B-row stream)" % (args.c3_rows, args.c3_columns),
+        "vs_baseline": None, "dtype": "utf8 (XXH64 of 16 bytes)" if utf8 else "int64 (XXH64)",
+        "data": ("synthetic 16-char lowercase hex of a uniform u64" if utf8 else
+                 "synthetic int64 uniform over 2^64") + ", 5% NULL, generated in HBM",
+        "config": {"workload": "C3: %d rows/GPU x %d %s columns, one HLL plan (one batch of the "
+                               "1B-row stream)" % (args.c3_rows, args.c3_columns, "utf8" if utf8 else "int64"),
                    "rows_per_gpu": args.c3_rows, "columns": args.c3_columns},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel_ms": kernel_ms,
                      "algorithmic_bytes_per_launch": bpr * args.c3_rows},
-        "valu_roofline": valu_roofline(local, float(args.c3_rows) * args.c3_columns, kernel_ms),
+        # (the register-only hash-rate probe times the 8-byte hashLong, not 16-byte strings)
+        "valu_roofline": None if utf8 else valu_roofline(local, float(args.c3_rows) * args.c3_columns,
+                                                         kernel_ms),
         "check": {"column0_estimate": est, "rows_column0": args.c3_rows},
     }
 

@@ -344,7 +344,10 @@ __global__ __launch_bounds__(kBlock) void dq_freq_insert_kernel(FreqKeySpec ks,
       const unsigned long long want = ((unsigned long long)tag << 32) | kReady | k.len;
       uint32_t s = (uint32_t)(k.hash & (kLdsSlots - 1));
       for (int probe = 0; probe < kLdsProbe * 4 && !done; ) {
-        unsigned long long c = atomicCAS(&lds[s].ctrl, 0ull, 1ull);  // 1 = BUSY
+        // a hit (the common case once the few groups are in) needs no CAS: read ctrl, compare
+        // the key, add; only an empty slot is claimed with a CAS
+        unsigned long long c = __hip_atomic_load(&lds[s].ctrl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (c == 0ull) c = atomicCAS(&lds[s].ctrl, 0ull, 1ull);  // 1 = BUSY
         if (c == 0ull) {
           lds[s].k0 = k.k0;
           lds[s].k1 = k.k1;

@@ -18,6 +18,7 @@ ColumnProfiler.scala:18-57, 357-424, 658-710.
 """
 from __future__ import annotations
 
+import re
 import ctypes
 import json
 from collections import OrderedDict
@@ -260,6 +261,33 @@ def _find_target_columns_for_histograms(schema, generic, threshold) -> List[str]
             if schema[c] in _HISTOGRAM_TYPES and generic.typeOf(c) in ok_types and count <= threshold]
 
 
+_IDENT = re.compile(r"^[A-Za-z_][A-Za-z0-9_]*$")
+
+
+def _bool_histograms(data, columns: Sequence[str]) -> Dict[str, Distribution]:
+    """A boolean column has at most three groups ("true", "false", "NullValue"), so its exact
+    histogram is three counts: all boolean target columns go through ONE fused scan (Size +
+    Completeness + Compliance(c) per column) instead of one group-by per column.  Same
+    (value.toString, count) pairs as computeHistograms (:564-606); empty groups do not exist
+    in a group-by, so zero counts are dropped."""
+    from .analyzers import Completeness, Compliance, Size
+    from .engine import run_scan
+    size = Size()
+    per_col = {c: (Completeness(c), Compliance("histogram %s" % c, c)) for c in columns}
+    st = run_scan([size] + [a for pair in per_col.values() for a in pair], data)
+    n = st[size].numMatches
+    out = {}
+    for c, (comp, true_) in per_col.items():
+        non_null = st[comp].numMatches if st[comp] is not None else 0
+        t = st[true_].numMatches if st[true_] is not None else 0
+        counts = {"true": t, "false": non_null - t, NULL_FIELD_REPLACEMENT: n - non_null}
+        counts = {k: v for k, v in counts.items() if v > 0}
+        total = sum(counts.values())
+        out[c] = Distribution({k: DistributionValue(v, v / total) for k, v in sorted(counts.items())},
+                              len(counts))
+    return out
+
+
 def compute_histograms(data, target_columns: Sequence[str],
                        expected_groups: Optional[Dict[str, int]] = None) -> Dict[str, Distribution]:
     """computeHistograms (:564-606): exact (column, value.toString) counts, NULL -> "NullValue",
@@ -268,7 +296,12 @@ def compute_histograms(data, target_columns: Sequence[str],
     from .javafmt import spark_cast_to_string
     schema = data.schema
     out = {}
+    bool_cols = [c for c in target_columns if schema[c] == "bool" and _IDENT.match(c)]
+    if bool_cols:
+        out.update(_bool_histograms(data, bool_cols))
     for c in target_columns:
+        if c in out:
+            continue
         dtype = schema[c]
         table = FrequencyTable([c], dict(schema), histogram=True)
         if expected_groups and c in expected_groups:  # the pass-1 estimate (<= the threshold)

@@ -119,3 +119,25 @@ def test_low_cardinality_many_rows(gpu):
     got = {int.from_bytes(k, "little", signed=True): int(c) for k, c in zip(keys, counts.tolist())}
     u, c = np.unique(vals, return_counts=True)
     assert got == dict(zip(u.tolist(), c.tolist()))
+
+
+@pytest.mark.parametrize("distinct,hint", [(90, 100), (3_000_000, 100)])
+def test_few_group_hint_single_launch_and_fallback(gpu, distinct, hint):
+    """dq_freq_expect_groups: a right hint takes one insert launch over the whole batch; a wrong
+    one (3M groups behind a hint of 100) overflows the optimistic table, which is cleared and
+    re-filled on the sized path.  Both must give the exact group-by."""
+    rng = np.random.default_rng(5)
+    n = 6_000_000  # more rows than one sized sub-launch (4M)
+    vals = rng.integers(0, distinct, n).astype(np.int64)
+    valid = rng.random(n) >= 0.02
+    table = d.Table({"v": d.Column.from_numpy(vals, valid, "int64")})
+    t = FrequencyTable(["v"], {"v": "int64"})
+    t.expect_groups(hint)
+    t.consume(table)
+    counts, keys = t.export()
+    s = t.summary()
+    t.close()
+    got = {int.from_bytes(k, "little", signed=True): int(c) for k, c in zip(keys, counts.tolist())}
+    u, c = np.unique(vals[valid], return_counts=True)
+    assert s.num_groups == len(u)
+    assert got == dict(zip(u.tolist(), c.tolist()))

@@ -214,3 +214,25 @@ def test_profiler_runner_and_json(gpu):
     j = json.loads(ColumnProfiles.toJson(list(profiles.profiles.values())))
     assert [c["column"] for c in j["columns"]] == ["item", "att1", "att2"]
     assert j["columns"][0]["dataType"] == "Integral" and j["columns"][0]["mean"] == 3.5
+
+
+def test_bool_histograms_fused_scan(gpu):
+    """Boolean profiler histograms come from one fused scan; they must equal the exact
+    (value.toString, count) group-by of computeHistograms (ColumnProfiler.scala:564-606)."""
+    from deequ_amd.profiles import compute_histograms
+    rng = np.random.default_rng(3)
+    n = 7000
+    cols = {"b0": [None if rng.random() < 0.1 else bool(rng.integers(0, 2)) for _ in range(n)],
+            "b1": [True] * n,                                   # one group
+            "b2": [None if i % 3 == 0 else False for i in range(n)]}
+    table = product_table({c: ["bool", v] for c, v in cols.items()})
+    hist = compute_histograms(table, list(cols))
+    for c, vals in cols.items():
+        want = {}
+        for v in vals:
+            k = "NullValue" if v is None else ("true" if v else "false")
+            want[k] = want.get(k, 0) + 1
+        got = hist[c]
+        assert got.numberOfBins == len(want), c
+        assert {k: v.absolute for k, v in got.values.items()} == want, c
+        assert all(v.ratio == v.absolute / n for v in got.values.values())
