@@ -8,10 +8,9 @@
 // and the merge (:121-139) = per-register max.  Because max is order-independent the result
 // is bitwise identical whatever the block/wave schedule.
 //
+// Strings and booleans only: numeric columns are hashed inside their value scan (dq_scan.hip).
 // Layout: blockIdx.y = HLL task (column, where), blockIdx.x = contiguous row chunk.  Each
-// workgroup keeps its 512 registers as u32 in LDS (2 KiB) and updates them with ds_max_u32,
-// skipping the atomic when the register already holds >= pw (after a few thousand rows almost
-// every update is a no-op, so the LDS traffic is one ds_read per row).  At the end every
+// workgroup keeps its 512 registers as u32 in LDS (2 KiB) and updates them with ds_max_u32.  At the end every
 // non-zero register is folded into the task's global registers with one atomicMax.  The host
 // packs the 512 registers into the 52 Long words of ApproxCountDistinctState.
 #include "dq_internal.h"
@@ -20,52 +19,7 @@ namespace dq {
 
 namespace {
 
-struct alignas(16) Vec16 {
-  uint32_t w[4];
-};
-
 __device__ inline void hll_update(uint32_t* regs, uint64_t x) { hll_update_lds(regs, x); }
-
-template <int RPL>
-__device__ inline uint32_t load_bits(const uint8_t* bm, int64_t row0, int64_t left) {
-  if constexpr (RPL == 16) {
-    if (left > 8) return (uint32_t)(*reinterpret_cast<const uint16_t*>(bm + (row0 >> 3)));
-    return (uint32_t)bm[row0 >> 3];
-  } else {
-    const uint32_t byte = bm[row0 >> 3];
-    return (byte >> (uint32_t)(row0 & 7)) & ((1u << RPL) - 1u);
-  }
-}
-
-template <typename T>
-__device__ void hll_fixed(uint32_t* regs, const DevColumn& col, const uint8_t* wt_bm,
-                          int64_t row_begin, int64_t row_end) {
-  constexpr int RPL = 16 / (int)sizeof(T);
-  constexpr uint32_t FULL = (1u << RPL) - 1u;
-  const T* __restrict__ values = static_cast<const T*>(col.values);
-  for (int64_t row0 = row_begin + (int64_t)threadIdx.x * RPL; row0 < row_end;
-       row0 += (int64_t)kBlock * RPL) {
-    const int64_t left = row_end - row0;
-    const uint32_t in = left >= RPL ? FULL : ((1u << (uint32_t)left) - 1u);
-    Vec16 vec;
-    if (left >= RPL) {
-      vec = *reinterpret_cast<const Vec16*>(values + row0);
-    } else {
-      T tmp[RPL];
-#pragma unroll
-      for (int k = 0; k < RPL; ++k) tmp[k] = k < left ? values[row0 + k] : T(0);
-      __builtin_memcpy(&vec, tmp, 16);
-    }
-    uint32_t sel = in;
-    if (col.validity) sel &= load_bits<RPL>(col.validity, row0, left);
-    if (wt_bm) sel &= load_bits<RPL>(wt_bm, row0, left);
-    const T* vals = reinterpret_cast<const T*>(&vec);
-#pragma unroll
-    for (int k = 0; k < RPL; ++k) {
-      if ((sel >> k) & 1u) hll_update(regs, spark_hash<T>(vals[k]));
-    }
-  }
-}
 
 __device__ void hll_bool(uint32_t* regs, const DevColumn& col, const uint8_t* wt_bm,
                          int64_t row_begin, int64_t row_end) {
@@ -219,12 +173,7 @@ __global__ __launch_bounds__(kBlock) void dq_hll_kernel(const HllTask* __restric
 
   switch (task.ctype) {
     case DQ_T_BOOL: hll_bool(regs, col, wt_bm, row_begin, row_end); break;
-    case DQ_T_INT8: hll_fixed<int8_t>(regs, col, wt_bm, row_begin, row_end); break;
-    case DQ_T_INT16: hll_fixed<int16_t>(regs, col, wt_bm, row_begin, row_end); break;
-    case DQ_T_INT32: hll_fixed<int32_t>(regs, col, wt_bm, row_begin, row_end); break;
-    case DQ_T_INT64: hll_fixed<int64_t>(regs, col, wt_bm, row_begin, row_end); break;
-    case DQ_T_FLOAT32: hll_fixed<float>(regs, col, wt_bm, row_begin, row_end); break;
-    case DQ_T_FLOAT64: hll_fixed<double>(regs, col, wt_bm, row_begin, row_end); break;
+    // (numeric columns are hashed inside their value scan: dq_scan_values_kernel, TF_HLL)
     case DQ_T_UTF8: hll_utf8(regs, col, wt_bm, row_begin, row_end); break;
     default: break;
   }

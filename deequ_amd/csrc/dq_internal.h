@@ -472,23 +472,4 @@ __device__ inline void hll_update_lds(uint32_t* regs, uint64_t x) {
   if (pw > regs[idx]) atomicMax(&regs[idx], pw);
 }
 
-// R hashes at once (bit k of `sel` = row k selected): all index/rank pairs first, then all R
-// register reads, so one LDS wait covers R rows instead of one per row, then the atomics that
-// still raise a register.  A read may be stale (another lane raised the register since), but
-// registers only grow, so a skipped update (cur >= pw) is always already covered.
-template <int R>
-__device__ inline void hll_update_lds_batch(uint32_t* regs, const uint64_t* h, uint32_t sel) {
-  uint32_t idx[R], pw[R], cur[R];
-#pragma unroll
-  for (int k = 0; k < R; ++k) {
-    hll_idx_rank(h[k], &idx[k], &pw[k]);
-    pw[k] = ((sel >> k) & 1u) ? pw[k] : 0u;
-  }
-#pragma unroll
-  for (int k = 0; k < R; ++k) cur[k] = regs[idx[k]];
-#pragma unroll
-  for (int k = 0; k < R; ++k)
-    if (pw[k] > cur[k]) atomicMax(&regs[idx[k]], pw[k]);
-}
-
 }  // namespace dq

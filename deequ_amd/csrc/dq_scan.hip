@@ -40,9 +40,6 @@ template <typename T> struct IsIntegral { static constexpr bool value = true; };
 template <> struct IsIntegral<float> { static constexpr bool value = false; };
 template <> struct IsIntegral<double> { static constexpr bool value = false; };
 
-struct alignas(16) Vec16 {
-  uint32_t w[4];
-};
 
 template <int NP>
 struct ThreadAcc {
@@ -102,20 +99,6 @@ __device__ inline void neumaier_add(double& s, double& c, double x) {
   const double t = s + x;
   c += (fabs(s) >= fabs(x)) ? ((s - t) + x) : ((x - t) + s);
   s = t;
-}
-
-template <int RPL>
-__device__ inline uint32_t load_bits(const uint8_t* bm, int64_t row0, int64_t left) {
-  // row0 % RPL == 0 and bit 0 of bm[0] is row 0, so the RPL bits never straddle a byte for
-  // RPL <= 8; RPL == 16 reads an aligned u16 (one byte at the very end, so no byte past
-  // ceil(n_rows / 8) is ever touched).
-  if constexpr (RPL == 16) {
-    if (left > 8) return (uint32_t)(*reinterpret_cast<const uint16_t*>(bm + (row0 >> 3)));
-    return (uint32_t)bm[row0 >> 3];
-  } else {
-    const uint32_t byte = bm[row0 >> 3];
-    return (byte >> (uint32_t)(row0 & 7)) & ((1u << RPL) - 1u);
-  }
 }
 
 // ----------------------------------------------------------------------------- merges
