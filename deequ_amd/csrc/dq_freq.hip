@@ -572,48 +572,47 @@ __device__ inline bool row_selected(const FreqKeySpec& ks, const DevColumn* cols
   return true;
 }
 
-__device__ inline uint32_t block_sum(uint32_t v, uint32_t* wsum) {
-  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
-  __syncthreads();
-  uint32_t t = 0;
-  for (int w = 0; w < kBlock / 64; ++w) t += wsum[w];
-  __syncthreads();
-  return t;
-}
 
+// Each wave stages a contiguous run of the block's rows: a first pass counts the wave's selected
+// rows (validity only), one atomicAdd per block reserves the block's records, and the second
+// pass writes every selected row at its ballot prefix -- no block barrier inside either loop.
 __global__ __launch_bounds__(kBlock) void dq_freq_stage_kernel(FreqKeySpec ks, const DevColumn* __restrict__ cols,
                                                                int64_t n_rows, FreqRec* out, uint32_t* sort_keys,
                                                                unsigned long long* cursor, uint32_t* hll) {
   __shared__ uint32_t regs[kHllM];
-  __shared__ uint32_t wsum[kBlock / 64];
+  __shared__ uint32_t wcount[kBlock / 64];
   __shared__ unsigned long long base_s;
   for (int i = threadIdx.x; i < kHllM; i += kBlock) regs[i] = 0u;
-  const int64_t per = (((n_rows + gridDim.x - 1) / gridDim.x) + 63) & ~(int64_t)63;
+  const int64_t per = (((n_rows + gridDim.x - 1) / gridDim.x) + kBlock - 1) & ~(int64_t)(kBlock - 1);
   const int64_t r0 = min((int64_t)blockIdx.x * per, n_rows);
   const int64_t r1 = min(r0 + per, n_rows);
-  uint32_t mine = 0;
-  for (int64_t row = r0 + threadIdx.x; row < r1; row += kBlock) mine += row_selected(ks, cols, row) ? 1u : 0u;
-  const uint32_t total = block_sum(mine, wsum);
-  if (threadIdx.x == 0) base_s = total ? atomicAdd(cursor, (unsigned long long)total) : 0ull;
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const int64_t wper = per / (kBlock / 64);  // a multiple of 64
+  const int64_t w0 = min(r0 + (int64_t)wave * wper, r1);
+  const int64_t w1 = min(w0 + wper, r1);
+  uint32_t cnt = 0;
+  for (int64_t b = w0; b < w1; b += 64) {
+    const int64_t row = b + lane;
+    cnt += (uint32_t)__popcll(__ballot(row < w1 && row_selected(ks, cols, row)));
+  }
+  if (lane == 0) wcount[wave] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t total = 0;
+    for (int v = 0; v < kBlock / 64; ++v) total += wcount[v];
+    base_s = total ? atomicAdd(cursor, (unsigned long long)total) : 0ull;
+  }
   __syncthreads();
   unsigned long long w = base_s;
+  for (uint32_t v = 0; v < wave; ++v) w += wcount[v];
   alignas(8) uint8_t scratch[kMaxLocalKey];
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  for (int64_t b0 = r0; b0 < r1; b0 += kBlock) {
-    const int64_t row = b0 + threadIdx.x;
-    const bool sel = row < r1 && row_selected(ks, cols, row);
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  for (int64_t b = w0; b < w1; b += 64) {
+    const int64_t row = b + lane;
+    const bool sel = row < w1 && row_selected(ks, cols, row);
     const uint64_t m = __ballot(sel);
-    if (lane == 0) wsum[wave] = (uint32_t)__popcll(m);
-    __syncthreads();
-    uint32_t before = 0, all = 0;
-    for (uint32_t v = 0; v < (uint32_t)(kBlock / 64); ++v) {
-      const uint32_t c = wsum[v];
-      before += v < wave ? c : 0u;
-      all += c;
-    }
     if (sel) {
-      const unsigned long long pos = w + before + (unsigned long long)__popcll(m & ((1ull << lane) - 1ull));
+      const unsigned long long pos = w + (unsigned long long)__popcll(m & lt_mask);
       Key k;
       bool too_long;
       FreqRec r;
@@ -630,8 +629,7 @@ __global__ __launch_bounds__(kBlock) void dq_freq_stage_kernel(FreqKeySpec ks, c
       out[pos] = r;
       sort_keys[pos] = key32;
     }
-    w += all;
-    __syncthreads();
+    w += (unsigned long long)__popcll(m);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < kHllM; i += kBlock)
