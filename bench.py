@@ -105,6 +105,35 @@ def c2_analyzers():
     return out
 
 
+def scan_without_hll(table, device: int, steps: int):
+    """The same fused pass without the 8 ApproxCountDistinct (57 analyzers), on the same table:
+    the HBM-bound side of the kernel next to the headline's VALU-bound one.
+    Reported beside the headline, never as `value`."""
+    import torch
+    import deequ_amd as d
+    from deequ_amd.engine import Plan, op_spec_for
+    analyzers = [a for a in c2_analyzers() if not isinstance(a, d.ApproxCountDistinct)]
+    plan = Plan([op_spec_for(a, table.schema) for a in analyzers], table.schema, device=device)
+    stream = torch.cuda.ExternalStream(plan.stream, device=torch.device("cuda", device))
+    try:
+        ms = []
+        for k in range(steps + 1):
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            plan.reset()
+            ev[0].record(stream)
+            plan.consume(table)
+            ev[1].record(stream)
+            plan.finish_raw()
+            if k:  # the first pass warms up
+                ms.append(ev[0].elapsed_time(ev[1]))
+    finally:
+        plan.close()
+    kernel_ms = sum(ms) / len(ms)
+    achieved = BYTES_PER_ROW * table.num_rows / (kernel_ms * 1e-3) / 1e9
+    return {"analyzers": len(analyzers), "kernel_ms": kernel_ms, "achieved": achieved,
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS}
+
+
 def cpu_baseline(sample_rows: int, threads: int):
     """The oracle's C restatement (Spark semantics: sequential per-partition aggregation,
     per-row Welford, partition states merged with State.sum) on `threads` host threads."""
@@ -602,6 +631,8 @@ def main():
         "valu_roofline": valu_roofline(local, float(args.rows) * n_hll, kernel_ms) if n_hll else None,
         "cpu_baseline": None,
     }
+    if rank == 0 and world == 1:
+        result["scan_without_hll"] = scan_without_hll(table, local, args.steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample_rows, threads)
