@@ -539,6 +539,7 @@ struct dq_plan : Stager {
   std::vector<OpSlot> slots;
   std::vector<ScanTask> scan_tasks;
   std::vector<ScanGroup> groups;
+  std::vector<int> group_per_cu;  // resident workgroups per CU of each group's kernel (0 = unknown)
   std::vector<HllTask> hll_tasks;    // ApproxCountDistinct not fused into the value scan
   std::vector<std::pair<int, int>> hll_sets;  // (column, where program) of each register set
   std::vector<HllTask> dtype_tasks;  // DataType: {column, type, where}
@@ -1070,7 +1071,13 @@ extern "C" dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, in
     if (G.kind != 0 && plan->n_cu > 0 && plan->scan_rounds > 0) {
       // the value scans are VALU-bound: one (or scan_rounds) full round(s) of resident
       // workgroups, split evenly over the group's tasks
-      const int per_cu = scan_group_blocks_per_cu(G.kind, G.ptype, G.np);
+      if (plan->group_per_cu.size() != plan->groups.size()) {  // once per plan
+        plan->group_per_cu.resize(plan->groups.size());
+        for (size_t q = 0; q < plan->groups.size(); ++q)
+          plan->group_per_cu[q] = plan->groups[q].kind == 0 ? 0 : scan_group_blocks_per_cu(
+              plan->groups[q].kind, plan->groups[q].ptype, plan->groups[q].np);
+      }
+      const int per_cu = plan->group_per_cu[g];
       if (per_cu > 0) bpt = std::max<int64_t>(1, (int64_t)plan->n_cu * per_cu * plan->scan_rounds / ng);
     }
     bpt = std::max<int64_t>(1, std::min<int64_t>(bpt, chunks));
