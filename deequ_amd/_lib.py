@@ -11,7 +11,9 @@ import os
 from ctypes import (POINTER, Structure, c_char_p, c_double, c_int, c_int32, c_int64, c_size_t,
                     c_uint8, c_uint64, c_void_p)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdeequ_amd.so")
+# DEEQU_AMD_LIB points at another build of the same library (A/B kernel experiments in one run)
+LIB_PATH = os.environ.get("DEEQU_AMD_LIB") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "libdeequ_amd.so")
 
 # ---------------------------------------------------------------- enums (mirror the header)
 DQ_OK, DQ_ERR_INVALID, DQ_ERR_UNSUPPORTED, DQ_ERR_DEVICE, DQ_ERR_OOM, DQ_ERR_STATE, DQ_ERR_SPACE = range(7)

@@ -1277,12 +1277,13 @@ extern "C" dq_status dq_plan_finish(dq_plan* plan, dq_state* out, int n_out) {
         break;
       case DQ_OP_MINIMUM:
         o.has_value = a.n_sel > 0;
-        if (is_integral(ptype)) o.value = (double)a.imin;
+        // integral columns: the kernel keeps min/max of (double)x, which equals (double)min(x)
+        if (is_integral(ptype)) o.value = a.fmin;
         else o.value = (a.fmin > a.fmax) ? std::numeric_limits<double>::quiet_NaN() : a.fmin;  // all NaN
         break;
       case DQ_OP_MAXIMUM:
         o.has_value = a.n_sel > 0;
-        if (is_integral(ptype)) o.value = (double)a.imax;
+        if (is_integral(ptype)) o.value = a.fmax;
         else o.value = a.nnan > 0 ? std::numeric_limits<double>::quiet_NaN() : a.fmax;
         break;
       default: break;

@@ -365,6 +365,9 @@ __device__ inline double vmax_f64(double a, double b) {
 // instructions: a selected-row test is one compare reused by every statistic (the min/max
 // updates AND it into their compare mask), and int64 -> double is cvt(hi) * 2^32 + cvt(lo) as
 // one fma (the same correctly rounded value as (double)xi).
+// Min/Max of an integral column are kept on (double)xi: Spark's state is min(col).cast(double)
+// (Minimum.scala:40) and round-to-nearest is monotone, so min((double)x) == (double)min(x); a
+// v_min_f64 / v_max_f64 pair on the converted value replaces two 64-bit compare-and-selects.
 template <typename T, int NP, int R>
 __device__ inline void accumulate_rows(ThreadAcc<NP>& a, const T* vals, uint32_t sel, double shift,
                                        double& dsum) {
@@ -374,18 +377,22 @@ __device__ inline void accumulate_rows(ThreadAcc<NP>& a, const T* vals, uint32_t
       const bool s = (sel >> k) & 1u;
       const int64_t xi = (int64_t)vals[k];
       a.isum += s ? xi : 0;
-      if (s & (xi < a.imin)) a.imin = xi;
-      if (s & (xi > a.imax)) a.imax = xi;
-      double dd;
-      if constexpr (sizeof(T) == 8) {  // xi - shift: cvt(hi) * 2^32 + (cvt(lo) - shift), one fma
-        dd = fma((double)(int32_t)((uint64_t)xi >> 32), 0x1p32,
-                 (double)(uint32_t)(uint64_t)xi - shift);
+      double xd;
+      if constexpr (sizeof(T) == 8) {  // cvt(hi) * 2^32 + cvt(lo), one rounding
+        xd = fma((double)(int32_t)((uint64_t)xi >> 32), 0x1p32, (double)(uint32_t)(uint64_t)xi);
       } else {
-        dd = (double)xi - shift;
+        xd = (double)xi;
       }
-      const double d = s ? dd : 0.0;
+      const double d = s ? (xd - shift) : 0.0;
       a.s1 += d;
       a.s2 = fma(d, d, a.s2);
+      // an unselected row offers a quiet NaN (one select on the high word), which the
+      // hardware min / max drop
+      const uint64_t xb = __builtin_bit_cast(uint64_t, xd);
+      const uint32_t xh = s ? (uint32_t)(xb >> 32) : 0x7ff80000u;
+      const double xn = __builtin_bit_cast(double, ((uint64_t)xh << 32) | (uint32_t)xb);
+      a.fmin = vmin_f64(a.fmin, xn);
+      a.fmax = vmax_f64(a.fmax, xn);
     }
   } else {
 #pragma unroll
@@ -544,7 +551,7 @@ __device__ inline void predicate_rows_wave(ThreadAcc<NP>& a, const FastPred* fps
 // returns 0 without touching memory) and a uniform "absent" mask is OR-ed in afterwards, so
 // no load sits behind a branch (which would force a vmcnt(0) per load).
 template <typename T, int NP, bool EXT>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu((NP <= 3 && !EXT) ? 6 : 1))) void dq_scan_values_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu((NP <= 3 && !EXT && sizeof(T) >= 4) ? 6 : 1))) void dq_scan_values_kernel(
     const ScanTask* __restrict__ tasks, const int32_t* __restrict__ group,
     const DevColumn* __restrict__ cols, const DevMask* __restrict__ masks, int64_t n_rows,
     ScanAcc* partials, uint32_t* __restrict__ hll_regs) {

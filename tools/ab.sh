@@ -1,0 +1,13 @@
+#!/bin/bash
+# A/B: the same bench with two builds of the library, alternated, in one box session.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+ARGS=${ARGS:-"--steps 10 --warmup 3 --no-cpu-baseline"}
+for i in 1 2 3; do
+  for v in old new; do
+    if [ $v = old ]; then export DEEQU_AMD_LIB=$PWD/gpurun_ab/lib_old.so; else unset DEEQU_AMD_LIB; fi
+    timeout -k 10 300 python -u bench.py $ARGS > gpurun_out/ab_${v}_$i.log 2>&1 || { echo "FAIL $v $i"; exit 1; }
+    python -c "import json,sys;d=json.loads(open('gpurun_out/ab_${v}_$i.log').read().strip().split('\n')[-1]);print('$v',$i,d['ms_per_step'],d.get('roofline',{}).get('kernel_ms'))"
+  done
+done
