@@ -39,6 +39,9 @@ def parse_args():
     p.add_argument("--cpu-sample-rows", type=int, default=256_000_000)
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, nproc)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-side-passes", action="store_true",
+                   help="skip the scan_without_hll pass (profiler runs: the kernel trace then "
+                        "holds only the headline launches)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     p.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5"],
                    help="c2 = the headline scan (default); c3 = HLL on 64 columns; c4 = group-by")
@@ -631,7 +634,7 @@ def main():
         "valu_roofline": valu_roofline(local, float(args.rows) * n_hll, kernel_ms) if n_hll else None,
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and not args.no_side_passes:
         result["scan_without_hll"] = scan_without_hll(table, local, args.steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)

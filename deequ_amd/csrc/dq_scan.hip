@@ -44,7 +44,7 @@ template <> struct IsIntegral<double> { static constexpr bool value = false; };
 template <int NP>
 struct ThreadAcc {
   uint32_t n_rows, n_wnn, n_sel;
-  uint64_t nan_wave;  // fp: ballot of the wave's selected NaN rows (wave-uniform)
+  uint64_t nan_wave;  // fp: selected NaN seen (a wave ballot in the tail, a lane flag in the main loop; OR-ed by ballot at the end)
   int64_t isum, imin, imax;
   double fs, fc, fmin, fmax;
   double shift, s1, s2;
@@ -412,8 +412,9 @@ __device__ inline void accumulate_rows(ThreadAcc<NP>& a, const T* vals, uint32_t
       const double xn = __builtin_bit_cast(double, ((uint64_t)xh << 32) | (uint32_t)xb);
       a.fmin = vmin_f64(a.fmin, xn);
       a.fmax = vmax_f64(a.fmax, xn);
-      // any selected NaN: a wave ballot OR-ed on the scalar unit
-      a.nan_wave |= __ballot(s & (x != x));
+      // any selected NaN.  The main loop (R > 1) tests its iteration's Σd once instead: a
+      // selected NaN makes it NaN (see nan_recheck)
+      if constexpr (R == 1) a.nan_wave |= __ballot(s & (x != x));
     }
   }
 }
@@ -661,7 +662,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu((NP <= 3
       wnb[u] = (wnb[u] | no_where) & FULL;
     }
     // ---- compute phase
-    double dsum = 0.0;
+    double dsum = -0.0;  // (-0.0 + d == d for every d: the first add folds away)
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const T* vals = reinterpret_cast<const T*>(&vec[u]);
@@ -684,7 +685,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu((NP <= 3
       }
     }
     if constexpr (!IsIntegral<T>::value) {
-      if (stats_on) neumaier_add(a.fs, a.fc, dsum);
+      if (stats_on) {
+        // NaN detection, one compare per iteration: a selected NaN makes this lane's Σd NaN
+        // (unselected rows contribute an exact 0), so only a NaN Σd -- a NaN, or +Inf and -Inf
+        // together -- re-tests the iteration's rows exactly.  Rare and lane-divergent.
+        if (__builtin_expect(dsum != dsum, 0)) {
+#pragma unroll
+          for (int u = 0; u < UNROLL; ++u) {
+            const T* vals = reinterpret_cast<const T*>(&vec[u]);
+            const uint32_t sel = vb[u] & wtb[u];
+#pragma unroll
+            for (int k = 0; k < RPL; ++k)
+              if (((sel >> k) & 1u) && vals[k] != vals[k]) a.nan_wave = 1u;
+          }
+        }
+        neumaier_add(a.fs, a.fc, dsum);
+      }
     }
   }
   // ---- ragged end of the chunk: one row per lane

@@ -216,6 +216,45 @@ def test_special_float_values(gpu):
     assert math.isnan(only_nan[d.Minimum("f")].minValue)
 
 
+@pytest.mark.parametrize("ftype", ["float64", "float32"])
+def test_special_float_values_in_main_loop(gpu, ftype):
+    """NaN / ±Inf far from the ragged tail, where the scan tests a lane's Σd once per
+    iteration: a selected NaN wins max; +Inf with -Inf (Σd NaN, no NaN value) must not; a NaN
+    on a row the `where` filter drops must not either."""
+    n = 300_000
+    rng = np.random.default_rng(11)
+    base = rng.uniform(-1e3, 1e3, n).astype(np.float32 if ftype == "float32" else np.float64)
+    g = np.ones(n, dtype=np.int64)
+
+    def run(vals, gs, where=None):
+        pt = product_table({"f": [ftype, [float(v) for v in vals]], "g": ["int64", gs.tolist()]})
+        return d.run_scan([d.Minimum("f", where), d.Maximum("f", where), d.Sum("f", where)], pt), where
+
+    v = base.copy()
+    v[123_457] = np.nan
+    st, w = run(v, g)
+    assert math.isnan(st[d.Maximum("f", w)].maxValue)
+    assert st[d.Minimum("f", w)].minValue == float(np.nanmin(v))
+    assert math.isnan(st[d.Sum("f", w)].sum_value)
+
+    v = base.copy()
+    v[200_001], v[200_002] = np.inf, -np.inf  # same lane, same iteration
+    st, w = run(v, g)
+    assert st[d.Maximum("f", w)].maxValue == math.inf
+    assert st[d.Minimum("f", w)].minValue == -math.inf
+    assert math.isnan(st[d.Sum("f", w)].sum_value)
+
+    v = base.copy()
+    v[77_777] = np.nan
+    gs = g.copy()
+    gs[77_777] = 0
+    st, w = run(v, gs, "g > 0")
+    keep = np.arange(n) != 77_777
+    assert st[d.Maximum("f", w)].maxValue == float(v[keep].max())
+    assert st[d.Minimum("f", w)].minValue == float(v[keep].min())
+    assert not math.isnan(st[d.Sum("f", w)].sum_value)
+
+
 def test_int64_extremes_and_wraparound(gpu):
     big = [2 ** 63 - 1, 2 ** 63 - 1, -(2 ** 63), 5, None]
     pt = product_table({"x": ["int64", big]})

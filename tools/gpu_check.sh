@@ -33,7 +33,7 @@ if [[ $STEPS == *bench* ]]; then
 fi
 if [[ $STEPS == *prof* ]]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv \
-    -- python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_$TAG.log" 2>&1
+    -- python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-side-passes > "$OUT/prof_$TAG.log" 2>&1
   st=$?; tail -3 "$OUT/prof_$TAG.log"; ok_or_stop $st prof
   find "$OUT/prof_$TAG" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats_$TAG.csv" \; 2>/dev/null
   head -20 "$OUT/kernel_stats_$TAG.csv" 2>/dev/null

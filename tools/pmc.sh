@@ -10,7 +10,7 @@ TAG=${TAG:-r01}
 ROWS=${ROWS:-1000000000}
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_${C}_$TAG" -o run \
-    -- python -u bench.py --steps 2 --warmup 1 --rows $ROWS --no-cpu-baseline > "$OUT/pmc_${C}_$TAG.log" 2>&1
+    -- python -u bench.py --steps 2 --warmup 1 --rows $ROWS --no-cpu-baseline --no-side-passes > "$OUT/pmc_${C}_$TAG.log" 2>&1
   st=$?
   if [ $st -ne 0 ]; then echo "STOP: pmc $C exit $st"; tail -5 "$OUT/pmc_${C}_$TAG.log"; exit $st; fi
 done

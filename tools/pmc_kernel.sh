@@ -14,7 +14,7 @@ for G in "${GROUPS_[@]}"; do
   C=$(echo "$G" | tr ',' ' ')
   D="$OUT/pmck_${WL}_${TAG}_$k"
   timeout -s KILL ${TL:-180} rocprofv3 --pmc $C --output-format csv -d "$D" -o run \
-    -- python -u bench.py --workload $WL --steps 1 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$D.log" 2>&1
+    -- python -u bench.py --workload $WL --steps 1 --warmup 1 --no-cpu-baseline --no-side-passes ${BENCH_ARGS:-} > "$D.log" 2>&1
   st=$?
   if [ $st -ne 0 ]; then echo "STOP: pmc pass '$G' exit $st"; tail -5 "$D.log"; exit $st; fi
   k=$((k + 1))
