@@ -76,6 +76,50 @@ __device__ int classify_utf8(const Src& p, int32_t n) {
   return DT_STRING;
 }
 
+// The same classification, 8 bytes at a time, for strings of <= 24 bytes (the word-loaded
+// form).  The DFA above accepts: an optional sign, then an optional single space, then a body of
+// digits and '.' -- no '.' is Integral, exactly one is Fractional, anything else fails.  So the
+// prefix is located from the first two bytes, and the body is tested with per-byte SWAR flags
+// (bit 7 of each byte): non-digit, '.', and "inside [pos, n)".  No per-byte loop, no branches
+// per byte.
+__device__ inline uint64_t swar_nondigit(uint64_t x) {  // bit 7 set iff the byte is not '0'..'9'
+  const uint64_t t = x ^ 0x3030303030303030ull;
+  return (((t & 0x7f7f7f7f7f7f7f7full) + 0x7676767676767676ull) | t) & 0x8080808080808080ull;
+}
+__device__ inline uint64_t swar_is(uint64_t x, uint64_t rep) {  // bit 7 set iff the byte == rep's
+  const uint64_t t = x ^ rep;
+  return ~((((t & 0x7f7f7f7f7f7f7f7full) + 0x7f7f7f7f7f7f7f7full) | t)) & 0x8080808080808080ull;
+}
+__device__ inline uint64_t swar_bytes_below(int32_t m) {  // bytes [0, m) of a word (bit 7 flags)
+  const uint64_t all = 0x8080808080808080ull;
+  return m <= 0 ? 0ull : m >= 8 ? all : (all & ((1ull << (8 * m)) - 1ull));
+}
+
+__device__ int classify_utf8_words(const WordSrc& ws, int32_t n) {
+  const uint32_t sh = ws.sh * 8u;
+  // the string's bytes 8k..8k+7 as one word (funnel shift of the aligned words)
+  const uint64_t s0 = sh ? (ws.w0 >> sh) | (ws.w1 << (64u - sh)) : ws.w0;
+  const uint64_t s1 = sh ? (ws.w1 >> sh) | (ws.w2 << (64u - sh)) : ws.w1;
+  const uint64_t s2 = sh ? (ws.w2 >> sh) | (ws.w3 << (64u - sh)) : ws.w2;
+  const uint32_t b0 = (uint32_t)s0 & 0xffu;
+  int32_t pos = (n > 0 && (b0 == '+' || b0 == '-')) ? 1 : 0;
+  if (pos < n && (((uint32_t)(s0 >> (8 * pos))) & 0xffu) == ' ') ++pos;
+  uint64_t bad = 0;
+  int dots = 0;
+  const uint64_t words[3] = {s0, s1, s2};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const uint64_t in = swar_bytes_below(n - 8 * k) & ~swar_bytes_below(pos - 8 * k);
+    const uint64_t dot = swar_is(words[k], 0x2e2e2e2e2e2e2e2eull) & in;
+    bad |= swar_nondigit(words[k]) & in & ~dot;
+    dots += __builtin_popcountll(dot);
+  }
+  if (bad == 0 && dots <= 1) return dots ? DT_FRACTIONAL : DT_INTEGRAL;
+  if (n == 4 && (uint32_t)s0 == 0x65757274u) return DT_BOOLEAN;                       // "true"
+  if (n == 5 && (s0 & 0xffffffffffull) == 0x65736c6166ull) return DT_BOOLEAN;          // "false"
+  return DT_STRING;
+}
+
 template <typename F>
 __device__ inline int classify_float(F x) {
   // Double.toString / Float.toString: plain notation for 1e-3 <= |x| < 1e7 (and 0)
@@ -90,7 +134,7 @@ __device__ int classify_row(const DevColumn& c, int64_t row) {
     case DQ_T_UTF8: {
       const int32_t b = c.offsets[row], e = c.offsets[row + 1];
       const uint8_t* p = static_cast<const uint8_t*>(c.values) + b;
-      return e - b <= 24 ? classify_utf8(WordSrc(p, e - b), e - b) : classify_utf8(PtrSrc{p}, e - b);
+      return e - b <= 24 ? classify_utf8_words(WordSrc(p, e - b), e - b) : classify_utf8(PtrSrc{p}, e - b);
     }
     case DQ_T_BOOL: return DT_BOOLEAN;
     case DQ_T_FLOAT32: return classify_float(static_cast<const float*>(c.values)[row]);

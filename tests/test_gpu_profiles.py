@@ -75,6 +75,21 @@ def test_datatype_random_strings_match_oracle(gpu, n):
         assert got.counts() == O.datatype_state(ot, "s", where), where
 
 
+def test_datatype_numeric_looking_strings_match_oracle(gpu):
+    """Digit-heavy strings of 0..30 bytes: the word-at-a-time classifier (<= 24 bytes) and the
+    byte DFA (longer) against the oracle's regexes, prefixes and '.' counts included."""
+    rng = np.random.default_rng(29)
+    toks = ["0", "5", "9", "12", "345", ".", "-", "+", " ", "e", "true", "false"]
+    vals = []
+    for _ in range(30000):
+        s = "".join(toks[int(rng.integers(0, len(toks) if rng.random() < 0.2 else 6))]
+                    for _ in range(int(rng.integers(0, 16))))
+        vals.append(None if rng.random() < 0.05 else s[:int(rng.integers(0, 31))])
+    spec = {"s": ["string", vals]}
+    table, ot = product_table(spec), oracle_table(spec)
+    assert d.DataType("s").computeStateFrom(table).counts() == O.datatype_state(ot, "s")
+
+
 def test_datatype_numeric_columns_match_oracle(gpu):
     rng = np.random.default_rng(3)
     n = 5000

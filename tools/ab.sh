@@ -1,5 +1,8 @@
 #!/bin/bash
 # A/B: the same bench with two builds of the library, alternated, in one box session.
+# Baseline build (untracked; .so files travel with gpurun):
+#   git archive <rev> deequ_amd/csrc include | tar -x -C /tmp/old && make -C /tmp/old/deequ_amd/csrc
+#   mkdir -p gpurun_ab && cp /tmp/old/deequ_amd/libdeequ_amd.so gpurun_ab/lib_old.so
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
