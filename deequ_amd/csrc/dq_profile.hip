@@ -35,6 +35,8 @@ struct PtrSrc {
 struct WordSrc {
   uint64_t w0, w1, w2, w3;
   uint32_t sh;
+  __device__ WordSrc(uint64_t a, uint64_t b, uint64_t c, uint64_t d, uint32_t s)
+      : w0(a), w1(b), w2(c), w3(d), sh(s) {}  // words already loaded (bytes past the string: any)
   __device__ WordSrc(const uint8_t* p, int32_t n) {
     const uintptr_t a = (uintptr_t)p;
     const uint64_t* w = reinterpret_cast<const uint64_t*>(a & ~(uintptr_t)7);
@@ -97,22 +99,30 @@ __device__ inline uint64_t swar_bytes_below(int32_t m) {  // bytes [0, m) of a w
 
 __device__ int classify_utf8_words(const WordSrc& ws, int32_t n) {
   const uint32_t sh = ws.sh * 8u;
-  // the string's bytes 8k..8k+7 as one word (funnel shift of the aligned words)
+  // the string's bytes 8k..8k+7 as one word (funnel shift of the aligned words); words past the
+  // string's length are not formed (a branch uniform across a column of similar lengths)
   const uint64_t s0 = sh ? (ws.w0 >> sh) | (ws.w1 << (64u - sh)) : ws.w0;
-  const uint64_t s1 = sh ? (ws.w1 >> sh) | (ws.w2 << (64u - sh)) : ws.w1;
-  const uint64_t s2 = sh ? (ws.w2 >> sh) | (ws.w3 << (64u - sh)) : ws.w2;
   const uint32_t b0 = (uint32_t)s0 & 0xffu;
   int32_t pos = (n > 0 && (b0 == '+' || b0 == '-')) ? 1 : 0;
   if (pos < n && (((uint32_t)(s0 >> (8 * pos))) & 0xffu) == ' ') ++pos;
-  uint64_t bad = 0;
-  int dots = 0;
-  const uint64_t words[3] = {s0, s1, s2};
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const uint64_t in = swar_bytes_below(n - 8 * k) & ~swar_bytes_below(pos - 8 * k);
-    const uint64_t dot = swar_is(words[k], 0x2e2e2e2e2e2e2e2eull) & in;
-    bad |= swar_nondigit(words[k]) & in & ~dot;
+  // word 0: bytes [pos, n); later words: bytes below n only (pos <= 2)
+  uint64_t in = swar_bytes_below(n) & ~swar_bytes_below(pos);
+  uint64_t dot = swar_is(s0, 0x2e2e2e2e2e2e2e2eull) & in;
+  uint64_t bad = swar_nondigit(s0) & in & ~dot;
+  int dots = __builtin_popcountll(dot);
+  if (n > 8 && bad == 0) {  // (a failed first word decides: String or Boolean from word 0)
+    const uint64_t s1 = sh ? (ws.w1 >> sh) | (ws.w2 << (64u - sh)) : ws.w1;
+    in = swar_bytes_below(n - 8);
+    dot = swar_is(s1, 0x2e2e2e2e2e2e2e2eull) & in;
+    bad |= swar_nondigit(s1) & in & ~dot;
     dots += __builtin_popcountll(dot);
+    if (n > 16) {
+      const uint64_t s2 = sh ? (ws.w2 >> sh) | (ws.w3 << (64u - sh)) : ws.w2;
+      in = swar_bytes_below(n - 16);
+      dot = swar_is(s2, 0x2e2e2e2e2e2e2e2eull) & in;
+      bad |= swar_nondigit(s2) & in & ~dot;
+      dots += __builtin_popcountll(dot);
+    }
   }
   if (bad == 0 && dots <= 1) return dots ? DT_FRACTIONAL : DT_INTEGRAL;
   if (n == 4 && (uint32_t)s0 == 0x65757274u) return DT_BOOLEAN;                       // "true"
@@ -164,6 +174,54 @@ __global__ __launch_bounds__(kBlock) void dq_datatype_kernel(const HllTask* __re
   const int64_t r0 = (int64_t)blockIdx.x * per_block;
   const int64_t r1 = min(r0 + per_block, n_rows);
   uint64_t c[5] = {0, 0, 0, 0, 0};
+  if (col.type == DQ_T_UTF8) {  // uniform
+    // U rows per lane per step, every load of the step issued before any classification: the
+    // string words come through a buffer descriptor over the (8-byte aligned) value bytes, so the
+    // four word loads per row are unconditional (out of range reads 0) and overlap across rows.
+    constexpr int U = 4;
+    const uint8_t* vals = static_cast<const uint8_t*>(col.values);
+    const uintptr_t al = (uintptr_t)vals & ~(uintptr_t)7;
+    const uint32_t delta = (uint32_t)((uintptr_t)vals - al);
+    const uint32_t span = (delta + (uint32_t)col.offsets[n_rows] + 7u) & ~7u;  // the last valid byte's word
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(al), 0, (int)span, 0x00020000);
+    for (int64_t base = r0 + threadIdx.x; base < r1; base += U * kBlock) {
+      int32_t ob[U], oe[U];
+      bool sel[U];
+      uint64_t w[U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t row = base + (int64_t)u * kBlock;
+        const bool in = row < r1;
+        const int64_t rr = in ? row : r0;
+        ob[u] = col.offsets[rr];
+        oe[u] = col.offsets[rr + 1];
+        sel[u] = in && (col.validity == nullptr || bit_at(col.validity, rr)) && (wt == nullptr || bit_at(wt, rr));
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t a = (delta + (uint32_t)ob[u]) & ~7u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(a + 8u * k), 0, 0);
+          w[u][k] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t row = base + (int64_t)u * kBlock;
+        if (row >= r1) break;
+        const int32_t n = oe[u] - ob[u];
+        int k = DT_NULL;
+        if (sel[u]) {
+          k = n <= 24 ? classify_utf8_words(WordSrc(w[u][0], w[u][1], w[u][2], w[u][3], (delta + (uint32_t)ob[u]) & 7u), n)
+                      : classify_utf8(PtrSrc{vals + ob[u]}, n);
+        }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) c[i] += (k == i) ? 1u : 0u;
+      }
+    }
+  } else
   for (int64_t row = r0 + threadIdx.x; row < r1; row += kBlock) {
     // conditionalSelection: a row whose filter is not TRUE is a NULL input (Analyzer.scala:409-420)
     const bool valid = (col.validity == nullptr || bit_at(col.validity, row)) && (wt == nullptr || bit_at(wt, row));
