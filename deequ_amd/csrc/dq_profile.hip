@@ -372,6 +372,55 @@ __device__ int parse_double(const Src& p, int32_t n, double* out) {
   return 1;
 }
 
+// 8 ASCII digits (first digit in the low byte) -> their value: pairs, quads, then the 8-digit
+// number, three multiply-adds on the whole word.
+__device__ inline uint64_t swar_digits8(uint64_t x) {
+  x -= 0x3030303030303030ull;
+  x = (x * 10u + (x >> 8)) & 0x00ff00ff00ff00ffull;
+  x = (x * 100u + (x >> 16)) & 0x0000ffff0000ffffull;
+  return (x * 10000u + (x >> 32)) & 0xffffffffull;
+}
+
+// parse_long on the word-loaded form, with a fast path for the common shape: an optional sign
+// and 1..16 digits (no '.', so no overflow is possible).  The digits are right-aligned in a
+// 16-byte window padded with '0' and converted 8 at a time; anything else takes parse_long.
+__device__ bool parse_long_words(const WordSrc& ws, int32_t n, int64_t* out) {
+  if (n >= 1 && n <= 17) {
+    const uint32_t sh = ws.sh * 8u;
+    const uint64_t s0 = sh ? (ws.w0 >> sh) | (ws.w1 << (64u - sh)) : ws.w0;
+    const uint64_t s1 = sh ? (ws.w1 >> sh) | (ws.w2 << (64u - sh)) : ws.w1;
+    const uint64_t s2 = sh ? (ws.w2 >> sh) | (ws.w3 << (64u - sh)) : ws.w2;
+    const uint32_t b0 = (uint32_t)s0 & 0xffu;
+    const bool neg = b0 == '-';
+    const int32_t start = (neg || b0 == '+') ? 1 : 0;
+    const int32_t nd = n - start;
+    if (nd >= 1 && nd <= 16) {
+      const unsigned __int128 raw =
+          start ? (((unsigned __int128)s2 << 120) | ((unsigned __int128)s1 << 56) | (unsigned __int128)(s0 >> 8))
+                : (((unsigned __int128)s1 << 64) | (unsigned __int128)s0);
+      const uint32_t pad = 8u * (uint32_t)(16 - nd);  // bits of '0' fill below the digits
+      const unsigned __int128 zeros = ((unsigned __int128)0x3030303030303030ull << 64) | 0x3030303030303030ull;
+      const unsigned __int128 fill = pad ? (zeros & ((((unsigned __int128)1) << pad) - 1)) : 0;
+      const unsigned __int128 v = (raw << pad) | fill;
+      const uint64_t lo = (uint64_t)v, hi = (uint64_t)(v >> 64);
+      if ((swar_nondigit(lo) | swar_nondigit(hi)) == 0) {
+        const int64_t r = (int64_t)(swar_digits8(lo) * 100000000ull + swar_digits8(hi));
+        *out = neg ? -r : r;
+        return true;
+      }
+    }
+  }
+  return parse_long(ws, n, out);
+}
+
+__device__ inline bool cast_one(const WordSrc& p, int32_t n, int to_type, int64_t* lv, double* dv,
+                                uint32_t* unsup) {
+  if (to_type == DQ_T_INT64) return parse_long_words(p, n, lv);
+  const int r = parse_double(p, n, dv);
+  *unsup += r == 2;
+  return r == 1;
+}
+
 template <typename Src>
 __device__ inline bool cast_one(const Src& p, int32_t n, int to_type, int64_t* lv, double* dv, uint32_t* unsup) {
   if (to_type == DQ_T_INT64) return parse_long(p, n, lv);

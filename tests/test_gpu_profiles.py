@@ -163,6 +163,21 @@ def test_cast_to_long_matches_spark(gpu):
     assert got == [None if v is None else _spark_to_long(v) for v in vals]
 
 
+def test_cast_to_long_random_digit_strings(gpu):
+    """The word-at-a-time path (sign + 1..16 digits) and its fall-backs (longer, '.', junk)."""
+    rng = np.random.default_rng(41)
+    alpha = "0123456789" * 8 + "-+. a"
+    vals = []
+    for _ in range(20000):
+        s = "".join(alpha[int(rng.integers(0, len(alpha)))] for _ in range(int(rng.integers(0, 21))))
+        if s and rng.random() < 0.3:
+            s = "-+"[int(rng.integers(0, 2))] + s[1:]
+        vals.append(s)
+    col = d.Column.from_pylist(vals, "string")
+    got = cast_string_column(col, "int64").to_pylist()
+    assert got == [_spark_to_long(v) for v in vals]
+
+
 def test_cast_to_double_matches_java(gpu):
     rng = np.random.default_rng(9)
     vals = ["1.5", "-0.25", ".5", "5.", ".", "-.", "", "  2.0  ", "- 1.5", "+3", "1e3", "1E-3", "2.5f", "7d",
