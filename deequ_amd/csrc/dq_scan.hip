@@ -19,8 +19,10 @@
 //   n_sel          : Σ valid ∧ where-TRUE              (Completeness numerator, Mean count, n)
 //   isum           : wrapping int64 sum (Spark Sum over integral types is LongType)
 //   fs + fc        : Neumaier-compensated fp64 sum     (Spark: sequential fp64 sum)
-//   imin/imax, fmin/fmax/nnan : Spark NaN-safe min/max (NaN is the largest double); nnan > 0
-//                    iff a selected value is NaN, fmin > fmax iff every selected value is NaN
+//   fmin/fmax/nnan : Spark NaN-safe min/max (NaN is the largest double) of (double)x for every
+//                    column type (integral min/max commute with the monotone cast); nnan > 0 iff
+//                    a selected value is NaN, fmin > fmax iff every selected value is NaN.
+//                    (imin/imax stay in the partial layout, unused by the value scan)
 //   mean, m2       : moments about the mean, from per-lane shifted sums then Chan merges
 //                    with the exact formula of StandardDeviationState.sum
 //                    (StandardDeviation.scala:37-44); no per-element fp64 divide
