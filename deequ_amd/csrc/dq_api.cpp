@@ -497,6 +497,43 @@ static int fast_form(const Program& prog, const int32_t* types, FastPred* fp) {
   return -1;
 }
 
+// The specialised 8-byte value scan (dq_scan_fast.hip) runs a task with no `where`, on an
+// int64 / fp64 column, with at most one inline `column CMP literal` predicate.  Its compare is
+// `x < lit` or `x == lit` (CS_INV negates), so the task's predicate is rewritten here:
+// x <= l -> x < l + 1 (int64) / x < nextafter(l, +inf) (fp64).  Returns false (general kernel)
+// for every other shape.
+static bool fast_variant(ScanTask* t, int* variant) {
+  if (t->ptype != DQ_T_INT64 && t->ptype != DQ_T_FLOAT64) return false;
+  if (t->n_preds > 1) return false;
+  int v = 0;
+  if (t->n_preds == 1) {
+    FastPred fp = t->preds[0];
+    if (fp.kind != FP_CMP) return false;
+    const uint32_t cs = fp.cmp_sel & 3u;
+    if (cs == CS_MASKS) return false;
+    const bool f64 = fp.as_f64 || t->ptype == DQ_T_FLOAT64;
+    if (!f64 && t->ptype != DQ_T_INT64) return false;
+    if (cs == CS_LE) {
+      if (f64) {
+        if (!(fp.lit_f < HUGE_VAL)) return false;  // +inf (or NaN): general kernel
+        fp.lit_f = std::nextafter(fp.lit_f, HUGE_VAL);
+      } else {
+        if (fp.lit_i == INT64_MAX) return false;
+        fp.lit_i += 1;
+      }
+      fp.cmp_sel = (fp.cmp_sel & CS_INV) | CS_LT;
+    }
+    if (f64 && !fp.as_f64) fp.lit_f = (double)fp.lit_i;  // (fp columns: literals are compared as fp)
+    const bool lt = (fp.cmp_sel & 3u) == CS_LT;
+    v = f64 ? (lt ? 3 : 4) : (lt ? 1 : 2);
+    t->preds[0] = fp;
+  }
+  if (t->flags & TF_STATS) v |= FAST_STATS;
+  if (t->flags & TF_HLL) v |= FAST_HLL;
+  *variant = v;
+  return true;
+}
+
 // ------------------------------------------------------------------------------ plan
 enum Target { TGT_HOST_SIZE = 0, TGT_SCAN = 1, TGT_HLL = 2, TGT_DTYPE = 3, TGT_STRLEN = 4, TGT_CORR = 5 };
 
@@ -516,7 +553,7 @@ struct TaskBuild {
 
 // Scan tasks launched by one kernel specialisation (see launch_scan_group).
 struct ScanGroup {
-  int kind;   // 0 = validity/mask only, 1 = reads values
+  int kind;   // 0 = validity/mask only, 1 = reads values, 2 = the specialised 8-byte value scan
   int ptype;  // value type (kind 1)
   int np;     // inline predicates (kind 1)
   std::vector<int32_t> tasks;
@@ -798,14 +835,21 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
   for (auto& tb : tasks) plan->scan_tasks.push_back(tb.t);
   // group tasks by kernel specialisation: (needs values, value type, #inline predicates)
   std::vector<int32_t> group_ids;
+  const char* fast_env = std::getenv("DQ_SCAN_FAST");
+  const bool fast_on = !(fast_env && fast_env[0] == '0');
   for (size_t i = 0; i < plan->scan_tasks.size(); ++i) {
-    const ScanTask& t = plan->scan_tasks[i];
-    const int kind = (t.flags & TF_VALUES) ? 1 : 0;
+    ScanTask& t = plan->scan_tasks[i];
+    int kind = (t.flags & TF_VALUES) ? 1 : 0;
     const int ptype = kind ? t.ptype : 0;
     bool ext = (t.flags & TF_WHERE) != 0;
     for (int p = 0; p < t.n_preds; ++p) ext = ext || t.preds[p].kind == FP_MASK;
     // np = exact inline-predicate count of a plain task, -1 = the EXT kernel (where/masks)
-    const int np = kind ? (ext ? -1 : (t.n_preds <= 4 ? t.n_preds : kMaxPreds)) : 0;
+    int np = kind ? (ext ? -1 : (t.n_preds <= 4 ? t.n_preds : kMaxPreds)) : 0;
+    int variant = -1;
+    if (fast_on && kind == 1 && !ext && fast_variant(&t, &variant)) {
+      kind = 2;  // dq_scan_fast_kernel; np carries the variant
+      np = variant;
+    }
     ScanGroup* g = nullptr;
     for (auto& gg : plan->groups)
       if (gg.kind == kind && gg.ptype == ptype && gg.np == np) g = &gg;
@@ -1074,8 +1118,11 @@ extern "C" dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, in
       if (plan->group_per_cu.size() != plan->groups.size()) {  // once per plan
         plan->group_per_cu.resize(plan->groups.size());
         for (size_t q = 0; q < plan->groups.size(); ++q)
-          plan->group_per_cu[q] = plan->groups[q].kind == 0 ? 0 : scan_group_blocks_per_cu(
-              plan->groups[q].kind, plan->groups[q].ptype, plan->groups[q].np);
+          plan->group_per_cu[q] = plan->groups[q].kind == 0 ? 0
+                                  : plan->groups[q].kind == 2
+                                      ? scan_fast_blocks_per_cu(plan->groups[q].ptype, plan->groups[q].np)
+                                      : scan_group_blocks_per_cu(plan->groups[q].kind, plan->groups[q].ptype,
+                                                                 plan->groups[q].np);
       }
       const int per_cu = plan->group_per_cu[g];
       if (per_cu > 0) bpt = std::max<int64_t>(1, (int64_t)plan->n_cu * per_cu * plan->scan_rounds / ng);
@@ -1114,9 +1161,14 @@ extern "C" dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, in
     const int32_t* d_groups = static_cast<const int32_t*>(plan->d_groups.ptr);
     for (size_t g = 0; g < plan->groups.size(); ++g) {
       const ScanGroup& G = plan->groups[g];
-      DQ_HIP(launch_scan_group(G.kind, G.ptype, G.np, d_tasks, d_groups + G.dev_offset, (int)G.tasks.size(),
-                               d_cols, d_masks, n_rows, (int)group_bpt[g], parts + group_base[g],
-                               static_cast<uint32_t*>(plan->d_regs.ptr), plan->stream));
+      if (G.kind == 2)
+        DQ_HIP(launch_scan_fast(G.ptype, G.np, d_tasks, d_groups + G.dev_offset, (int)G.tasks.size(), d_cols, n_rows,
+                                (int)group_bpt[g], parts + group_base[g], static_cast<uint32_t*>(plan->d_regs.ptr),
+                                plan->stream));
+      else
+        DQ_HIP(launch_scan_group(G.kind, G.ptype, G.np, d_tasks, d_groups + G.dev_offset, (int)G.tasks.size(),
+                                 d_cols, d_masks, n_rows, (int)group_bpt[g], parts + group_base[g],
+                                 static_cast<uint32_t*>(plan->d_regs.ptr), plan->stream));
     }
     DQ_HIP(launch_scan_reduce(parts, static_cast<const PartRange*>(plan->d_ranges.ptr), n_scan,
                               static_cast<ScanAcc*>(plan->d_acc.ptr), plan->stream));

@@ -248,6 +248,15 @@ hipError_t launch_scan_group(int kind, int ptype, int np, const ScanTask* d_task
                              const int32_t* d_group, int n_group, const DevColumn* d_cols,
                              const DevMask* d_masks, int64_t n_rows, int blocks_per_task,
                              ScanAcc* d_partials, uint32_t* d_hll_regs, hipStream_t stream);
+// The specialised 8-byte value scan (dq_scan_fast.hip): `variant` = predicate form (low 3 bits:
+// 0 none, 1 int64 `<`, 2 int64 `==`, 3 fp64 `<`, 4 fp64 `==`; CS_INV of the task's predicate
+// negates it) | FAST_STATS | FAST_HLL.
+constexpr int FAST_STATS = 8;
+constexpr int FAST_HLL = 16;
+hipError_t launch_scan_fast(int ptype, int variant, const ScanTask* d_tasks, const int32_t* d_group, int n_group,
+                            const DevColumn* d_cols, int64_t n_rows, int blocks_per_task, ScanAcc* d_partials,
+                            uint32_t* d_hll_regs, hipStream_t stream);
+int scan_fast_blocks_per_cu(int ptype, int variant);  // 0 = unknown
 hipError_t launch_diag_hash(int blocks, int iters, bool with_hll, uint64_t* sink, hipStream_t s);
 int scan_group_blocks_per_cu(int kind, int ptype, int np);  // 0 = unknown
 hipError_t launch_scan_reduce(const ScanAcc* d_partials, const PartRange* d_ranges, int n_tasks,
