@@ -26,6 +26,7 @@ DQ_COL_DEVICE = 0x1
  DQ_OP_MAX_LENGTH, DQ_OP_CORRELATION) = range(1, 14)
 
 DQ_P_COLUMN, DQ_P_LIT_INT, DQ_P_LIT_FLOAT, DQ_P_LIT_NULL, DQ_P_COALESCE, DQ_P_LIT_STRING = 1, 2, 3, 4, 5, 6
+DQ_P_CAST_DOUBLE = 7
 DQ_P_EQ, DQ_P_NE, DQ_P_LT, DQ_P_LE, DQ_P_GT, DQ_P_GE, DQ_P_EQ_NULLSAFE = 10, 11, 12, 13, 14, 15, 16
 DQ_P_IS_NULL, DQ_P_IS_NOT_NULL = 20, 21
 DQ_P_AND, DQ_P_OR, DQ_P_NOT, DQ_P_TRUE, DQ_P_FALSE = 30, 31, 32, 33, 34
@@ -100,6 +101,7 @@ SIGNATURES = {
     "dq_plan_consume": (c_int, [c_void_p, POINTER(DqColumn), c_int, c_int64]),
     "dq_plan_finish": (c_int, [c_void_p, POINTER(DqState), c_int]),
     "dq_plan_reset": (c_int, [c_void_p]),
+    "dq_plan_op_status": (c_int, [c_void_p, c_int]),
     "dq_plan_stream": (c_void_p, [c_void_p]),
     "dq_state_merge": (c_int, [POINTER(DqState), POINTER(DqState), POINTER(DqState)]),
     "dq_state_metric": (c_int, [POINTER(DqState), POINTER(c_double)]),

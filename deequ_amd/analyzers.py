@@ -123,10 +123,34 @@ class Analyzer:
 
 
 class ScanShareableAnalyzer(Analyzer):
-    """Runs in the single fused pass; one dq_op per analyzer."""
+    """Runs in the single fused pass; one dq_op per analyzer (ScanShareableAnalyzer,
+    Analyzer.scala:169-197).  The two hooks mirror the reference's seam so a subclass can
+    override them exactly as AnalysisTest.scala:206-280 does:
+
+    * aggregationFunctions(schema) -> the dq_op this analyzer contributes to the plan (the
+      reference's Seq[Column]); an exception here fails every shareable analyzer of the run
+      (AnalysisRunner.scala:305-323);
+    * fromAggregationResult(raw) -> the State from this analyzer's POD dq_state (the reference
+      reads its Row slice at `offset`); an exception here fails this analyzer only (:340-353).
+    """
 
     DQ_KIND = 0
     where: Optional[str] = None
+
+    def aggregationFunctions(self, schema):
+        from .engine import op_spec_for
+        return op_spec_for(self, schema)
+
+    def fromAggregationResult(self, raw) -> Optional[State]:
+        from .engine import OpUnsupported
+        from .states import state_from_dq
+        if isinstance(raw, OpUnsupported):
+            raise raw.error
+        return state_from_dq(raw)
+
+    def metricFromAggregationResult(self, raw, aggregateWith=None, saveStatesWith=None):
+        """Analyzer.metricFromAggregationResult (Analyzer.scala:185-195)."""
+        return self.calculateMetric(self.fromAggregationResult(raw), aggregateWith, saveStatesWith)
 
     def computeStateFrom(self, data) -> Optional[State]:
         from .engine import run_scan

@@ -309,6 +309,11 @@ static dq_status validate_predicate(const dq_predicate& p, const int32_t* types,
       case DQ_P_LIT_INT: st.push_back(V_INT); break;
       case DQ_P_LIT_FLOAT: st.push_back(V_FLT); break;
       case DQ_P_LIT_NULL: st.push_back(V_INT); break;
+      case DQ_P_CAST_DOUBLE:  // Cast(-> DoubleType) of a string or a number
+        if (st.empty()) return fail(DQ_ERR_INVALID, "predicate stack underflow");
+        if (st.back() == V_BOOL) return fail(DQ_ERR_UNSUPPORTED, "cast of a boolean to double");
+        st.back() = V_FLT;
+        break;
       case DQ_P_TRUE: case DQ_P_FALSE: st.push_back(V_BOOL); break;
       case DQ_P_COALESCE: {
         if (st.size() < 2) return fail(DQ_ERR_INVALID, "predicate stack underflow");
@@ -543,6 +548,8 @@ struct OpSlot {
   int task;
   int pred;        // COMPLIANCE: predicate slot within the task
   bool has_where;
+  int prog_pred = -1;   // generic predicate program evaluating this op's predicate (mask form)
+  int prog_where = -1;  // ... and its `where` filter
 };
 
 struct TaskBuild {
@@ -584,6 +591,8 @@ struct dq_plan : Stager {
   std::vector<CorrTask> corr_tasks;  // Correlation: {x, y, where}
   std::vector<Program> programs;  // generic predicate programs -> batch masks
   // device state
+  DevBuf d_unsup;  // per generic program: a row hit DQ_P_CAST_DOUBLE off its exact fast path
+  std::vector<dq_status> op_status;  // per op, after dq_plan_finish
   DevBuf d_tasks, d_groups, d_ranges, d_hll, d_progs, d_insns, d_pool, d_acc, d_partials, d_regs,
       d_cols, d_masks, d_mask_words, d_dtype, d_dtype_counts, d_len, d_len_out, d_corr, d_corr_part, d_corr_acc;
   int64_t mask_words = 0;
@@ -700,6 +709,7 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
       for (int c : wp.columns) plan->col_used[c] = true;
       where_prog = add_program(plan, std::move(wp));
       slot.has_where = true;
+      slot.prog_where = where_prog;
     }
     switch (op.kind) {
       case DQ_OP_SIZE: {
@@ -742,6 +752,7 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
           const int prog = add_program(plan, std::move(pp));
           fp.kind = FP_MASK;
           fp.mask = prog;
+          slot.prog_pred = prog;
           t = -1;  // prefer an existing task with the same filter: masks need no values
           for (size_t k = 0; k < tasks.size(); ++k)
             if (tasks[k].where_prog == where_prog && tasks[k].t.n_preds < kMaxPreds) t = (int)k;
@@ -897,6 +908,7 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
       (s = upload(plan->d_progs, progs.data(), progs.size() * sizeof(PredProgram))) != DQ_OK ||
       (s = upload(plan->d_insns, insns.data(), insns.size() * sizeof(PredInsn))) != DQ_OK ||
       (s = upload(plan->d_pool, pool.data(), pool.size())) != DQ_OK ||
+      (s = plan->d_unsup.ensure(std::max<size_t>(1, plan->programs.size()) * sizeof(uint32_t))) != DQ_OK ||
       (s = plan->d_acc.ensure(std::max<size_t>(1, plan->scan_tasks.size()) * sizeof(ScanAcc))) != DQ_OK ||
       (s = plan->d_regs.ensure(std::max<size_t>(1, plan->hll_sets.size()) * kHllM * sizeof(uint32_t))) != DQ_OK ||
       (s = plan->d_cols.ensure(std::max(1, n_columns) * sizeof(DevColumn))) != DQ_OK ||
@@ -939,10 +951,22 @@ extern "C" dq_status dq_plan_destroy(dq_plan* plan) {
 
 extern "C" void* dq_plan_stream(dq_plan* plan) { return plan ? (void*)plan->stream : nullptr; }
 
+extern "C" dq_status dq_plan_op_status(dq_plan* plan, int op) {
+  if (!plan) return fail(DQ_ERR_INVALID, "plan is NULL");
+  if (op < 0 || op >= (int)plan->slots.size()) return fail(DQ_ERR_INVALID, "op index out of range");
+  if (plan->op_status.size() != plan->slots.size()) return fail(DQ_ERR_STATE, "dq_plan_finish has not run");
+  if (plan->op_status[op] != DQ_OK)
+    return fail(plan->op_status[op], "a string -> double cast in this op's predicate met a number off the exact "
+                                     "fast path (> 19 significant digits, |exponent| > 22 or hex): route it to Spark");
+  return DQ_OK;
+}
+
 extern "C" dq_status dq_plan_reset(dq_plan* plan) {
   if (!plan) return fail(DQ_ERR_INVALID, "plan is NULL");
   DQ_HIP(hipSetDevice(plan->ctx->device));
   DQ_HIP(launch_init_acc(static_cast<ScanAcc*>(plan->d_acc.ptr), (int)plan->scan_tasks.size(), plan->stream));
+  DQ_HIP(hipMemsetAsync(plan->d_unsup.ptr, 0, std::max<size_t>(1, plan->programs.size()) * sizeof(uint32_t),
+                        plan->stream));
   if (!plan->hll_sets.empty())
     DQ_HIP(hipMemsetAsync(plan->d_regs.ptr, 0, plan->hll_sets.size() * kHllM * sizeof(uint32_t), plan->stream));
   if (!plan->dtype_tasks.empty())
@@ -1153,7 +1177,8 @@ extern "C" dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, in
     DQ_HIP(launch_predicates(static_cast<const PredProgram*>(plan->d_progs.ptr), n_progs,
                              static_cast<const PredInsn*>(plan->d_insns.ptr),
                              static_cast<const uint8_t*>(plan->d_pool.ptr), d_cols, n_rows,
-                             static_cast<uint64_t*>(plan->d_mask_words.ptr), plan->mask_words, plan->stream));
+                             static_cast<uint64_t*>(plan->d_mask_words.ptr), plan->mask_words,
+                             static_cast<uint32_t*>(plan->d_unsup.ptr), plan->stream));
 
   if (n_scan > 0) {
     ScanAcc* parts = static_cast<ScanAcc*>(plan->d_partials.ptr);
@@ -1251,7 +1276,17 @@ extern "C" dq_status dq_plan_finish(dq_plan* plan, dq_state* out, int n_out) {
     DQ_HIP(hipMemcpyAsync(acc.data(), plan->d_acc.ptr, acc.size() * sizeof(ScanAcc), hipMemcpyDeviceToHost, plan->stream));
   if (!regs.empty())
     DQ_HIP(hipMemcpyAsync(regs.data(), plan->d_regs.ptr, regs.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, plan->stream));
+  std::vector<uint32_t> unsup(plan->programs.size());
+  if (!unsup.empty())
+    DQ_HIP(hipMemcpyAsync(unsup.data(), plan->d_unsup.ptr, unsup.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                          plan->stream));
   DQ_HIP(hipStreamSynchronize(plan->stream));
+  plan->op_status.assign(plan->slots.size(), DQ_OK);
+  for (size_t i = 0; i < plan->slots.size(); ++i) {
+    const OpSlot& s = plan->slots[i];
+    if ((s.prog_pred >= 0 && unsup[s.prog_pred]) || (s.prog_where >= 0 && unsup[s.prog_where]))
+      plan->op_status[i] = DQ_ERR_UNSUPPORTED;
+  }
   plan->desc_pending = false;
   plan->host_tmp.clear();
 

@@ -266,8 +266,8 @@ hipError_t launch_hll(const HllTask* d_tasks, int n_tasks, const DevColumn* d_co
                       uint32_t* d_registers, hipStream_t stream);
 hipError_t launch_predicates(const PredProgram* d_progs, int n_progs, const PredInsn* d_insns,
                              const uint8_t* d_pool, const DevColumn* d_cols, int64_t n_rows,
-                             uint64_t* d_mask_words,
-                             int64_t words_per_mask, hipStream_t stream);
+                             uint64_t* d_mask_words, int64_t words_per_mask, uint32_t* d_unsup,
+                             hipStream_t stream);
 hipError_t launch_realign_bitmap(const uint8_t* src, int64_t bit_offset, int64_t n_bits,
                                  uint8_t* dst, hipStream_t stream);
 hipError_t launch_init_acc(ScanAcc* d_acc, int n, hipStream_t stream);

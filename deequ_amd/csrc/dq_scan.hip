@@ -99,16 +99,15 @@ __device__ inline bool apply_cmp(int op, int ord) {
 
 // Lane statistics -> block partial.  The moments are formed per wave (the shift is
 // wave-uniform, so the lanes' Σd and Σd² simply add), from the wave-uniform main-loop counts
-// plus the lanes' tail counts.  fp columns carry (fs, fc) = compensated Σd about the shift, so
-// Σx = n * shift + Σd, the product's rounding error kept exactly by an fma.  Lane 0 carries
-// the wave's totals into the block reduction; the other lanes carry identities.
+// plus the lanes' tail counts.  fp columns carry (fs, fc) = compensated Σx of the selected values
+// (the Sum) and s1 = Σd about the shift (the moments).  Lane 0 carries the wave's totals into the
+// block reduction; the other lanes carry identities.
 
 template <typename T, int NP>
 __device__ inline void thread_finish(const ThreadAcc<NP>& t, int n_preds, ScanAcc* out) {
   const bool lane0 = (threadIdx.x & 63) == 0;
   const uint64_t n_w = wave_sum_u64((uint64_t)t.n_sel) + t.n_sel_w;  // lane 0
-  const double s1 = IsIntegral<T>::value ? t.s1 : (t.fs + t.fc);
-  const double S1 = wave_sum_f64(s1), S2 = wave_sum_f64(t.s2);     // lane 0
+  const double S1 = wave_sum_f64(t.s1), S2 = wave_sum_f64(t.s2);     // lane 0
   double mean = 0.0, m2 = 0.0;
   double fs = t.fs, fc = t.fc;
   uint64_t n_out = 0;
@@ -118,11 +117,6 @@ __device__ inline void thread_finish(const ThreadAcc<NP>& t, int n_preds, ScanAc
     mean = t.shift + S1 / n;
     m2 = S2 - S1 * S1 / n;
     m2 = (m2 < 0.0) ? 0.0 : m2;  // rounding; NaN/Inf propagate
-    if constexpr (!IsIntegral<T>::value) {
-      const double p = n * t.shift;
-      const double pe = (p - p == 0.0) ? fma(n, t.shift, -p) : 0.0;
-      two_sum_merge(fs, fc, p, pe);
-    }
   }
   // (the ragged tail runs diverged, so lanes may hold different copies of the flag: OR them)
   const bool wave_nan = __ballot(t.nan_wave != 0) != 0;
@@ -177,10 +171,11 @@ __device__ inline void accumulate_rows(ThreadAcc<NP>& a, const T* vals, uint32_t
     for (int k = 0; k < R; ++k) {
       const bool s = (sel >> k) & 1u;
       const double x = (double)vals[k];
-      // the fp64 sum is n_sel * shift + Σd (compensated per iteration by the caller), so one
-      // masked d feeds both the sum and the moments
+      // the fp64 Sum is taken over the raw values (compensated per iteration by the caller):
+      // n * shift + Σd would lose what x - shift rounds away when |x| >> |shift|
       const double d = s ? (x - shift) : 0.0;
-      dsum += d;
+      dsum += s ? x : 0.0;
+      a.s1 += d;
       a.s2 = fma(d, d, a.s2);
       // min / max through minnum / maxnum of the value, or of a quiet NaN (one select on the
       // high word) for an unselected row: minnum / maxnum drop a NaN operand, so a NaN never
@@ -400,6 +395,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu((NP <= 3
     if (m) {
       const int src = __builtin_ctzll(m);
       shift = __shfl(x, src, 64);
+      // near DBL_MAX, x - shift could overflow for values of the other sign: no shift then
+      if (!(fabs(shift) <= 0x1p1000)) shift = 0.0;
       break;
     }
   }

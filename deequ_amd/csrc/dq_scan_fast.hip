@@ -152,8 +152,8 @@ struct FastAcc {
   uint32_t n_sel;      // selected rows (lane)
   uint32_t n_rows;     // rows visited (lane)
   uint64_t isum;       // Σ xm, wrapping (int64 columns)
-  double s1, s2;       // Σd, Σd² with d = xm - c (int64: s1 is Σd; fp64: the per-iteration Σd goes to fs/fc)
-  double fs, fc;       // compensated Σd (fp64)
+  double s1, s2;       // Σd, Σd² with d = xm - c
+  double fs, fc;       // compensated Σxm (fp64): the Sum, stand-ins included (removed at the end)
   double fmin, fmax;   // fp64: of x; int64: of d = x - c (exact, see fast_row), x = d + c at the end
   uint32_t sel_w;      // wave-uniform: selected rows counted from the bitmap on the scalar unit (SCNT)
   uint64_t pc;         // wave-uniform: Σ over visited rows of cmp(xm) (before negation)
@@ -191,11 +191,10 @@ __device__ inline void fast_row(FastAcc& a, uint32_t lo, uint32_t hi, uint32_t m
     } else {
       if constexpr (INT) a.isum += ((uint64_t)hi << 32) | lo;
       d = xd - shift;
-      if constexpr (INT) {
-        a.s1 += d;
-      } else {
-        dsum += d;
-      }
+      a.s1 += d;
+      // fp64 Sum from the raw values (compensated per iteration by the caller), not from
+      // n * c + Σd: x - c rounds when |x| >> |c|, and [1e308, -1e308, 5] must sum to 5
+      if constexpr (!INT) dsum += xd;
       xn = xd;
     }
     a.s2 = fma(d, d, a.s2);
@@ -299,7 +298,7 @@ __device__ inline void fast_compute(FastAcc& a, const FastLoad& L, uint32_t no_v
                  __builtin_popcount(L.sw[u][3]);
   }
   double dsum = -0.0;
-  // statistics + predicate of all rows first: for fp64 the iteration's Σd tells whether a
+  // statistics + predicate of all rows first: for fp64 the iteration's Σx tells whether a
   // selected NaN is present (it would be NaN), which the hash needs to know
 #pragma unroll
   for (int j = 0; j < UNROLL * 2; ++j)
@@ -467,7 +466,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DQ_FAST_
       okv = bit != 0u;
       if (FP) {
         const double x = __builtin_bit_cast(double, ((uint64_t)vhi << 32) | vlo);
-        okv = okv && (x - x == 0.0);
+        // (finite and not near DBL_MAX: x - c must not overflow for values of the other sign)
+        okv = okv && (x - x == 0.0) && fabs(x) <= 0x1p1000;
       }
       ok = okv;
       if (INT_STATS) {
@@ -611,7 +611,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DQ_FAST_
   uint64_t isum = 0u;
   double mean = 0.0, m2 = 0.0, fs = 0.0, fc = 0.0;
   if constexpr (STATS) {
-    const double S1 = wave_sum_f64(FP ? (a.fs + a.fc) : a.s1);  // lane 0
+    const double S1 = wave_sum_f64(a.s1);  // lane 0
     const double S2 = wave_sum_f64(a.s2);
     isum = a.isum;
     fs = a.fs;
@@ -623,10 +623,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DQ_FAST_
         mean = (exact_stats ? (found_any ? shift_any : 0.0) : shift) + S1 / n;
         m2 = S2 - S1 * S1 / n;
         m2 = (m2 < 0.0) ? 0.0 : m2;  // rounding; NaN/Inf propagate
-        if constexpr (FP) {  // Σx = n * c + Σd, the product's rounding error kept by an fma
-          const double p = n * shift;
-          const double pe = (p - p == 0.0) ? fma(n, shift, -p) : 0.0;
-          two_sum_merge(fs, fc, p, pe);
+      }
+      if constexpr (FP) {  // the stand-in copies out of Σx: - n_unsel * c, its rounding kept by an fma
+        if (unsel_w > 0) {
+          const double u = (double)unsel_w;
+          const double p = u * shift;
+          const double pe = (p - p == 0.0) ? fma(u, shift, -p) : 0.0;
+          two_sum_merge(fs, fc, -p, -pe);
         }
       }
     }

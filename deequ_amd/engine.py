@@ -126,6 +126,8 @@ class Plan:
 
     def finish(self) -> List[Optional[State]]:
         out = self.finish_raw()
+        for i in range(self.n_ops):  # an op the GPU could not evaluate exactly fails loudly
+            L.check(L.lib().dq_plan_op_status(self.handle, i))
         return [state_from_dq(out[i]) for i in range(self.n_ops)]
 
     def reset(self) -> None:
@@ -145,6 +147,35 @@ class Plan:
             self.close()
         except Exception:
             pass
+
+
+class OpUnsupported:
+    """In place of an op's POD state: the batch held input the GPU could not evaluate exactly
+    for this op (dq_plan_op_status); the error is raised by fromAggregationResult, so only this
+    analyzer fails -- the JNI layer would rerun it on Spark."""
+
+    def __init__(self, error: Exception):
+        self.error = error
+
+
+def run_scan_raw(specs: Sequence[OpSpec], data) -> List:
+    """One fused GPU pass over every batch of `data` for the given ops; the POD dq_states
+    (copies, in op order) for each analyzer's fromAggregationResult, or OpUnsupported."""
+    plan = Plan(specs, data.schema)
+    try:
+        for batch in data.batches():
+            plan.consume(batch)
+        out = plan.finish_raw()
+        res = []
+        for i in range(plan.n_ops):
+            try:
+                L.check(L.lib().dq_plan_op_status(plan.handle, i))
+                res.append(L.DqState.from_buffer_copy(out[i]))
+            except L.DeequAmdError as e:
+                res.append(OpUnsupported(e))
+        return res
+    finally:
+        plan.close()
 
 
 def run_scan(analyzers: Sequence, data) -> Dict[object, Optional[State]]:

@@ -294,14 +294,34 @@ class FrequenciesAndNumRows(State):
         """Null-safe outer join adding counts (GroupingAnalyzers.scala:128-148)."""
         if not isinstance(other, FrequenciesAndNumRows):
             raise TypeError("cannot sum FrequenciesAndNumRows with %s" % type(other).__name__)
-        if other.table.dtypes != self.table.dtypes or other.table.histogram != self.table.histogram:
+        a, b = self, other
+        if a.table.histogram and b.table.histogram and a.table.dtypes != b.table.dtypes:
+            # Histogram states persisted by Spark deequ (or by HdfsStateProvider) are keyed by the
+            # column cast to string (Histogram.scala:63-66); a freshly computed one keeps the
+            # column's type on the device.  Sum them over string keys, as the reference does.
+            a, b = a.as_string_keys(), b.as_string_keys()
+        if b.table.dtypes != a.table.dtypes or b.table.histogram != a.table.histogram:
             raise ValueError("frequency states over different key columns cannot be summed")
+        self, other = a, b
         out = FrequencyTable.like(self.table)
         out.merge_from(self.table)
         out.merge_from(other.table)
         return FrequenciesAndNumRows(out)
 
     __add__ = sum
+
+    def as_string_keys(self) -> "FrequenciesAndNumRows":
+        """A Histogram state keyed by its values cast to string (Spark's Cast to StringType, NULL
+        -> "NullValue", Histogram.scala:63-66, 108): the form the reference persists."""
+        if not self.table.histogram or self.table.dtypes == ["string"]:
+            return self
+        from .javafmt import spark_cast_to_string
+        dtype = self.table.dtypes[0]
+        out: Dict[tuple, int] = {}
+        for (v,), c in self.frequencies().items():
+            k = ("NullValue" if v is None else spark_cast_to_string(v, dtype),)
+            out[k] = out.get(k, 0) + c
+        return FrequenciesAndNumRows.from_frequencies(self.columns, ["string"], out, self.numRows, histogram=True)
 
     def frequencies(self, raw: bool = False) -> Dict:
         """{key tuple: count} on the host (decoded Python values), or with `raw` the encoded

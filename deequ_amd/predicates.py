@@ -21,6 +21,8 @@ from decimal import Decimal, InvalidOperation
 from fractions import Fraction
 from typing import Dict, List, Tuple
 
+import numpy as np
+
 from . import _lib as L
 
 Insn = Tuple[int, int, int, float]  # (opcode, arg, i64, f64)
@@ -208,6 +210,10 @@ class _Parser:
         if kind == "DBL":
             return ("lit", "dbl", float(text))
         if kind == "STR":
+            # Spark 2.2's grammar concatenates adjacent string literals (`constant: STRING+`), so
+            # the 'a''b' that Check.isContainedIn writes for a quote (Check.scala:908-910) is "ab"
+            while self.peek()[0] == "STR":
+                text += self.take()[1]
             return ("lit", "str", text)
         if kind == "ID":
             up = text.upper()
@@ -261,6 +267,14 @@ class _Compiler:
                     return k
             return "null"
         return "bool"
+
+    def _has_f32(self, node) -> bool:
+        """A FloatType column, directly or inside a COALESCE."""
+        if node[0] == "col":
+            return node[1] in self.schema and self.schema[node[1]][1] == "float32"
+        if node[0] == "coalesce":
+            return any(self._has_f32(x) for x in node[1])
+        return False
 
     def emit(self, opcode, arg=0, i64=0, f64=0.0):
         self.code.append((opcode, arg, int(i64), float(f64)))
@@ -319,8 +333,19 @@ class _Compiler:
             self.emit(self._OPS[op], L.DQ_CMP_AS_INT64)
             return
         if "str" in (ta, tb) and "null" not in (ta, tb):
-            # Spark 2.2 casts the string side to double here (PromoteStrings)
-            raise UnsupportedPredicate("comparison of a string with a number")
+            # Spark 2.2 PromoteStrings: a string compared with a number is Cast to DoubleType
+            # (java.lang.Double.parseDouble of the trimmed text, NULL when unparsable) and the
+            # comparison runs in double (e.g. `item > 3` on a string column, CheckTest.scala:193)
+            if "bool" in (ta, tb):
+                raise UnsupportedPredicate("comparison of a string with a boolean")
+            for node, kind in ((a, ta), (b, tb)):
+                if kind == "str":
+                    self.emit_value(node, "str")
+                    self.emit(L.DQ_P_CAST_DOUBLE)
+                else:
+                    self.emit_value(node, "dbl")
+            self.emit(self._OPS[op], L.DQ_CMP_AS_FLOAT64)
+            return
         if ta == "null" or tb == "null":
             if op == "<=>":  # x <=> NULL  ==  x IS NULL
                 other = a if tb == "null" else b
@@ -331,6 +356,21 @@ class _Compiler:
             self.emit(L.DQ_P_LIT_NULL)  # any other comparison with NULL is NULL
             self.emit(L.DQ_P_LIT_NULL)
             self.emit(L.DQ_P_EQ, L.DQ_CMP_AS_INT64)
+            return
+        if "int" in (ta, tb) and (self._has_f32(a) or self._has_f32(b)):
+            # Spark 2.2 coerces float vs int / long to FloatType: the integral side is rounded to
+            # float first.  Exact here for a literal (rounded once on the host, then compared in
+            # fp64, which orders float values the same); an integral column would need a rounding
+            # per row, which the IR does not have.
+            f32_side, int_side = (a, b) if self._has_f32(a) else (b, a)
+            if f32_side[0] != "col" or int_side[0] != "lit":
+                raise UnsupportedPredicate("float column compared with an integral expression (FloatType)")
+            for node in (a, b):
+                if node is int_side:
+                    self.emit(L.DQ_P_LIT_FLOAT, f64=float(np.float32(int_side[2])))
+                else:
+                    self.emit_value(node, "dbl")
+            self.emit(self._OPS[op], L.DQ_CMP_AS_FLOAT64)
             return
         if "dbl" in (ta, tb):
             self.emit_value(a, "dbl")
@@ -395,6 +435,11 @@ class _Compiler:
             self.emit(L.DQ_P_IS_NULL if t == "isnull" else L.DQ_P_IS_NOT_NULL)
         elif t == "in":
             x, items = node[1], node[2]
+            kinds = {self.vtype(v) for v in [x] + list(items)} - {"null"}
+            if "str" in kinds and len(kinds) > 1:
+                # Spark 2.2 InConversion widens a string/number IN list to StringType (string
+                # comparison of the numbers' text), not to double as a plain comparison does
+                raise UnsupportedPredicate("IN list mixing strings and numbers")
             for k, item in enumerate(items):
                 self.emit_cmp("=", x, item)
                 if k:

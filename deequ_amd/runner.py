@@ -143,7 +143,7 @@ class AnalysisRunner:
     @staticmethod
     def _runScanningAnalyzers(data, analyzers, aggregateWith, saveStatesWith) -> AnalyzerContext:
         from .analyzers import GroupingAnalyzer
-        from .engine import op_spec_for, op_supported, run_scan
+        from .engine import op_spec_for, op_supported, run_scan_raw
         shareable = [a for a in analyzers if isinstance(a, ScanShareableAnalyzer)]
         grouping = [a for a in analyzers if isinstance(a, GroupingAnalyzer)]
         others = [a for a in analyzers if not isinstance(a, (ScanShareableAnalyzer, GroupingAnalyzer))]
@@ -158,14 +158,14 @@ class AnalysisRunner:
             except Exception as e:  # noqa: BLE001
                 results[a] = a.toFailureMetric(e)
         if eligible:
-            try:
-                states = run_scan(eligible, data)
-                for a in eligible:
-                    try:
-                        results[a] = a.calculateMetric(states[a], aggregateWith, saveStatesWith)
-                    except Exception as e:  # noqa: BLE001 - one analyzer fails (:348-352)
+            try:  # AnalysisRunner.scala:305-323: one fused pass; any error fails them all
+                raw = run_scan_raw([a.aggregationFunctions(data.schema) for a in eligible], data)
+                for i, a in enumerate(eligible):
+                    try:  # successOrFailureMetricFrom (:340-353): an error fails this one
+                        results[a] = a.metricFromAggregationResult(raw[i], aggregateWith, saveStatesWith)
+                    except Exception as e:  # noqa: BLE001
                         results[a] = a.toFailureMetric(e)
-            except Exception as e:  # noqa: BLE001 - the whole pass fails (:320-323)
+            except Exception as e:  # noqa: BLE001
                 for a in eligible:
                     results[a] = a.toFailureMetric(e)
         tables = OrderedDict()
@@ -197,23 +197,59 @@ class AnalysisRunner:
     @staticmethod
     def runOnAggregatedStates(schema: Dict[str, str], analysis: "Analysis", stateLoaders,
                               saveStatesWith=None) -> AnalyzerContext:
-        """Metrics from the merge of persisted states (AnalysisRunner.scala:385-460)."""
+        """Metrics from the merge of persisted states, no data scan (AnalysisRunner.scala:385-460):
+        every analyzer's states are summed over the loaders (aggregateStateTo, Analyzer.scala:
+        130-147); scanning analyzers compute their metric from that; grouping analyzers of one
+        grouping-column set share the one frequency state any of them has (only the first of a
+        set is persisted, :543; findStateForParticularGrouping, :462-476)."""
+        from .analyzers import GroupingAnalyzer
+        from .states import merge
         analyzers = _distinct(analysis.analyzers)
+        if not analyzers or not stateLoaders:
+            return AnalyzerContext.empty()
         results = OrderedDict()
+        passed = []
         for a in analyzers:
             err = Preconditions.findFirstFailing(schema, a.preconditions())
             if err is not None:
                 results[a] = a.toFailureMetric(err)
+            else:
+                passed.append(a)
+        aggregated = {}
+        for a in passed:
+            try:
+                state = None
+                for loader in stateLoaders:
+                    state = merge(loader.load(a), state)
+                aggregated[a] = state
+            except Exception as e:  # noqa: BLE001
+                results[a] = a.toFailureMetric(e)
+        grouping = OrderedDict()
+        for a in passed:
+            if a in results:
+                continue
+            if isinstance(a, GroupingAnalyzer):
+                grouping.setdefault(tuple(sorted(a.groupingColumns())), []).append(a)
                 continue
             try:
-                from .states import merge
-                state = merge(*[loader.load(a) for loader in stateLoaders])
+                state = aggregated.get(a)
                 if state is not None and saveStatesWith is not None:
                     saveStatesWith.persist(a, state)
                 results[a] = a.computeMetricFrom(state)
             except Exception as e:  # noqa: BLE001
                 results[a] = a.toFailureMetric(e)
-        return AnalyzerContext(results)
+        for _, group in grouping.items():
+            states = [aggregated.get(a) for a in group if aggregated.get(a) is not None]
+            for a in group:
+                try:
+                    if not states:  # require(states.nonEmpty) (:474)
+                        raise ValueError("no persisted frequency state for grouping %s" % a.groupingColumns())
+                    results[a] = a.computeMetricFrom(states[0])
+                except Exception as e:  # noqa: BLE001
+                    results[a] = a.toFailureMetric(e)
+            if states and saveStatesWith is not None:
+                saveStatesWith.persist(group[0], states[0])
+        return AnalyzerContext(OrderedDict((a, results[a]) for a in analyzers if a in results))
 
 
 class AnalysisRunBuilder:

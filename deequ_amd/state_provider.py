@@ -36,6 +36,9 @@ from .states import (ApproxCountDistinctState, CorrelationState, DataTypeHistogr
                      MinState, NumMatches, NumMatchesAndCount, StandardDeviationState, SumState)
 
 COUNT_COL = "com_amazon_deequ_dq_metrics_count"  # Analyzer.scala:363-364
+# Histogram's state is `data.select(col.cast(string)).groupBy(column).count()`
+# (Histogram.scala:63-66): Spark names that count column "count".
+HISTOGRAM_COUNT_COL = "count"
 
 _M32 = 0xFFFFFFFF
 
@@ -172,7 +175,8 @@ class HdfsStateProvider:
         arrays = [pa.array([r[0][i] for r in rows], type=getattr(pa, _PA_TYPES[t])()) for i, t in enumerate(types)]
         arrays.append(pa.array([r[1] for r in rows], type=pa.int64()))
         os.makedirs(directory)
-        pq.write_table(pa.Table.from_arrays(arrays, names=names + [COUNT_COL]),
+        count_col = HISTOGRAM_COUNT_COL if table.histogram else COUNT_COL
+        pq.write_table(pa.Table.from_arrays(arrays, names=names + [count_col]),
                        os.path.join(directory, "part-00000.snappy.parquet"))
         self._write(self._path(ident, "-num_rows.bin"), struct.pack(">q", state.numRows))
 
@@ -212,18 +216,37 @@ class HdfsStateProvider:
     def _load_frequencies(self, ident: str, analyzer):
         import pyarrow.parquet as pq
         from .frequencies import FrequenciesAndNumRows
-        table = pq.read_table(self._path(ident, "-frequencies.pqt"))
+        # file by file: Histogram("count")'s state has two columns named "count", which
+        # pyarrow's dataset reader (read_table of a directory) refuses to unify
+        directory = self._path(ident, "-frequencies.pqt")
+        parts = sorted(f for f in os.listdir(directory) if f.endswith(".parquet")) if os.path.isdir(directory) else []
+        tables = [pq.ParquetFile(os.path.join(directory, f)).read() for f in parts] or \
+            [pq.ParquetFile(directory).read()]
+        table = tables[0] if len(tables) == 1 else _concat(tables)
         num_rows = struct.unpack(">q", self._read(self._path(ident, "-num_rows.bin")))[0]
-        names = [n for n in table.column_names if n != COUNT_COL]
-        dtypes = [_dtype_of(table.schema.field(n).type) for n in names]
-        counts = table.column(COUNT_COL).to_pylist()
-        cols = [table.column(n).to_pylist() for n in names]
+        # the count column: deequ's name for grouping states, Spark's "count" for Histogram;
+        # anything else (a state written by another tool) -- the last column
+        # (by position: Histogram("count") gives two columns named "count")
+        names_all = list(table.column_names)
+        ci = names_all.index(COUNT_COL) if COUNT_COL in names_all else len(names_all) - 1
+        keys = [i for i in range(len(names_all)) if i != ci]
+        names = [names_all[i] for i in keys]
+        dtypes = [_dtype_of(table.schema.field(i).type) for i in keys]
+        counts = table.column(ci).to_pylist()
+        cols = [table.column(i).to_pylist() for i in keys]
         freqs: Dict[tuple, int] = {}
         for i, c in enumerate(counts):
             key = tuple(col[i] for col in cols)
             freqs[key] = freqs.get(key, 0) + int(c)
         return FrequenciesAndNumRows.from_frequencies(names, dtypes, freqs, num_rows,
                                                       histogram=isinstance(analyzer, Histogram))
+
+
+def _concat(tables):
+    import pyarrow as pa
+    cols = [pa.chunked_array([c for t in tables for c in t.column(i).chunks], type=tables[0].schema.field(i).type)
+            for i in range(tables[0].num_columns)]
+    return pa.Table.from_arrays(cols, names=tables[0].column_names)
 
 
 def _dtype_of(t) -> str:
@@ -236,4 +259,4 @@ def _dtype_of(t) -> str:
     raise ValueError("unsupported frequency column type %s" % t)
 
 
-__all__: List[str] = ["HdfsStateProvider", "scala_string_hash", "COUNT_COL"]
+__all__: List[str] = ["HdfsStateProvider", "scala_string_hash", "COUNT_COL", "HISTOGRAM_COUNT_COL"]

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define DQ_ABI_VERSION 2
+#define DQ_ABI_VERSION 3
 
 /* ---------------------------------------------------------------- status codes */
 typedef enum dq_status {
@@ -106,6 +106,12 @@ typedef enum dq_pred_opcode {
   DQ_P_LIT_NULL = 4,   /* push NULL                                                         */
   DQ_P_COALESCE = 5,   /* pop b, a; push a if a non-NULL else b                             */
   DQ_P_LIT_STRING = 6, /* push UTF-8 literal strings[i64 .. i64 + arg) of the predicate      */
+  DQ_P_CAST_DOUBLE = 7, /* pop value; push it as fp64: Spark 2.2 Cast(-> DoubleType), which a
+                           comparison of a string with a number inserts (PromoteStrings): a string
+                           through java.lang.Double.parseDouble of its trimmed text, NULL when
+                           unparsable.  A well-formed string off the exact fast path (> 19
+                           significant digits, |exponent| > 22, hex) makes the op report
+                           DQ_ERR_UNSUPPORTED from dq_plan_op_status (route it to Spark).    */
   DQ_P_EQ = 10, DQ_P_NE = 11, DQ_P_LT = 12, DQ_P_LE = 13, DQ_P_GT = 14, DQ_P_GE = 15,
   DQ_P_EQ_NULLSAFE = 16, /* <=>                                                             */
   DQ_P_IS_NULL = 20,   /* pop value; push boolean (never NULL)                              */
@@ -209,6 +215,11 @@ dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, int n_columns
 
 /* Wait for all consumed batches and write one dq_state per op (in op order). */
 dq_status dq_plan_finish(dq_plan* plan, dq_state* out, int n_out);
+
+/* Status of op `op` after dq_plan_finish: DQ_OK, or DQ_ERR_UNSUPPORTED when a batch held input
+ * the GPU could not evaluate exactly for that op (DQ_P_CAST_DOUBLE off its fast path); the JNI
+ * layer then fails or reroutes that analyzer only (AnalysisRunner.scala:340-353 scope). */
+dq_status dq_plan_op_status(dq_plan* plan, int op);
 
 /* Clear accumulated results so the plan can scan a new dataset. */
 dq_status dq_plan_reset(dq_plan* plan);

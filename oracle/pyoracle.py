@@ -593,6 +593,39 @@ class _Tok:
         return False
 
 
+def _java_to_string(v) -> str:
+    """Cast(-> StringType) of an int / double literal or value (Java toString)."""
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, int):
+        return str(v)
+    return java_double_to_string(float(v))
+
+
+def java_parse_double(s: str) -> Optional[float]:
+    """java.lang.Double.parseDouble of String.trim() (chars <= U+0020 trimmed), None when it
+    throws NumberFormatException: Spark 2.2's Cast(StringType -> DoubleType)."""
+    import re
+    t = s
+    while t and ord(t[0]) <= 0x20:
+        t = t[1:]
+    while t and ord(t[-1]) <= 0x20:
+        t = t[:-1]
+    m = re.fullmatch(r"([+-]?)(NaN|Infinity|((\d+\.?\d*|\.\d+)([eE][+-]?\d+)?)[fFdD]?)", t)
+    if m:
+        sign, body = m.group(1), m.group(2)
+        if body == "NaN":
+            return float("nan")
+        if body == "Infinity":
+            return float("-inf") if sign == "-" else float("inf")
+        num = body.rstrip("fFdD")
+        return float(sign + num)
+    hm = re.fullmatch(r"([+-]?)0[xX]([0-9a-fA-F]*\.?[0-9a-fA-F]*)[pP]([+-]?\d+)[fFdD]?", t)
+    if hm and hm.group(2).strip("."):
+        return float.fromhex(hm.group(1) + "0x" + hm.group(2) + "p" + hm.group(3))
+    return None
+
+
 def eval_predicate(text: str, table: OTable) -> List[Optional[bool]]:
     """Evaluate a deequ SQL predicate string (the numeric subset deequ's checks emit:
     comparisons, IN, BETWEEN, IS [NOT] NULL, COALESCE, AND/OR/NOT, string equality)
@@ -612,8 +645,11 @@ def eval_predicate(text: str, table: OTable) -> List[Optional[bool]]:
         if t[0] == "num":
             return ("lit", ("int" if all(ch.isdigit() for ch in t[1]) else
                             ("double" if "e" in t[1].lower() else "decimal")), t[1])
-        if t[0] == "str":
-            return ("lit", "string", t[1])
+        if t[0] == "str":  # adjacent literals concatenate (Spark 2.2 grammar: STRING+)
+            v = t[1]
+            while tk.peek()[0] == "str":
+                v += tk.next()[1]
+            return ("lit", "string", v)
         if t[0] == "id":
             if t[1].upper() == "COALESCE":
                 assert tk.next() == ("op", "(")
@@ -699,8 +735,9 @@ def eval_predicate(text: str, table: OTable) -> List[Optional[bool]]:
             return "null", lambda r: None
         if node[0] == "col":
             col = table[node[1]]
-            kind = ("int" if col.dtype in _INTEGRAL else "double" if col.dtype in _FRACTIONAL
-                    else col.dtype)
+            # FloatType keeps its own kind: Spark 2.2 compares float vs int/long as FloatType
+            kind = ("int" if col.dtype in _INTEGRAL else "float" if col.dtype == "float32"
+                    else "double" if col.dtype in _FRACTIONAL else col.dtype)
             return kind, lambda r, c=col: c.values[r]
         if node[0] == "paren":
             return typed(node[1])
@@ -722,8 +759,11 @@ def eval_predicate(text: str, table: OTable) -> List[Optional[bool]]:
         return "bool", lambda r, n=node: ev(n, r)
 
     def _common(kinds):
+        # Spark 2.2 TypeCoercion: float vs int/long -> FloatType; decimal vs float/double -> double
         if "double" in kinds:
             return "double"
+        if "float" in kinds:
+            return "double" if "decimal" in kinds else "float"
         if "decimal" in kinds:
             return "decimal"
         if "int" in kinds:
@@ -735,6 +775,9 @@ def eval_predicate(text: str, table: OTable) -> List[Optional[bool]]:
             return None
         if dst == "double":
             return float(v)
+        if dst == "float":
+            import numpy as _np
+            return float(_np.float32(v))
         if dst == "decimal":
             from fractions import Fraction
             return Fraction(v) if not isinstance(v, float) else Fraction(v)
@@ -749,8 +792,8 @@ def eval_predicate(text: str, table: OTable) -> List[Optional[bool]]:
         kb, gb = typed(b)
         if ka == kb:
             return ka, ga, kb, gb, ka
-        if "string" in (ka, kb) and ka in ("int", "double", "decimal", "string") and kb in (
-                "int", "double", "decimal", "string"):
+        if "string" in (ka, kb) and ka in ("int", "float", "double", "decimal", "string") and kb in (
+                "int", "float", "double", "decimal", "string"):
             # Spark 2.2 PromoteStrings: numeric vs string compares as double
             return ka, ga, kb, gb, "double_from_string"
         target = _common([ka, kb])
@@ -782,10 +825,10 @@ def eval_predicate(text: str, table: OTable) -> List[Optional[bool]]:
                     return x is None and y is None
             if x is None or y is None:
                 return None
-            if target == "double_from_string":
-                try:
-                    x, y = float(x), float(y)
-                except ValueError:
+            if target == "double_from_string":  # Cast(-> DoubleType): Java parseDouble
+                x = java_parse_double(x) if isinstance(x, str) else float(x)
+                y = java_parse_double(y) if isinstance(y, str) else float(y)
+                if x is None or y is None:
                     return None
             else:
                 x, y = conv(x, ka, target), conv(y, kb, target)
@@ -804,6 +847,18 @@ def eval_predicate(text: str, table: OTable) -> List[Optional[bool]]:
             x = gx(r)
             if x is None:
                 return None
+            kinds = {kx} | {typed(item)[0] for item in node[2]}
+            if "string" in kinds and kinds - {"string", "null"}:
+                # Spark 2.2 InConversion: a string/number IN list compares as strings
+                xs = x if kx == "string" else _java_to_string(x)
+                saw_null = False
+                for item in node[2]:
+                    v = typed(item)[1](r)
+                    if v is None:
+                        saw_null = True
+                    elif xs == (v if isinstance(v, str) else _java_to_string(v)):
+                        return True
+                return None if saw_null else False
             saw_null = False
             for item in node[2]:
                 res = ev(("cmp", "=", node[1], item), r)

@@ -133,6 +133,7 @@ TABLES = {
 }
 
 A = "analyzers/AnalyzerTests.scala"
+C = "checks/CheckTest.scala"
 EMPTY = "empty"  # the metric is a Failure(EmptyStateException)
 H_FULL = -(0.75 * math.log(0.75) + 0.25 * math.log(0.25))  # AnalyzerTests.scala:135-136
 NH = T + "analyzers/NullHandlingTests.scala"
@@ -225,6 +226,24 @@ CASES = [
     ("corr_commutative", "dfInformative", "Correlation", ["att2", "att1"], 1.0, T + A + ":651-654"),
     ("null_corr", "dfNullColumns", "Correlation", ["numericCol", "numericCol2"], EMPTY, NH + ":93,124"),
     ("null_corr3", "dfNullColumns", "Correlation", ["numericCol", "numericCol3"], EMPTY, NH + ":125"),
+    # ApproxCountDistinct with a `where` filter: `unique < 4` on a STRING column is Spark's
+    # implicit string -> double cast (PromoteStrings); the GPU path evaluates it on the device
+    ("acd_where_string_cast", "dfUnique", "ApproxCountDistinct", ["uniqueWithNulls", "unique < 4"], 2.0, T + A + ":551-558"),
+    # where-filtered checks (CheckTest.scala:174-290): the Compliance analyzers their checks build
+    # (Check.satisfies / isLessThan... -> Constraint.complianceConstraint, Constraint.scala:265-279)
+    # and the metric each check's assertion pins: the default `_ == 1.0` or the custom `_ == 0.5`
+    ("check_satisfies_where", "dfNumeric", "Compliance", ["rule1", "att1 < att2", "att1 > 3"], 1.0, T + C + ":174-190"),
+    ("check_satisfies_where_half", "dfNumeric", "Compliance", ["rule3", "att2 > 0", "att1 > 0"], 0.5, T + C + ":180-190"),
+    ("check_lt", "dfNumeric", "Compliance", ["att1 is less than att2", "att1 < att2"], 0.5, T + C + ":192-211"),
+    ("check_le", "dfNumeric", "Compliance", ["att1 is less than or equal to att3", "att1 <= att3"], 0.5, T + C + ":213-234"),
+    ("check_gt", "dfNumeric", "Compliance", ["att2 is greater than att1", "att2 > att1"], 0.5, T + C + ":236-255"),
+    ("check_ge", "dfNumeric", "Compliance", ["att3 is greater than or equal to att1", "att3 >= att1"], 0.5, T + C + ":257-278"),
+    ("check_lt_where_item", "dfNumeric", "Compliance", ["att1 is less than att2", "att1 < att2", "item > 3"], 1.0, T + C + ":193-194,207 (where on the string column item)"),
+    ("check_le_where_item", "dfNumeric", "Compliance", ["att1 is less than or equal to att3", "att1 <= att3", "item > 3"], 1.0, T + C + ":215-216,229"),
+    ("check_gt_where_item", "dfNumeric", "Compliance", ["att2 is greater than att1", "att2 > att1", "item > 3"], 1.0, T + C + ":238-239,251"),
+    ("check_ge_where_item", "dfNumeric", "Compliance", ["att3 is greater than or equal to att1", "att3 >= att1", "item > 3"], 1.0, T + C + ":260-261,273"),
+    # FilterableCheckTest.scala:31-34 (plumbing only: the analyzers a filtered check builds)
+    ("filterable_completeness_where", "dfMissing", "Completeness", ["att1", "item = '1'"], 1.0, T + "checks/FilterableCheckTest.scala:31-34 (Completeness with where)"),
 ]
 
 # Known answers that need the union of two tables (state merge == union):

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
     # the ctypes signature table covers the whole header too
     assert declared == set(_lib.SIGNATURES), declared ^ set(_lib.SIGNATURES)
-    assert _lib.lib().dq_abi_version() == 2
+    assert _lib.lib().dq_abi_version() == 3
 
 
 def test_library_reports_no_device_without_gpu_cleanly():
@@ -169,6 +169,10 @@ def _interp(code, pool, table, names, nrows):
                 st.append(("s", pool[i64:i64 + arg].decode("utf-8")))
             elif op in (L.DQ_P_TRUE, L.DQ_P_FALSE):
                 st.append(("b", op == L.DQ_P_TRUE))
+            elif op == L.DQ_P_CAST_DOUBLE:  # Cast(-> DoubleType): Java parseDouble of a string
+                a = st.pop()
+                v = a[1] if a[1] is None else (O.java_parse_double(a[1]) if a[0] == "s" else float(a[1]))
+                st.append(("f", v))
             elif op == L.DQ_P_COALESCE:
                 b, a = st.pop(), st.pop()
                 r_ = a if a[1] is not None else b
@@ -218,6 +222,10 @@ PREDICATES = [
     "i IS NOT NULL AND f IS NULL", "s = 'k1'", "s IN ('k1', 'k2')", "s != 'k0'", "s > 'k1'",
     "s IS NULL", "b = true", "b", "NOT b", "i > -3", "i < 2 AND (s = 'k1' OR f > 1000.5)",
     "f > 1000.5", "i <=> NULL", "i = NULL", "TRUE", "FALSE", "i >= 3 OR i < 3",
+    # Spark 2.2 PromoteStrings: string vs number compares Cast(string AS DOUBLE) in double
+    "sn > 3", "sn <= 2.5", "3 < sn", "sn = f", "sn != -1", "i > '2'",
+    # FloatType vs an int literal compares in FloatType (rounded once on the host)
+    "g = 16777217", "g > 16777217",
 ]
 
 
@@ -231,18 +239,23 @@ def test_predicate_compiler_matches_oracle_semantics(text):
     fv[0] = float("nan")
     sv = [None if rng.random() < 0.2 else "k%d" % x for x in rng.integers(0, 4, n)]
     bv = [None if rng.random() < 0.2 else bool(x) for x in rng.integers(0, 2, n)]
+    texts = ["1", " 2 ", "2.5", "-1", "3e0", "x", "", "NaN", "4d", "1000.0"]
+    snv = [None if rng.random() < 0.1 else texts[k] for k in rng.integers(0, len(texts), n)]
+    gv = [float(x) for x in rng.choice([16777216.0, 16777218.0, 3.0, 16777220.0], n)]
     table = {"i": O.OColumn("int64", iv), "f": O.OColumn("float64", fv),
-             "s": O.OColumn("string", sv), "b": O.OColumn("bool", bv)}
-    names = ["i", "f", "s", "b"]
+             "s": O.OColumn("string", sv), "b": O.OColumn("bool", bv),
+             "sn": O.OColumn("string", snv), "g": O.OColumn("float32", gv)}
+    names = ["i", "f", "s", "b", "sn", "g"]
     schema = {nm: (k, table[nm].dtype) for k, nm in enumerate(names)}
     prog = compile_predicate(text, schema)
     assert _interp(prog.code, prog.pool, table, names, n) == O.eval_predicate(text, table)
 
 
-@pytest.mark.parametrize("text", ["s > 3", "i + 1 > 2", "upper(s) = 'A'", "i > 'x'"])
+@pytest.mark.parametrize("text", ["i + 1 > 2", "upper(s) = 'A'", "s IN (1, 2)", "i IN ('1', 2)",
+                                  "b > '1'", "g = i"])
 def test_unsupported_predicates_are_rejected(text):
     from deequ_amd.predicates import UnsupportedPredicate, compile_predicate
-    schema = {"i": (0, "int64"), "s": (1, "string")}
+    schema = {"i": (0, "int64"), "s": (1, "string"), "b": (2, "bool"), "g": (3, "float32")}
     with pytest.raises((UnsupportedPredicate, ValueError)):
         compile_predicate(text, schema)
 
