@@ -26,6 +26,7 @@ from .states import (ApproxCountDistinctState, CorrelationState, DataTypeHistogr
                      NumMatches,
                      NumMatchesAndCount, StandardDeviationState, State, SumState)
 from .state_provider import HdfsStateProvider
+from .arrow import ArrowBatch, ArrowTable
 from .table import Column, PartitionedTable, Table
 
 __all__ = [n for n in dir() if not n.startswith("_")]

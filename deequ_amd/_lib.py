@@ -81,6 +81,25 @@ class DqFreqGroup(Structure):
                 ("reserved", c_int32)]
 
 
+class ArrowSchema(Structure):
+    """struct ArrowSchema of the Arrow C Data Interface (include/deequ_amd.h)."""
+
+
+ArrowSchema._fields_ = [("format", c_char_p), ("name", c_char_p), ("metadata", c_char_p), ("flags", c_int64),
+                        ("n_children", c_int64), ("children", POINTER(POINTER(ArrowSchema))),
+                        ("dictionary", POINTER(ArrowSchema)), ("release", c_void_p), ("private_data", c_void_p)]
+
+
+class ArrowArray(Structure):
+    """struct ArrowArray of the Arrow C Data Interface."""
+
+
+ArrowArray._fields_ = [("length", c_int64), ("null_count", c_int64), ("offset", c_int64), ("n_buffers", c_int64),
+                       ("n_children", c_int64), ("buffers", POINTER(c_void_p)),
+                       ("children", POINTER(POINTER(ArrowArray))), ("dictionary", POINTER(ArrowArray)),
+                       ("release", c_void_p), ("private_data", c_void_p)]
+
+
 # measurement entry points (include/deequ_amd_diag.h; not part of the drop-in boundary)
 DIAG_SIGNATURES = {
     "dq_diag_hash_rate": (c_int, [c_int, c_int, c_int, POINTER(c_double)]),
@@ -101,6 +120,10 @@ SIGNATURES = {
     "dq_plan_consume": (c_int, [c_void_p, POINTER(DqColumn), c_int, c_int64]),
     "dq_plan_finish": (c_int, [c_void_p, POINTER(DqState), c_int]),
     "dq_plan_reset": (c_int, [c_void_p]),
+    "dq_arrow_columns": (c_int, [POINTER(ArrowSchema), POINTER(ArrowArray), c_int, POINTER(c_int32),
+                                 POINTER(DqColumn), c_int, POINTER(c_int), POINTER(c_int64)]),
+    "dq_plan_consume_arrow": (c_int, [c_void_p, POINTER(ArrowSchema), POINTER(ArrowArray), c_int]),
+    "dq_freq_consume_arrow": (c_int, [c_void_p, POINTER(ArrowSchema), POINTER(ArrowArray), c_int]),
     "dq_plan_op_status": (c_int, [c_void_p, c_int]),
     "dq_plan_stream": (c_void_p, [c_void_p]),
     "dq_state_merge": (c_int, [POINTER(DqState), POINTER(DqState), POINTER(DqState)]),

@@ -1649,3 +1649,6 @@ extern "C" dq_status dq_cast_utf8(dq_ctx* ctx, const dq_column* src, int64_t n_r
 
 // The frequency group-by shares the staging helpers above.
 #include "dq_freq_api.inc"
+
+// Arrow C Data Interface entry points over dq_plan_consume / dq_freq_consume.
+#include "dq_arrow.inc"

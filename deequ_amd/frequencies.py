@@ -115,7 +115,12 @@ class FrequencyTable:
         L.check(L.lib().dq_freq_expect_groups(self.handle, int(groups)))
 
     def consume(self, batch) -> None:
+        from .arrow import ArrowBatch
         from .table import dq_columns
+        if isinstance(batch, ArrowBatch):  # the Arrow C Data Interface entry point
+            schema, array = batch.c_structs(self.names)
+            L.check(L.lib().dq_freq_consume_arrow(self.handle, ctypes.byref(schema), ctypes.byref(array), 0))
+            return
         cols = dq_columns(batch, self.names)
         L.check(L.lib().dq_freq_consume(self.handle, cols, len(self.names), batch.num_rows))
 

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define DQ_ABI_VERSION 3
+#define DQ_ABI_VERSION 4
 
 /* ---------------------------------------------------------------- status codes */
 typedef enum dq_status {
@@ -221,6 +221,64 @@ dq_status dq_plan_finish(dq_plan* plan, dq_state* out, int n_out);
  * layer then fails or reroutes that analyzer only (AnalysisRunner.scala:340-353 scope). */
 dq_status dq_plan_op_status(dq_plan* plan, int op);
 
+/* ---------------------------------------------------------------- Arrow C Data Interface
+ * The JVM side of the seam hands Spark partitions over as Arrow record batches
+ * (ArrowUtils / ArrowWriter -> org.apache.arrow.c.Data.exportVectorSchemaRoot), i.e. the
+ * standard C Data Interface structs below (layout fixed by the Arrow specification).  These
+ * entry points replace the hand-filled dq_column array of dq_plan_consume / dq_freq_consume at
+ * the launch sites AnalysisRunner.scala:313 (data.agg) and GroupingAnalyzers.scala:53-80.
+ *
+ * Accepted input: a struct array ("+s", one child per plan column, in plan column order -- a
+ * record batch) or a single top-level array (a one-column batch).  Child formats: "b" bool,
+ * "c" int8, "s" int16, "i" int32, "l" int64, "f" float32, "g" float64, "u" utf8.  Offsets of
+ * sliced arrays (struct offset + child offset) are honoured; a NULL validity buffer means no
+ * NULLs.  Rejected with DQ_ERR_UNSUPPORTED (route the batch to Spark): dictionary-encoded,
+ * nested, large_utf8 ("U"), decimal, temporal formats and struct-level NULL rows.  Malformed
+ * structs (released, buffer counts, children shorter than the batch) give DQ_ERR_INVALID.
+ * The caller keeps ownership: release callbacks are never invoked by the library, and the
+ * buffers must stay valid until the next call on the plan / table returns (host buffers) or
+ * until the plan's stream has drained (DQ_COL_DEVICE: buffers in HBM on the context's GPU). */
+#ifndef ARROW_C_DATA_INTERFACE
+#define ARROW_C_DATA_INTERFACE
+#define ARROW_FLAG_DICTIONARY_ORDERED 1
+#define ARROW_FLAG_NULLABLE 2
+#define ARROW_FLAG_MAP_KEYS_SORTED 4
+struct ArrowSchema {
+  const char* format;
+  const char* name;
+  const char* metadata;
+  int64_t flags;
+  int64_t n_children;
+  struct ArrowSchema** children;
+  struct ArrowSchema* dictionary;
+  void (*release)(struct ArrowSchema*);
+  void* private_data;
+};
+struct ArrowArray {
+  int64_t length;
+  int64_t null_count;
+  int64_t offset;
+  int64_t n_buffers;
+  int64_t n_children;
+  const void** buffers;
+  struct ArrowArray** children;
+  struct ArrowArray* dictionary;
+  void (*release)(struct ArrowArray*);
+  void* private_data;
+};
+#endif /* ARROW_C_DATA_INTERFACE */
+
+/* Map an Arrow batch onto dq_columns without touching any GPU (pure host; the JNI layer can
+ * call it to derive the plan's column types): types[i] / columns[i] for each of the batch's
+ * columns (at most max_columns), *n_columns and *n_rows.  `flags` = DQ_COL_DEVICE when the
+ * buffers are device pointers.  DQ_ERR_SPACE (with *n_columns set) when max_columns is short. */
+dq_status dq_arrow_columns(const struct ArrowSchema* schema, const struct ArrowArray* array, int flags,
+                           int32_t* types, dq_column* columns, int max_columns, int* n_columns,
+                           int64_t* n_rows);
+/* dq_plan_consume of one Arrow batch (its columns in plan column order). */
+dq_status dq_plan_consume_arrow(dq_plan* plan, const struct ArrowSchema* schema,
+                                const struct ArrowArray* array, int flags);
+
 /* Clear accumulated results so the plan can scan a new dataset. */
 dq_status dq_plan_reset(dq_plan* plan);
 
@@ -299,6 +357,9 @@ dq_status dq_freq_reserve(dq_freq* f, int64_t rows);
 dq_status dq_freq_expect_groups(dq_freq* f, int64_t groups);
 dq_status dq_freq_reset(dq_freq* f);
 dq_status dq_freq_consume(dq_freq* f, const dq_column* columns, int n_columns, int64_t n_rows);
+/* dq_freq_consume of one Arrow batch (dq_plan_consume_arrow's rules; all the batch's columns). */
+dq_status dq_freq_consume_arrow(dq_freq* f, const struct ArrowSchema* schema, const struct ArrowArray* array,
+                                int flags);
 dq_status dq_freq_get_summary(dq_freq* f, dq_freq_summary* out);
 /* Number of groups and total encoded key bytes (to size dq_freq_export's buffers). */
 dq_status dq_freq_size(dq_freq* f, int64_t* n_groups, int64_t* key_bytes);

@@ -1279,3 +1279,119 @@ def histogram_metric(state: FrequenciesAndNumRows, max_detail_bins: int = 1000):
         "number_of_bins": len(state.frequencies),
         "values": {k[0]: (c, c / state.num_rows) for k, c in top},
     }
+
+
+# ---------------------------------------------------------------------------- ColumnProfiler
+# `ColumnProfiler.profile` (profiles/ColumnProfiler.scala:91-208) restated over the functions
+# above: pass 1 (:220-238) Completeness + ApproxCountDistinct (+ DataType for string columns) +
+# Size; type decision `DataType.determineType` (DataType.scala:116-143) or the schema type
+# (:401-420); pass 2 (:240-251, casts :427-445) Min/Max/Mean/StdDev/Sum of the numeric columns,
+# string columns typed Integral / Fractional cast to LongType / DoubleType first; pass 3
+# (:535-606) exact histograms of the columns with approxNumDistinct <= threshold:
+# (value.toString, count), NULL -> "NullValue", ratio = count / sum of the column's counts.
+DT_UNKNOWN, DT_FRACTIONAL, DT_INTEGRAL, DT_BOOLEAN, DT_STRING = 0, 1, 2, 3, 4  # DataTypeInstances
+
+
+def spark_string_to_long(s: str) -> Optional[int]:
+    """Spark 2.2.2 Cast(StringType -> LongType) = `UTF8String.toLong`: optional sign, digits,
+    optionally '.' and digits (truncated); no trimming; NULL on anything else or overflow."""
+    b = s.encode("utf-8")
+    if not b:
+        return None
+    neg = b[:1] == b"-"
+    i = 1 if (neg or b[:1] == b"+") else 0
+    if i and len(b) == 1:
+        return None
+    r = 0
+    while i < len(b):
+        c = b[i]
+        i += 1
+        if c == 0x2E:  # '.'
+            break
+        if not 0x30 <= c <= 0x39:
+            return None
+        r = r * 10 + (c - 0x30)
+    if any(not 0x30 <= c <= 0x39 for c in b[i:]):
+        return None
+    r = -r if neg else r
+    return r if -(1 << 63) <= r < (1 << 63) else None
+
+
+def determine_type(counts: Sequence[int]) -> int:
+    """`DataType.determineType` (DataType.scala:116-143) on the DataTypeHistogram counts
+    (null, fractional, integral, boolean, string)."""
+    n_null, n_frac, n_int, n_bool, n_str = counts
+    total = sum(counts)
+    if total == 0 or n_null == total:
+        return DT_UNKNOWN
+    if n_str > 0 or (n_bool > 0 and (n_int > 0 or n_frac > 0)):
+        return DT_STRING
+    if n_bool > 0:
+        return DT_BOOLEAN
+    if n_frac > 0:
+        return DT_FRACTIONAL
+    return DT_INTEGRAL
+
+
+def _schema_type(dtype: str) -> int:
+    """extractGenericStatistics' schema mapping (ColumnProfiler.scala:401-420)."""
+    if dtype in ("int16", "int32", "int64"):
+        return DT_INTEGRAL
+    if dtype in _FRACTIONAL:
+        return DT_FRACTIONAL
+    if dtype == "bool":
+        return DT_BOOLEAN
+    return DT_UNKNOWN
+
+
+def column_profiles(table: OTable, threshold: int = 120,
+                    predefined: Optional[Dict[str, int]] = None) -> Dict[str, dict]:
+    """{column: profile fields} as ColumnProfiler.profile builds them (no KLL, the reference's
+    default).  Numeric fields are the Spark one-partition values (sequential sum, Welford).
+    `predefined` types replace both inference and the schema type (typeOf, :31-46)."""
+    predefined = predefined or {}
+    n_rows = len(next(iter(table.values())).values) if table else 0
+    out: Dict[str, dict] = {}
+    for name, col in table.items():
+        comp = completeness_state(table, name)
+        words = approx_count_distinct_state(table, name).words
+        approx = int(hll_count(words))  # Double.toLong of a rounded count
+        p = {"completeness": comp.metric_value(), "approx": approx, "words": tuple(words),
+             "typeCounts": {}, "inferred": False}
+        if name in predefined:
+            p["dataType"] = predefined[name]
+        elif col.dtype == "string":
+            counts = datatype_state(table, name)
+            p["dataType"] = determine_type(counts)
+            p["inferred"] = True
+            p["typeCounts"] = dict(zip(("Unknown", "Fractional", "Integral", "Boolean", "String"), counts))
+        else:
+            p["dataType"] = _schema_type(col.dtype)
+        # pass 2 on the (cast) column
+        if p["dataType"] in (DT_INTEGRAL, DT_FRACTIONAL):
+            if col.dtype == "string":
+                if p["dataType"] == DT_INTEGRAL:
+                    cast = OColumn("int64", [None if v is None else spark_string_to_long(v) for v in col.values])
+                else:
+                    cast = OColumn("float64", [None if v is None else java_parse_double(v) for v in col.values])
+            else:
+                cast = col
+            t1 = {name: cast}
+            for key, fn in (("minimum", min_state), ("maximum", max_state), ("mean", mean_state),
+                            ("stdDev", stddev_state), ("sum", sum_state)):
+                st = fn(t1, name)
+                p[key] = None if st is None else st.metric_value()
+            p["numeric_values"] = [v for v in cast.values if v is not None]
+        # pass 3
+        p["histogram"] = None
+        if approx <= threshold and p["dataType"] in (DT_STRING, DT_BOOLEAN, DT_INTEGRAL, DT_FRACTIONAL) \
+                and col.dtype in ("string", "bool", "float64", "float32", "int32", "int64", "int16"):
+            counts: Dict[str, int] = {}
+            for v in col.values:
+                k = "NullValue" if v is None else _spark_cast_string(v, col.dtype)
+                counts[k] = counts.get(k, 0) + 1
+            total = sum(counts.values())
+            p["histogram"] = {k: (c, c / total) for k, c in counts.items()}
+        out[name] = p
+    out["__numRecords__"] = n_rows  # type: ignore[assignment]
+    return out

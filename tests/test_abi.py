@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
     # the ctypes signature table covers the whole header too
     assert declared == set(_lib.SIGNATURES), declared ^ set(_lib.SIGNATURES)
-    assert _lib.lib().dq_abi_version() == 3
+    assert _lib.lib().dq_abi_version() == 4
 
 
 def test_library_reports_no_device_without_gpu_cleanly():

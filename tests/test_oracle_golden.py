@@ -147,3 +147,26 @@ def test_hll_rare_rank_fixture_is_rare():
             else:
                 assert (x >> 32) & 0x7FFFFF == 0 and (x >> 23) & 0xFFFFFFFF != 0
     assert any(e["kind"] == "rare2" for e in fx["int64"])
+
+
+@pytest.mark.parametrize("case", KA["profile_cases"], ids=[c["id"] for c in KA["profile_cases"]])
+def test_oracle_profiles_known_answers(case):
+    """O.column_profiles pinned by every ColumnProfilerTest.scala known answer."""
+    spec = KA["tables"][case["table"]]
+    cols = case["restrict"] or list(spec)
+    ot = oracle_table({c: spec[c] for c in cols})
+    p = O.column_profiles(ot, case["threshold"], {k: int(v) for k, v in case["predefined"].items()})[case["column"]]
+    e = case["expect"]
+    if "histogram_values" in e:
+        assert p["histogram"] == {k: tuple(v) for k, v in e["histogram_values"].items()}, case["source"]
+        return
+    assert ("mean" in p) == (e["kind"] == "numeric"), case["source"]
+    assert (p["completeness"], p["approx"], p["dataType"], p["inferred"], p["typeCounts"]) == \
+        (e["completeness"], e["approx"], e["dataType"], e["inferred"], e["typeCounts"]), case["source"]
+    if e["histogram"] is None:
+        assert p["histogram"] is None
+    else:
+        assert p["histogram"] == {k: tuple(v) for k, v in e["histogram"]["values"].items()}
+    if e["kind"] == "numeric":
+        for f in ("mean", "maximum", "minimum", "sum", "stdDev"):
+            assert p[f] == e[f], (case["source"], f)
