@@ -37,7 +37,9 @@ def parse_args():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--rows", type=int, default=1_000_000_000, help="rows per GPU")
     p.add_argument("--cpu-sample-rows", type=int, default=256_000_000)
-    p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, nproc)")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="0 = every CPU this process may use (sched_getaffinity, capped by OMP_NUM_THREADS: "
+                        "the GPU box's host share for one GPU)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-side-passes", action="store_true",
                    help="skip the scan_without_hll pass (profiler runs: the kernel trace then "
@@ -137,6 +139,19 @@ def scan_without_hll(table, device: int, steps: int):
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS}
 
 
+def host_cpu_share() -> int:
+    """The host cores this run may use: the CPUs in its affinity mask, capped by OMP_NUM_THREADS
+    when the launcher sets it (the GPU box sets 16 per GPU; nproc there counts the whole host)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
 def cpu_baseline(sample_rows: int, threads: int):
     """The oracle's C restatement (Spark semantics: sequential per-partition aggregation,
     per-row Welford, partition states merged with State.sum) on `threads` host threads."""
@@ -148,6 +163,7 @@ def cpu_baseline(sample_rows: int, threads: int):
                 "sample": "unavailable: %s" % e}
     secs = cdq_oracle.time_c2_scan(sample_rows, threads)
     return {"value": sample_rows / secs, "unit": "rows/s", "cores": threads, "kind": "port",
+            "host_cpus": os.cpu_count(),
             "sample": "%d rows x 8 cols (C2 distributions, 5%% NULL), 65 analyzers (8 HLL), C restatement "
                       "of Spark 2.2.2 aggregation (oracle/dq_oracle.c), %d threads, %.2f s"
                       % (sample_rows, threads, secs)}
@@ -308,34 +324,58 @@ def run_c3(args, world, rank, local):
     }
 
 
+def _column_bytes(col) -> float:
+    """Arrow bytes of one column: values (utf8: int32 offsets + chars; bool: bits) + validity bits."""
+    n = col.length
+    valid = n / 8.0 if col.validity is not None else 0.0
+    if col.dtype == "string":
+        return 4.0 * (n + 1) + float(col.values.numel() - 16) + valid
+    if col.dtype == "bool":
+        return n / 8.0 + valid
+    return float(n * col.values.element_size()) + valid
+
+
+def _step_roofline(bytes_per_step: float, step_s: float, what: str, traffic=None):
+    achieved = bytes_per_step / step_s / 1e9
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel_ms": step_s * 1e3,
+            "algorithmic_bytes_per_launch": bytes_per_step, "timed_unit": what}
+
+
 def run_c4(args, world, rank, local):
-    """Uniqueness/Distinctness/Entropy/CountDistinct (one GPU group-by) + Histogram on C4."""
-    import torch
+    """Uniqueness/Distinctness/Entropy/CountDistinct (one GPU group-by) + Histogram on C4; on N
+    GPUs every rank groups its own shard and the tables meet in the key-hash all-to-all."""
     import deequ_amd as d
-    if world > 1:
-        raise SystemExit("c4 runs on one GPU (the key-hash all-to-all is a separate path)")
-    data = make_c4_batches(args.c4_rows, args.c4_batch, args.c4_distinct, rank, local)
+    from deequ_amd.distributed import ShardedTable
+    shard = make_c4_batches(args.c4_rows, args.c4_batch, args.c4_distinct, rank, local)
+    data = ShardedTable(shard) if world > 1 else shard
     analyzers = [d.Uniqueness(["key"]), d.Distinctness(["key"]), d.Entropy("key"),
                  d.CountDistinct(["key"]), d.Histogram("key")]
 
     def step(ev=None):
-        ctx = d.AnalysisRunner.onData(data).addAnalyzers(analyzers).run()
-        return ctx
+        return d.AnalysisRunner.onData(data).addAnalyzers(analyzers).run()
     elapsed, _, ctx = _timed(args, world, step)
     metrics = {str(a): ctx.metric(a).value.get() for a in analyzers[:4]}
     hist = ctx.metric(analyzers[4]).value.get()
-    in_bytes = args.c4_rows * (4 + 12 + 1.0 / 8)
+    in_bytes = sum(_column_bytes(b.columns["key"]) for b in shard.batches())
+    groups = metrics[str(analyzers[3])] / world  # the groups this rank's share of the table holds
+    # SURVEY §8(d) C4: input + one write of the final table (8 B hash + 8 B count + 8 B key ref)
+    algo = in_bytes + 24.0 * groups
     step_s = elapsed / args.steps
     return {
-        "metric": "rows/sec for the frequency family (C4 group-by)", "value": args.c4_rows * args.steps / elapsed,
+        "metric": "rows/sec for the frequency family (C4 group-by)",
+        "value": args.c4_rows * world * args.steps / elapsed,
         "unit": "rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "utf8 keys, int64 counts",
         "data": "synthetic 12-digit keys uniform in [0, %d), 1%% NULL, generated in HBM" % args.c4_distinct,
         "config": {"workload": "C4: %d rows/GPU in %d-row utf8 batches; Uniqueness, Distinctness, Entropy, "
                                "CountDistinct + Histogram, all from one GPU group-by of the key (the "
-                               "reference runs Histogram as a second job)" % (args.c4_rows, args.c4_batch)},
-        "input_gbs_per_pass": in_bytes / step_s / 1e9,
+                               "reference runs Histogram as a second job)%s"
+                               % (args.c4_rows, args.c4_batch,
+                                  "; key-hash all-to-all over %d ranks" % world if world > 1 else "")},
+        "roofline": _step_roofline(algo, step_s, "one whole group-by step per GPU (stage, sort, aggregate, "
+                                                 "metrics, top-N), HBM-bound by design"),
         "check": dict(metrics, histogram_bins=hist.numberOfBins),
     }
 
@@ -446,7 +486,9 @@ def run_c1(args, world, rank, local):
     AnalysisRunner.onData(...).addAnalyzers(...).run() per step (plan, fused scan, states,
     metrics), every rank on its own 10M-row Item shard."""
     import deequ_amd as d
-    data = make_c1_table(args.c1_rows, rank, local)
+    from deequ_amd.distributed import ShardedTable
+    shard = make_c1_table(args.c1_rows, rank, local)
+    data = ShardedTable(shard) if world > 1 else shard  # metrics of the union of the shards
     analyzers = c1_analyzers()
 
     def step(ev=None):
@@ -468,12 +510,12 @@ def run_c1(args, world, rank, local):
 
 def run_c5(args, world, rank, local):
     """ColumnProfilerRunner over the C5 table: 3 passes (generic stats + HLL + DataType; numeric
-    stats; exact histograms of the low-cardinality columns)."""
-    import deequ_amd as d
+    stats; exact histograms of the low-cardinality columns); on N GPUs every rank profiles its
+    shard and the passes' states / tables meet in the collectives of a ShardedTable."""
+    from deequ_amd.distributed import ShardedTable
     from deequ_amd.profiles import ColumnProfilerRunner
-    if world > 1:
-        raise SystemExit("c5 runs on one GPU")
-    data = make_c5_table(args.c5_rows, rank, local)
+    shard = make_c5_table(args.c5_rows, rank, local)
+    data = ShardedTable(shard) if world > 1 else shard
 
     def step(ev=None):
         return ColumnProfilerRunner().onData(data).run()
@@ -481,17 +523,28 @@ def run_c5(args, world, rank, local):
     p = profiles.profiles
     n_hist = sum(1 for c in p.values() if c.histogram is not None)
     step_s = elapsed / args.steps
+    cols = shard.columns
+    pass1 = sum(_column_bytes(c) for c in cols.values())
+    numeric = [n for n, c in cols.items() if c.dtype in ("int64", "float64")]
+    cast = [n for n, c in cols.items() if c.dtype == "string" and p[n].dataType in (1, 2)]
+    rows = args.c5_rows
+    # pass 2: numeric columns + each cast string column read once, cast written (8 B + bit) and scanned
+    pass2 = sum(_column_bytes(cols[n]) for n in numeric) + sum(_column_bytes(cols[n]) + 2 * rows * (8 + 1 / 8.0)
+                                                                for n in cast)
+    pass3 = sum(_column_bytes(cols[n]) for n, c in p.items() if c.histogram is not None)
     return {
-        "metric": "rows/sec for ColumnProfilerRunner (C5)", "value": args.c5_rows * args.steps / elapsed,
+        "metric": "rows/sec for ColumnProfilerRunner (C5)", "value": args.c5_rows * world * args.steps / elapsed,
         "unit": "rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "int64/fp64/utf8/bool", "data": "synthetic C5 table generated in HBM (seed 5, 5% NULL)",
-        "config": {"workload": "C5: %d rows x 100 columns (40 int64, 30 fp64, 10 low- and 10 high-cardinality "
+        "config": {"workload": "C5: %d rows/GPU x 100 columns (40 int64, 30 fp64, 10 low- and 10 high-cardinality "
                                "utf8, 10 bool); ColumnProfilerRunner, 3 passes, KLL off (reference default)"
                                % args.c5_rows},
+        "roofline": _step_roofline(pass1 + pass2 + pass3, step_s,
+                                   "one whole profile per GPU (3 passes; bytes = every column read by each pass)"),
         "check": {"columns": len(p), "histograms": n_hist,
                   "s00_distinct": p["s00"].approximateNumDistinctValues,
-                  "l00_completeness": p["l00"].completeness},
+                  "l00_completeness": p["l00"].completeness, "numRecords": profiles.numRecords},
     }
 
 
@@ -527,8 +580,27 @@ def _timed(args, world, step):
     return elapsed, kernel_ms, out
 
 
+def _spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: start N ranks (one process per GPU) through
+    torch.distributed.run as a CHILD process -- nothing here has touched the GPU yet -- and
+    return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse_args()
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and world_env is None:
+        sys.exit(_spawn_ranks(args.gpus))
+    if world_env is not None and int(world_env) != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%s: launch one rank per GPU" % (args.gpus, world_env))
     import torch
     import torch.distributed as dist
 
@@ -637,7 +709,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_side_passes:
         result["scan_without_hll"] = scan_without_hll(table, local, args.steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        threads = args.cpu_threads or host_cpu_share()
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample_rows, threads)
     if rank == 0:
         print(json.dumps(result))

@@ -157,6 +157,13 @@ SIGNATURES = {
                                         POINTER(c_int64)]),
     "dq_freq_summary_from_histogram": (c_int, [POINTER(c_int64), c_int64, POINTER(c_int64), c_int64, c_int64,
                                                POINTER(DqFreqSummary)]),
+    "dq_group_unique_id": (c_int, [POINTER(c_uint8)]),
+    "dq_group_create": (c_int, [c_void_p, c_int, c_int, POINTER(c_uint8), POINTER(c_void_p)]),
+    "dq_group_destroy": (c_int, [c_void_p]),
+    "dq_group_allgather_merge": (c_int, [c_void_p, POINTER(DqState), c_int]),
+    "dq_states_merge_ranks": (c_int, [POINTER(DqState), c_int, c_int, POINTER(DqState)]),
+    "dq_group_freq_exchange": (c_int, [c_void_p, c_void_p, c_void_p, POINTER(c_int64)]),
+    "dq_group_freq_summary": (c_int, [c_void_p, c_void_p, c_int64, POINTER(DqFreqSummary)]),
 }
 
 _lib = None

@@ -422,43 +422,6 @@ class DataType(ScanShareableAnalyzer):
             return HistogramMetric(self.column, Failure(wrap_if_necessary(empty_state_exception(self))))
         return HistogramMetric(self.column, _S(data_type_distribution(state)))
 
-    # column types whose frequency table groups exactly as Histogram's string cast does
-    # (distinct values <-> distinct strings); floats are excluded: Histogram merges NaN payloads
-    SHARES_FREQUENCIES = ("string", "bool", "int8", "int16", "int32", "int64")
-
-    def metricFromFrequencies(self, state):
-        """The metric from the frequency table of `column` that a FrequencyBasedAnalyzer of the
-        same run already built (no second group-by).  Histogram.scala:54-69 groups
-        `col.cast(string)` with NULL replaced by "NullValue"; the shared table holds the
-        non-NULL groups, so the NULL bin is numRows - (grouped rows), plus the count of a
-        literal "NullValue" string when the column holds one (the replacement merges them)."""
-        from .metrics import Distribution, DistributionValue, HistogramMetric, Success as _S
-        if state is None:
-            return HistogramMetric(self.column, Failure(wrap_if_necessary(empty_state_exception(self))))
-        try:
-            from .frequencies import decode_key
-            from .javafmt import spark_cast_to_string
-            dtype = state.table.dtypes[0]
-            s = state.summary()
-            n_rows = s.num_rows
-            null_key = NULL_FIELD_REPLACEMENT.encode("utf-8")
-            literal = state.table.lookup(null_key) if dtype == "string" else 0
-            null_bin = (n_rows - s.grouped_rows) + literal
-            counts, keys = state.table.top(self.maxDetailBins)
-            items = []
-            for k, c in zip(keys, counts.tolist()):
-                if dtype == "string" and k == null_key:
-                    continue  # merged into the NULL bin
-                items.append((spark_cast_to_string(decode_key(k, [dtype])[0], dtype), c))
-            if null_bin:
-                items.append((NULL_FIELD_REPLACEMENT, null_bin))
-            items.sort(key=lambda kv: (-kv[1], kv[0].encode("utf-8")))
-            bins = s.num_groups + (1 if null_bin and not literal else 0)
-            values = {k: DistributionValue(c, c / n_rows) for k, c in items[:self.maxDetailBins]}
-            return HistogramMetric(self.column, _S(Distribution(values, bins)))
-        except Exception as e:  # noqa: BLE001
-            return self.toFailureMetric(e)
-
     def toFailureMetric(self, error):
         from .metrics import HistogramMetric
         return HistogramMetric(self.column, Failure(wrap_if_necessary(error)))

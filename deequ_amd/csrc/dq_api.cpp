@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -1652,3 +1653,6 @@ extern "C" dq_status dq_cast_utf8(dq_ctx* ctx, const dq_column* src, int64_t n_r
 
 // Arrow C Data Interface entry points over dq_plan_consume / dq_freq_consume.
 #include "dq_arrow.inc"
+
+// RCCL groups: the sharded path's collectives for drivers that are not torch.
+#include "dq_group.inc"

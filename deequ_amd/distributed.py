@@ -50,6 +50,110 @@ def allgather_merge(states, n_ops: int, group=None, device: Optional[int] = None
     return out
 
 
+# ---------------------------------------------------------------- sharded datasets
+class ShardedTable:
+    """A dataset spread over the ranks of a process group: rank r holds the row shard `local`
+    (a Table / PartitionedTable / ArrowTable), the dataset is the union of all shards -- the
+    contiguous row ranges of SURVEY §8(e), as Spark's partitions are spread over executors.
+
+    Every entry point that takes data (AnalysisRunner, ColumnProfiler, run_scan,
+    compute_frequencies) accepts a ShardedTable and is then COLLECTIVE: every rank calls it with
+    the same analyzers, scans only its own shard on its own GPU, and gets the metrics of the
+    whole dataset.  Scan states meet in one all-gather folded in rank order (merge_scan_results),
+    frequency tables in the key-hash all-to-all (exchange_frequencies)."""
+
+    def __init__(self, local, group=None):
+        self.local = local
+        self.group = group
+
+    @property
+    def schema(self):
+        return self.local.schema
+
+    def batches(self):
+        return self.local.batches()
+
+    def count(self) -> int:
+        """Rows of this rank's shard (what the local staging is sized for)."""
+        return self.local.count()
+
+    @property
+    def num_rows(self) -> int:
+        return self.count()
+
+    def global_count(self) -> int:
+        """Rows of the whole dataset (collective)."""
+        import torch
+        import torch.distributed as dist
+        n = torch.tensor([self.local.count()], dtype=torch.int64)
+        if _comm_device(self.group) == "cuda":
+            n = n.to(_cuda_device())
+        dist.all_reduce(n, op=dist.ReduceOp.SUM, group=self.group)
+        return int(n.item())
+
+    def with_local(self, local) -> "ShardedTable":
+        return ShardedTable(local, self.group)
+
+
+def is_sharded(data) -> bool:
+    return isinstance(data, ShardedTable)
+
+
+def _cuda_device() -> int:
+    from .engine import current_device
+    return current_device()
+
+
+def merge_scan_results(local, error, kinds, group=None):
+    """The fused scan's results of every rank -> the whole dataset's (collective).
+
+    `local` = this rank's list of DqState / OpUnsupported (None if its scan raised `error`).
+    First every rank learns every rank's outcome (one all_gather_object of a few bytes): if any
+    rank's aggregation failed, every rank raises -- the all-fail scope of
+    AnalysisRunner.scala:320-323 over the whole dataset.  Then the POD states meet in ONE
+    all-gather and fold in rank order (allgather_merge); an op unsupported on any rank's shard is
+    unsupported for the dataset (the per-op scope of :340-353)."""
+    import torch.distributed as dist
+    from .engine import OpUnsupported
+    n = len(kinds)
+    world = dist.get_world_size(group)
+    unsup = [] if local is None else [i for i, r in enumerate(local) if isinstance(r, OpUnsupported)]
+    outcome = (None if error is None else "%s: %s" % (type(error).__name__, error), unsup)
+    outcomes = [None] * world
+    dist.all_gather_object(outcomes, outcome, group=group)
+    for r, (err, _) in enumerate(outcomes):
+        if err is not None:
+            if error is not None:
+                raise error
+            raise L.DeequAmdError(L.DQ_ERR_STATE, "the fused scan failed on rank %d: %s" % (r, err))
+    arr = (L.DqState * max(1, n))()
+    for i in range(n):
+        if isinstance(local[i], OpUnsupported):
+            arr[i] = L.DqState()
+            arr[i].kind = kinds[i]  # an empty state: the identity of Analyzers.merge
+        else:
+            arr[i] = local[i]
+    merged = allgather_merge(arr, n, group=group,
+                             device=_cuda_device() if _comm_device(group) == "cuda" else None)
+    out = [L.DqState.from_buffer_copy(merged[i]) for i in range(n)]
+    for r, (_, bad) in enumerate(outcomes):
+        for i in bad:
+            out[i] = OpUnsupported(L.UnsupportedOnGpu(
+                L.DQ_ERR_UNSUPPORTED, "rank %d's shard held input the GPU cannot evaluate exactly for this op" % r))
+    return out
+
+
+def allreduce_flag(flag: bool, group=None) -> bool:
+    """True on every rank if `flag` is true on any rank (collective)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1 if flag else 0], dtype=torch.int64)
+    if _comm_device(group) == "cuda":
+        t = t.to(_cuda_device())
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return bool(t.item())
+
+
 # ---------------------------------------------------------------- frequency family
 # The one real exchange step of the path (SURVEY §8(e)).  Spark shuffles partial group counts by
 # key hash into `spark.sql.shuffle.partitions` and finishes the aggregate per partition
@@ -181,6 +285,16 @@ class _DistributedTableView:
             cut = items[n - 1][0]
             items = [ck for ck in items if ck[0] >= cut]
         return np.array([c for c, _ in items], dtype=np.int64), [k for _, k in items]
+
+    def lookup(self, key: bytes) -> int:
+        """Count of one encoded key over the whole dataset (its owner holds it; collective)."""
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([self._s.owned.lookup(key)], dtype=torch.int64)
+        if _comm_device(self._s.group) == "cuda":
+            t = t.to(self._s.owned.torch_device)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self._s.group)
+        return int(t.item())
 
     def export(self):
         fr = self._s.frequencies(raw=True)

@@ -163,9 +163,7 @@ class OpUnsupported:
         self.error = error
 
 
-def run_scan_raw(specs: Sequence[OpSpec], data) -> List:
-    """One fused GPU pass over every batch of `data` for the given ops; the POD dq_states
-    (copies, in op order) for each analyzer's fromAggregationResult, or OpUnsupported."""
+def _scan_local(specs: Sequence[OpSpec], data) -> List:
     plan = Plan(specs, data.schema)
     try:
         for batch in data.batches():
@@ -183,15 +181,30 @@ def run_scan_raw(specs: Sequence[OpSpec], data) -> List:
         plan.close()
 
 
-def run_scan(analyzers: Sequence, data) -> Dict[object, Optional[State]]:
-    """One fused GPU pass over every batch of `data` for all `analyzers`."""
-    schema = data.schema
-    specs = [op_spec_for(a, schema) for a in analyzers]
-    plan = Plan(specs, schema)
+def run_scan_raw(specs: Sequence[OpSpec], data) -> List:
+    """One fused GPU pass over every batch of `data` for the given ops; the POD dq_states
+    (copies, in op order) for each analyzer's fromAggregationResult, or OpUnsupported.  With a
+    ShardedTable every rank scans its shard and the results are those of the whole dataset
+    (collective, distributed.merge_scan_results)."""
+    from .distributed import is_sharded, merge_scan_results
+    if not is_sharded(data):
+        return _scan_local(specs, data)
+    local, error = None, None
     try:
-        for batch in data.batches():
-            plan.consume(batch)
-        states = plan.finish()
-    finally:
-        plan.close()
+        local = _scan_local(specs, data.local)
+    except Exception as e:  # noqa: BLE001 - reported to every rank before anyone raises
+        error = e
+    return merge_scan_results(local, error, [s.kind for s in specs], data.group)
+
+
+def run_scan(analyzers: Sequence, data) -> Dict[object, Optional[State]]:
+    """One fused GPU pass over every batch of `data` for all `analyzers` (collective over the
+    ranks for a ShardedTable); an op the GPU could not evaluate exactly raises."""
+    schema = data.schema
+    raw = run_scan_raw([op_spec_for(a, schema) for a in analyzers], data)
+    states = []
+    for r in raw:
+        if isinstance(r, OpUnsupported):
+            raise r.error
+        states.append(state_from_dq(r))
     return dict(zip(analyzers, states))

@@ -251,7 +251,11 @@ def _unpack_groups(groups, n: int, raw: bytes) -> Tuple[np.ndarray, List[bytes]]
 
 
 def compute_frequencies(data, grouping_columns: Sequence[str], histogram: bool = False) -> "FrequenciesAndNumRows":
-    """FrequencyBasedAnalyzer.computeFrequencies over every batch of `data` (one pass)."""
+    """FrequencyBasedAnalyzer.computeFrequencies over every batch of `data` (one pass); over a
+    ShardedTable, the key-hash exchanged table of the whole dataset (collective)."""
+    from .distributed import compute_frequencies_distributed, is_sharded
+    if is_sharded(data):
+        return compute_frequencies_distributed(data.local, grouping_columns, histogram, group=data.group)
     schema = data.schema
     table = FrequencyTable(grouping_columns, {c: schema[c] for c in schema}, histogram)
     table.reserve(data.count())

@@ -233,8 +233,27 @@ def _cast_numeric_string_columns(columns, data, generic):
             targets[c] = "float64"
     if not targets:
         return data
+    from .distributed import allreduce_flag, is_sharded
+    if is_sharded(data):  # every rank casts its shard; a rank's unsupported value fails them all
+        local, error = None, None
+        try:
+            local = _cast_batches(data.local, targets)
+        except L.UnsupportedOnGpu as e:
+            error = e
+        if allreduce_flag(error is not None, data.group):
+            raise error or L.UnsupportedOnGpu(L.DQ_ERR_UNSUPPORTED, "another rank's shard needs Spark's exact "
+                                                                  "(slow-path) string to double parse")
+        return data.with_local(local)
+    return _cast_batches(data, targets)
+
+
+def _cast_batches(data, targets):
+    from .arrow import ArrowBatch
+    from .table import PartitionedTable, Table
     parts = []
     for batch in data.batches():
+        if isinstance(batch, ArrowBatch):  # zero-copy host view of the record batch
+            batch = Table.from_arrow(batch.batch)
         cols = OrderedDict()
         for name, col in batch.columns.items():
             cols[name] = cast_string_column(col, targets[name]) if name in targets else col
@@ -292,8 +311,7 @@ def compute_histograms(data, target_columns: Sequence[str],
                        expected_groups: Optional[Dict[str, int]] = None) -> Dict[str, Distribution]:
     """computeHistograms (:564-606): exact (column, value.toString) counts, NULL -> "NullValue",
     one GPU group-by per target column; ratio = count / (sum of the column's counts)."""
-    from .frequencies import FrequencyTable, decode_key
-    from .javafmt import spark_cast_to_string
+    from .frequencies import FrequencyTable
     schema = data.schema
     out = {}
     bool_cols = [c for c in target_columns if schema[c] == "bool" and _IDENT.match(c)]
@@ -303,6 +321,12 @@ def compute_histograms(data, target_columns: Sequence[str],
         if c in out:
             continue
         dtype = schema[c]
+        from .distributed import is_sharded
+        if is_sharded(data):  # the key-hash exchanged table of the whole dataset (collective)
+            from .frequencies import compute_frequencies
+            counts, keys = compute_frequencies(data, [c], histogram=True).table.export()
+            out[c] = _histogram_distribution(counts, keys, dtype)
+            continue
         table = FrequencyTable([c], dict(schema), histogram=True)
         if expected_groups and c in expected_groups:  # the pass-1 estimate (<= the threshold)
             table.expect_groups(int(expected_groups[c]) + 1)
@@ -312,15 +336,22 @@ def compute_histograms(data, target_columns: Sequence[str],
             counts, keys = table.export()
         finally:
             table.close()
-        per_value: Dict[str, int] = {}
-        for k, n in zip(keys, counts.tolist()):
-            v = decode_key(k, [dtype], histogram=True)[0]
-            s = NULL_FIELD_REPLACEMENT if v is None else spark_cast_to_string(v, dtype)
-            per_value[s] = per_value.get(s, 0) + int(n)
-        total = sum(per_value.values())
-        values = {s: DistributionValue(n, n / total) for s, n in sorted(per_value.items())}
-        out[c] = Distribution(values, len(values))
+        out[c] = _histogram_distribution(counts, keys, dtype)
     return out
+
+
+def _histogram_distribution(counts, keys, dtype) -> Distribution:
+    """(value.toString, count) pairs of one column, ratio = count / sum (:590-602)."""
+    from .frequencies import decode_key
+    from .javafmt import spark_cast_to_string
+    per_value: Dict[str, int] = {}
+    for k, n in zip(keys, list(counts)):
+        v = decode_key(k, [dtype], histogram=True)[0]
+        s = NULL_FIELD_REPLACEMENT if v is None else spark_cast_to_string(v, dtype)
+        per_value[s] = per_value.get(s, 0) + int(n)
+    total = sum(per_value.values())
+    values = {s: DistributionValue(n, n / total) for s, n in sorted(per_value.items())}
+    return Distribution(values, len(values))
 
 
 def _create_profiles(columns, generic, numeric, histograms) -> ColumnProfiles:

@@ -417,6 +417,45 @@ dq_status dq_freq_count_histogram(dq_freq* f, int64_t* hist, int64_t n_bins, int
 dq_status dq_freq_summary_from_histogram(const int64_t* hist, int64_t n_bins, const int64_t* big,
                                          int64_t n_big, int64_t num_rows, dq_freq_summary* out);
 
+/* ---------------------------------------------------------------- multi-GPU groups (RCCL)
+ * One process (or one JVM executor thread) per GPU, each with its own dq_ctx, joined into a
+ * dq_group -- an RCCL communicator over xGMI -- so that a driver that is not torch (the JNI shim)
+ * can run the sharded path.  Each rank scans its own row shard; the group then
+ * replaces Spark's final aggregation (AnalysisRunner.scala:313: partial states of every partition
+ * merged by the aggregate) and the shuffle of the frequency family (GroupingAnalyzers.scala:
+ * 67-72).  Every dq_group_* call is collective: all ranks call it in the same order. */
+typedef struct dq_group dq_group;
+
+#define DQ_GROUP_ID_BYTES 128
+
+/* A fresh group id on the rank that creates the group (ncclGetUniqueId); the caller ships the
+ * bytes to every other rank (e.g. through the Spark driver) before dq_group_create. */
+dq_status dq_group_unique_id(uint8_t id[DQ_GROUP_ID_BYTES]);
+dq_status dq_group_create(dq_ctx* ctx, int n_ranks, int rank, const uint8_t id[DQ_GROUP_ID_BYTES],
+                          dq_group** out);
+dq_status dq_group_destroy(dq_group* g);
+
+/* In place: states[0..n_ops) of this rank's shard become those of the whole dataset -- ONE
+ * all-gather of the POD states over RCCL, then the fold in rank order of dq_states_merge_ranks
+ * (deterministic: every rank computes the same bytes). */
+dq_status dq_group_allgather_merge(dq_group* g, dq_state* states, int n_ops);
+
+/* The fold dq_group_allgather_merge applies (host only): gathered = n_ranks blocks of n_ops
+ * states in rank order; out[i] = Analyzers.merge of gathered[r * n_ops + i] over r = 0, 1, ...
+ * (State.sum per kind, Analyzer.scala:367-386; e.g. StandardDeviation.scala:37-44). */
+dq_status dq_states_merge_ranks(const dq_state* gathered, int n_ranks, int n_ops, dq_state* out);
+
+/* The key-hash exchange: every rank partitions `local` by owner (dq_freq_partition), the parts
+ * travel in one RCCL all-to-all (grouped send/recv), and each rank merges what it receives into
+ * `owned` (an empty table with the same key columns) -- which then holds the keys this rank owns,
+ * disjoint across ranks.  *num_rows = the dataset's numRows (sum over ranks). */
+dq_status dq_group_freq_exchange(dq_group* g, dq_freq* local, dq_freq* owned, int64_t* num_rows);
+
+/* dq_freq_summary of the whole dataset from the owned tables: the count-of-counts histograms
+ * all-reduced (sum) over RCCL, counts beyond the histogram all-gathered, then the fixed-order
+ * dq_freq_summary_from_histogram -- equal, bit for bit, to a single table over all rows. */
+dq_status dq_group_freq_summary(dq_group* g, dq_freq* owned, int64_t num_rows, dq_freq_summary* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -130,3 +130,49 @@ def test_allgather_merge_equals_whole_table(world):
                 assert got.value == want.max_value
             elif kind == L.DQ_OP_APPROX_COUNT_DISTINCT:
                 assert list(got.words) == list(want.words)
+
+
+@pytest.mark.parametrize("world", [1, 2, 5])
+def test_c_abi_rank_fold_equals_whole_table(world):
+    """dq_states_merge_ranks -- the fold dq_group_allgather_merge applies after its RCCL
+    all-gather -- on the shards' states equals the whole table's states, and the same bytes as
+    the torch.distributed route's fold."""
+    from deequ_amd import _lib as L
+    from deequ_amd.distributed import merge_raw
+    from deequ_amd.group import merge_ranks
+    n = 3000
+    shards = [_states_for(_table(r * n // world, (r + 1) * n // world)) for r in range(world)]
+    n_ops = len(shards[0])
+    gathered = (L.DqState * (world * n_ops))()
+    for r, local in enumerate(shards):
+        for i, (kind, st) in enumerate(local):
+            gathered[r * n_ops + i] = _to_dq(kind, st)
+    out = merge_ranks(gathered, world, n_ops)
+    for i in range(n_ops):
+        acc = L.DqState.from_buffer_copy(gathered[i])
+        for r in range(1, world):
+            acc = merge_raw(acc, gathered[r * n_ops + i])
+        assert bytes(acc) == bytes(out[i])
+    whole = _states_for(_table(0, n))
+    for i, (kind, want) in enumerate(whole):
+        got = out[i]
+        if want is None:
+            assert not got.has_value
+        elif kind in (L.DQ_OP_SIZE, L.DQ_OP_COMPLETENESS):
+            assert (got.num_matches, got.count if kind == L.DQ_OP_COMPLETENESS else 0) == \
+                (want.num_matches, want.count if kind == L.DQ_OP_COMPLETENESS else 0)
+        elif kind == L.DQ_OP_APPROX_COUNT_DISTINCT:
+            assert list(got.words) == list(want.words)
+        elif kind == L.DQ_OP_STDDEV:
+            assert got.n == want.n and got.m2 == pytest.approx(want.m2, rel=1e-12)
+        elif kind in (L.DQ_OP_MINIMUM, L.DQ_OP_MAXIMUM):
+            assert got.value == (want.min_value if kind == L.DQ_OP_MINIMUM else want.max_value)
+
+
+def test_c_abi_rank_fold_rejects_bad_arguments():
+    from deequ_amd import _lib as L
+    arr = (L.DqState * 2)()
+    out = (L.DqState * 2)()
+    assert L.lib().dq_states_merge_ranks(arr, 0, 2, out) == L.DQ_ERR_INVALID
+    arr[0].kind, arr[1].kind = L.DQ_OP_SUM, L.DQ_OP_MEAN  # kinds differ across ranks
+    assert L.lib().dq_states_merge_ranks(arr, 2, 1, out) != L.DQ_OK
