@@ -41,6 +41,8 @@ def parse_args():
                    help="0 = every CPU this process may use (sched_getaffinity, capped by OMP_NUM_THREADS: "
                         "the GPU box's host share for one GPU)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--e2e-batch-rows", type=int, default=62_500_000,
+                   help="host-resident C2 batch streamed to 1e9 rows for the PCIe-inclusive rate (0 = skip)")
     p.add_argument("--no-side-passes", action="store_true",
                    help="skip the scan_without_hll pass (profiler runs: the kernel trace then "
                         "holds only the headline launches)")
@@ -137,6 +139,62 @@ def scan_without_hll(table, device: int, steps: int):
     achieved = BYTES_PER_ROW * table.num_rows / (kernel_ms * 1e-3) / 1e9
     return {"analyzers": len(analyzers), "kernel_ms": kernel_ms, "achieved": achieved,
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS}
+
+
+def host_ingest(args, device: int):
+    """The JNI path's rate: the C2 suite over 1e9 rows that start in HOST memory -- one host batch
+    of `e2e_batch_rows` x 8 columns (Arrow layout, 5% NULL) consumed repeatedly through
+    dq_plan_consume, whose copies into the two HBM staging slots overlap the previous batch's scan.
+    Timed once with pageable buffers and once with the same buffers page-locked
+    (dq_host_register).  Reported beside the headline, never as `value` (PCIe-bound, not HBM)."""
+    import numpy as np
+    import torch
+    import deequ_amd as d
+    from deequ_amd import _lib
+    from deequ_amd.engine import Plan, op_spec_for
+    rows = args.e2e_batch_rows
+    reps = max(1, (args.rows + rows - 1) // rows)
+    rng = np.random.default_rng(42)
+    cols = {}
+    for k in range(8):
+        name = ("i%d" % k) if k < 4 else ("f%d" % (k - 4))
+        if k < 4:
+            vals = rng.integers(-2 ** 30, 2 ** 32, rows, dtype=np.int64)
+        elif k < 6:
+            vals = rng.random(rows) * 1e6
+        else:
+            vals = rng.standard_normal(rows) * 1e2 + 1e3
+        bits = np.packbits(rng.random(rows) >= 0.05, bitorder="little")
+        cols[name] = d.Column("int64" if k < 4 else "float64", rows, vals, bits)
+    table = d.Table(cols)
+    analyzers = c2_analyzers()
+    plan = Plan([op_spec_for(a, table.schema) for a in analyzers], table.schema, device=device)
+    bufs = [b for c in cols.values() for b in (c.values, c.validity)]
+
+    def one_pass():
+        plan.reset()
+        for _ in range(reps):
+            plan.consume(table)
+        plan.finish_raw()
+    out = {"batch_rows": rows, "batches_per_pass": reps, "rows_per_pass": rows * reps,
+           "bytes_per_row": BYTES_PER_ROW}
+    try:
+        for label in ("pageable", "pinned"):
+            if label == "pinned":
+                for b in bufs:
+                    _lib.check(_lib.lib().dq_host_register(b.ctypes.data, b.nbytes))
+            one_pass()  # warm
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            one_pass()
+            secs = time.perf_counter() - t0
+            out[label + "_rows_per_s"] = rows * reps / secs
+            out[label + "_pcie_gbs"] = rows * reps * BYTES_PER_ROW / secs / 1e9
+    finally:
+        for b in bufs:
+            _lib.lib().dq_host_unregister(b.ctypes.data)
+        plan.close()
+    return out
 
 
 def host_cpu_share() -> int:
@@ -708,6 +766,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_side_passes:
         result["scan_without_hll"] = scan_without_hll(table, local, args.steps)
+        if args.e2e_batch_rows > 0:
+            result["host_ingest"] = host_ingest(args, local)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or host_cpu_share()
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample_rows, threads)

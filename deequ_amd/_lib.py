@@ -120,6 +120,8 @@ SIGNATURES = {
     "dq_plan_consume": (c_int, [c_void_p, POINTER(DqColumn), c_int, c_int64]),
     "dq_plan_finish": (c_int, [c_void_p, POINTER(DqState), c_int]),
     "dq_plan_reset": (c_int, [c_void_p]),
+    "dq_host_register": (c_int, [c_void_p, c_size_t]),
+    "dq_host_unregister": (c_int, [c_void_p]),
     "dq_arrow_columns": (c_int, [POINTER(ArrowSchema), POINTER(ArrowArray), c_int, POINTER(c_int32),
                                  POINTER(DqColumn), c_int, POINTER(c_int), POINTER(c_int64)]),
     "dq_plan_consume_arrow": (c_int, [c_void_p, POINTER(ArrowSchema), POINTER(ArrowArray), c_int]),

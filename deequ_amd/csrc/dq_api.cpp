@@ -569,13 +569,30 @@ struct ScanGroup {
 };
 
 // Per-batch column staging shared by scan plans and frequency tables: host buffers are copied
-// (and sliced bitmaps realigned) into device buffers owned here; device buffers are used in
-// place when their layout allows.
+// (and sliced bitmaps realigned, utf8 offsets rebased -- on the device) into device buffers
+// owned here; device buffers are used in place when their layout allows.
+//
+// Host batches (the JNI path: Arrow buffers in host memory) are double-buffered when the owner
+// sets a copy stream: batch k's copies go into staging slot k % 2 on `copy_stream` while the
+// kernels of batch k - 1 still run on `stream` (which waits for the copies by event), and a slot
+// is refilled only after the kernels that read it two batches ago have finished.
 struct Stager {
   hipStream_t stream = nullptr;
+  hipStream_t copy_stream = nullptr;  // nullptr: copies on `stream` (single slot)
+  int slot = 0;                       // staging slot of the batch being prepared
   std::vector<int32_t> col_types;
-  std::vector<DevBuf> stage_values, stage_validity, stage_offsets;
-  std::vector<std::vector<uint8_t>> host_tmp;  // realigned host buffers alive until sync
+  std::vector<DevBuf> stage_values[2], stage_validity[2], stage_offsets[2], stage_raw[2];
+  std::vector<std::vector<uint8_t>> host_tmp;  // host buffers alive until their copies are done
+
+  void resize_stage(int n_columns) {
+    for (int k = 0; k < 2; ++k) {
+      stage_values[k].resize(n_columns);
+      stage_validity[k].resize(n_columns);
+      stage_offsets[k].resize(n_columns);
+      stage_raw[k].resize(n_columns);
+    }
+  }
+  hipStream_t copies() const { return copy_stream ? copy_stream : stream; }
 };
 
 struct dq_plan : Stager {
@@ -606,11 +623,20 @@ struct dq_plan : Stager {
   int target_blocks = 2048;
   int n_cu = 0;          // compute units of the device (0 = unknown)
   int scan_rounds = 6;   // value-scan grids: whole rounds of resident workgroups (DQ_SCAN_ROUNDS)
+  // host batches: staging slot k % 2, filled on copy_stream while the previous batch scans
+  uint64_t batch_seq = 0;
+  hipEvent_t copy_done[2] = {nullptr, nullptr}, scan_done[2] = {nullptr, nullptr};
 
   ~dq_plan() {
     if (stream) {
       (void)hipStreamSynchronize(stream);
     }
+    if (copy_stream) (void)hipStreamSynchronize(copy_stream);
+    for (int k = 0; k < 2; ++k) {
+      if (copy_done[k]) (void)hipEventDestroy(copy_done[k]);
+      if (scan_done[k]) (void)hipEventDestroy(scan_done[k]);
+    }
+    if (copy_stream) (void)hipStreamDestroy(copy_stream);
     if (desc_done) (void)hipEventDestroy(desc_done);
     if (h_desc) (void)hipHostFree(h_desc);
     if (stream) (void)hipStreamDestroy(stream);
@@ -918,6 +944,11 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
     return s;
   }
   hipError_t e = hipStreamCreateWithFlags(&plan->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&plan->copy_stream, hipStreamNonBlocking);
+  for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+    e = hipEventCreateWithFlags(&plan->copy_done[k], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&plan->scan_done[k], hipEventDisableTiming);
+  }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&plan->desc_done, hipEventDisableTiming);
   plan->h_desc_size = std::max(1, n_columns) * sizeof(DevColumn) +
                       std::max<size_t>(1, plan->programs.size()) * sizeof(DevMask) +
@@ -927,9 +958,7 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
     delete plan;
     return fail(DQ_ERR_DEVICE, std::string("stream/event/pinned allocation failed: ") + hipGetErrorString(e));
   }
-  plan->stage_values.resize(n_columns);
-  plan->stage_validity.resize(n_columns);
-  plan->stage_offsets.resize(n_columns);
+  plan->resize_stage(n_columns);
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess)
   {
@@ -962,6 +991,18 @@ extern "C" dq_status dq_plan_op_status(dq_plan* plan, int op) {
   return DQ_OK;
 }
 
+extern "C" dq_status dq_host_register(void* ptr, size_t bytes) {
+  if (!ptr || bytes == 0) return fail(DQ_ERR_INVALID, "NULL or empty host buffer");
+  DQ_HIP(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_host_unregister(void* ptr) {
+  if (!ptr) return fail(DQ_ERR_INVALID, "NULL host buffer");
+  DQ_HIP(hipHostUnregister(ptr));
+  return DQ_OK;
+}
+
 extern "C" dq_status dq_plan_reset(dq_plan* plan) {
   if (!plan) return fail(DQ_ERR_INVALID, "plan is NULL");
   DQ_HIP(hipSetDevice(plan->ctx->device));
@@ -981,12 +1022,23 @@ extern "C" dq_status dq_plan_reset(dq_plan* plan) {
   return DQ_OK;
 }
 
-// Realign an LSB-first bitmap on the host: out bit i = in bit (off + i).
-static void host_realign(const uint8_t* src, int64_t off, int64_t n, std::vector<uint8_t>& dst) {
-  const int64_t nb = (n + 7) >> 3;
-  dst.assign((size_t)nb + 8, 0);
-  for (int64_t i = 0; i < n; ++i)
-    if ((src[(off + i) >> 3] >> ((off + i) & 7)) & 1u) dst[i >> 3] |= (uint8_t)(1u << (i & 7));
+// Host bitmap (bits [off, off + n)) -> LSB-first device bitmap at bit 0: the covering bytes
+// are copied as they are and realigned by a kernel on the copy stream (no per-bit host work).
+static dq_status stage_host_bitmap(Stager* st, DevBuf& dst, DevBuf& raw, const uint8_t* src, int64_t off,
+                                   int64_t n) {
+  const size_t vbytes = (size_t)((n + 7) >> 3);
+  DQ_TRY(dst.ensure(vbytes + 8));
+  if (vbytes == 0) return DQ_OK;
+  if ((off & 7) == 0) {
+    DQ_HIP(hipMemcpyAsync(dst.ptr, src + (off >> 3), vbytes, hipMemcpyHostToDevice, st->copies()));
+    return DQ_OK;
+  }
+  const size_t first = (size_t)(off >> 3), last = (size_t)((off + n - 1) >> 3);
+  DQ_TRY(raw.ensure(last - first + 1 + 8));
+  DQ_HIP(hipMemcpyAsync(raw.ptr, src + first, last - first + 1, hipMemcpyHostToDevice, st->copies()));
+  DQ_HIP(launch_realign_bitmap(static_cast<const uint8_t*>(raw.ptr), off & 7, n, static_cast<uint8_t*>(dst.ptr),
+                               st->copies()));
+  return DQ_OK;
 }
 
 static dq_status prepare_column(Stager* plan, int c, const dq_column& col, int64_t n_rows,
@@ -998,6 +1050,11 @@ static dq_status prepare_column(Stager* plan, int c, const dq_column& col, int64
   if (!col.values && n_rows > 0) return fail(DQ_ERR_INVALID, "column values are NULL");
   if (t == DQ_T_UTF8 && !col.offsets) return fail(DQ_ERR_INVALID, "utf8 column without offsets");
   const bool device = (col.flags & DQ_COL_DEVICE) != 0;
+  const int k = plan->slot;
+  DevBuf& sval = plan->stage_values[k][c];
+  DevBuf& svalid = plan->stage_validity[k][c];
+  DevBuf& soffs = plan->stage_offsets[k][c];
+  DevBuf& sraw = plan->stage_raw[k][c];
   const int64_t off = col.offset;
   dc->type = t;
   dc->pad = 0;
@@ -1011,22 +1068,13 @@ static dq_status prepare_column(Stager* plan, int c, const dq_column& col, int64
       if ((off & 7) == 0) {
         dc->validity = col.validity + (off >> 3);
       } else {
-        DQ_TRY(plan->stage_validity[c].ensure(vbytes + 8));
-        DQ_HIP(launch_realign_bitmap(col.validity, off, n_rows,
-                                     static_cast<uint8_t*>(plan->stage_validity[c].ptr), plan->stream));
-        dc->validity = static_cast<const uint8_t*>(plan->stage_validity[c].ptr);
+        DQ_TRY(svalid.ensure(vbytes + 8));
+        DQ_HIP(launch_realign_bitmap(col.validity, off, n_rows, static_cast<uint8_t*>(svalid.ptr), plan->stream));
+        dc->validity = static_cast<const uint8_t*>(svalid.ptr);
       }
     } else {
-      DQ_TRY(plan->stage_validity[c].ensure(vbytes + 8));
-      const uint8_t* src = col.validity + (off >> 3);
-      if (off & 7) {
-        plan->host_tmp.emplace_back();
-        host_realign(col.validity, off, n_rows, plan->host_tmp.back());
-        src = plan->host_tmp.back().data();
-      }
-      if (vbytes)
-        DQ_HIP(hipMemcpyAsync(plan->stage_validity[c].ptr, src, vbytes, hipMemcpyHostToDevice, plan->stream));
-      dc->validity = static_cast<const uint8_t*>(plan->stage_validity[c].ptr);
+      DQ_TRY(stage_host_bitmap(plan, svalid, sraw, col.validity, off, n_rows));
+      dc->validity = static_cast<const uint8_t*>(svalid.ptr);
     }
   }
   // ---- values
@@ -1034,21 +1082,15 @@ static dq_status prepare_column(Stager* plan, int c, const dq_column& col, int64
     if (device && (off & 7) == 0) {
       dc->values = static_cast<const uint8_t*>(col.values) + (off >> 3);
     } else if (device) {
-      DQ_TRY(plan->stage_values[c].ensure(vbytes + 8));
+      DQ_TRY(sval.ensure(vbytes + 8));
       DQ_HIP(launch_realign_bitmap(static_cast<const uint8_t*>(col.values), off, n_rows,
-                                   static_cast<uint8_t*>(plan->stage_values[c].ptr), plan->stream));
-      dc->values = plan->stage_values[c].ptr;
+                                   static_cast<uint8_t*>(sval.ptr), plan->stream));
+      dc->values = sval.ptr;
     } else {
-      DQ_TRY(plan->stage_values[c].ensure(vbytes + 8));
-      const uint8_t* src = static_cast<const uint8_t*>(col.values) + (off >> 3);
-      if (off & 7) {
-        plan->host_tmp.emplace_back();
-        host_realign(static_cast<const uint8_t*>(col.values), off, n_rows, plan->host_tmp.back());
-        src = plan->host_tmp.back().data();
-      }
-      if (vbytes)
-        DQ_HIP(hipMemcpyAsync(plan->stage_values[c].ptr, src, vbytes, hipMemcpyHostToDevice, plan->stream));
-      dc->values = plan->stage_values[c].ptr;
+      // (the bool bitmap's own raw staging: validity may be using sraw in this slot)
+      DevBuf& braw = plan->stage_offsets[k][c];
+      DQ_TRY(stage_host_bitmap(plan, sval, braw, static_cast<const uint8_t*>(col.values), off, n_rows));
+      dc->values = sval.ptr;
     }
   } else if (t == DQ_T_UTF8) {
     const int32_t* offs = col.offsets + off;
@@ -1056,21 +1098,20 @@ static dq_status prepare_column(Stager* plan, int c, const dq_column& col, int64
       dc->offsets = offs;
       dc->values = col.values;
     } else {
-      // rebase offsets to the batch's first byte and copy only the referenced bytes
-      int32_t first = n_rows > 0 ? offs[0] : 0;
-      int32_t last = n_rows > 0 ? offs[n_rows] : 0;
-      plan->host_tmp.emplace_back((size_t)(n_rows + 1) * sizeof(int32_t));
-      int32_t* reb = reinterpret_cast<int32_t*>(plan->host_tmp.back().data());
-      for (int64_t i = 0; i <= n_rows; ++i) reb[i] = offs[i] - first;
-      DQ_TRY(plan->stage_offsets[c].ensure((size_t)(n_rows + 1) * sizeof(int32_t)));
-      DQ_TRY(plan->stage_values[c].ensure((size_t)(last - first) + 16));
-      DQ_HIP(hipMemcpyAsync(plan->stage_offsets[c].ptr, reb, (size_t)(n_rows + 1) * sizeof(int32_t),
-                            hipMemcpyHostToDevice, plan->stream));
+      // copy the n + 1 offsets and only the referenced bytes; rebase the offsets on the device
+      const int32_t first = n_rows > 0 ? offs[0] : 0;
+      const int32_t last = n_rows > 0 ? offs[n_rows] : 0;
+      DQ_TRY(soffs.ensure((size_t)(n_rows + 1) * sizeof(int32_t)));
+      DQ_TRY(sval.ensure((size_t)(last - first) + 16));
+      DQ_HIP(hipMemcpyAsync(soffs.ptr, offs, (size_t)(n_rows + 1) * sizeof(int32_t), hipMemcpyHostToDevice,
+                            plan->copies()));
+      if (first != 0)
+        DQ_HIP(launch_rebase_offsets(static_cast<int32_t*>(soffs.ptr), n_rows + 1, first, plan->copies()));
       if (last > first)
-        DQ_HIP(hipMemcpyAsync(plan->stage_values[c].ptr, static_cast<const uint8_t*>(col.values) + first,
-                              (size_t)(last - first), hipMemcpyHostToDevice, plan->stream));
-      dc->offsets = static_cast<const int32_t*>(plan->stage_offsets[c].ptr);
-      dc->values = plan->stage_values[c].ptr;
+        DQ_HIP(hipMemcpyAsync(sval.ptr, static_cast<const uint8_t*>(col.values) + first, (size_t)(last - first),
+                              hipMemcpyHostToDevice, plan->copies()));
+      dc->offsets = static_cast<const int32_t*>(soffs.ptr);
+      dc->values = sval.ptr;
     }
   } else {
     const size_t es = (size_t)type_size(t);
@@ -1079,11 +1120,11 @@ static dq_status prepare_column(Stager* plan, int c, const dq_column& col, int64
     if (device && ((uintptr_t)src & 15) == 0) {
       dc->values = src;
     } else {
-      DQ_TRY(plan->stage_values[c].ensure(bytes + 16));
+      DQ_TRY(sval.ensure(bytes + 16));
       if (bytes)
-        DQ_HIP(hipMemcpyAsync(plan->stage_values[c].ptr, src, bytes,
-                              device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, plan->stream));
-      dc->values = plan->stage_values[c].ptr;
+        DQ_HIP(hipMemcpyAsync(sval.ptr, src, bytes, device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                              device ? plan->stream : plan->copies()));
+      dc->values = sval.ptr;
     }
   }
   return DQ_OK;
@@ -1108,11 +1149,20 @@ extern "C" dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, in
   DevMask* h_masks = reinterpret_cast<DevMask*>(static_cast<uint8_t*>(plan->h_desc) +
                                                 std::max(1, n_columns) * sizeof(DevColumn));
   bool any_host = false;
+  for (int c = 0; c < n_columns; ++c)
+    if (plan->col_used[c] && !(columns[c].flags & DQ_COL_DEVICE)) any_host = true;
+  const int slot = (int)(plan->batch_seq & 1u);
+  plan->slot = slot;
+  // this slot's staging was last read by the batch two before: its kernels must have finished
+  if (any_host) DQ_HIP(hipStreamWaitEvent(plan->copy_stream, plan->scan_done[slot], 0));
   for (int c = 0; c < n_columns; ++c) {
     std::memset(&h_cols[c], 0, sizeof(DevColumn));
     if (!plan->col_used[c]) continue;
-    if (!(columns[c].flags & DQ_COL_DEVICE)) any_host = true;
     DQ_TRY(prepare_column(plan, c, columns[c], n_rows, &h_cols[c]));
+  }
+  if (any_host) {  // the kernels of this batch start once its copies have landed
+    DQ_HIP(hipEventRecord(plan->copy_done[slot], plan->copy_stream));
+    DQ_HIP(hipStreamWaitEvent(plan->stream, plan->copy_done[slot], 0));
   }
   // generic predicates -> masks
   const int n_progs = (int)plan->programs.size();
@@ -1230,10 +1280,12 @@ extern "C" dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, in
                        plan->stream));
   }
   plan->total_rows += n_rows;
-  if (any_host) {  // caller's host buffers may be released once we return
-    DQ_HIP(hipStreamSynchronize(plan->stream));
+  DQ_HIP(hipEventRecord(plan->scan_done[slot], plan->stream));
+  ++plan->batch_seq;
+  if (any_host) {  // the caller's host buffers may be released once we return: wait for the
+    // copies only -- the scan of this batch keeps running while the caller prepares the next
+    DQ_HIP(hipEventSynchronize(plan->copy_done[slot]));
     plan->host_tmp.clear();
-    plan->desc_pending = false;
   }
   return DQ_OK;
 }
@@ -1625,9 +1677,7 @@ extern "C" dq_status dq_cast_utf8(dq_ctx* ctx, const dq_column* src, int64_t n_r
   Stager st;
   DQ_HIP(hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking));
   st.col_types.assign(1, DQ_T_UTF8);
-  st.stage_values.resize(1);
-  st.stage_validity.resize(1);
-  st.stage_offsets.resize(1);
+  st.resize_stage(1);
   DevColumn dc;
   DevBuf d_unsup;
   dq_status s = prepare_column(&st, 0, *src, n_rows, &dc);

@@ -268,6 +268,7 @@ hipError_t launch_predicates(const PredProgram* d_progs, int n_progs, const Pred
                              const uint8_t* d_pool, const DevColumn* d_cols, int64_t n_rows,
                              uint64_t* d_mask_words, int64_t words_per_mask, uint32_t* d_unsup,
                              hipStream_t stream);
+hipError_t launch_rebase_offsets(int32_t* d_offs, int64_t n, int32_t first, hipStream_t stream);
 hipError_t launch_realign_bitmap(const uint8_t* src, int64_t bit_offset, int64_t n_bits,
                                  uint8_t* dst, hipStream_t stream);
 hipError_t launch_init_acc(ScanAcc* d_acc, int n, hipStream_t stream);

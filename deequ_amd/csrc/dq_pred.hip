@@ -239,6 +239,20 @@ hipError_t launch_predicates(const PredProgram* d_progs, int n_progs, const Pred
   return hipGetLastError();
 }
 
+// offs[i] -= first: utf8 offsets of a host batch copied verbatim, rebased to its first byte
+__global__ void dq_rebase_offsets_kernel(int32_t* __restrict__ offs, int64_t n, int32_t first) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    offs[i] -= first;
+}
+
+hipError_t launch_rebase_offsets(int32_t* d_offs, int64_t n, int32_t first, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  int64_t blocks = (n + 1023) / 1024;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(dq_rebase_offsets_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, d_offs, n, first);
+  return hipGetLastError();
+}
+
 hipError_t launch_realign_bitmap(const uint8_t* src, int64_t bit_offset, int64_t n_bits,
                                  uint8_t* dst, hipStream_t stream) {
   const int64_t n_bytes = (n_bits + 7) >> 3;

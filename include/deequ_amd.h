@@ -279,6 +279,14 @@ dq_status dq_arrow_columns(const struct ArrowSchema* schema, const struct ArrowA
 dq_status dq_plan_consume_arrow(dq_plan* plan, const struct ArrowSchema* schema,
                                 const struct ArrowArray* array, int flags);
 
+/* Page-lock a host buffer the caller will hand over again and again (e.g. the JNI layer's Arrow
+ * allocator pool), so its batches cross PCIe by DMA at full rate instead of through the
+ * runtime's pageable staging; unregister before freeing it.  Host batches are double-buffered in
+ * HBM either way: dq_plan_consume returns once a batch's bytes are on the device, while its scan
+ * still runs, so the caller fills the next batch during the scan. */
+dq_status dq_host_register(void* ptr, size_t bytes);
+dq_status dq_host_unregister(void* ptr);
+
 /* Clear accumulated results so the plan can scan a new dataset. */
 dq_status dq_plan_reset(dq_plan* plan);
 
