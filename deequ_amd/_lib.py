@@ -116,6 +116,7 @@ SIGNATURES = {
     "dq_ctx_destroy": (c_int, [c_void_p]),
     "dq_plan_create": (c_int, [c_void_p, POINTER(DqOp), c_int, POINTER(c_int32), c_int, POINTER(c_void_p)]),
     "dq_plan_destroy": (c_int, [c_void_p]),
+    "dq_plan_create_packed": (c_int, [c_void_p, c_char_p, c_size_t, POINTER(c_int32), c_int, POINTER(c_void_p)]),
     "dq_op_supported": (c_int, [POINTER(DqOp), POINTER(c_int32), c_int]),
     "dq_plan_consume": (c_int, [c_void_p, POINTER(DqColumn), c_int, c_int64]),
     "dq_plan_finish": (c_int, [c_void_p, POINTER(DqState), c_int]),

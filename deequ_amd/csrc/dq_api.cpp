@@ -1706,3 +1706,6 @@ extern "C" dq_status dq_cast_utf8(dq_ctx* ctx, const dq_column* src, int64_t n_r
 
 // RCCL groups: the sharded path's collectives for drivers that are not torch.
 #include "dq_group.inc"
+
+// The analyzer list as the JVM serializes it.
+#include "dq_packed.inc"

@@ -70,6 +70,30 @@ class OpSpec:
             _fill_pred(op.where, self.where)
 
 
+PACKED_MAGIC = 0x504F5144  # "DQOP", include/deequ_amd.h
+
+
+def pack_ops(specs: Sequence[OpSpec]) -> bytes:
+    """The analyzer list in the byte layout of dq_plan_create_packed -- what the JVM side's
+    GpuPlanEncoder writes into a little-endian ByteBuffer."""
+    import struct
+
+    def pred(p):
+        if p is None:
+            return [], b""
+        arr, pool, n_pool = p
+        return [(arr[i].opcode, arr[i].arg, arr[i].i64, arr[i].f64) for i in range(len(arr))], \
+            (pool.raw[:n_pool] if pool is not None else b"")
+    out = [struct.pack("<III", PACKED_MAGIC, 1, len(specs))]
+    for s in specs:
+        pc, ps = pred(s.predicate)
+        wc, ws = pred(s.where)
+        out.append(struct.pack("<7i", s.kind, s.column, s.column2, len(pc), len(ps), len(wc), len(ws)))
+        out += [struct.pack("<iiqd", *ins) for ins in pc] + [ps]
+        out += [struct.pack("<iiqd", *ins) for ins in wc] + [ws]
+    return b"".join(out)
+
+
 def schema_index(schema: Dict[str, str]) -> Dict[str, tuple]:
     return {name: (i, dtype) for i, (name, dtype) in enumerate(schema.items())}
 

@@ -204,6 +204,19 @@ dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
                          const int32_t* column_types, int n_columns, dq_plan** out);
 dq_status dq_plan_destroy(dq_plan* plan);
 
+/* dq_plan_create from the analyzer list serialized as bytes -- what the JVM side builds with a
+ * little-endian ByteBuffer (GpuPlanEncoder), so the JNI stub passes one byte[]
+ * and the library, not hand-written JNI code, decodes and validates it.  Layout:
+ *   u32 magic 0x504F5144 ("DQOP"), u32 version 1, u32 n_ops, then per op
+ *   i32 kind, i32 column, i32 column2,
+ *   i32 n_pred, i32 pred_strings_len, i32 n_where, i32 where_strings_len,
+ *   n_pred x {i32 opcode, i32 arg, i64 i64, f64 f64} (24 B), pred_strings_len bytes,
+ *   n_where x {...}, where_strings_len bytes.
+ * A truncated or inconsistent blob is DQ_ERR_INVALID (checked before any device work). */
+#define DQ_PACKED_MAGIC 0x504F5144u
+dq_status dq_plan_create_packed(dq_ctx* ctx, const uint8_t* blob, size_t blob_len, const int32_t* column_types,
+                                int n_columns, dq_plan** out);
+
 /* Check whether a single op is GPU-eligible for the given schema without building a plan. */
 dq_status dq_op_supported(const dq_op* op, const int32_t* column_types, int n_columns);
 
