@@ -57,10 +57,13 @@ class ArrowBatch:
         self.batch = batch
         self.num_rows = batch.num_rows
         self._exports: Dict[tuple, _Exported] = {}
+        self._schema = None
 
     @property
     def schema(self) -> Dict[str, str]:
-        return OrderedDict((f.name, dtype_of(f.type)) for f in self.batch.schema)
+        if self._schema is None:
+            self._schema = OrderedDict((f.name, dtype_of(f.type)) for f in self.batch.schema)
+        return self._schema
 
     def c_structs(self, names: Sequence[str]):
         """(ArrowSchema, ArrowArray) of the batch's columns `names`, in that order."""
@@ -107,7 +110,9 @@ class ArrowTable:
 
     @property
     def schema(self) -> Dict[str, str]:
-        return OrderedDict((f.name, dtype_of(f.type)) for f in self.arrow_schema)
+        if getattr(self, "_schema", None) is None:
+            self._schema = OrderedDict((f.name, dtype_of(f.type)) for f in self.arrow_schema)
+        return self._schema
 
     def batches(self) -> List[ArrowBatch]:
         return self.parts

@@ -66,15 +66,15 @@ static bool is_numeric(int t) { return t >= DQ_T_INT8 && t <= DQ_T_FLOAT64; }
 static bool is_integral(int t) { return t >= DQ_T_INT8 && t <= DQ_T_INT64; }
 static bool valid_type(int t) { return t >= DQ_T_BOOL && t <= DQ_T_UTF8; }
 
-// Device block pool.  hipMalloc / hipFree of multi-GB buffers cost milliseconds to seconds (and
-// hipFree synchronises the device); the frequency path sizes its staging and sort buffers by the
-// batch, for every table.  Freed blocks of at least kPoolMin bytes are therefore kept per device
+// Device block pool.  hipMalloc / hipFree of multi-GB buffers cost milliseconds to seconds, and
+// every hipFree synchronises the device -- a profiler run creates and drops dozens of small
+// tables and plans, each free a device-wide stall.  Freed blocks are therefore kept per device
 // and handed out again (best fit within 2x of the request).  A block may still be in use by a
 // stream when it is freed: it is reused only after a device synchronisation.  On an allocation
 // failure the device's cached blocks are released and the allocation retried.
 class BlockPool {
  public:
-  static constexpr size_t kPoolMin = (size_t)16 << 20;
+  static constexpr size_t kPoolMin = 0;  // every block (DevBuf rounds requests up to 256 B)
   static constexpr size_t kPoolMaxCached = (size_t)128 << 30;
 
   static BlockPool& get() {
@@ -460,6 +460,12 @@ static int fast_form(const Program& prog, const int32_t* types, FastPred* fp) {
     fp->kind = FP_CONST;
     fp->lit_i = c[0].opcode == DQ_P_TRUE ? 1 : 0;
     return -2;
+  }
+  if (c.size() == 1 && c[0].opcode == DQ_P_COLUMN && types[c[0].arg] == DQ_T_BOOL) {
+    // a boolean column as the predicate (`where b`, profiler pass-3 histograms): counted from
+    // the value and validity bitmaps by the bits scan, no predicate kernel
+    fp->kind = FP_BOOL;
+    return c[0].arg;
   }
   if (c.size() == 2 && c[0].opcode == DQ_P_COLUMN &&
       (c[1].opcode == DQ_P_IS_NULL || c[1].opcode == DQ_P_IS_NOT_NULL)) {

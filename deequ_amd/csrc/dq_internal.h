@@ -41,7 +41,8 @@ enum FastPredKind : int32_t {
   FP_IS_NULL = 3,
   FP_IS_NOT_NULL = 4,
   FP_CONST = 5,         // constant TRUE/FALSE/NULL (lit_i: 1 true, 0 false, -1 null)
-  FP_MASK = 6           // precomputed DevMask[mask]
+  FP_MASK = 6,          // precomputed DevMask[mask]
+  FP_BOOL = 7           // the primary (a bool column) itself: TRUE = value bit, NULL = invalid
 };
 
 enum CmpOp : int32_t { CMP_EQ = 0, CMP_NE, CMP_LT, CMP_LE, CMP_GT, CMP_GE, CMP_EQNS };

@@ -568,6 +568,18 @@ __global__ __launch_bounds__(kBlock) void dq_scan_bits_kernel(
           nn = mn[w] & in;
           break;
         }
+        case FP_BOOL: {  // the primary bool column's value bits (same tail rule as validity)
+          const uint8_t* vb = static_cast<const uint8_t*>(cols[task.primary].values) + (w << 2);
+          uint32_t bits = 0u;
+          if (left >= 32) {
+            bits = *reinterpret_cast<const uint32_t*>(vb);
+          } else {
+            for (int b = 0; b < (int)((left + 7) >> 3); ++b) bits |= (uint32_t)vb[b] << (8 * b);
+          }
+          r = bits & valid;
+          nn = valid;
+          break;
+        }
         default: break;
       }
       pm[p] += __builtin_popcount(wt & nn & r);

@@ -94,8 +94,26 @@ def pack_ops(specs: Sequence[OpSpec]) -> bytes:
     return b"".join(out)
 
 
+_SCHEMA_CACHE: Dict[tuple, tuple] = {}
+
+
+def _schema_info(schema: Dict[str, str]):
+    """(name -> (index, dtype), dq type codes) of a schema, memoised on its contents: a profiler
+    run builds hundreds of ops over the same 100-column schema."""
+    key = tuple(schema.items())
+    hit = _SCHEMA_CACHE.get(key)
+    if hit is None:
+        idx = {name: (i, dtype) for i, (name, dtype) in enumerate(schema.items())}
+        codes = [L.TYPE_CODES[t] for t in schema.values()]
+        hit = (idx, (ctypes.c_int32 * max(1, len(codes)))(*codes))
+        if len(_SCHEMA_CACHE) > 256:
+            _SCHEMA_CACHE.clear()
+        _SCHEMA_CACHE[key] = hit
+    return hit
+
+
 def schema_index(schema: Dict[str, str]) -> Dict[str, tuple]:
-    return {name: (i, dtype) for i, (name, dtype) in enumerate(schema.items())}
+    return _schema_info(schema)[0]
 
 
 def op_spec_for(analyzer, schema: Dict[str, str]) -> OpSpec:
@@ -113,7 +131,7 @@ def op_spec_for(analyzer, schema: Dict[str, str]) -> OpSpec:
 
 def op_supported(spec: OpSpec, schema: Dict[str, str]) -> None:
     """Raises UnsupportedOnGpu / DeequAmdError if the op is not GPU-eligible."""
-    types = (ctypes.c_int32 * max(1, len(schema)))(*[L.TYPE_CODES[t] for t in schema.values()])
+    types = _schema_info(schema)[1]
     op = L.DqOp()
     spec.fill(op)
     L.check(L.lib().dq_op_supported(ctypes.byref(op), types, len(schema)))

@@ -165,10 +165,12 @@ class Table:
         if len(lengths) > 1:
             raise ValueError("columns have different lengths: %s" % sorted(lengths))
         self.num_rows = lengths.pop() if lengths else 0
+        self._schema = OrderedDict((k, c.dtype) for k, c in self.columns.items())
 
     @property
     def schema(self) -> Dict[str, str]:
-        return OrderedDict((k, c.dtype) for k, c in self.columns.items())
+        """{name: dtype} in column order (computed once: the columns of a Table are fixed)."""
+        return self._schema
 
     @staticmethod
     def from_pydict(data: Dict[str, tuple]) -> "Table":

@@ -188,9 +188,10 @@ int dq_abi_version(void);
 /* Number of gfx950 devices visible to this process (0 on a host without a GPU). */
 dq_status dq_device_count(int* out);
 
-/* Give the device blocks the library keeps cached for reuse (staging / sort buffers of the
- * frequency group-by, >= 16 MiB each, at most 128 GiB) back to the HIP runtime.  No reference
- * counterpart: Spark's executors free their memory through the JVM. */
+/* Give the device blocks the library keeps cached for reuse (every buffer a plan or frequency
+ * table freed -- staging, sort buffers, tables; at most 128 GiB -- kept so that a free is not a
+ * device-wide hipFree synchronisation) back to the HIP runtime.  No reference counterpart:
+ * Spark's executors free their memory through the JVM. */
 dq_status dq_release_cached_memory(int device);
 
 dq_status dq_ctx_create(int device, int flags, dq_ctx** out);
