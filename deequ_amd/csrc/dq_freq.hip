@@ -129,8 +129,11 @@ __device__ inline uint64_t fixed_bits(const DevColumn& c, int64_t row) {
 // Spark 2.2 groups by UnsafeRow bytes); strings = UTF-8 bytes, prefixed by a u32 length when
 // several columns are combined; Histogram NULLs = "NullValue" for strings (merging with a
 // literal "NullValue", Histogram.scala:63-64) and the empty key for other types.
+// want_hash = false: an inline key (len <= 16, k.ptr == nullptr) is returned without its table
+// hash (k.hash = 0) -- the LDS pre-aggregation only needs a cheap one (lds_hash below), and
+// most rows of a low-cardinality column never reach the global table.
 __device__ bool make_key(const FreqKeySpec& ks, const DevColumn* cols, int64_t row, Key& k,
-                         uint8_t* scratch, bool& too_long) {
+                         uint8_t* scratch, bool& too_long, bool want_hash = true) {
   k.k0 = k.k1 = 0;
   k.ptr = nullptr;
   k.len = 0;
@@ -154,7 +157,7 @@ __device__ bool make_key(const FreqKeySpec& ks, const DevColumn* cols, int64_t r
       if (n <= 16) {
         k.k0 = ld_partial(p, n < 8 ? n : 8);
         k.k1 = n > 8 ? ld_partial(p + 8, n - 8) : 0;
-        k.hash = hash_inline(k.k0, k.k1, n);
+        k.hash = want_hash ? hash_inline(k.k0, k.k1, n) : 0;
       } else {
         k.ptr = p;
         k.hash = xxh64_any(p, n, 42);
@@ -162,7 +165,7 @@ __device__ bool make_key(const FreqKeySpec& ks, const DevColumn* cols, int64_t r
       return true;
     }
     if (!valid) {  // Histogram NULL of a non-string column: the empty key
-      k.hash = hash_inline(0, 0, 0);
+      k.hash = want_hash ? hash_inline(0, 0, 0) : 0;
       return true;
     }
     k.k0 = fixed_bits(c, row);
@@ -171,7 +174,7 @@ __device__ bool make_key(const FreqKeySpec& ks, const DevColumn* cols, int64_t r
       if (c.type == DQ_T_FLOAT32 && (k.k0 & 0x7fffffffull) > 0x7f800000ull) k.k0 = 0x7fc00000ull;
     }
     k.len = (uint32_t)width_of(c.type);
-    k.hash = hash_inline(k.k0, 0, k.len);
+    k.hash = want_hash ? hash_inline(k.k0, 0, k.len) : 0;
     return true;
   }
   // several columns: concatenate into scratch
@@ -299,6 +302,17 @@ __device__ bool global_insert(const FreqTable& T, const Key& k, unsigned long lo
   return false;
 }
 
+// Slot and tag of an inline key in a workgroup's LDS table: a 32-bit mix (two 32-bit multiplies
+// instead of XXH64's six 64-bit ones); keys are compared exactly, so any spread will do.
+__device__ inline uint32_t lds_hash(uint64_t k0, uint64_t k1, uint32_t len) {
+  uint32_t a = ((uint32_t)k0 ^ (uint32_t)(k1 >> 32)) * 0x9E3779B1u;
+  uint32_t b = ((uint32_t)(k0 >> 32) ^ (uint32_t)k1 ^ (len << 24)) * 0x85EBCA77u;
+  uint32_t h = a ^ __builtin_amdgcn_alignbit(b, b, 13);
+  h ^= h >> 15;
+  h *= 0xC2B2AE3Du;
+  return h ^ (h >> 13);
+}
+
 struct LdsSlot {
   unsigned long long ctrl;  // as the global ctrl (READY unused: LDS keys are written before ctrl)
   unsigned long long k0, k1;
@@ -329,20 +343,21 @@ __global__ __launch_bounds__(kBlock) void dq_freq_insert_kernel(FreqKeySpec ks,
   for (int64_t row = row_begin + threadIdx.x; row < row_end; row += kBlock) {
     Key k;
     bool too_long;
-    if (!make_key(ks, cols, row, k, scratch, too_long)) {
+    if (!make_key(ks, cols, row, k, scratch, too_long, false)) {
       if (too_long) atomicOr(T.overflow, 4u);
       continue;
     }
+    const bool lazy = k.ptr == nullptr && k.len <= 16;  // inline key: k.hash not computed yet
     bool done = false;
-    if (k.len <= 16 && lds_open) {
+    if (lazy && lds_open) {
       // LDS table: claim by CAS on ctrl after the key words are known; a racing claimer of the
       // same slot either wins (and writes the same-or-other key) or re-probes.  Keys are written
       // BEFORE ctrl by the winner, so readers compare after seeing a non-zero ctrl... which needs
       // the key in the same atomic: LDS slots therefore publish k0/k1 first under a per-slot
       // two-phase (ctrl = BUSY, then ctrl = want) and readers re-probe the slot while BUSY.
-      const uint32_t tag = tag_of(k.hash);
-      const unsigned long long want = ((unsigned long long)tag << 32) | kReady | k.len;
-      uint32_t s = (uint32_t)(k.hash & (kLdsSlots - 1));
+      const uint32_t lh = lds_hash(k.k0, k.k1, k.len);
+      const unsigned long long want = ((unsigned long long)lh << 32) | kReady | k.len;
+      uint32_t s = lh & (kLdsSlots - 1);
       for (int probe = 0; probe < kLdsProbe * 4 && !done; ) {
         // a hit (the common case once the few groups are in) needs no CAS: read ctrl, compare
         // the key, add; only an empty slot is claimed with a CAS
@@ -368,7 +383,10 @@ __global__ __launch_bounds__(kBlock) void dq_freq_insert_kernel(FreqKeySpec ks,
       }
       if (!done && ++lds_misses > 32) lds_open = 0;  // LDS is full of other keys: stop probing it
     }
-    if (!done && !global_insert(T, k, 1ull)) break;
+    if (!done) {
+      if (lazy) k.hash = hash_inline(k.k0, k.k1, k.len);
+      if (!global_insert(T, k, 1ull)) break;
+    }
   }
   __syncthreads();
   // flush the LDS groups

@@ -49,6 +49,17 @@ __device__ inline uint32_t ld32(const uint8_t* p) {
   return (w[0] >> sh) | (w[1] << (32u - sh));
 }
 
+// [p, p + n), n <= 7, little-endian and zero padded: the one or two aligned 8-byte words that
+// hold a byte of the range (never a word without one, so never beyond the page of a valid byte).
+__device__ inline uint64_t ld_tail(const uint8_t* p, uint32_t n) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(a & ~(uintptr_t)7);
+  const uint32_t sh = (uint32_t)(a & 7) * 8u;
+  uint64_t v = w[0] >> sh;
+  if (sh && (a & 7) + n > 8) v |= w[1] << (64u - sh);
+  return v & ((1ull << (8u * n)) - 1ull);
+}
+
 // XXH64 (Spark XXH64.hashUnsafeBytes) over [p, p + len).
 __device__ uint64_t xxh64_bytes(const uint8_t* p, int64_t len, uint64_t seed) {
   const uint8_t* end = p + len;
@@ -106,16 +117,20 @@ __device__ inline W64 xxh64_short_dev(const uint8_t* p, uint32_t len, const uint
     h.hi ^= k.hi;
     h = w64_mul<kP1, kP4>(w64_rotl<27>(h));
   }
+  // the < 8-byte tail: loaded once (the aligned words holding it), its 4-byte word and single
+  // bytes then come out of that register instead of one memory access each
+  uint64_t tail = i < len ? ld_tail(p + i, len - i) : 0ull;
   if (i + 4 <= len) {
-    const uint32_t w = ld32(p + i);
+    const uint32_t w = (uint32_t)tail;
+    tail >>= 32;
     const uint64_t pr = (uint64_t)w * (uint32_t)kP1;
     h.lo ^= (uint32_t)pr;
     h.hi ^= (uint32_t)(pr >> 32) + w * (uint32_t)(kP1 >> 32);
     h = w64_mul<kP2, kP3>(w64_rotl<23>(h));
     i += 4;
   }
-  for (; i < len; ++i) {
-    const uint32_t b = p[i];
+  for (; i < len; ++i, tail >>= 8) {
+    const uint32_t b = (uint32_t)tail & 0xffu;
     const uint64_t pr = (uint64_t)b * (uint32_t)kP5;
     h.lo ^= (uint32_t)pr;
     h.hi ^= (uint32_t)(pr >> 32) + b * (uint32_t)(kP5 >> 32);
