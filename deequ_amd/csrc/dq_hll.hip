@@ -21,14 +21,37 @@ namespace {
 
 __device__ inline void hll_update(uint32_t* regs, uint64_t x) { hll_update_lds(regs, x); }
 
+// A boolean column hashes to one of two values (hashInt(1) / hashInt(0)), so its registers are
+// those two updates, made when the workgroup's rows hold a selected true / a selected false:
+// 32 rows per lane per step from the value, validity and `where` bitmaps, no per-row hash or
+// LDS atomic.  (row_begin is a multiple of kScanRowAlign, so rows map to whole 32-bit words.)
+__device__ inline uint32_t bitmap_word(const uint8_t* bm, int64_t row0, int64_t left) {
+  const uint8_t* p = bm + (row0 >> 3);
+  if (left >= 32) return *reinterpret_cast<const uint32_t*>(p);
+  uint32_t v = 0u;  // tail: byte loads, never past ceil(n_rows / 8)
+  for (int b = 0; b < (int)((left + 7) >> 3); ++b) v |= (uint32_t)p[b] << (8 * b);
+  return v;
+}
+
 __device__ void hll_bool(uint32_t* regs, const DevColumn& col, const uint8_t* wt_bm,
                          int64_t row_begin, int64_t row_end) {
   const uint8_t* bits = static_cast<const uint8_t*>(col.values);
-  const uint64_t h1 = xxh64_u32(1u, 42), h0 = xxh64_u32(0u, 42);
-  for (int64_t row = row_begin + threadIdx.x; row < row_end; row += kBlock) {
-    bool sel = !col.validity || ((col.validity[row >> 3] >> (row & 7)) & 1u);
-    if (wt_bm) sel = sel && ((wt_bm[row >> 3] >> (row & 7)) & 1u);
-    if (sel) hll_update(regs, ((bits[row >> 3] >> (row & 7)) & 1u) ? h1 : h0);
+  uint32_t any_true = 0u, any_false = 0u;
+  for (int64_t row0 = row_begin + (int64_t)threadIdx.x * 32; row0 < row_end; row0 += (int64_t)kBlock * 32) {
+    const int64_t left = row_end - row0;
+    const uint32_t in = left >= 32 ? 0xffffffffu : ((1u << (uint32_t)left) - 1u);
+    uint32_t sel = in;
+    if (col.validity) sel &= bitmap_word(col.validity, row0, left);
+    if (wt_bm) sel &= bitmap_word(wt_bm, row0, left);
+    const uint32_t v = bitmap_word(bits, row0, left);
+    any_true |= sel & v;
+    any_false |= sel & ~v;
+  }
+  const bool t = __syncthreads_or(any_true != 0u);
+  const bool f = __syncthreads_or(any_false != 0u);
+  if (threadIdx.x == 0) {
+    if (t) hll_update(regs, xxh64_u32(1u, 42));
+    if (f) hll_update(regs, xxh64_u32(0u, 42));
   }
 }
 
