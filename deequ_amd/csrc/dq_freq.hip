@@ -340,27 +340,20 @@ __global__ __launch_bounds__(kBlock) void dq_freq_insert_kernel(FreqKeySpec ks,
   const int64_t row_end = row_begin + per_block < n_rows ? row_begin + per_block : n_rows;
   alignas(8) uint8_t scratch[kMaxLocalKey];
   unsigned long long lds_misses = 0;
-  for (int64_t row = row_begin + threadIdx.x; row < row_end; row += kBlock) {
-    Key k;
-    bool too_long;
-    if (!make_key(ks, cols, row, k, scratch, too_long, false)) {
-      if (too_long) atomicOr(T.overflow, 4u);
-      continue;
-    }
+  // One row through the LDS table (claiming, probing) and, failing that, the global table.
+  // Returns false on a global table overflow.
+  auto insert_row = [&](Key& k) -> bool {
     const bool lazy = k.ptr == nullptr && k.len <= 16;  // inline key: k.hash not computed yet
     bool done = false;
     if (lazy && lds_open) {
       // LDS table: claim by CAS on ctrl after the key words are known; a racing claimer of the
-      // same slot either wins (and writes the same-or-other key) or re-probes.  Keys are written
-      // BEFORE ctrl by the winner, so readers compare after seeing a non-zero ctrl... which needs
-      // the key in the same atomic: LDS slots therefore publish k0/k1 first under a per-slot
-      // two-phase (ctrl = BUSY, then ctrl = want) and readers re-probe the slot while BUSY.
+      // same slot either wins (and writes the same-or-other key) or re-probes.  LDS slots publish
+      // k0/k1 under a per-slot two-phase (ctrl = BUSY, then ctrl = want) and readers re-probe
+      // the slot while BUSY.
       const uint32_t lh = lds_hash(k.k0, k.k1, k.len);
       const unsigned long long want = ((unsigned long long)lh << 32) | kReady | k.len;
       uint32_t s = lh & (kLdsSlots - 1);
       for (int probe = 0; probe < kLdsProbe * 4 && !done; ) {
-        // a hit (the common case once the few groups are in) needs no CAS: read ctrl, compare
-        // the key, add; only an empty slot is claimed with a CAS
         unsigned long long c = __hip_atomic_load(&lds[s].ctrl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (c == 0ull) c = atomicCAS(&lds[s].ctrl, 0ull, 1ull);  // 1 = BUSY
         if (c == 0ull) {
@@ -385,7 +378,56 @@ __global__ __launch_bounds__(kBlock) void dq_freq_insert_kernel(FreqKeySpec ks,
     }
     if (!done) {
       if (lazy) k.hash = hash_inline(k.k0, k.k1, k.len);
-      if (!global_insert(T, k, 1ull)) break;
+      if (!global_insert(T, k, 1ull)) return false;
+    }
+    return true;
+  };
+  if (ks.n_keys == 1) {
+    // Single-column keys (no scratch): R rows per lane per step, the common case -- the key is
+    // already in its home slot -- as independent loads (R slot words read together, ONE acquire
+    // fence, R key compares, R counter adds), so the LDS round trips overlap instead of chaining
+    // row after row.  Anything else (empty or busy slot, collision) takes insert_row.
+    constexpr int R = 4;
+    bool overflowed = false;
+    for (int64_t base = row_begin; base < row_end && !overflowed; base += (int64_t)kBlock * R) {
+      Key k[R];
+      bool ok[R];
+      uint32_t slot[R];
+      unsigned long long want[R], c[R];
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const int64_t row = base + (int64_t)j * kBlock + threadIdx.x;
+        bool too_long = false;
+        ok[j] = row < row_end && make_key(ks, cols, row, k[j], scratch, too_long, false);
+        if (!ok[j] && too_long) atomicOr(T.overflow, 4u);
+        const bool fast = ok[j] && k[j].ptr == nullptr && k[j].len <= 16 && lds_open;
+        const uint32_t lh = fast ? lds_hash(k[j].k0, k[j].k1, k[j].len) : 0u;
+        want[j] = fast ? (((unsigned long long)lh << 32) | kReady | k[j].len) : 0ull;
+        slot[j] = lh & (kLdsSlots - 1);
+      }
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        c[j] = want[j] ? __hip_atomic_load(&lds[slot[j]].ctrl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0ull;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the keys published before those ctrl words
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        bool hit = false;
+        if (want[j] && c[j] == want[j])
+          hit = __hip_atomic_load(&lds[slot[j]].k0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == k[j].k0 &&
+                __hip_atomic_load(&lds[slot[j]].k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == k[j].k1;
+        if (hit) atomicAdd(&lds[slot[j]].count, 1u);
+        else if (ok[j] && !insert_row(k[j])) overflowed = true;
+      }
+    }
+  } else {
+    for (int64_t row = row_begin + threadIdx.x; row < row_end; row += kBlock) {
+      Key k;
+      bool too_long;
+      if (!make_key(ks, cols, row, k, scratch, too_long, false)) {
+        if (too_long) atomicOr(T.overflow, 4u);
+        continue;
+      }
+      if (!insert_row(k)) break;
     }
   }
   __syncthreads();
@@ -983,10 +1025,10 @@ __global__ __launch_bounds__(kBlock) void dq_freq_heap_need_kernel(FreqKeySpec k
 }
 
 hipError_t launch_freq_insert(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
-                              const FreqTable& T, hipStream_t stream) {
+                              const FreqTable& T, hipStream_t stream, int max_blocks) {
   if (n_rows <= 0) return hipSuccess;
   int64_t blocks = (n_rows + 4095) / 4096;
-  if (blocks > 4096) blocks = 4096;
+  if (blocks > max_blocks) blocks = max_blocks;
   hipLaunchKernelGGL(dq_freq_insert_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, ks, d_cols,
                      n_rows, T);
   return hipGetLastError();

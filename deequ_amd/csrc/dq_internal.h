@@ -203,7 +203,8 @@ struct FreqIn {  // groups to merge in; heap offsets in k0 refer to `heap`
 };
 
 hipError_t launch_freq_insert(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
-                              const FreqTable& T, hipStream_t stream);
+                              const FreqTable& T, hipStream_t stream,
+                              int max_blocks = 4096);
 hipError_t launch_freq_hist(const FreqTable& T, unsigned long long* d_hist, unsigned long long* d_big,
                             unsigned long long* d_nbig, unsigned long long big_cap, hipStream_t stream);
 hipError_t launch_freq_export(const FreqTable& T, unsigned long long min_count, const FreqOut& out,
