@@ -638,7 +638,8 @@ __device__ inline bool row_selected(const FreqKeySpec& ks, const DevColumn* cols
 // pass writes every selected row at its ballot prefix -- no block barrier inside either loop.
 __global__ __launch_bounds__(kBlock) void dq_freq_stage_kernel(FreqKeySpec ks, const DevColumn* __restrict__ cols,
                                                                int64_t n_rows, FreqRec* out, uint32_t* sort_keys,
-                                                               unsigned long long* cursor, uint32_t* hll) {
+                                                               unsigned long long* cursor, uint32_t* hll,
+                                                               unsigned long long* long_key) {
   __shared__ uint32_t regs[kHllM];
   __shared__ uint32_t wcount[kBlock / 64];
   __shared__ unsigned long long base_s;
@@ -682,9 +683,10 @@ __global__ __launch_bounds__(kBlock) void dq_freq_stage_kernel(FreqKeySpec ks, c
         r.k1 = k.k1 | ((unsigned long long)k.len << kRecLenShift);
         key32 = (uint32_t)(k.hash >> 32);
         sketch_update(regs, k.hash);
-      } else {  // cannot happen on a batch the host routed here; keep the reserved slot inert
+      } else {  // a key longer than 15 bytes: the host rolls this batch back to the general path
         r.k0 = 0;
         r.k1 = (unsigned long long)kRecHole << kRecLenShift;
+        atomicMax(long_key, (unsigned long long)(k.len > 15 ? k.len : 16));
       }
       out[pos] = r;
       sort_keys[pos] = key32;
@@ -945,12 +947,12 @@ hipError_t launch_freq_part_scatter(const FreqTable& T, int n_parts, const unsig
 
 hipError_t launch_freq_stage(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, FreqRec* d_out,
                              uint32_t* d_sort_keys, unsigned long long* d_cursor, uint32_t* d_hll,
-                             hipStream_t stream) {
+                             unsigned long long* d_long_key, hipStream_t stream) {
   if (n_rows <= 0) return hipSuccess;
   int64_t blocks = (n_rows + kBlock * 16 - 1) / (kBlock * 16);
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(dq_freq_stage_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, ks, d_cols, n_rows, d_out,
-                     d_sort_keys, d_cursor, d_hll);
+                     d_sort_keys, d_cursor, d_hll, d_long_key);
   return hipGetLastError();
 }
 

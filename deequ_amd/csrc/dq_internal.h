@@ -225,7 +225,7 @@ hipError_t launch_freq_part_scatter(const FreqTable& T, int n_parts, const unsig
 // hash bits) + an HLL sketch of their hashes (to size the table), sort by the key's top `bits`
 // bits (the slice), then aggregate every slice's bucket in LDS (split buckets merge atomically).
 hipError_t launch_freq_stage(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, FreqRec* d_out,
-                             uint32_t* d_sort_keys, unsigned long long* d_cursor, uint32_t* d_hll,
+                             uint32_t* d_sort_keys, unsigned long long* d_cursor, uint32_t* d_hll, unsigned long long* d_long_key,
                              hipStream_t stream);
 hipError_t launch_freq_slice_keys(const FreqRec* d_recs, uint64_t n, int bits, int from_records, uint32_t* d_keys,
                                   hipStream_t stream);
