@@ -760,31 +760,29 @@ __device__ inline void emit_retry(FreqRec* retry, unsigned long long* n_retry, c
   for (unsigned long long j = 0; j < copies; ++j) retry[at + j] = r;
 }
 
-__global__ __launch_bounds__(kBlock) void dq_freq_agg_kernel(FreqTable T, const FreqRec* __restrict__ recs,
-                                                             const uint64_t* __restrict__ off,
-                                                             const uint32_t* __restrict__ piece_start,
-                                                             uint64_t n_buckets, int table_empty, FreqRec* retry,
-                                                             unsigned long long* n_retry,
-                                                             unsigned long long* new_groups) {
+// The LDS image of one slice (dq_freq_agg_kernel, dq_freq_agg_region_kernel).
+struct AggLds {
+  unsigned long long K0[kFreqSliceSlots], K1[kFreqSliceSlots];
+  uint32_t C[kFreqSliceSlots];
+  int overflow;
+  uint32_t fresh;
+  unsigned long long retry_base;
+};
+
+// Aggregate records [r0, r1) of slice b.  owner: the work item holds the slice's whole bucket
+// (load the slice, count in LDS, write it back with plain stores); otherwise it is one piece of a
+// split bucket (count in LDS, merge into the slice with device-scope atomics).
+__device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restrict__ recs, uint64_t r0, uint64_t r1,
+                         uint64_t b, bool owner, int table_empty, FreqRec* retry, unsigned long long* n_retry,
+                         unsigned long long* new_groups) {
   constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
-  __shared__ unsigned long long K0[S], K1[S];
-  __shared__ uint32_t C[S];
-  __shared__ int overflow;
-  __shared__ uint32_t fresh;
-  __shared__ unsigned long long retry_base;
-  const uint32_t n_items = piece_start[n_buckets];
-  for (uint32_t w = blockIdx.x; w < n_items; w += gridDim.x) {
-    // the bucket of work item w: piece_start[b] <= w < piece_start[b + 1]
-    uint64_t lo = 0, hi = n_buckets;
-    while (hi - lo > 1) {
-      const uint64_t mid = (lo + hi) >> 1;
-      if (piece_start[mid] <= w) lo = mid;
-      else hi = mid;
-    }
-    const uint64_t b = lo;
-    const bool owner = piece_start[b + 1] - piece_start[b] == 1u;
-    const uint64_t r0 = off[b] + (uint64_t)(w - piece_start[b]) * kFreqAggPiece;
-    const uint64_t r1 = min(off[b + 1], r0 + kFreqAggPiece);
+  unsigned long long* K0 = L.K0;
+  unsigned long long* K1 = L.K1;
+  uint32_t* C = L.C;
+  int& overflow = L.overflow;
+  uint32_t& fresh = L.fresh;
+  unsigned long long& retry_base = L.retry_base;
+  {
     FreqSlot* slice = T.slots + (b << kFreqSliceLog);
     for (uint32_t s = threadIdx.x; s < S; s += kBlock) {
       if (owner && !table_empty) {
@@ -901,6 +899,192 @@ __global__ __launch_bounds__(kBlock) void dq_freq_agg_kernel(FreqTable T, const 
   }
 }
 
+__global__ __launch_bounds__(kBlock) void dq_freq_agg_kernel(FreqTable T, const FreqRec* __restrict__ recs,
+                                                             const uint64_t* __restrict__ off,
+                                                             const uint32_t* __restrict__ piece_start,
+                                                             uint64_t n_buckets, int table_empty, FreqRec* retry,
+                                                             unsigned long long* n_retry,
+                                                             unsigned long long* new_groups) {
+  __shared__ AggLds L;
+  const uint32_t n_items = piece_start[n_buckets];
+  for (uint32_t w = blockIdx.x; w < n_items; w += gridDim.x) {
+    // the bucket of work item w: piece_start[b] <= w < piece_start[b + 1]
+    uint64_t lo = 0, hi = n_buckets;
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (piece_start[mid] <= w) lo = mid;
+      else hi = mid;
+    }
+    const uint64_t b = lo;
+    const bool owner = piece_start[b + 1] - piece_start[b] == 1u;
+    const uint64_t r0 = off[b] + (uint64_t)(w - piece_start[b]) * kFreqAggPiece;
+    const uint64_t r1 = min(off[b + 1], r0 + kFreqAggPiece);
+    agg_item(L, T, recs, r0, r1, b, owner, table_empty, retry, n_retry, new_groups);
+  }
+}
+
+// ---- partition path (replaces the radix sort for large stagings) --------------------------
+// Two passes of an LDS multi-split put every staged record into the region of its slice:
+//  P1: stage array -> 2^b1 level-1 regions (top b1 bits of the table hash);
+//  P2: each level-1 region -> the 2^(bits-b1) slice regions under it.
+// A region has a fixed capacity (its expected share + a 6-sigma margin, sized on the host from
+// the row count and the sketch's distinct estimate); a workgroup reserves its records' room in a
+// region with ONE atomic per (tile, region), writes them from an LDS image sorted by region (runs
+// of ~32 records, coalesced), and records beyond a region's capacity go to an overflow list that
+// the sort path aggregates afterwards (skewed data).  Then dq_freq_agg_region_kernel aggregates
+// each slice region in LDS as the owner of its slice.  Per pass: 16 B read + 16 B written per
+// record (the sort moved 20 B keyed records three times, plus a key histogram pass).
+constexpr int kPartThreads = 1024;
+constexpr int kPartPerThread = 16;
+constexpr uint32_t kPartTile = (uint32_t)kPartThreads * kPartPerThread;  // records per tile
+constexpr uint32_t kPartSub = 4096;                                      // records per LDS round
+constexpr int kPartMaxBinBits = 11;
+constexpr uint32_t kPartNoBin = 0xFFFFu;
+
+struct PartLds {
+  FreqRec rec[kPartSub];
+  uint16_t bin[kPartSub];
+  uint32_t hist[1 << kPartMaxBinBits];
+  uint32_t start[1 << kPartMaxBinBits];
+  unsigned long long gbase[1 << kPartMaxBinBits];
+  uint32_t total;
+};
+
+__device__ inline uint64_t rec_hash(const FreqRec& r, bool* hole) {
+  unsigned long long k1;
+  uint32_t len;
+  rec_unpack(r, &k1, &len);
+  *hole = len == kRecHole;
+  return hash_inline(r.k0, k1, len);
+}
+
+// in_fill == nullptr: level 1, tile blockIdx.x of in[0, in_n).  Otherwise level 2: tile
+// blockIdx.x of region blockIdx.y (in + y * in_cap, min(in_fill[y], in_cap) records).
+// A record's output region = the top id_bits of its hash; its LDS bin = the low bin_bits of
+// that id (the higher id bits are the input region's, uniform over the tile).
+__global__ __launch_bounds__(kPartThreads) void dq_freq_part_kernel(
+    const FreqRec* __restrict__ in, uint64_t in_n, const unsigned long long* __restrict__ in_fill, uint64_t in_cap,
+    int id_bits, int bin_bits, FreqRec* __restrict__ out, uint64_t out_cap, unsigned long long* out_fill,
+    FreqRec* ovf, unsigned long long* ovf_n, uint64_t ovf_cap, unsigned int* flag) {
+  __shared__ PartLds L;
+  const uint32_t t = threadIdx.x;
+  const uint32_t nb = 1u << bin_bits;
+  uint64_t base_id = 0, begin, count;
+  if (in_fill) {
+    const uint64_t r = blockIdx.y;
+    const unsigned long long f = in_fill[r];
+    const uint64_t have = f < in_cap ? f : in_cap;
+    begin = (uint64_t)blockIdx.x * kPartTile;
+    if (begin >= have) return;
+    count = min((uint64_t)kPartTile, have - begin);
+    begin += r * in_cap;
+    base_id = r << bin_bits;
+  } else {
+    begin = (uint64_t)blockIdx.x * kPartTile;
+    if (begin >= in_n) return;
+    count = min((uint64_t)kPartTile, in_n - begin);
+  }
+  for (uint32_t i = t; i < nb; i += kPartThreads) L.hist[i] = 0u;
+  if (t == 0) L.total = 0u;
+  FreqRec rec[kPartPerThread];
+  uint32_t bin[kPartPerThread];
+#pragma unroll
+  for (int i = 0; i < kPartPerThread; ++i) {
+    const uint32_t j = (uint32_t)i * kPartThreads + t;
+    if (j < count) rec[i] = in[begin + j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kPartPerThread; ++i) {
+    const uint32_t j = (uint32_t)i * kPartThreads + t;
+    bin[i] = kPartNoBin;
+    if (j < count) {
+      bool hole;
+      const uint64_t h = rec_hash(rec[i], &hole);
+      if (!hole) bin[i] = (uint32_t)(h >> (64 - id_bits)) & (nb - 1u);
+    }
+  }
+  // rank of each record within its bin (LDS atomics), packed with the bin: rank << 16 | bin
+#pragma unroll
+  for (int i = 0; i < kPartPerThread; ++i)
+    if (bin[i] != kPartNoBin) bin[i] |= atomicAdd(&L.hist[bin[i]], 1u) << 16;
+  __syncthreads();
+  // exclusive scan of the bins by wave 0 (nb / 64 consecutive bins per lane), then the room of
+  // each bin in its output region: one atomic per non-empty bin
+  if (t < 64) {
+    const uint32_t per = (nb + 63u) / 64u;
+    uint32_t s = 0;
+    for (uint32_t k = 0; k < per; ++k) {
+      const uint32_t b = t * per + k;
+      if (b < nb) s += L.hist[b];
+    }
+    uint32_t incl = s;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(incl, d, 64);
+      if ((int)t >= d) incl += o;
+    }
+    uint32_t run = incl - s;
+    for (uint32_t k = 0; k < per; ++k) {
+      const uint32_t b = t * per + k;
+      if (b < nb) {
+        L.start[b] = run;
+        run += L.hist[b];
+      }
+    }
+    if (t == 63) L.total = incl;
+  }
+  __syncthreads();
+  for (uint32_t b = t; b < nb; b += kPartThreads) {
+    const uint32_t c = L.hist[b];
+    L.gbase[b] = c ? atomicAdd(&out_fill[base_id + b], (unsigned long long)c) : 0ull;
+  }
+  const uint32_t total = L.total;
+  __syncthreads();
+  for (uint32_t r0 = 0; r0 < total; r0 += kPartSub) {
+#pragma unroll
+    for (int i = 0; i < kPartPerThread; ++i) {
+      if ((bin[i] & 0xFFFFu) == kPartNoBin) continue;
+      const uint32_t b = bin[i] & 0xFFFFu;
+      const uint32_t p = L.start[b] + (bin[i] >> 16) - r0;
+      if (p < kPartSub) {
+        L.rec[p] = rec[i];
+        L.bin[p] = (uint16_t)b;
+      }
+    }
+    __syncthreads();
+    const uint32_t m = min(kPartSub, total - r0);
+    for (uint32_t j = t; j < m; j += kPartThreads) {
+      const uint32_t b = L.bin[j];
+      const uint64_t o = L.gbase[b] + (r0 + j - L.start[b]);
+      const FreqRec r = L.rec[j];
+      if (o < out_cap) {
+        out[(base_id + b) * out_cap + o] = r;
+      } else {  // the region is full: the overflow list (aggregated by the sort path)
+        const unsigned long long k = atomicAdd(ovf_n, 1ull);
+        if (k < ovf_cap) ovf[k] = r;
+        else atomicOr(flag, 1u);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Aggregate slice region b (records b * cap .. + min(fill[b], cap)) as its slice's owner.
+__global__ __launch_bounds__(kBlock) void dq_freq_agg_region_kernel(FreqTable T, const FreqRec* __restrict__ recs,
+                                                                    const unsigned long long* __restrict__ fill,
+                                                                    uint64_t cap, uint64_t n_slices, int table_empty,
+                                                                    FreqRec* retry, unsigned long long* n_retry,
+                                                                    unsigned long long* new_groups) {
+  __shared__ AggLds L;
+  for (uint64_t b = blockIdx.x; b < n_slices; b += gridDim.x) {
+    const unsigned long long f = fill[b];
+    const uint64_t r0 = b * cap;
+    const uint64_t r1 = r0 + (f < cap ? f : cap);
+    if (r1 == r0) continue;
+    agg_item(L, T, recs, r0, r1, b, true, table_empty, retry, n_retry, new_groups);
+  }
+}
+
 // Table growth: move every group of `old_slots` into the (empty, larger) table T.  All keys
 // are distinct, so a slot is claimed with its final ctrl word and nobody compares keys.
 __global__ __launch_bounds__(kBlock) void dq_freq_rehash_kernel(const FreqSlot* __restrict__ old_slots,
@@ -983,6 +1167,34 @@ hipError_t launch_freq_agg(const FreqTable& T, const FreqRec* d_recs, const uint
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(dq_freq_agg_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, d_recs, d_off,
                      d_piece_start, n_buckets, table_empty, d_retry, d_n_retry, d_new_groups);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_part(const FreqRec* d_in, uint64_t in_n, const unsigned long long* d_in_fill, uint64_t in_cap,
+                            uint64_t n_in_regions, int id_bits, int bin_bits, FreqRec* d_out, uint64_t out_cap,
+                            unsigned long long* d_out_fill, FreqRec* d_ovf, unsigned long long* d_ovf_n,
+                            uint64_t ovf_cap, unsigned int* d_flag, hipStream_t stream) {
+  if (bin_bits < 0 || bin_bits > kPartMaxBinBits || id_bits < bin_bits || id_bits > 32) return hipErrorInvalidValue;
+  dim3 grid;
+  if (d_in_fill) {
+    if (n_in_regions == 0 || n_in_regions > 65535) return hipErrorInvalidValue;
+    grid = dim3((unsigned)((in_cap + kPartTile - 1) / kPartTile), (unsigned)n_in_regions);
+  } else {
+    if (in_n == 0) return hipSuccess;
+    grid = dim3((unsigned)((in_n + kPartTile - 1) / kPartTile));
+  }
+  hipLaunchKernelGGL(dq_freq_part_kernel, grid, dim3(kPartThreads), 0, stream, d_in, in_n, d_in_fill, in_cap, id_bits,
+                     bin_bits, d_out, out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_agg_region(const FreqTable& T, const FreqRec* d_recs, const unsigned long long* d_fill,
+                                  uint64_t cap, uint64_t n_slices, int table_empty, FreqRec* d_retry,
+                                  unsigned long long* d_n_retry, unsigned long long* d_new_groups, hipStream_t stream) {
+  uint64_t blocks = n_slices < 65536 ? n_slices : 65536;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(dq_freq_agg_region_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, d_recs, d_fill, cap,
+                     n_slices, table_empty, d_retry, d_n_retry, d_new_groups);
   return hipGetLastError();
 }
 

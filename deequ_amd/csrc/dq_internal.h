@@ -239,6 +239,16 @@ hipError_t launch_freq_agg(const FreqTable& T, const FreqRec* d_recs, const uint
                            const uint32_t* d_piece_start, uint64_t n_buckets, uint64_t max_items, int table_empty,
                            FreqRec* d_retry, unsigned long long* d_n_retry, unsigned long long* d_new_groups,
                            hipStream_t stream);
+// Partition path (dq_freq.hip): stage array (d_in_fill == nullptr) or regions -> regions of
+// out_cap records by the top id_bits of the table hash; overflow -> d_ovf (d_flag bit 0 when
+// that is full too).  Then one owner work item per slice region.
+hipError_t launch_freq_part(const FreqRec* d_in, uint64_t in_n, const unsigned long long* d_in_fill, uint64_t in_cap,
+                            uint64_t n_in_regions, int id_bits, int bin_bits, FreqRec* d_out, uint64_t out_cap,
+                            unsigned long long* d_out_fill, FreqRec* d_ovf, unsigned long long* d_ovf_n,
+                            uint64_t ovf_cap, unsigned int* d_flag, hipStream_t stream);
+hipError_t launch_freq_agg_region(const FreqTable& T, const FreqRec* d_recs, const unsigned long long* d_fill,
+                                  uint64_t cap, uint64_t n_slices, int table_empty, FreqRec* d_retry,
+                                  unsigned long long* d_n_retry, unsigned long long* d_new_groups, hipStream_t stream);
 hipError_t launch_freq_rehash(const FreqSlot* d_old, uint64_t old_n, const FreqTable& T, hipStream_t stream);
 
 // ---------------------------------------------------------------- launchers (.hip files)

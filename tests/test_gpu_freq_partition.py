@@ -1,0 +1,113 @@
+"""The partition path of the sorted-bucket group-by (dq_freq_part_kernel P1/P2 +
+dq_freq_agg_region_kernel), forced onto small stagings with DQ_FREQ_PART_MIN=1, against the
+oracle, numpy and the radix-sort path (DQ_FREQ_PART=0).
+
+Covers: several key encodings and batches; a table that is not empty when the partition runs
+(a small staging budget aggregates early); high cardinality (many slice regions, P2 on); a hot
+key that overflows its region into the overflow list (aggregated afterwards by the sort path);
+a hot key large enough to fill the overflow list (the whole staging falls back to the sort);
+few groups (one pass, no P2).  Bit-exact: every group and count."""
+import numpy as np
+import pytest
+
+import deequ_amd as d
+import pyoracle as O
+from deequ_amd.frequencies import FrequencyTable, encode_key
+from helpers import oracle_table, product_table
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def part(monkeypatch):
+    monkeypatch.setenv("DQ_FREQ_PART_MIN", "1")
+    monkeypatch.setenv("DQ_FREQ_PATH", "sorted")
+
+
+def _export(t):
+    counts, keys = t.export()
+    return dict(zip(keys, counts.tolist()))
+
+
+def _int_groups(t):
+    counts, keys = t.export()
+    return {int.from_bytes(k, "little", signed=True): int(c) for k, c in zip(keys, counts.tolist())}
+
+
+@pytest.mark.parametrize("budget", [None, "3000"])
+def test_partition_matches_oracle(gpu, part, monkeypatch, budget):
+    if budget:
+        monkeypatch.setenv("DQ_FREQ_STAGE_BUDGET", budget)
+    rng = np.random.default_rng(11)
+    n = 20000
+    a = rng.integers(0, n // 3 + 1, n)
+    spec = {"key": ["string", [None if i % 19 == 0 else "k%d" % a[i] for i in range(n)]],
+            "i": ["int64", [None if i % 23 == 0 else int(a[i] % 1000) for i in range(n)]]}
+    table = product_table(spec)
+    schema = dict(table.schema)
+    for cols in (["key"], ["i"], ["key", "i"]):
+        t = FrequencyTable(cols, schema)
+        step = n // 4
+        for s in range(0, n, step):
+            t.consume(d.Table.from_pydict({c: (schema[c], table.columns[c].to_pylist()[s:s + step])
+                                           for c in schema}))
+        got = _export(t)
+        st = O.frequencies_state(oracle_table(spec), cols)
+        want = {encode_key(list(k), [spec[c][0] for c in cols]): c for k, c in st.frequencies.items()}
+        assert got == want, cols
+        s = t.summary()
+        assert s.num_groups == len(want)
+        assert s.num_unique == sum(1 for c in want.values() if c == 1)
+
+
+@pytest.mark.parametrize("n,distinct", [(3_000_000, 1_500_000), (5_000_000, 200_000), (2_000_000, 40)])
+def test_partition_counts_exact(gpu, part, n, distinct):
+    rng = np.random.default_rng(12)
+    vals = rng.integers(0, distinct, n)
+    valid = rng.random(n) > 0.01
+    table = d.Table({"v": d.Column.from_numpy(vals, valid, "int64")})
+    t = FrequencyTable(["v"], {"v": "int64"})
+    t.consume(table)
+    s = t.summary()
+    u, c = np.unique(vals[valid], return_counts=True)
+    assert s.num_groups == len(u)
+    assert s.num_unique == int((c == 1).sum())
+    assert s.grouped_rows == int(valid.sum())
+    if len(u) <= 1_000_000:
+        assert _int_groups(t) == dict(zip(u.tolist(), c.tolist()))
+
+
+@pytest.mark.parametrize("hot_frac", [0.5, 0.03])
+def test_partition_hot_key_overflow(gpu, part, hot_frac):
+    """0.03: the hot key's rows overflow its level-1 region into the overflow list; 0.5: they
+    overflow the list too and the staging is sorted instead.  Exact either way."""
+    rng = np.random.default_rng(13)
+    n = 4_000_000
+    vals = rng.integers(0, 300_000, n)
+    vals[rng.random(n) < hot_frac] = 987_654_321
+    table = d.Table({"v": d.Column.from_numpy(vals, None, "int64")})
+    t = FrequencyTable(["v"], {"v": "int64"})
+    t.consume(table)
+    u, c = np.unique(vals, return_counts=True)
+    assert _int_groups(t) == dict(zip(u.tolist(), c.tolist()))
+
+
+def test_partition_equals_sort_path_strings(gpu, monkeypatch):
+    """12-digit keys (the C4 shape) on both paths: identical groups and counts."""
+    rng = np.random.default_rng(14)
+    n = 2_000_000
+    keys = ["%012d" % v for v in rng.integers(0, 400_000, n)]
+    spec = {"key": ["string", keys]}
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DQ_FREQ_PART", mode)
+        monkeypatch.setenv("DQ_FREQ_PART_MIN", "1")
+        table = product_table(spec)
+        t = FrequencyTable(["key"], dict(table.schema))
+        t.consume(table)
+        res[mode] = _export(t)
+        t.close()
+    assert res["0"] == res["1"]
+    vals, cnt = np.unique(np.array(keys), return_counts=True)
+    assert len(res["1"]) == len(vals)
+    assert sorted(res["1"].values()) == sorted(cnt.tolist())
