@@ -475,6 +475,28 @@ __global__ __launch_bounds__(kBlock) void dq_freq_hist_kernel(FreqTable T, unsig
 }
 
 // Export groups: slots with count >= min_count (and, for count == tie_count, all of them).
+// smax (optional): the largest count of each slice; slices below min_count are not read.
+__global__ __launch_bounds__(kBlock) void dq_freq_export_slices_kernel(FreqTable T, unsigned long long min_count,
+                                                                       const uint32_t* __restrict__ smax, FreqOut out) {
+  const uint64_t n_slices = (T.mask + 1) >> kFreqSliceLog;
+  for (uint64_t b = blockIdx.x; b < n_slices; b += gridDim.x) {
+    if ((unsigned long long)smax[b] < min_count) continue;
+    const FreqSlot* slice = T.slots + (b << kFreqSliceLog);
+    for (uint32_t s = threadIdx.x; s < (uint32_t)kFreqSliceSlots; s += kBlock) {
+      const FreqSlot& e = slice[s];
+      if ((e.ctrl & kReady) && e.count >= min_count) {
+        const unsigned long long i = atomicAdd(out.n, 1ull);
+        if (i < out.cap) {
+          out.ctrl[i] = e.ctrl;
+          out.count[i] = e.count;
+          out.k0[i] = e.k0;
+          out.k1[i] = e.k1;
+        }
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void dq_freq_export_kernel(FreqTable T, unsigned long long min_count,
                                                                 FreqOut out) {
   const uint64_t n = T.mask + 1;
@@ -761,20 +783,93 @@ __device__ inline void emit_retry(FreqRec* retry, unsigned long long* n_retry, c
 }
 
 // The LDS image of one slice (dq_freq_agg_kernel, dq_freq_agg_region_kernel).
+constexpr int kAggLdsHist = 512;  // count-of-counts bins kept in LDS by a tracking aggregation
 struct AggLds {
   unsigned long long K0[kFreqSliceSlots], K1[kFreqSliceSlots];
   uint32_t C[kFreqSliceSlots];
   int overflow;
   uint32_t fresh;
+  uint32_t cmax;
   unsigned long long retry_base;
+  uint32_t hist[kAggLdsHist];
 };
+
+// What a partition-path aggregation into an EMPTY table also produces (nullptr / 0 = off):
+// the count-of-counts histogram of the new groups (so the metrics need no table scan), the
+// largest count of each slice (so a top-N export skips slices below its threshold), and every
+// slot of every slice written (zeros included), so the table needs no clearing beforehand.
+struct AggTrack {
+  unsigned long long* hist;   // kFreqHist bins
+  unsigned long long* big;    // counts >= kFreqHist
+  unsigned long long* n_big;
+  unsigned long long big_cap;
+  uint32_t* smax;             // per slice
+  int write_all;
+};
+
+__device__ inline void track_count(AggLds& L, const AggTrack& tr, uint32_t c) {
+  atomicMax(&L.cmax, c);
+  if (!tr.hist) return;
+  if (c < (uint32_t)kAggLdsHist) {
+    atomicAdd(&L.hist[c], 1u);
+  } else if (c < (uint32_t)kFreqHist) {
+    atomicAdd(&tr.hist[c], 1ull);
+  } else {
+    const unsigned long long i = atomicAdd(tr.n_big, 1ull);
+    if (i < tr.big_cap) tr.big[i] = c;
+  }
+}
+
+constexpr int kAggBatch = 8;
+
+// Count record r (table hash h) in the LDS slice image; false if the image is full.  (The
+// publishing lane's stores stay inside the loop iteration, with `done` tested by the loop: a
+// lane of the same wave spinning on BUSY must see them in its next iteration, so the publish
+// must not be sunk behind the loop -- an early return there hung the wave.)
+__device__ inline bool lds_count(unsigned long long* K0, unsigned long long* K1, uint32_t* C, const FreqRec& r,
+                                 uint64_t h) {
+  constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
+  uint32_t s = (uint32_t)(h & (S - 1));
+  bool done = false;
+  for (uint32_t probe = 0; probe < S && !done;) {
+    const unsigned long long c = atomicCAS(&K1[s], kLdsEmpty, kLdsBusy);
+    if (c == kLdsEmpty) {  // claimed: publish the key, then count
+      K0[s] = r.k0;
+      __threadfence_block();
+      atomicExch(&K1[s], r.k1);
+      atomicAdd(&C[s], 1u);
+      done = true;
+    } else if (c == kLdsBusy) {
+      // another lane is publishing this slot: look at it again
+    } else if (c == r.k1 && __hip_atomic_load(&K0[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == r.k0) {
+      atomicAdd(&C[s], 1u);
+      done = true;
+    } else {
+      s = (s + 1) & (S - 1);
+      ++probe;
+    }
+  }
+  return done;
+}
+
+// A piece holding more keys than LDS: the row goes straight to the slice (rare; not inlined).
+__device__ __noinline__ void piece_spill(const FreqTable& T, const FreqRec& r, unsigned long long k1, uint32_t len,
+                                         uint64_t h, FreqRec* retry, unsigned long long* n_retry) {
+  Key k;
+  k.k0 = r.k0;
+  k.k1 = k1;
+  k.len = len;
+  k.ptr = nullptr;
+  k.hash = h;
+  if (!global_insert<false>(T, k, 1ull)) emit_retry(retry, n_retry, r, 1ull);
+}
 
 // Aggregate records [r0, r1) of slice b.  owner: the work item holds the slice's whole bucket
 // (load the slice, count in LDS, write it back with plain stores); otherwise it is one piece of a
 // split bucket (count in LDS, merge into the slice with device-scope atomics).
 __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restrict__ recs, uint64_t r0, uint64_t r1,
                          uint64_t b, bool owner, int table_empty, FreqRec* retry, unsigned long long* n_retry,
-                         unsigned long long* new_groups) {
+                         unsigned long long* new_groups, const AggTrack* tr = nullptr) {
   constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
   unsigned long long* K0 = L.K0;
   unsigned long long* K1 = L.K1;
@@ -804,47 +899,31 @@ __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restric
     if (threadIdx.x == 0) {
       overflow = 0;
       fresh = 0u;
+      L.cmax = 0u;
     }
     __syncthreads();
-    for (uint64_t i = r0 + threadIdx.x; i < r1; i += kBlock) {
-      const FreqRec r = recs[i];
-      unsigned long long k1;
-      uint32_t len;
-      rec_unpack(r, &k1, &len);
-      if (len == kRecHole) continue;
-      const uint64_t h = hash_inline(r.k0, k1, len);
-      uint32_t s = (uint32_t)(h & (S - 1));
-      bool done = false;
-      for (uint32_t probe = 0; probe < S && !done;) {
-        const unsigned long long c = atomicCAS(&K1[s], kLdsEmpty, kLdsBusy);
-        if (c == kLdsEmpty) {  // claimed: publish the key, then count
-          K0[s] = r.k0;
-          __threadfence_block();
-          atomicExch(&K1[s], r.k1);
-          atomicAdd(&C[s], 1u);
-          done = true;
-        } else if (c == kLdsBusy) {
-          // another lane is publishing this slot: look at it again
-        } else if (c == r.k1 &&
-                   __hip_atomic_load(&K0[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == r.k0) {
-          atomicAdd(&C[s], 1u);
-          done = true;
-        } else {
-          s = (s + 1) & (S - 1);
-          ++probe;
-        }
+    // records are loaded kAggBatch per thread at a time, all loads in flight together (one
+    // dependent load per record made the loop latency-bound)
+    for (uint64_t base = r0; base < r1; base += (uint64_t)kBlock * kAggBatch) {
+      FreqRec rb[kAggBatch];
+#pragma unroll
+      for (int j = 0; j < kAggBatch; ++j) {
+        const uint64_t i = base + (uint64_t)j * kBlock + threadIdx.x;
+        if (i < r1) rb[j] = recs[i];
       }
-      if (!done) {
-        if (owner) {
-          overflow = 1;
-        } else {  // the piece holds more keys than LDS: this row goes straight to the slice
-          Key k;
-          k.k0 = r.k0;
-          k.k1 = k1;
-          k.len = len;
-          k.ptr = nullptr;
-          k.hash = h;
-          if (!global_insert<false>(T, k, 1ull)) emit_retry(retry, n_retry, r, 1ull);
+#pragma unroll
+      for (int j = 0; j < kAggBatch; ++j) {
+        const uint64_t i = base + (uint64_t)j * kBlock + threadIdx.x;
+        if (i >= r1) continue;
+        const FreqRec r = rb[j];
+        unsigned long long k1;
+        uint32_t len;
+        rec_unpack(r, &k1, &len);
+        if (len == kRecHole) continue;
+        const uint64_t h = hash_inline(r.k0, k1, len);
+        if (!lds_count(K0, K1, C, r, h)) {
+          if (owner) overflow = 1;
+          else piece_spill(T, r, k1, len, h, retry, n_retry);
         }
       }
     }
@@ -871,10 +950,17 @@ __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restric
       if (threadIdx.x == 0) retry_base = atomicAdd(n_retry, (unsigned long long)(r1 - r0));
       __syncthreads();
       for (uint64_t i = r0 + threadIdx.x; i < r1; i += kBlock) retry[retry_base + (i - r0)] = recs[i];
+      if (tr && tr->write_all)  // (the table was not cleared: the slice starts out empty)
+        for (uint32_t s = threadIdx.x; s < S; s += kBlock) slice[s] = FreqSlot{0ull, 0ull, 0ull, 0ull};
+      if (tr && tr->smax && threadIdx.x == 0) tr->smax[b] = 0xFFFFFFFFu;  // unknown: never skipped
     } else {
       for (uint32_t s = threadIdx.x; s < S; s += kBlock) {
         const uint32_t c = C[s];
-        if (!c) continue;
+        if (!c) {
+          if (tr && tr->write_all) slice[s] = FreqSlot{0ull, 0ull, 0ull, 0ull};
+          continue;
+        }
+        if (tr) track_count(L, *tr, c);
         FreqSlot& e = slice[s];
         if (!table_empty && (e.ctrl & kReady)) {
           e.count += c;
@@ -894,6 +980,7 @@ __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restric
       }
       __syncthreads();
       if (threadIdx.x == 0 && fresh) atomicAdd(new_groups, (unsigned long long)fresh);
+      if (tr && tr->smax && threadIdx.x == 0) tr->smax[b] = L.cmax;
     }
     __syncthreads();  // LDS is reused by the next work item
   }
@@ -938,8 +1025,11 @@ constexpr int kPartThreads = 1024;
 constexpr int kPartPerThread = 16;
 constexpr uint32_t kPartTile = (uint32_t)kPartThreads * kPartPerThread;  // records per tile
 constexpr uint32_t kPartSub = 4096;                                      // records per LDS round
-constexpr int kPartMaxBinBits = 11;
+constexpr int kPartMaxBinBits = kPartMaxBits;
 constexpr uint32_t kPartNoBin = 0xFFFFu;
+constexpr int kStageGroup = 4;  // rows per thread whose loads the fused stage issues together
+constexpr int kStagePer = 12;   // rows per thread per fused-stage tile (register budget)
+constexpr uint32_t kStageTile = (uint32_t)kPartThreads * kStagePer;
 
 struct PartLds {
   FreqRec rec[kPartSub];
@@ -956,6 +1046,85 @@ __device__ inline uint64_t rec_hash(const FreqRec& r, bool* hole) {
   rec_unpack(r, &k1, &len);
   *hole = len == kRecHole;
   return hash_inline(r.k0, k1, len);
+}
+
+// One tile's multi-split: each thread holds kPartPerThread records and their LDS bins (bin <
+// 2^bin_bits, or kPartNoBin for none); output region of a bin = base_id + bin.  Ranks come from
+// LDS atomics, the room in each region from ONE device atomic per (tile, non-empty bin), and the
+// records are written from an LDS image sorted by bin, kPartSub at a time (coalesced runs).
+template <int PER>
+__device__ inline void part_tile(PartLds& L, const FreqRec (&rec)[PER], uint32_t (&bin)[PER],
+                                 uint32_t nb, uint64_t base_id, FreqRec* __restrict__ out, uint64_t out_cap,
+                                 unsigned long long* out_fill, FreqRec* ovf, unsigned long long* ovf_n,
+                                 uint64_t ovf_cap, unsigned int* flag, unsigned long long* staged) {
+  const uint32_t t = threadIdx.x;
+  for (uint32_t i = t; i < nb; i += kPartThreads) L.hist[i] = 0u;
+  __syncthreads();
+  // rank of each record within its bin (LDS atomics), packed with the bin: rank << 16 | bin
+#pragma unroll
+  for (int i = 0; i < PER; ++i)
+    if (bin[i] != kPartNoBin) bin[i] |= atomicAdd(&L.hist[bin[i]], 1u) << 16;
+  __syncthreads();
+  // exclusive scan of the bins by wave 0 (nb / 64 consecutive bins per lane)
+  if (t < 64) {
+    const uint32_t per = (nb + 63u) / 64u;
+    uint32_t s = 0;
+    for (uint32_t k = 0; k < per; ++k) {
+      const uint32_t b = t * per + k;
+      if (b < nb) s += L.hist[b];
+    }
+    uint32_t incl = s;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(incl, d, 64);
+      if ((int)t >= d) incl += o;
+    }
+    uint32_t run = incl - s;
+    for (uint32_t k = 0; k < per; ++k) {
+      const uint32_t b = t * per + k;
+      if (b < nb) {
+        L.start[b] = run;
+        run += L.hist[b];
+      }
+    }
+    if (t == 63) {
+      L.total = incl;
+      if (staged && incl) atomicAdd(staged, (unsigned long long)incl);
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = t; b < nb; b += kPartThreads) {
+    const uint32_t c = L.hist[b];
+    L.gbase[b] = c ? atomicAdd(&out_fill[base_id + b], (unsigned long long)c) : 0ull;
+  }
+  const uint32_t total = L.total;
+  __syncthreads();
+  for (uint32_t r0 = 0; r0 < total; r0 += kPartSub) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      if ((bin[i] & 0xFFFFu) == kPartNoBin) continue;
+      const uint32_t b = bin[i] & 0xFFFFu;
+      const uint32_t p = L.start[b] + (bin[i] >> 16) - r0;
+      if (p < kPartSub) {
+        L.rec[p] = rec[i];
+        L.bin[p] = (uint16_t)b;
+      }
+    }
+    __syncthreads();
+    const uint32_t m = min(kPartSub, total - r0);
+    for (uint32_t j = t; j < m; j += kPartThreads) {
+      const uint32_t b = L.bin[j];
+      const uint64_t o = L.gbase[b] + (r0 + j - L.start[b]);
+      const FreqRec r = L.rec[j];
+      if (o < out_cap) {
+        out[(base_id + b) * out_cap + o] = r;
+      } else {  // the region is full: the overflow list (aggregated by the sort path)
+        const unsigned long long k = atomicAdd(ovf_n, 1ull);
+        if (k < ovf_cap) ovf[k] = r;
+        else atomicOr(flag, 1u);
+      }
+    }
+    __syncthreads();
+  }
 }
 
 // in_fill == nullptr: level 1, tile blockIdx.x of in[0, in_n).  Otherwise level 2: tile
@@ -984,8 +1153,6 @@ __global__ __launch_bounds__(kPartThreads) void dq_freq_part_kernel(
     if (begin >= in_n) return;
     count = min((uint64_t)kPartTile, in_n - begin);
   }
-  for (uint32_t i = t; i < nb; i += kPartThreads) L.hist[i] = 0u;
-  if (t == 0) L.total = 0u;
   FreqRec rec[kPartPerThread];
   uint32_t bin[kPartPerThread];
 #pragma unroll
@@ -993,7 +1160,6 @@ __global__ __launch_bounds__(kPartThreads) void dq_freq_part_kernel(
     const uint32_t j = (uint32_t)i * kPartThreads + t;
     if (j < count) rec[i] = in[begin + j];
   }
-  __syncthreads();
 #pragma unroll
   for (int i = 0; i < kPartPerThread; ++i) {
     const uint32_t j = (uint32_t)i * kPartThreads + t;
@@ -1004,84 +1170,175 @@ __global__ __launch_bounds__(kPartThreads) void dq_freq_part_kernel(
       if (!hole) bin[i] = (uint32_t)(h >> (64 - id_bits)) & (nb - 1u);
     }
   }
-  // rank of each record within its bin (LDS atomics), packed with the bin: rank << 16 | bin
+  part_tile(L, rec, bin, nb, base_id, out, out_cap, out_fill, ovf, ovf_n, ovf_cap, flag, nullptr);
+}
+
+// Stage + level-1 partition fused: the rows of one batch become records written straight into
+// their level-1 regions (top b1 bits of the table hash), so the staging is not written and read
+// back in row order.  Tiles of kPartTile rows, grid-stride.  The sketch, the staged count and
+// the long-key flag are kept as by dq_freq_stage_kernel.  Single-string keys (the common case)
+// load their offsets, then their bytes, for all of a thread's rows at once.
+template <bool ONE_STRING>
+__global__ __launch_bounds__(kPartThreads) void dq_freq_stage_part_kernel(
+    FreqKeySpec ks, const DevColumn* __restrict__ cols, int64_t n_rows, int b1, FreqRec* __restrict__ out,
+    uint64_t cap1, unsigned long long* fill1, FreqRec* ovf, unsigned long long* ovf_n, uint64_t ovf_cap,
+    unsigned int* flag, uint32_t* hll, unsigned long long* long_key, unsigned long long* staged) {
+  __shared__ PartLds L;
+  __shared__ uint32_t regs[kHllM];
+  const uint32_t t = threadIdx.x;
+  const uint32_t nb = 1u << b1;
+  for (uint32_t i = t; i < (uint32_t)kHllM; i += kPartThreads) regs[i] = 0u;
+  __syncthreads();
+  const DevColumn& c0 = cols[ks.key_cols[0]];
+  alignas(8) uint8_t scratch[kMaxLocalKey];
+  const int64_t n_tiles = (n_rows + kStageTile - 1) / kStageTile;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const int64_t row0 = tile * (int64_t)kStageTile;
+    FreqRec rec[kStagePer];
+    uint32_t bin[kStagePer];
+    uint32_t too_long = 0u;
+    if constexpr (ONE_STRING) {
+      // two groups of kStageGroup rows: the offsets of a group, then its key words, all in flight
+      // together (the whole tile at once would not fit the register file)
+      constexpr int G = kStageGroup;
+      const uint8_t* base = static_cast<const uint8_t*>(c0.values);
 #pragma unroll
-  for (int i = 0; i < kPartPerThread; ++i)
-    if (bin[i] != kPartNoBin) bin[i] |= atomicAdd(&L.hist[bin[i]], 1u) << 16;
-  __syncthreads();
-  // exclusive scan of the bins by wave 0 (nb / 64 consecutive bins per lane), then the room of
-  // each bin in its output region: one atomic per non-empty bin
-  if (t < 64) {
-    const uint32_t per = (nb + 63u) / 64u;
-    uint32_t s = 0;
-    for (uint32_t k = 0; k < per; ++k) {
-      const uint32_t b = t * per + k;
-      if (b < nb) s += L.hist[b];
-    }
-    uint32_t incl = s;
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t o = __shfl_up(incl, d, 64);
-      if ((int)t >= d) incl += o;
-    }
-    uint32_t run = incl - s;
-    for (uint32_t k = 0; k < per; ++k) {
-      const uint32_t b = t * per + k;
-      if (b < nb) {
-        L.start[b] = run;
-        run += L.hist[b];
-      }
-    }
-    if (t == 63) L.total = incl;
-  }
-  __syncthreads();
-  for (uint32_t b = t; b < nb; b += kPartThreads) {
-    const uint32_t c = L.hist[b];
-    L.gbase[b] = c ? atomicAdd(&out_fill[base_id + b], (unsigned long long)c) : 0ull;
-  }
-  const uint32_t total = L.total;
-  __syncthreads();
-  for (uint32_t r0 = 0; r0 < total; r0 += kPartSub) {
+      for (int g = 0; g < kStagePer; g += G) {
+        int32_t ob[G], oe[G];
+        uint32_t valid = 0u;
 #pragma unroll
-    for (int i = 0; i < kPartPerThread; ++i) {
-      if ((bin[i] & 0xFFFFu) == kPartNoBin) continue;
-      const uint32_t b = bin[i] & 0xFFFFu;
-      const uint32_t p = L.start[b] + (bin[i] >> 16) - r0;
-      if (p < kPartSub) {
-        L.rec[p] = rec[i];
-        L.bin[p] = (uint16_t)b;
+        for (int i = 0; i < G; ++i) {
+          const int64_t row = row0 + (g + i) * kPartThreads + t;
+          ob[i] = oe[i] = 0;
+          if (row < n_rows) {
+            ob[i] = c0.offsets[row];
+            oe[i] = c0.offsets[row + 1];
+            if (col_valid(c0, row)) valid |= 1u << i;
+          }
+        }
+        uint64_t w0[G], w1[G], w2[G];
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+          // the (at most 3) aligned words holding a key of <= 15 bytes; words past the key are
+          // not loaded (they could lie past the buffer)
+          const uint32_t n = (uint32_t)(oe[i] - ob[i]);
+          const uintptr_t a = (uintptr_t)(base + ob[i]);
+          const uint64_t* w = reinterpret_cast<const uint64_t*>(a & ~(uintptr_t)7);
+          const uint32_t span = (uint32_t)(a & 7) + n;  // bytes from the first word's start
+          w0[i] = w1[i] = w2[i] = 0;
+          if (((valid >> i) & 1u) && n > 0 && n <= 15) {
+            w0[i] = w[0];
+            if (span > 8) w1[i] = w[1];
+            if (span > 16) w2[i] = w[2];
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+          const int64_t row = row0 + (g + i) * kPartThreads + t;
+          bin[g + i] = kPartNoBin;
+          if (row >= n_rows) continue;
+          uint64_t k0, k1;
+          uint32_t n;
+          if ((valid >> i) & 1u) {
+            n = (uint32_t)(oe[i] - ob[i]);
+            if (n > 15) {
+              too_long = max(too_long, n);
+              continue;
+            }
+            const uint32_t sh = (uint32_t)((uintptr_t)(base + ob[i]) & 7) * 8u;
+            // bytes 0..7 and 8..15 of the key from the three words, then masked to n bytes
+            const uint64_t lo = sh ? (w0[i] >> sh) | (w1[i] << (64u - sh)) : w0[i];
+            const uint64_t hi = sh ? (w1[i] >> sh) | (w2[i] << (64u - sh)) : w1[i];
+            k0 = n >= 8 ? lo : (n ? lo & ((1ull << (8u * n)) - 1ull) : 0ull);
+            k1 = n > 8 ? hi & ((1ull << (8u * (n - 8u))) - 1ull) : 0ull;
+          } else if (ks.null_as_key) {  // Histogram NULL: "NullValue"
+            n = 9;
+            k0 = 0x756c61566c6c754eull;  // "NullValu"
+            k1 = 0x65ull;                // "e"
+          } else {
+            continue;
+          }
+          const uint64_t h = hash_inline(k0, k1, n);
+          rec[g + i].k0 = k0;
+          rec[g + i].k1 = k1 | ((unsigned long long)n << kRecLenShift);
+          bin[g + i] = (uint32_t)(h >> (64 - b1)) & (nb - 1u);
+          sketch_update(regs, h);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < kStagePer; ++i) {
+        const int64_t row = row0 + i * kPartThreads + t;
+        bin[i] = kPartNoBin;
+        if (row >= n_rows) continue;
+        Key k;
+        bool tl;
+        if (!make_key(ks, cols, row, k, scratch, tl)) {
+          if (tl) too_long = max(too_long, (uint32_t)kMaxLocalKey + 1u);
+          continue;
+        }
+        if (k.len > 15 || k.ptr != nullptr) {
+          too_long = max(too_long, k.len > 15 ? k.len : 16u);
+          continue;
+        }
+        rec[i].k0 = k.k0;
+        rec[i].k1 = k.k1 | ((unsigned long long)k.len << kRecLenShift);
+        bin[i] = (uint32_t)(k.hash >> (64 - b1)) & (nb - 1u);
+        sketch_update(regs, k.hash);
       }
     }
-    __syncthreads();
-    const uint32_t m = min(kPartSub, total - r0);
-    for (uint32_t j = t; j < m; j += kPartThreads) {
-      const uint32_t b = L.bin[j];
-      const uint64_t o = L.gbase[b] + (r0 + j - L.start[b]);
-      const FreqRec r = L.rec[j];
-      if (o < out_cap) {
-        out[(base_id + b) * out_cap + o] = r;
-      } else {  // the region is full: the overflow list (aggregated by the sort path)
-        const unsigned long long k = atomicAdd(ovf_n, 1ull);
-        if (k < ovf_cap) ovf[k] = r;
-        else atomicOr(flag, 1u);
-      }
-    }
-    __syncthreads();
+    if (too_long) atomicMax(long_key, (unsigned long long)too_long);
+    part_tile(L, rec, bin, nb, 0, out, cap1, fill1, ovf, ovf_n, ovf_cap, flag, staged);
   }
+  __syncthreads();
+  for (uint32_t i = t; i < (uint32_t)kHllM; i += kPartThreads)
+    if (regs[i]) atomicMax(&hll[i], regs[i]);
+}
+
+// Copy regions (min(fill, cap) records each) to out[prefix[r] ..]: the partitioned staging
+// laid out contiguously again for the sort path (rare: skew, or a table of few slices).
+__global__ __launch_bounds__(kBlock) void dq_freq_compact_kernel(const FreqRec* __restrict__ in,
+                                                                 const unsigned long long* __restrict__ fill,
+                                                                 uint64_t cap, const unsigned long long* __restrict__ prefix,
+                                                                 FreqRec* __restrict__ out) {
+  const uint64_t r = blockIdx.y;
+  const unsigned long long f = fill[r];
+  const uint64_t have = f < cap ? f : cap;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < have; i += (uint64_t)gridDim.x * kBlock)
+    out[prefix[r] + i] = in[r * cap + i];
 }
 
 // Aggregate slice region b (records b * cap .. + min(fill[b], cap)) as its slice's owner.
+// tr: see AggTrack (table_empty only).
 __global__ __launch_bounds__(kBlock) void dq_freq_agg_region_kernel(FreqTable T, const FreqRec* __restrict__ recs,
                                                                     const unsigned long long* __restrict__ fill,
                                                                     uint64_t cap, uint64_t n_slices, int table_empty,
                                                                     FreqRec* retry, unsigned long long* n_retry,
-                                                                    unsigned long long* new_groups) {
+                                                                    unsigned long long* new_groups, AggTrack tr) {
   __shared__ AggLds L;
+  const bool track = tr.hist != nullptr;
+  if (track) {
+    for (int i = threadIdx.x; i < kAggLdsHist; i += kBlock) L.hist[i] = 0u;
+    __syncthreads();
+  }
   for (uint64_t b = blockIdx.x; b < n_slices; b += gridDim.x) {
     const unsigned long long f = fill[b];
     const uint64_t r0 = b * cap;
     const uint64_t r1 = r0 + (f < cap ? f : cap);
-    if (r1 == r0) continue;
-    agg_item(L, T, recs, r0, r1, b, true, table_empty, retry, n_retry, new_groups);
+    if (r1 == r0) {
+      if (tr.write_all) {
+        FreqSlot* slice = T.slots + (b << kFreqSliceLog);
+        for (uint32_t s = threadIdx.x; s < (uint32_t)kFreqSliceSlots; s += kBlock) slice[s] = FreqSlot{0ull, 0ull, 0ull, 0ull};
+      }
+      if (tr.smax && threadIdx.x == 0) tr.smax[b] = 0u;
+      continue;
+    }
+    agg_item(L, T, recs, r0, r1, b, true, table_empty, retry, n_retry, new_groups, track || tr.write_all ? &tr : nullptr);
+  }
+  if (track) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < kAggLdsHist; i += kBlock)
+      if (L.hist[i]) atomicAdd(&tr.hist[i], (unsigned long long)L.hist[i]);
   }
 }
 
@@ -1188,13 +1445,49 @@ hipError_t launch_freq_part(const FreqRec* d_in, uint64_t in_n, const unsigned l
   return hipGetLastError();
 }
 
+hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, const DevColumn* d_cols, int64_t n_rows, int b1,
+                                  FreqRec* d_out,
+                                  uint64_t cap1, unsigned long long* d_fill1, FreqRec* d_ovf, unsigned long long* d_ovf_n,
+                                  uint64_t ovf_cap, unsigned int* d_flag, uint32_t* d_hll, unsigned long long* d_long_key,
+                                  unsigned long long* d_staged, hipStream_t stream) {
+  if (n_rows <= 0) return hipSuccess;
+  if (b1 < 1 || b1 > kPartMaxBinBits) return hipErrorInvalidValue;
+  const int64_t tiles = (n_rows + kStageTile - 1) / kStageTile;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t blocks = tiles < (int64_t)cus * 2 ? tiles : (int64_t)cus * 2;
+  if (one_string)
+    hipLaunchKernelGGL(dq_freq_stage_part_kernel<true>, dim3((unsigned)blocks), dim3(kPartThreads), 0, stream, ks, d_cols,
+                       n_rows, b1, d_out, cap1, d_fill1, d_ovf, d_ovf_n, ovf_cap, d_flag, d_hll, d_long_key, d_staged);
+  else
+    hipLaunchKernelGGL(dq_freq_stage_part_kernel<false>, dim3((unsigned)blocks), dim3(kPartThreads), 0, stream, ks, d_cols,
+                       n_rows, b1, d_out, cap1, d_fill1, d_ovf, d_ovf_n, ovf_cap, d_flag, d_hll, d_long_key, d_staged);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_compact(const FreqRec* d_in, const unsigned long long* d_fill, uint64_t cap, uint64_t n_regions,
+                               const unsigned long long* d_prefix, FreqRec* d_out, hipStream_t stream) {
+  if (n_regions == 0) return hipSuccess;
+  if (n_regions > 65535) return hipErrorInvalidValue;
+  uint64_t bx = (cap + kBlock * 8 - 1) / (kBlock * 8);
+  if (bx > 64) bx = 64;
+  if (bx < 1) bx = 1;
+  hipLaunchKernelGGL(dq_freq_compact_kernel, dim3((unsigned)bx, (unsigned)n_regions), dim3(kBlock),
+                     0, stream, d_in, d_fill, cap, d_prefix, d_out);
+  return hipGetLastError();
+}
+
 hipError_t launch_freq_agg_region(const FreqTable& T, const FreqRec* d_recs, const unsigned long long* d_fill,
                                   uint64_t cap, uint64_t n_slices, int table_empty, FreqRec* d_retry,
-                                  unsigned long long* d_n_retry, unsigned long long* d_new_groups, hipStream_t stream) {
+                                  unsigned long long* d_n_retry, unsigned long long* d_new_groups,
+                                  unsigned long long* d_hist, unsigned long long* d_big, unsigned long long* d_n_big,
+                                  unsigned long long big_cap, uint32_t* d_smax, int write_all, hipStream_t stream) {
   uint64_t blocks = n_slices < 65536 ? n_slices : 65536;
   if (blocks < 1) blocks = 1;
+  if (!table_empty && (d_hist || d_smax || write_all)) return hipErrorInvalidValue;
+  AggTrack tr{d_hist, d_big, d_n_big, big_cap, d_smax, write_all};
   hipLaunchKernelGGL(dq_freq_agg_region_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, d_recs, d_fill, cap,
-                     n_slices, table_empty, d_retry, d_n_retry, d_new_groups);
+                     n_slices, table_empty, d_retry, d_n_retry, d_new_groups, tr);
   return hipGetLastError();
 }
 
@@ -1260,7 +1553,14 @@ hipError_t launch_freq_hist(const FreqTable& T, unsigned long long* d_hist, unsi
 }
 
 hipError_t launch_freq_export(const FreqTable& T, unsigned long long min_count, const FreqOut& out,
-                              hipStream_t stream) {
+                              hipStream_t stream, const uint32_t* d_smax) {
+  if (d_smax && min_count > 0) {
+    const uint64_t n_slices = (T.mask + 1) >> kFreqSliceLog;
+    const uint64_t blocks = n_slices < 16384 ? n_slices : 16384;
+    hipLaunchKernelGGL(dq_freq_export_slices_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, min_count,
+                       d_smax, out);
+    return hipGetLastError();
+  }
   const uint64_t n = T.mask + 1;
   uint64_t blocks = (n + kBlock * 16 - 1) / (kBlock * 16);
   if (blocks > 8192) blocks = 8192;

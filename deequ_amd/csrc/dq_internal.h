@@ -158,6 +158,8 @@ constexpr int kFreqSliceLog = 11;
 constexpr uint64_t kFreqSliceSlots = 1ull << kFreqSliceLog;
 // Records per aggregation work item of a split (hot) bucket in the sorted-bucket path.
 constexpr uint64_t kFreqAggPiece = 32768;
+// Largest LDS bin count (log2) of one partition pass (dq_freq_part_kernel).
+constexpr int kPartMaxBits = 11;
 
 // A staged row of the sorted-bucket path: key bytes 0..14 (zero padded) in k0 and the low 7
 // bytes of k1, the key length (<= 15) in the top byte of k1.
@@ -208,7 +210,7 @@ hipError_t launch_freq_insert(const FreqKeySpec& ks, const DevColumn* d_cols, in
 hipError_t launch_freq_hist(const FreqTable& T, unsigned long long* d_hist, unsigned long long* d_big,
                             unsigned long long* d_nbig, unsigned long long big_cap, hipStream_t stream);
 hipError_t launch_freq_export(const FreqTable& T, unsigned long long min_count, const FreqOut& out,
-                              hipStream_t stream);
+                              hipStream_t stream, const uint32_t* d_smax = nullptr);
 hipError_t launch_freq_import(const FreqTable& T, const FreqIn& in, hipStream_t stream);
 hipError_t launch_freq_lookup(const FreqTable& T, const uint8_t* d_key, uint32_t len, unsigned long long* d_out,
                               hipStream_t stream);
@@ -246,9 +248,24 @@ hipError_t launch_freq_part(const FreqRec* d_in, uint64_t in_n, const unsigned l
                             uint64_t n_in_regions, int id_bits, int bin_bits, FreqRec* d_out, uint64_t out_cap,
                             unsigned long long* d_out_fill, FreqRec* d_ovf, unsigned long long* d_ovf_n,
                             uint64_t ovf_cap, unsigned int* d_flag, hipStream_t stream);
+// With an empty table it can also produce the count-of-counts histogram (d_hist, counts >=
+// kFreqHist into d_big), each slice's largest count (d_smax) and write every slot (write_all:
+// the table needs no clearing).
+// Stage + level-1 partition in one pass (records straight into their 2^b1 level-1 regions);
+// regions -> contiguous (prefix = exclusive sum of the clamped fills) for the sort path.
+// one_string: the only key column is utf8 (the kernel's batched-load fast path).
+hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, const DevColumn* d_cols, int64_t n_rows, int b1,
+                                  FreqRec* d_out,
+                                  uint64_t cap1, unsigned long long* d_fill1, FreqRec* d_ovf, unsigned long long* d_ovf_n,
+                                  uint64_t ovf_cap, unsigned int* d_flag, uint32_t* d_hll, unsigned long long* d_long_key,
+                                  unsigned long long* d_staged, hipStream_t stream);
+hipError_t launch_freq_compact(const FreqRec* d_in, const unsigned long long* d_fill, uint64_t cap, uint64_t n_regions,
+                               const unsigned long long* d_prefix, FreqRec* d_out, hipStream_t stream);
 hipError_t launch_freq_agg_region(const FreqTable& T, const FreqRec* d_recs, const unsigned long long* d_fill,
                                   uint64_t cap, uint64_t n_slices, int table_empty, FreqRec* d_retry,
-                                  unsigned long long* d_n_retry, unsigned long long* d_new_groups, hipStream_t stream);
+                                  unsigned long long* d_n_retry, unsigned long long* d_new_groups,
+                                  unsigned long long* d_hist, unsigned long long* d_big, unsigned long long* d_n_big,
+                                  unsigned long long big_cap, uint32_t* d_smax, int write_all, hipStream_t stream);
 hipError_t launch_freq_rehash(const FreqSlot* d_old, uint64_t old_n, const FreqTable& T, hipStream_t stream);
 
 // ---------------------------------------------------------------- launchers (.hip files)

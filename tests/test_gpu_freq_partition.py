@@ -60,7 +60,8 @@ def test_partition_matches_oracle(gpu, part, monkeypatch, budget):
         assert s.num_unique == sum(1 for c in want.values() if c == 1)
 
 
-@pytest.mark.parametrize("n,distinct", [(3_000_000, 1_500_000), (5_000_000, 200_000), (2_000_000, 40)])
+@pytest.mark.parametrize("n,distinct", [(3_000_000, 1_500_000), (5_000_000, 200_000), (2_000_000, 40),
+                                        (2_000_000, 10)])
 def test_partition_counts_exact(gpu, part, n, distinct):
     rng = np.random.default_rng(12)
     vals = rng.integers(0, distinct, n)
@@ -73,6 +74,10 @@ def test_partition_counts_exact(gpu, part, n, distinct):
     assert s.num_groups == len(u)
     assert s.num_unique == int((c == 1).sum())
     assert s.grouped_rows == int(valid.sum())
+    ent = -np.sum((c / n) * np.log(c / n))
+    assert abs(s.entropy - ent) <= 1e-9 * abs(ent)
+    counts, _ = t.top(5)  # (the slice maxima let the export skip slices below the threshold)
+    assert sorted(counts.tolist(), reverse=True)[:5] == sorted(c.tolist(), reverse=True)[:5]
     if len(u) <= 1_000_000:
         assert _int_groups(t) == dict(zip(u.tolist(), c.tolist()))
 
@@ -111,3 +116,32 @@ def test_partition_equals_sort_path_strings(gpu, monkeypatch):
     vals, cnt = np.unique(np.array(keys), return_counts=True)
     assert len(res["1"]) == len(vals)
     assert sorted(res["1"].values()) == sorted(cnt.tolist())
+
+
+@pytest.mark.parametrize("long_frac", [0.0, 0.2])
+def test_region_staging_batches_and_rollback(gpu, part, long_frac):
+    """Region staging across several batches; a batch holding a key longer than 15 bytes is
+    rolled back (fills, overflow and staged counts restored) and grouped on the general path
+    after the regions staged so far are aggregated."""
+    rng = np.random.default_rng(15)
+    n = 40000
+    a = rng.integers(0, 9000, n)
+    keys = [None if i % 29 == 0 else ("a-much-longer-grouping-key-%d" % a[i] if rng.random() < long_frac
+                                      else "%012d" % a[i]) for i in range(n)]
+    spec = {"key": ["string", keys]}
+    table = product_table(spec)
+    schema = dict(table.schema)
+    for hist in (False, True):
+        t = FrequencyTable(["key"], schema, histogram=hist)
+        step = n // 5
+        for s in range(0, n, step):
+            t.consume(d.Table.from_pydict({"key": ("string", keys[s:s + step])}))
+        got = _export(t)
+        want = {}
+        for k in keys:
+            if k is None and not hist:
+                continue
+            kb = b"NullValue" if k is None else k.encode()
+            want[kb] = want.get(kb, 0) + 1
+        assert got == want, hist
+        t.close()
