@@ -820,7 +820,13 @@ __device__ inline void track_count(AggLds& L, const AggTrack& tr, uint32_t c) {
   }
 }
 
-constexpr int kAggBatch = 8;
+#ifndef DQ_AGG_BATCH
+#define DQ_AGG_BATCH 8
+#endif
+#ifndef DQ_LDS_READ_PROBE
+#define DQ_LDS_READ_PROBE 0
+#endif
+constexpr int kAggBatch = DQ_AGG_BATCH;  // records per thread loaded together
 
 // Count record r (table hash h) in the LDS slice image; false if the image is full.  (The
 // publishing lane's stores stay inside the loop iteration, with `done` tested by the loop: a
@@ -832,7 +838,13 @@ __device__ inline bool lds_count(unsigned long long* K0, unsigned long long* K1,
   uint32_t s = (uint32_t)(h & (S - 1));
   bool done = false;
   for (uint32_t probe = 0; probe < S && !done;) {
+#if DQ_LDS_READ_PROBE
+    // a plain read first: only an EMPTY slot is worth a compare-and-swap
+    unsigned long long c = __hip_atomic_load(&K1[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (c == kLdsEmpty) c = atomicCAS(&K1[s], kLdsEmpty, kLdsBusy);
+#else
     const unsigned long long c = atomicCAS(&K1[s], kLdsEmpty, kLdsBusy);
+#endif
     if (c == kLdsEmpty) {  // claimed: publish the key, then count
       K0[s] = r.k0;
       __threadfence_block();
@@ -867,6 +879,7 @@ __device__ __noinline__ void piece_spill(const FreqTable& T, const FreqRec& r, u
 // Aggregate records [r0, r1) of slice b.  owner: the work item holds the slice's whole bucket
 // (load the slice, count in LDS, write it back with plain stores); otherwise it is one piece of a
 // split bucket (count in LDS, merge into the slice with device-scope atomics).
+template <int NT, bool OWNER_ONLY>
 __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restrict__ recs, uint64_t r0, uint64_t r1,
                          uint64_t b, bool owner, int table_empty, FreqRec* retry, unsigned long long* n_retry,
                          unsigned long long* new_groups, const AggTrack* tr = nullptr) {
@@ -879,7 +892,7 @@ __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restric
   unsigned long long& retry_base = L.retry_base;
   {
     FreqSlot* slice = T.slots + (b << kFreqSliceLog);
-    for (uint32_t s = threadIdx.x; s < S; s += kBlock) {
+    for (uint32_t s = threadIdx.x; s < S; s += NT) {
       if (owner && !table_empty) {
         const FreqSlot e = slice[s];
         const uint32_t len = (uint32_t)(e.ctrl & kLenMask);
@@ -904,16 +917,16 @@ __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restric
     __syncthreads();
     // records are loaded kAggBatch per thread at a time, all loads in flight together (one
     // dependent load per record made the loop latency-bound)
-    for (uint64_t base = r0; base < r1; base += (uint64_t)kBlock * kAggBatch) {
+    for (uint64_t base = r0; base < r1; base += (uint64_t)NT * kAggBatch) {
       FreqRec rb[kAggBatch];
 #pragma unroll
       for (int j = 0; j < kAggBatch; ++j) {
-        const uint64_t i = base + (uint64_t)j * kBlock + threadIdx.x;
+        const uint64_t i = base + (uint64_t)j * NT + threadIdx.x;
         if (i < r1) rb[j] = recs[i];
       }
 #pragma unroll
       for (int j = 0; j < kAggBatch; ++j) {
-        const uint64_t i = base + (uint64_t)j * kBlock + threadIdx.x;
+        const uint64_t i = base + (uint64_t)j * NT + threadIdx.x;
         if (i >= r1) continue;
         const FreqRec r = rb[j];
         unsigned long long k1;
@@ -922,14 +935,14 @@ __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restric
         if (len == kRecHole) continue;
         const uint64_t h = hash_inline(r.k0, k1, len);
         if (!lds_count(K0, K1, C, r, h)) {
-          if (owner) overflow = 1;
+          if (OWNER_ONLY || owner) overflow = 1;
           else piece_spill(T, r, k1, len, h, retry, n_retry);
         }
       }
     }
     __syncthreads();
-    if (!owner) {  // merge the piece's counts into the shared slice
-      for (uint32_t s = threadIdx.x; s < S; s += kBlock) {
+    if (!OWNER_ONLY && !owner) {  // merge the piece's counts into the shared slice
+      for (uint32_t s = threadIdx.x; s < S; s += NT) {
         const uint32_t c = C[s];
         if (!c) continue;
         const unsigned long long kk1 = K1[s];
@@ -949,12 +962,12 @@ __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restric
     } else if (overflow) {  // the slice is full: leave it untouched, hand the bucket's rows back
       if (threadIdx.x == 0) retry_base = atomicAdd(n_retry, (unsigned long long)(r1 - r0));
       __syncthreads();
-      for (uint64_t i = r0 + threadIdx.x; i < r1; i += kBlock) retry[retry_base + (i - r0)] = recs[i];
+      for (uint64_t i = r0 + threadIdx.x; i < r1; i += NT) retry[retry_base + (i - r0)] = recs[i];
       if (tr && tr->write_all)  // (the table was not cleared: the slice starts out empty)
-        for (uint32_t s = threadIdx.x; s < S; s += kBlock) slice[s] = FreqSlot{0ull, 0ull, 0ull, 0ull};
+        for (uint32_t s = threadIdx.x; s < S; s += NT) slice[s] = FreqSlot{0ull, 0ull, 0ull, 0ull};
       if (tr && tr->smax && threadIdx.x == 0) tr->smax[b] = 0xFFFFFFFFu;  // unknown: never skipped
     } else {
-      for (uint32_t s = threadIdx.x; s < S; s += kBlock) {
+      for (uint32_t s = threadIdx.x; s < S; s += NT) {
         const uint32_t c = C[s];
         if (!c) {
           if (tr && tr->write_all) slice[s] = FreqSlot{0ull, 0ull, 0ull, 0ull};
@@ -1006,7 +1019,7 @@ __global__ __launch_bounds__(kBlock) void dq_freq_agg_kernel(FreqTable T, const 
     const bool owner = piece_start[b + 1] - piece_start[b] == 1u;
     const uint64_t r0 = off[b] + (uint64_t)(w - piece_start[b]) * kFreqAggPiece;
     const uint64_t r1 = min(off[b + 1], r0 + kFreqAggPiece);
-    agg_item(L, T, recs, r0, r1, b, owner, table_empty, retry, n_retry, new_groups);
+    agg_item<kBlock, false>(L, T, recs, r0, r1, b, owner, table_empty, retry, n_retry, new_groups);
   }
 }
 
@@ -1309,8 +1322,13 @@ __global__ __launch_bounds__(kBlock) void dq_freq_compact_kernel(const FreqRec* 
 }
 
 // Aggregate slice region b (records b * cap .. + min(fill[b], cap)) as its slice's owner.
-// tr: see AggTrack (table_empty only).
-__global__ __launch_bounds__(kBlock) void dq_freq_agg_region_kernel(FreqTable T, const FreqRec* __restrict__ recs,
+// tr: see AggTrack (table_empty only).  512 threads: more waves per CU than three 256-thread
+// slices' LDS images would give.
+#ifndef DQ_AGG_THREADS
+#define DQ_AGG_THREADS 512
+#endif
+constexpr int kAggRegionThreads = DQ_AGG_THREADS;
+__global__ __launch_bounds__(kAggRegionThreads) void dq_freq_agg_region_kernel(FreqTable T, const FreqRec* __restrict__ recs,
                                                                     const unsigned long long* __restrict__ fill,
                                                                     uint64_t cap, uint64_t n_slices, int table_empty,
                                                                     FreqRec* retry, unsigned long long* n_retry,
@@ -1318,7 +1336,7 @@ __global__ __launch_bounds__(kBlock) void dq_freq_agg_region_kernel(FreqTable T,
   __shared__ AggLds L;
   const bool track = tr.hist != nullptr;
   if (track) {
-    for (int i = threadIdx.x; i < kAggLdsHist; i += kBlock) L.hist[i] = 0u;
+    for (int i = threadIdx.x; i < kAggLdsHist; i += kAggRegionThreads) L.hist[i] = 0u;
     __syncthreads();
   }
   for (uint64_t b = blockIdx.x; b < n_slices; b += gridDim.x) {
@@ -1328,16 +1346,16 @@ __global__ __launch_bounds__(kBlock) void dq_freq_agg_region_kernel(FreqTable T,
     if (r1 == r0) {
       if (tr.write_all) {
         FreqSlot* slice = T.slots + (b << kFreqSliceLog);
-        for (uint32_t s = threadIdx.x; s < (uint32_t)kFreqSliceSlots; s += kBlock) slice[s] = FreqSlot{0ull, 0ull, 0ull, 0ull};
+        for (uint32_t s = threadIdx.x; s < (uint32_t)kFreqSliceSlots; s += kAggRegionThreads) slice[s] = FreqSlot{0ull, 0ull, 0ull, 0ull};
       }
       if (tr.smax && threadIdx.x == 0) tr.smax[b] = 0u;
       continue;
     }
-    agg_item(L, T, recs, r0, r1, b, true, table_empty, retry, n_retry, new_groups, track || tr.write_all ? &tr : nullptr);
+    agg_item<kAggRegionThreads, true>(L, T, recs, r0, r1, b, true, table_empty, retry, n_retry, new_groups, track || tr.write_all ? &tr : nullptr);
   }
   if (track) {
     __syncthreads();
-    for (int i = threadIdx.x; i < kAggLdsHist; i += kBlock)
+    for (int i = threadIdx.x; i < kAggLdsHist; i += kAggRegionThreads)
       if (L.hist[i]) atomicAdd(&tr.hist[i], (unsigned long long)L.hist[i]);
   }
 }
@@ -1486,7 +1504,7 @@ hipError_t launch_freq_agg_region(const FreqTable& T, const FreqRec* d_recs, con
   if (blocks < 1) blocks = 1;
   if (!table_empty && (d_hist || d_smax || write_all)) return hipErrorInvalidValue;
   AggTrack tr{d_hist, d_big, d_n_big, big_cap, d_smax, write_all};
-  hipLaunchKernelGGL(dq_freq_agg_region_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, d_recs, d_fill, cap,
+  hipLaunchKernelGGL(dq_freq_agg_region_kernel, dim3((unsigned)blocks), dim3(kAggRegionThreads), 0, stream, T, d_recs, d_fill, cap,
                      n_slices, table_empty, d_retry, d_n_retry, d_new_groups, tr);
   return hipGetLastError();
 }
