@@ -46,7 +46,6 @@ def parse_args():
     p.add_argument("--no-side-passes", action="store_true",
                    help="skip the scan_without_hll pass (profiler runs: the kernel trace then "
                         "holds only the headline launches)")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     p.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5"],
                    help="c2 = the headline scan (default); c3 = HLL on 64 columns; c4 = group-by")
     p.add_argument("--c1-rows", type=int, default=10_000_000, help="rows per GPU")
@@ -372,9 +371,8 @@ def run_c3(args, world, rank, local):
         "config": {"workload": "C3: %d rows/GPU x %d %s columns, one HLL plan (one batch of the "
                                "1B-row stream)" % (args.c3_rows, args.c3_columns, "utf8" if utf8 else "int64"),
                    "rows_per_gpu": args.c3_rows, "columns": args.c3_columns},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel_ms": kernel_ms,
-                     "algorithmic_bytes_per_launch": bpr * args.c3_rows},
+        "roofline": _step_roofline(bpr * args.c3_rows, kernel_ms / 1e3, "one HLL plan pass (scan kernels, HIP events)",
+                                   workload=None if utf8 else "c3", default_size=args.c3_rows == 125_000_000),
         # (the register-only hash-rate probe times the 8-byte hashLong, not 16-byte strings)
         "valu_roofline": None if utf8 else valu_roofline(local, float(args.c3_rows) * args.c3_columns,
                                                          kernel_ms),
@@ -393,11 +391,31 @@ def _column_bytes(col) -> float:
     return float(n * col.values.element_size()) + valid
 
 
-def _step_roofline(bytes_per_step: float, step_s: float, what: str, traffic=None):
+def _pmc_traffic(workload: str):
+    """HBM bytes per step of `workload` at its default size, from the PMC pass committed under
+    profiles/ (tools/pmc_traffic.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of this same bench,
+    read = 2 x FETCH_SIZE on gfx950).  Counters cannot be read inside an unprofiled run, so this
+    is a COPIED profile value, labelled as such in the line (traffic_source); None if absent."""
+    path = os.path.join(ROOT, "profiles", "r02_traffic_%s_r02.json" % workload)
+    try:
+        with open(path) as f:
+            return json.load(f)["hbm_bytes_per_step"], os.path.relpath(path, ROOT)
+    except Exception:  # noqa: BLE001
+        return None, None
+
+
+def _step_roofline(bytes_per_step: float, step_s: float, what: str, traffic=None, workload=None,
+                   default_size=True):
     achieved = bytes_per_step / step_s / 1e9
-    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel_ms": step_s * 1e3,
-            "algorithmic_bytes_per_launch": bytes_per_step, "timed_unit": what}
+    src = None
+    if traffic is None and workload and default_size:
+        traffic, src = _pmc_traffic(workload)
+    out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel_ms": step_s * 1e3,
+           "algorithmic_bytes_per_launch": bytes_per_step, "timed_unit": what}
+    if src:
+        out["traffic_source"] = "copied from %s (PMC pass of this bench at its default size)" % src
+    return out
 
 
 def run_c4(args, world, rank, local):
@@ -432,8 +450,11 @@ def run_c4(args, world, rank, local):
                                "reference runs Histogram as a second job)%s"
                                % (args.c4_rows, args.c4_batch,
                                   "; key-hash all-to-all over %d ranks" % world if world > 1 else "")},
-        "roofline": _step_roofline(algo, step_s, "one whole group-by step per GPU (stage, sort, aggregate, "
-                                                 "metrics, top-N), HBM-bound by design"),
+        "roofline": _step_roofline(algo, step_s, "one whole group-by step per GPU (stage + level-1 partition, "
+                                                 "level-2 partition, slice aggregation, top-N), HBM-bound by design",
+                                   workload="c4" if world == 1 else None,
+                                   default_size=(args.c4_rows, args.c4_batch, args.c4_distinct)
+                                   == (1_000_000_000, 125_000_000, 201_500_000)),
         "check": dict(metrics, histogram_bins=hist.numberOfBins),
     }
 
@@ -599,7 +620,8 @@ def run_c5(args, world, rank, local):
                                "utf8, 10 bool); ColumnProfilerRunner, 3 passes, KLL off (reference default)"
                                % args.c5_rows},
         "roofline": _step_roofline(pass1 + pass2 + pass3, step_s,
-                                   "one whole profile per GPU (3 passes; bytes = every column read by each pass)"),
+                                   "one whole profile per GPU (3 passes; bytes = every column read by each pass)",
+                                   workload="c5" if world == 1 else None, default_size=args.c5_rows == 100_000_000),
         "check": {"columns": len(p), "histograms": n_hist,
                   "s00_distinct": p["s00"].approximateNumDistinctValues,
                   "l00_completeness": p["l00"].completeness, "numRecords": profiles.numRecords},
@@ -729,15 +751,9 @@ def main():
     rows_total = args.rows * world * args.steps
     value = rows_total / elapsed
     achieved = BYTES_PER_ROW * args.rows / (kernel_ms * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            with open(args.traffic_json) as f:
-                tj = json.load(f)
-            if tj.get("rows") == args.rows:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:  # noqa: BLE001
-            traffic = None
+    traffic, traffic_src = (None, None)
+    if args.rows == 1_000_000_000 and n_hll == 8:
+        traffic, traffic_src = _pmc_traffic("c2")
 
     result = {
         "metric": "rows/sec & HBM GB/s for analyzer-suite scan, 1B rows x 8 cols, 1/2/4/8 GPUs",
@@ -757,10 +773,12 @@ def main():
                    "rows_per_gpu": args.rows, "columns": 8, "analyzers": n_ops,
                    "parallelism": "dp%d (row shards, states all-gathered over RCCL)" % world},
         "hbm_gbs": achieved,
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel_ms": kernel_ms,
-                     "algorithmic_bytes_per_launch": BYTES_PER_ROW * args.rows},
+        "roofline": dict({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                          "kernel_ms": kernel_ms,
+                          "algorithmic_bytes_per_launch": BYTES_PER_ROW * args.rows},
+                         **({"traffic_source": "copied from %s (PMC pass of this bench at its default size)"
+                             % traffic_src} if traffic_src else {})),
         "valu_roofline": valu_roofline(local, float(args.rows) * n_hll, kernel_ms) if n_hll else None,
         "cpu_baseline": None,
     }

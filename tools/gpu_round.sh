@@ -6,14 +6,11 @@
 # merged gpurun_out/ stays small.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-TAG=${TAG:-r01}
+TAG=${TAG:-r02}
 TAG=$TAG bash tools/gpu_check.sh || exit $?
 TAG=$TAG WL="c1 c3 c4 c5" bash tools/gpu_workloads.sh || exit $?
 TAG=${TAG}u WL=c3 BENCH_ARGS="--c3-type utf8" bash tools/gpu_workloads.sh || exit $?
-TAG=$TAG bash tools/pmc.sh || exit $?
-WL=c2 KERNEL=dq_scan_values_kernel TAG=$TAG \
-  PASSES="SQ_INSTS_VALU,SQ_WAVES,GRBM_GUI_ACTIVE,SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_WAVE_CYCLES" \
-  bash tools/pmc_kernel.sh || exit $?
+TAG=$TAG bash tools/pmc_round.sh || exit $?
 find gpurun_out -name "*kernel_trace.csv" -delete
 find gpurun_out -path "*pmck_*" -name "*counter_collection.csv" -delete
 echo "ROUND DONE"
