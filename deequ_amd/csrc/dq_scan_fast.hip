@@ -81,6 +81,25 @@ __device__ inline void hll_rank_fast(W64 h, uint32_t& byte_off, uint32_t& rank) 
   rank = add1_sat(ffbh32(w_hi));
 }
 
+#ifndef DQ_FAST_MIN_HLL
+#define DQ_FAST_MIN_HLL 1
+#endif
+// The min form of the register update (DQ_FAST_MIN_HLL): a register's rank is nlz(w) + 1 of its
+// smallest w = (x << 9) | W_PADDING, so the workgroup keeps, per register, the MINIMUM of
+// s = bits 54..24 of x (in bits 30..0; one alignbit and one and from the hash halves) with
+// ds_min_u32, and turns it into a rank once, when folding: rank = nlz32(s) for s != 0 (s = 0:
+// rank >= 32, the exact re-rank below).  That drops the per-row v_ffbh and +1 of the max form.
+// An untouched register keeps 0xFFFFFFFF, which no s reaches (bit 31 is clear).
+__device__ inline void hll_key_min(W64 h, uint32_t& byte_off, uint32_t& s) {
+  byte_off = (h.hi >> 21) & 0x7fcu;
+  const uint32_t xlo = h.lo ^ h.hi;
+  s = __builtin_amdgcn_alignbit(h.hi, xlo, 24) & 0x7fffffffu;
+}
+__device__ inline uint32_t hll_min_to_rank(uint32_t s) {
+  if (s == 0xFFFFFFFFu) return 0u;
+  return s ? (uint32_t)__builtin_clz(s) : kRankMarker;
+}
+
 // The exact rank of the same row (64-bit leading-zero count), for the marker re-rank.
 __device__ inline uint32_t hll_rank_exact(W64 h) {
   const W64 x = xxh64_final(h);
@@ -98,6 +117,10 @@ __device__ inline bool is_nan_rare(double x) {
 
 __device__ inline void lds_max(uint32_t* regs, uint32_t byte_off, uint32_t v) {
   __hip_atomic_fetch_max(reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(regs) + byte_off), v,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ inline void lds_min(uint32_t* regs, uint32_t byte_off, uint32_t v) {
+  __hip_atomic_fetch_min(reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(regs) + byte_off), v,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
@@ -223,10 +246,17 @@ __device__ inline void fast_row(FastAcc& a, uint32_t lo, uint32_t hi, uint32_t m
         hhi = 0x7ff80000u;
       }
     }
+#if DQ_FAST_MIN_HLL
+    uint32_t off, s;
+    hll_key_min(hash_halves<T>(hlo, hhi), off, s);
+    if constexpr (!MEMBER) s |= ~m;  // an unselected row leaves the minimum alone
+    lds_min(lregs, off, s);
+#else
     uint32_t off, rank;
     hll_rank_fast(hash_halves<T>(hlo, hhi), off, rank);
     if constexpr (!MEMBER) rank &= m;
     lds_max(lregs, off, rank);
+#endif
   }
 }
 
@@ -426,7 +456,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DQ_FAST_
   __shared__ uint32_t lflag[kHllM / 32];
   __shared__ uint32_t s_nan;  // a selected NaN seen (fp64 statistics)
   if constexpr (HLL) {
-    for (int r = threadIdx.x; r < kHllM; r += kBlock) lregs[r] = 0u;
+    for (int r = threadIdx.x; r < kHllM; r += kBlock) lregs[r] = DQ_FAST_MIN_HLL ? 0xFFFFFFFFu : 0u;
   }
   if (threadIdx.x == 0) s_nan = 0u;
   __syncthreads();
@@ -562,6 +592,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DQ_FAST_
 
   if constexpr (HLL) {
     __syncthreads();
+#if DQ_FAST_MIN_HLL
+    for (int r = threadIdx.x; r < kHllM; r += kBlock) lregs[r] = hll_min_to_rank(lregs[r]);
+    __syncthreads();
+#endif
     // Registers holding the marker: re-rank them exactly over this workgroup's rows (rare).
     bool mine = false;
     if (threadIdx.x < kHllM / 32) lflag[threadIdx.x] = 0u;
