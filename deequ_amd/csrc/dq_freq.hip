@@ -32,6 +32,9 @@ constexpr unsigned long long kLenMask = (1ull << 24) - 1;
 constexpr int kLdsSlots = 1024;       // LDS pre-aggregation slots per workgroup
 constexpr int kLdsProbe = 8;          // linear probes in LDS before going global
 constexpr int kMaxLocalKey = 64;      // encoded multi-column keys are built in registers/scratch
+#ifndef DQ_INSERT_R
+#define DQ_INSERT_R 4
+#endif
 
 __device__ inline unsigned long long atom_or(unsigned long long* p, unsigned long long v) {
   return __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -213,6 +216,73 @@ __device__ bool make_key(const FreqKeySpec& ks, const DevColumn* cols, int64_t r
   return true;
 }
 
+// Keys of G rows (row_j = base + j * stride, j < G) of ONE utf8 key column, with the loads of
+// all G rows issued together: the validity bits and offsets first, then the (at most 3) aligned
+// words of each key of <= 15 bytes.  Per row: sel = in range and a key (a NULL is a key only for
+// Histogram: "NullValue"); lng = a selected key longer than 15 bytes (the caller builds it with
+// make_key).  Words past a key are never loaded (they could lie past the buffer).
+template <int G>
+__device__ inline void string_keys(const DevColumn& c0, bool null_as_key, int64_t base, int64_t stride,
+                                   int64_t end, uint64_t (&k0)[G], uint64_t (&k1)[G], uint32_t (&len)[G],
+                                   uint32_t& sel, uint32_t& lng) {
+  const uint8_t* bytes = static_cast<const uint8_t*>(c0.values);
+  int32_t ob[G], oe[G];
+  uint32_t valid = 0u, inr = 0u;
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    const int64_t row = base + j * stride;
+    ob[j] = oe[j] = 0;
+    if (row < end) {
+      inr |= 1u << j;
+      ob[j] = c0.offsets[row];
+      oe[j] = c0.offsets[row + 1];
+      if (col_valid(c0, row)) valid |= 1u << j;
+    }
+  }
+  uint64_t w0[G], w1[G], w2[G];
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    const uint32_t n = (uint32_t)(oe[j] - ob[j]);
+    const uintptr_t a = (uintptr_t)(bytes + ob[j]);
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(a & ~(uintptr_t)7);
+    const uint32_t span = (uint32_t)(a & 7) + n;  // bytes from the first word's start
+    w0[j] = w1[j] = w2[j] = 0;
+    if (((valid >> j) & 1u) && n > 0 && n <= 15) {
+      w0[j] = w[0];
+      if (span > 8) w1[j] = w[1];
+      if (span > 16) w2[j] = w[2];
+    }
+  }
+  sel = 0u;
+  lng = 0u;
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    k0[j] = k1[j] = 0ull;
+    len[j] = 0u;
+    if (!((inr >> j) & 1u)) continue;
+    if ((valid >> j) & 1u) {
+      const uint32_t n = (uint32_t)(oe[j] - ob[j]);
+      sel |= 1u << j;
+      len[j] = n;
+      if (n > 15) {
+        lng |= 1u << j;
+        continue;
+      }
+      const uint32_t sh = (uint32_t)((uintptr_t)(bytes + ob[j]) & 7) * 8u;
+      // bytes 0..7 and 8..15 of the key from the three words, then masked to n bytes
+      const uint64_t lo = sh ? (w0[j] >> sh) | (w1[j] << (64u - sh)) : w0[j];
+      const uint64_t hi = sh ? (w1[j] >> sh) | (w2[j] << (64u - sh)) : w1[j];
+      k0[j] = n >= 8 ? lo : (n ? lo & ((1ull << (8u * n)) - 1ull) : 0ull);
+      k1[j] = n > 8 ? hi & ((1ull << (8u * (n - 8u))) - 1ull) : 0ull;
+    } else if (null_as_key) {  // Histogram NULL: "NullValue"
+      sel |= 1u << j;
+      len[j] = 9;
+      k0[j] = 0x756c61566c6c754eull;  // "NullValu"
+      k1[j] = 0x65ull;                // "e"
+    }
+  }
+}
+
 // Hash bit use: the top bucket_bits select the slice, the low kFreqSliceLog bits the first
 // probe, bits 12..43 the 32-bit tag kept in ctrl (independent of both).
 __device__ inline uint32_t tag_of(uint64_t h) {
@@ -323,7 +393,7 @@ struct LdsSlot {
 }  // namespace
 
 // Group-by of one batch: LDS pre-aggregation per workgroup, overflow rows to the global table.
-__global__ __launch_bounds__(kBlock) void dq_freq_insert_kernel(FreqKeySpec ks,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void dq_freq_insert_kernel(FreqKeySpec ks,
                                                                 const DevColumn* __restrict__ cols,
                                                                 int64_t n_rows, FreqTable T) {
   __shared__ LdsSlot lds[kLdsSlots];
@@ -387,18 +457,34 @@ __global__ __launch_bounds__(kBlock) void dq_freq_insert_kernel(FreqKeySpec ks,
     // already in its home slot -- as independent loads (R slot words read together, ONE acquire
     // fence, R key compares, R counter adds), so the LDS round trips overlap instead of chaining
     // row after row.  Anything else (empty or busy slot, collision) takes insert_row.
-    constexpr int R = 4;
+    constexpr int R = DQ_INSERT_R;
     bool overflowed = false;
+    const bool one_string = cols[ks.key_cols[0]].type == DQ_T_UTF8;
     for (int64_t base = row_begin; base < row_end && !overflowed; base += (int64_t)kBlock * R) {
       Key k[R];
       bool ok[R];
       uint32_t slot[R];
       unsigned long long want[R], c[R];
+      uint32_t s_sel = 0u, s_lng = 0u;
+      uint64_t sk0[R], sk1[R];
+      uint32_t slen[R];
+      if (one_string)  // all R rows' offsets, then all their key words, in flight together
+        string_keys<R>(cols[ks.key_cols[0]], ks.null_as_key != 0, base + threadIdx.x, kBlock, row_end, sk0, sk1,
+                       slen, s_sel, s_lng);
 #pragma unroll
       for (int j = 0; j < R; ++j) {
         const int64_t row = base + (int64_t)j * kBlock + threadIdx.x;
         bool too_long = false;
-        ok[j] = row < row_end && make_key(ks, cols, row, k[j], scratch, too_long, false);
+        if (one_string && !((s_lng >> j) & 1u)) {
+          ok[j] = (s_sel >> j) & 1u;
+          k[j].k0 = sk0[j];
+          k[j].k1 = sk1[j];
+          k[j].len = slen[j];
+          k[j].ptr = nullptr;
+          k[j].hash = 0;
+        } else {
+          ok[j] = row < row_end && make_key(ks, cols, row, k[j], scratch, too_long, false);
+        }
         if (!ok[j] && too_long) atomicOr(T.overflow, 4u);
         const bool fast = ok[j] && k[j].ptr == nullptr && k[j].len <= 16 && lds_open;
         const uint32_t lh = fast ? lds_hash(k[j].k0, k[j].k1, k[j].len) : 0u;
@@ -1034,22 +1120,33 @@ __global__ __launch_bounds__(kBlock) void dq_freq_agg_kernel(FreqTable T, const 
 // the sort path aggregates afterwards (skewed data).  Then dq_freq_agg_region_kernel aggregates
 // each slice region in LDS as the owner of its slice.  Per pass: 16 B read + 16 B written per
 // record (the sort moved 20 B keyed records three times, plus a key histogram pass).
-constexpr int kPartThreads = 1024;
+#ifndef DQ_PART_NT
+#define DQ_PART_NT 512
+#endif
+#ifndef DQ_PART_SUB
+#define DQ_PART_SUB 2048
+#endif
+// 512-thread workgroups with LDS images of 2048 records: two workgroups per CU (registers allow
+// 4 waves per SIMD), so one workgroup's load / reservation latency hides behind the other's
+// LDS scatter and writes.
+constexpr int kPartThreads = DQ_PART_NT;
 constexpr int kPartPerThread = 16;
 constexpr uint32_t kPartTile = (uint32_t)kPartThreads * kPartPerThread;  // records per tile
-constexpr uint32_t kPartSub = 4096;                                      // records per LDS round
+constexpr uint32_t kPartSub = DQ_PART_SUB;                               // records per LDS round
 constexpr int kPartMaxBinBits = kPartMaxBits;
+constexpr int kStageBinBits = 9;  // the level-1 split of the fused stage (dq_freq_api.inc kRegionBits)
 constexpr uint32_t kPartNoBin = 0xFFFFu;
 constexpr int kStageGroup = 4;  // rows per thread whose loads the fused stage issues together
 constexpr int kStagePer = 12;   // rows per thread per fused-stage tile (register budget)
 constexpr uint32_t kStageTile = (uint32_t)kPartThreads * kStagePer;
 
-struct PartLds {
+template <int MAXB>
+struct PartLdsT {
   FreqRec rec[kPartSub];
   uint16_t bin[kPartSub];
-  uint32_t hist[1 << kPartMaxBinBits];
-  uint32_t start[1 << kPartMaxBinBits];
-  unsigned long long gbase[1 << kPartMaxBinBits];
+  uint32_t hist[MAXB];
+  uint32_t start[MAXB];
+  unsigned long long gbase[MAXB];
   uint32_t total;
 };
 
@@ -1065,8 +1162,8 @@ __device__ inline uint64_t rec_hash(const FreqRec& r, bool* hole) {
 // 2^bin_bits, or kPartNoBin for none); output region of a bin = base_id + bin.  Ranks come from
 // LDS atomics, the room in each region from ONE device atomic per (tile, non-empty bin), and the
 // records are written from an LDS image sorted by bin, kPartSub at a time (coalesced runs).
-template <int PER>
-__device__ inline void part_tile(PartLds& L, const FreqRec (&rec)[PER], uint32_t (&bin)[PER],
+template <int PER, int MAXB>
+__device__ inline void part_tile(PartLdsT<MAXB>& L, const FreqRec (&rec)[PER], uint32_t (&bin)[PER],
                                  uint32_t nb, uint64_t base_id, FreqRec* __restrict__ out, uint64_t out_cap,
                                  unsigned long long* out_fill, FreqRec* ovf, unsigned long long* ovf_n,
                                  uint64_t ovf_cap, unsigned int* flag, unsigned long long* staged) {
@@ -1148,7 +1245,7 @@ __global__ __launch_bounds__(kPartThreads) void dq_freq_part_kernel(
     const FreqRec* __restrict__ in, uint64_t in_n, const unsigned long long* __restrict__ in_fill, uint64_t in_cap,
     int id_bits, int bin_bits, FreqRec* __restrict__ out, uint64_t out_cap, unsigned long long* out_fill,
     FreqRec* ovf, unsigned long long* ovf_n, uint64_t ovf_cap, unsigned int* flag) {
-  __shared__ PartLds L;
+  __shared__ PartLdsT<(1 << kPartMaxBinBits)> L;
   const uint32_t t = threadIdx.x;
   const uint32_t nb = 1u << bin_bits;
   uint64_t base_id = 0, begin, count;
@@ -1192,11 +1289,11 @@ __global__ __launch_bounds__(kPartThreads) void dq_freq_part_kernel(
 // the long-key flag are kept as by dq_freq_stage_kernel.  Single-string keys (the common case)
 // load their offsets, then their bytes, for all of a thread's rows at once.
 template <bool ONE_STRING>
-__global__ __launch_bounds__(kPartThreads) void dq_freq_stage_part_kernel(
+__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(4))) void dq_freq_stage_part_kernel(
     FreqKeySpec ks, const DevColumn* __restrict__ cols, int64_t n_rows, int b1, FreqRec* __restrict__ out,
     uint64_t cap1, unsigned long long* fill1, FreqRec* ovf, unsigned long long* ovf_n, uint64_t ovf_cap,
     unsigned int* flag, uint32_t* hll, unsigned long long* long_key, unsigned long long* staged) {
-  __shared__ PartLds L;
+  __shared__ PartLdsT<(1 << kStageBinBits)> L;
   __shared__ uint32_t regs[kHllM];
   const uint32_t t = threadIdx.x;
   const uint32_t nb = 1u << b1;
@@ -1211,69 +1308,26 @@ __global__ __launch_bounds__(kPartThreads) void dq_freq_stage_part_kernel(
     uint32_t bin[kStagePer];
     uint32_t too_long = 0u;
     if constexpr (ONE_STRING) {
-      // two groups of kStageGroup rows: the offsets of a group, then its key words, all in flight
-      // together (the whole tile at once would not fit the register file)
+      // groups of kStageGroup rows: their offsets, then their key words, all in flight together
+      // (the whole tile at once would not fit the register file)
       constexpr int G = kStageGroup;
-      const uint8_t* base = static_cast<const uint8_t*>(c0.values);
 #pragma unroll
       for (int g = 0; g < kStagePer; g += G) {
-        int32_t ob[G], oe[G];
-        uint32_t valid = 0u;
+        uint64_t k0[G], k1[G];
+        uint32_t len[G], sel, lng;
+        string_keys<G>(c0, ks.null_as_key != 0, row0 + g * kPartThreads + t, kPartThreads, n_rows, k0, k1, len, sel,
+                       lng);
 #pragma unroll
         for (int i = 0; i < G; ++i) {
-          const int64_t row = row0 + (g + i) * kPartThreads + t;
-          ob[i] = oe[i] = 0;
-          if (row < n_rows) {
-            ob[i] = c0.offsets[row];
-            oe[i] = c0.offsets[row + 1];
-            if (col_valid(c0, row)) valid |= 1u << i;
-          }
-        }
-        uint64_t w0[G], w1[G], w2[G];
-#pragma unroll
-        for (int i = 0; i < G; ++i) {
-          // the (at most 3) aligned words holding a key of <= 15 bytes; words past the key are
-          // not loaded (they could lie past the buffer)
-          const uint32_t n = (uint32_t)(oe[i] - ob[i]);
-          const uintptr_t a = (uintptr_t)(base + ob[i]);
-          const uint64_t* w = reinterpret_cast<const uint64_t*>(a & ~(uintptr_t)7);
-          const uint32_t span = (uint32_t)(a & 7) + n;  // bytes from the first word's start
-          w0[i] = w1[i] = w2[i] = 0;
-          if (((valid >> i) & 1u) && n > 0 && n <= 15) {
-            w0[i] = w[0];
-            if (span > 8) w1[i] = w[1];
-            if (span > 16) w2[i] = w[2];
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < G; ++i) {
-          const int64_t row = row0 + (g + i) * kPartThreads + t;
           bin[g + i] = kPartNoBin;
-          if (row >= n_rows) continue;
-          uint64_t k0, k1;
-          uint32_t n;
-          if ((valid >> i) & 1u) {
-            n = (uint32_t)(oe[i] - ob[i]);
-            if (n > 15) {
-              too_long = max(too_long, n);
-              continue;
-            }
-            const uint32_t sh = (uint32_t)((uintptr_t)(base + ob[i]) & 7) * 8u;
-            // bytes 0..7 and 8..15 of the key from the three words, then masked to n bytes
-            const uint64_t lo = sh ? (w0[i] >> sh) | (w1[i] << (64u - sh)) : w0[i];
-            const uint64_t hi = sh ? (w1[i] >> sh) | (w2[i] << (64u - sh)) : w1[i];
-            k0 = n >= 8 ? lo : (n ? lo & ((1ull << (8u * n)) - 1ull) : 0ull);
-            k1 = n > 8 ? hi & ((1ull << (8u * (n - 8u))) - 1ull) : 0ull;
-          } else if (ks.null_as_key) {  // Histogram NULL: "NullValue"
-            n = 9;
-            k0 = 0x756c61566c6c754eull;  // "NullValu"
-            k1 = 0x65ull;                // "e"
-          } else {
+          if (!((sel >> i) & 1u)) continue;
+          if ((lng >> i) & 1u) {
+            too_long = max(too_long, len[i]);
             continue;
           }
-          const uint64_t h = hash_inline(k0, k1, n);
-          rec[g + i].k0 = k0;
-          rec[g + i].k1 = k1 | ((unsigned long long)n << kRecLenShift);
+          const uint64_t h = hash_inline(k0[i], k1[i], len[i]);
+          rec[g + i].k0 = k0[i];
+          rec[g + i].k1 = k1[i] | ((unsigned long long)len[i] << kRecLenShift);
           bin[g + i] = (uint32_t)(h >> (64 - b1)) & (nb - 1u);
           sketch_update(regs, h);
         }
@@ -1469,11 +1523,11 @@ hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, const 
                                   uint64_t ovf_cap, unsigned int* d_flag, uint32_t* d_hll, unsigned long long* d_long_key,
                                   unsigned long long* d_staged, hipStream_t stream) {
   if (n_rows <= 0) return hipSuccess;
-  if (b1 < 1 || b1 > kPartMaxBinBits) return hipErrorInvalidValue;
+  if (b1 < 1 || b1 > kStageBinBits) return hipErrorInvalidValue;
   const int64_t tiles = (n_rows + kStageTile - 1) / kStageTile;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const int64_t blocks = tiles < (int64_t)cus * 2 ? tiles : (int64_t)cus * 2;
+  const int64_t blocks = tiles < (int64_t)cus * 4 ? tiles : (int64_t)cus * 4;
   if (one_string)
     hipLaunchKernelGGL(dq_freq_stage_part_kernel<true>, dim3((unsigned)blocks), dim3(kPartThreads), 0, stream, ks, d_cols,
                        n_rows, b1, d_out, cap1, d_fill1, d_ovf, d_ovf_n, ovf_cap, d_flag, d_hll, d_long_key, d_staged);
