@@ -455,8 +455,23 @@ def run_c4(args, world, rank, local):
                                    workload="c4" if world == 1 else None,
                                    default_size=(args.c4_rows, args.c4_batch, args.c4_distinct)
                                    == (1_000_000_000, 125_000_000, 201_500_000)),
+        # SURVEY §8(d) C4 asks for the table accesses per row beside the streaming fraction: the
+        # partition path moves each staged row's 16-B record three times (stage write, level-2
+        # split read + write, aggregation read) and touches the HBM table only in whole-slice
+        # writes -- no per-row table probe (the probes are in LDS).
+        "table_access": {"record_passes_per_row": 3, "record_bytes": 16, "global_table_probes_per_row": 0,
+                         "table_slots_written_per_row": _c4_table_slots(groups) / float(args.c4_rows)},
         "check": dict(metrics, histogram_bins=hist.numberOfBins),
     }
+
+
+def _c4_table_slots(groups: float) -> float:
+    """Slots of the table the partition path sizes for `groups` (power of two, load <= 0.5 of 1.15 x the
+    estimate; dq_freq_api.inc materialize)."""
+    cap = 65536.0
+    while groups * 1.15 + 4096 > 0.5 * cap:
+        cap *= 2
+    return cap
 
 
 def _strings_from_ints(ids, width: int, prefix: bytes, dev):
