@@ -873,6 +873,7 @@ constexpr int kAggLdsHist = 512;  // count-of-counts bins kept in LDS by a track
 struct AggLds {
   unsigned long long K0[kFreqSliceSlots], K1[kFreqSliceSlots];
   uint32_t C[kFreqSliceSlots];
+  uint32_t G[kFreqSliceSlots];  // the table tag of a slot claimed in this work item
   int overflow;
   uint32_t fresh;
   uint32_t cmax;
@@ -918,8 +919,8 @@ constexpr int kAggBatch = DQ_AGG_BATCH;  // records per thread loaded together
 // publishing lane's stores stay inside the loop iteration, with `done` tested by the loop: a
 // lane of the same wave spinning on BUSY must see them in its next iteration, so the publish
 // must not be sunk behind the loop -- an early return there hung the wave.)
-__device__ inline bool lds_count(unsigned long long* K0, unsigned long long* K1, uint32_t* C, const FreqRec& r,
-                                 uint64_t h) {
+__device__ inline bool lds_count(unsigned long long* K0, unsigned long long* K1, uint32_t* C, uint32_t* G,
+                                 const FreqRec& r, uint64_t h) {
   constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
   uint32_t s = (uint32_t)(h & (S - 1));
   bool done = false;
@@ -933,6 +934,7 @@ __device__ inline bool lds_count(unsigned long long* K0, unsigned long long* K1,
 #endif
     if (c == kLdsEmpty) {  // claimed: publish the key, then count
       K0[s] = r.k0;
+      G[s] = tag_of(h);  // (written back with the slot: no second hash of the key)
       __threadfence_block();
       atomicExch(&K1[s], r.k1);
       atomicAdd(&C[s], 1u);
@@ -965,10 +967,13 @@ __device__ __noinline__ void piece_spill(const FreqTable& T, const FreqRec& r, u
 // Aggregate records [r0, r1) of slice b.  owner: the work item holds the slice's whole bucket
 // (load the slice, count in LDS, write it back with plain stores); otherwise it is one piece of a
 // split bucket (count in LDS, merge into the slice with device-scope atomics).
+// pre (optional): the item's first NT * kAggBatch records, already loaded by the caller (thread
+// t holds records r0 + j * NT + t), so they were in flight during the previous item.
 template <int NT, bool OWNER_ONLY>
 __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restrict__ recs, uint64_t r0, uint64_t r1,
                          uint64_t b, bool owner, int table_empty, FreqRec* retry, unsigned long long* n_retry,
-                         unsigned long long* new_groups, const AggTrack* tr = nullptr) {
+                         unsigned long long* new_groups, const AggTrack* tr = nullptr,
+                         const FreqRec (*pre)[kAggBatch] = nullptr) {
   constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
   unsigned long long* K0 = L.K0;
   unsigned long long* K1 = L.K1;
@@ -1005,10 +1010,15 @@ __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restric
     // dependent load per record made the loop latency-bound)
     for (uint64_t base = r0; base < r1; base += (uint64_t)NT * kAggBatch) {
       FreqRec rb[kAggBatch];
+      if (pre && base == r0) {
 #pragma unroll
-      for (int j = 0; j < kAggBatch; ++j) {
-        const uint64_t i = base + (uint64_t)j * NT + threadIdx.x;
-        if (i < r1) rb[j] = recs[i];
+        for (int j = 0; j < kAggBatch; ++j) rb[j] = (*pre)[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < kAggBatch; ++j) {
+          const uint64_t i = base + (uint64_t)j * NT + threadIdx.x;
+          if (i < r1) rb[j] = recs[i];
+        }
       }
 #pragma unroll
       for (int j = 0; j < kAggBatch; ++j) {
@@ -1020,7 +1030,7 @@ __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restric
         rec_unpack(r, &k1, &len);
         if (len == kRecHole) continue;
         const uint64_t h = hash_inline(r.k0, k1, len);
-        if (!lds_count(K0, K1, C, r, h)) {
+        if (!lds_count(K0, K1, C, L.G, r, h)) {
           if (OWNER_ONLY || owner) overflow = 1;
           else piece_spill(T, r, k1, len, h, retry, n_retry);
         }
@@ -1061,21 +1071,22 @@ __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restric
         }
         if (tr) track_count(L, *tr, c);
         FreqSlot& e = slice[s];
+        bool is_new = false;
         if (!table_empty && (e.ctrl & kReady)) {
           e.count += c;
         } else {
           const unsigned long long k1 = K1[s];
           const uint32_t len = (uint32_t)(k1 >> kRecLenShift);
-          const unsigned long long key1 = k1 & kRecKeyMask;
-          const uint64_t h = hash_inline(K0[s], key1, len);
           FreqSlot n;
-          n.ctrl = ((unsigned long long)tag_of(h) << 32) | kReady | len;
+          n.ctrl = ((unsigned long long)L.G[s] << 32) | kReady | len;
           n.count = c;
           n.k0 = K0[s];
-          n.k1 = key1;
+          n.k1 = k1 & kRecKeyMask;
           e = n;
-          atomicAdd(&fresh, 1u);
+          is_new = true;
         }
+        const uint64_t nb = __ballot(is_new);  // one LDS add per wave, not one per new group
+        if (nb && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(nb)) atomicAdd(&fresh, (uint32_t)__popcll(nb));
       }
       __syncthreads();
       if (threadIdx.x == 0 && fresh) atomicAdd(new_groups, (unsigned long long)fresh);
@@ -1382,7 +1393,13 @@ __global__ __launch_bounds__(kBlock) void dq_freq_compact_kernel(const FreqRec* 
 #define DQ_AGG_THREADS 512
 #endif
 constexpr int kAggRegionThreads = DQ_AGG_THREADS;
-__global__ __launch_bounds__(kAggRegionThreads) void dq_freq_agg_region_kernel(FreqTable T, const FreqRec* __restrict__ recs,
+#ifndef DQ_AGG_PREFETCH
+#define DQ_AGG_PREFETCH 0  // measured: the extra registers cost more than the overlap gains (C4 33.2 vs 34.9-39.2 ms)
+#endif
+#ifndef DQ_AGG_WAVES
+#define DQ_AGG_WAVES 4
+#endif
+__global__ __launch_bounds__(kAggRegionThreads) __attribute__((amdgpu_waves_per_eu(DQ_AGG_WAVES))) void dq_freq_agg_region_kernel(FreqTable T, const FreqRec* __restrict__ recs,
                                                                     const unsigned long long* __restrict__ fill,
                                                                     uint64_t cap, uint64_t n_slices, int table_empty,
                                                                     FreqRec* retry, unsigned long long* n_retry,
@@ -1393,19 +1410,38 @@ __global__ __launch_bounds__(kAggRegionThreads) void dq_freq_agg_region_kernel(F
     for (int i = threadIdx.x; i < kAggLdsHist; i += kAggRegionThreads) L.hist[i] = 0u;
     __syncthreads();
   }
-  for (uint64_t b = blockIdx.x; b < n_slices; b += gridDim.x) {
+  // software pipeline: the next item's first records are loaded while this item is counted
+  auto item_end = [&](uint64_t b) -> uint64_t {
     const unsigned long long f = fill[b];
+    return b * cap + (f < cap ? f : cap);
+  };
+  auto load_first = [&](uint64_t b, FreqRec (&out)[kAggBatch]) {
+    const uint64_t r0 = b * cap, r1 = item_end(b);
+#pragma unroll
+    for (int j = 0; j < kAggBatch; ++j) {
+      const uint64_t i = r0 + (uint64_t)j * kAggRegionThreads + threadIdx.x;
+      if (i < r1) out[j] = recs[i];
+    }
+  };
+  FreqRec cur[kAggBatch];
+  if (DQ_AGG_PREFETCH && blockIdx.x < n_slices) load_first(blockIdx.x, cur);
+  for (uint64_t b = blockIdx.x; b < n_slices; b += gridDim.x) {
     const uint64_t r0 = b * cap;
-    const uint64_t r1 = r0 + (f < cap ? f : cap);
+    const uint64_t r1 = item_end(b);
+    FreqRec nxt[kAggBatch];
+    if (DQ_AGG_PREFETCH && b + gridDim.x < n_slices) load_first(b + gridDim.x, nxt);
     if (r1 == r0) {
       if (tr.write_all) {
         FreqSlot* slice = T.slots + (b << kFreqSliceLog);
         for (uint32_t s = threadIdx.x; s < (uint32_t)kFreqSliceSlots; s += kAggRegionThreads) slice[s] = FreqSlot{0ull, 0ull, 0ull, 0ull};
       }
       if (tr.smax && threadIdx.x == 0) tr.smax[b] = 0u;
-      continue;
+    } else {
+      agg_item<kAggRegionThreads, true>(L, T, recs, r0, r1, b, true, table_empty, retry, n_retry, new_groups,
+                                        track || tr.write_all ? &tr : nullptr, DQ_AGG_PREFETCH ? &cur : nullptr);
     }
-    agg_item<kAggRegionThreads, true>(L, T, recs, r0, r1, b, true, table_empty, retry, n_retry, new_groups, track || tr.write_all ? &tr : nullptr);
+#pragma unroll
+    for (int j = 0; j < kAggBatch; ++j) cur[j] = nxt[j];
   }
   if (track) {
     __syncthreads();
