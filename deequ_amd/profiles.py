@@ -149,11 +149,30 @@ class ColumnProfiler:
 
         if printStatusUpdates:
             print("### PROFILING: Computing generic column statistics in pass (1/3)...")
+        # Pass 2's statistics of a column whose type the schema already fixes as numeric (a native
+        # int / float column, not predefined otherwise) are known before pass 1 runs and read the
+        # same uncast column, so they ride along in pass 1's scan: the column is read once and its
+        # statistics and HLL come out of one fused kernel (the states are the same aggregations
+        # over the same rows; only string columns typed numeric by pass 1 wait for pass 2's cast).
+        numeric_types = (DataTypeInstances.Integral, DataTypeInstances.Fractional)
+
+        def _fixed_numeric(c):
+            if schema[c] == "string":
+                return False
+            t = predefined[c] if c in predefined else _known_type(schema[c])
+            return t in numeric_types
+
+        def _stats(c):
+            return [Minimum(c), Maximum(c), Mean(c), StandardDeviation(c), Sum(c)]
+
+        early = [c for c in relevant if _fixed_numeric(c)]
         first = []
         for c in relevant:
             first += [Completeness(c), ApproxCountDistinct(c)]
             if schema[c] == "string" and c not in predefined:
                 first.append(DataType(c))
+        for c in early:
+            first += _stats(c)
         ctx1 = AnalysisRunner.onData(data).addAnalyzers(first).addAnalyzer(Size()).run()
         generic = _extract_generic_statistics(relevant, schema, ctx1, predefined)
 
@@ -162,10 +181,13 @@ class ColumnProfiler:
         casted = _cast_numeric_string_columns(relevant, data, generic)
         second = []
         for c in relevant:
-            if generic.typeOf(c) in (DataTypeInstances.Integral, DataTypeInstances.Fractional):
-                second += [Minimum(c), Maximum(c), Mean(c), StandardDeviation(c), Sum(c)]
-        ctx2 = AnalysisRunner.onData(casted).addAnalyzers(second).run()
-        numeric = _extract_numeric_statistics(ctx2)
+            if c not in early and generic.typeOf(c) in numeric_types:
+                second += _stats(c)
+        numeric = _extract_numeric_statistics(ctx1)
+        if second:
+            ctx2 = AnalysisRunner.onData(casted).addAnalyzers(second).run()
+            for k, v in _extract_numeric_statistics(ctx2).items():
+                numeric[k].update(v)
 
         if printStatusUpdates:
             print("### PROFILING: Computing histograms of low-cardinality columns in pass (3/3)...")
