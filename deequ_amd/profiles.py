@@ -339,17 +339,19 @@ def compute_histograms(data, target_columns: Sequence[str],
     bool_cols = [c for c in target_columns if schema[c] == "bool" and _IDENT.match(c)]
     if bool_cols:
         out.update(_bool_histograms(data, bool_cols))
-    for c in target_columns:
-        if c in out:
-            continue
-        dtype = schema[c]
-        from .distributed import is_sharded
-        if is_sharded(data):  # the key-hash exchanged table of the whole dataset (collective)
-            from .frequencies import compute_frequencies
+    from .distributed import is_sharded
+    from .engine import current_device
+    rest = [c for c in target_columns if c not in out]
+    if is_sharded(data):  # the key-hash exchanged table of the whole dataset (collective, in order)
+        from .frequencies import compute_frequencies
+        for c in rest:
             counts, keys = compute_frequencies(data, [c], histogram=True).table.export()
-            out[c] = _histogram_distribution(counts, keys, dtype)
-            continue
-        table = FrequencyTable([c], dict(schema), histogram=True)
+            out[c] = _histogram_distribution(counts, keys, schema[c])
+        return out
+    device = current_device()
+
+    def one(c):
+        table = FrequencyTable([c], dict(schema), histogram=True, device=device)
         if expected_groups and c in expected_groups:  # the pass-1 estimate (<= the threshold)
             table.expect_groups(int(expected_groups[c]) + 1)
         try:
@@ -358,7 +360,19 @@ def compute_histograms(data, target_columns: Sequence[str],
             counts, keys = table.export()
         finally:
             table.close()
-        out[c] = _histogram_distribution(counts, keys, dtype)
+        return _histogram_distribution(counts, keys, schema[c])
+
+    if len(rest) <= 1:
+        for c in rest:
+            out[c] = one(c)
+        return out
+    # Each table has its own HIP stream and the library releases the GIL in every call, so the
+    # group-bys of several columns run concurrently on the device (each alone is latency-bound:
+    # few groups, LDS pre-aggregation).  Results are per column, so the order does not matter.
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=min(len(rest), 8)) as ex:
+        for c, dist in zip(rest, ex.map(one, rest)):
+            out[c] = dist
     return out
 
 
