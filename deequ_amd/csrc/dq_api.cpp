@@ -158,6 +158,11 @@ class BlockPool {
 // Streams and pinned host blocks are recycled too: the profiler creates dozens of plans and
 // frequency tables per run, and hipStreamCreate / hipStreamDestroy / hipHostMalloc each cost
 // the host up to a millisecond (measured: ~1 ms host gaps before every table in a C5 trace).
+static bool getenv_flag(const char* name) {  // test knobs: set and not "0"
+  const char* e = std::getenv(name);
+  return e && e[0] && e[0] != '0';
+}
+
 class StreamPool {
  public:
   static StreamPool& get() {
@@ -695,7 +700,11 @@ struct dq_plan : Stager {
   std::vector<int> group_per_cu;  // resident workgroups per CU of each group's kernel (0 = unknown)
   std::vector<HllTask> hll_tasks;    // ApproxCountDistinct not fused into the value scan
   std::vector<std::pair<int, int>> hll_sets;  // (column, where program) of each register set
-  std::vector<HllTask> dtype_tasks;  // DataType: {column, type, where}
+  std::vector<HllTask> dtype_tasks;  // DataType: {column, type, where, count index}
+  // HLL + DataType of the same utf8 (column, where): one fused string pass (dq_string_pass_kernel);
+  // the HLL and DataType kernels launch only the tasks not fused here
+  std::vector<StrTask> str_tasks;
+  std::vector<HllTask> hll_launch, dtype_launch;
   std::vector<HllTask> len_tasks;    // MinLength / MaxLength: {column, type, where}
   std::vector<CorrTask> corr_tasks;  // Correlation: {x, y, where}
   std::vector<Program> programs;  // generic predicate programs -> batch masks
@@ -703,7 +712,7 @@ struct dq_plan : Stager {
   DevBuf d_unsup;  // per generic program: a row hit DQ_P_CAST_DOUBLE off its exact fast path
   std::vector<dq_status> op_status;  // per op, after dq_plan_finish
   DevBuf d_tasks, d_groups, d_ranges, d_hll, d_progs, d_insns, d_pool, d_acc, d_partials, d_regs,
-      d_cols, d_masks, d_mask_words, d_dtype, d_dtype_counts, d_len, d_len_out, d_corr, d_corr_part, d_corr_acc;
+      d_cols, d_masks, d_mask_words, d_dtype, d_dtype_counts, d_len, d_len_out, d_corr, d_corr_part, d_corr_acc, d_str;
   int64_t mask_words = 0;
   // pinned descriptor staging (DevColumn + DevMask arrays) guarded by an event
   void* h_desc = nullptr;
@@ -917,8 +926,9 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
         for (size_t k = 0; k < plan->dtype_tasks.size(); ++k)
           if (plan->dtype_tasks[k].column == op.column && plan->dtype_tasks[k].where_mask == where_prog)
             t = (int)k;
-        if (t < 0) {
-          plan->dtype_tasks.push_back(HllTask{op.column, column_types[op.column], where_prog, 0});
+        if (t < 0) {  // (reg_set = the task's index into the counts: launches may take a subset)
+          plan->dtype_tasks.push_back(HllTask{op.column, column_types[op.column], where_prog,
+                                              (int32_t)plan->dtype_tasks.size()});
           t = (int)plan->dtype_tasks.size() - 1;
         }
         slot.task = t;
@@ -1012,12 +1022,36 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
     pool += p.pool;
   }
   pool.append(8, '\0');
+  // HLL and DataType of the same utf8 (column, where) -- every string column of the profiler's
+  // pass 1 -- run as one string pass (one read of the strings); the rest keep their own kernels
+  plan->str_tasks.clear();
+  plan->hll_launch.clear();
+  plan->dtype_launch.clear();
+  {
+    std::vector<bool> dt_fused(plan->dtype_tasks.size(), false);
+    for (const HllTask& h : plan->hll_tasks) {
+      int dt = -1;
+      if (h.ctype == DQ_T_UTF8 && !getenv_flag("DQ_NO_STRING_PASS"))
+        for (size_t k = 0; k < plan->dtype_tasks.size(); ++k)
+          if (!dt_fused[k] && plan->dtype_tasks[k].column == h.column && plan->dtype_tasks[k].where_mask == h.where_mask)
+            dt = (int)k;
+      if (dt >= 0) {
+        dt_fused[dt] = true;
+        plan->str_tasks.push_back(StrTask{h.column, h.where_mask, h.reg_set, dt});
+      } else {
+        plan->hll_launch.push_back(h);
+      }
+    }
+    for (size_t k = 0; k < plan->dtype_tasks.size(); ++k)
+      if (!dt_fused[k]) plan->dtype_launch.push_back(plan->dtype_tasks[k]);
+  }
   dq_status s = DQ_OK;
   if ((s = upload(plan->d_tasks, plan->scan_tasks.data(), plan->scan_tasks.size() * sizeof(ScanTask))) != DQ_OK ||
       (s = upload(plan->d_groups, group_ids.data(), group_ids.size() * sizeof(int32_t))) != DQ_OK ||
       (s = plan->d_ranges.ensure(std::max<size_t>(1, plan->scan_tasks.size()) * sizeof(PartRange))) != DQ_OK ||
-      (s = upload(plan->d_hll, plan->hll_tasks.data(), plan->hll_tasks.size() * sizeof(HllTask))) != DQ_OK ||
-      (s = upload(plan->d_dtype, plan->dtype_tasks.data(), plan->dtype_tasks.size() * sizeof(HllTask))) != DQ_OK ||
+      (s = upload(plan->d_hll, plan->hll_launch.data(), plan->hll_launch.size() * sizeof(HllTask))) != DQ_OK ||
+      (s = upload(plan->d_dtype, plan->dtype_launch.data(), plan->dtype_launch.size() * sizeof(HllTask))) != DQ_OK ||
+      (s = upload(plan->d_str, plan->str_tasks.data(), plan->str_tasks.size() * sizeof(StrTask))) != DQ_OK ||
       (s = plan->d_dtype_counts.ensure(std::max<size_t>(1, plan->dtype_tasks.size()) * 5 * sizeof(uint64_t))) != DQ_OK ||
       (s = upload(plan->d_len, plan->len_tasks.data(), plan->len_tasks.size() * sizeof(HllTask))) != DQ_OK ||
       (s = plan->d_len_out.ensure(std::max<size_t>(1, plan->len_tasks.size()) * 3 * sizeof(uint64_t))) != DQ_OK ||
@@ -1341,14 +1375,22 @@ extern "C" dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, in
     DQ_HIP(launch_scan_reduce(parts, static_cast<const PartRange*>(plan->d_ranges.ptr), n_scan,
                               static_cast<ScanAcc*>(plan->d_acc.ptr), plan->stream));
   }
-  const int n_hll = (int)plan->hll_tasks.size();
+  const int n_str = (int)plan->str_tasks.size();
+  if (n_str > 0) {
+    int64_t bpt = std::max<int64_t>(1, plan->target_blocks / n_str);
+    bpt = std::min<int64_t>(bpt, chunks);
+    DQ_HIP(launch_string_pass(static_cast<const StrTask*>(plan->d_str.ptr), n_str, d_cols, d_masks, n_rows, (int)bpt,
+                              static_cast<uint32_t*>(plan->d_regs.ptr),
+                              static_cast<unsigned long long*>(plan->d_dtype_counts.ptr), plan->stream));
+  }
+  const int n_hll = (int)plan->hll_launch.size();
   if (n_hll > 0) {
     int64_t bpt = std::max<int64_t>(1, plan->target_blocks / n_hll);
     bpt = std::min<int64_t>(bpt, chunks);
     DQ_HIP(launch_hll(static_cast<const HllTask*>(plan->d_hll.ptr), n_hll, d_cols, d_masks, n_rows, (int)bpt,
                       static_cast<uint32_t*>(plan->d_regs.ptr), plan->stream));
   }
-  const int n_dt = (int)plan->dtype_tasks.size();
+  const int n_dt = (int)plan->dtype_launch.size();
   if (n_dt > 0) {
     int64_t bpt = std::max<int64_t>(1, plan->target_blocks / n_dt);
     bpt = std::min<int64_t>(bpt, (n_rows + kBlock - 1) / kBlock);

@@ -119,6 +119,15 @@ struct HllTask {
   int32_t reg_set;     // HLL: register set (registers + reg_set * kHllM); unused elsewhere
 };
 
+// Profiler pass 1 on a utf8 column (dq_profile.hip): the DataType counts (dt_index * 5 ..) and
+// the HLL registers (reg_set) of one (column, where), both from one read of the strings.
+struct StrTask {
+  int32_t column;
+  int32_t where_mask;  // -1 = none
+  int32_t reg_set;
+  int32_t dt_index;
+};
+
 // Correlation task (dq_pair.hip) and its running state CorrelationState(n, xAvg, yAvg, ck, xMk, yMk).
 struct CorrTask {
   int32_t x, y;
@@ -290,6 +299,9 @@ hipError_t launch_diag_hash(int blocks, int iters, bool with_hll, uint64_t* sink
 int scan_group_blocks_per_cu(int kind, int ptype, int np);  // 0 = unknown
 hipError_t launch_scan_reduce(const ScanAcc* d_partials, const PartRange* d_ranges, int n_tasks,
                               ScanAcc* d_acc, hipStream_t stream);
+hipError_t launch_string_pass(const StrTask* d_tasks, int n_tasks, const DevColumn* d_cols, const DevMask* d_masks,
+                              int64_t n_rows, int blocks_per_task, uint32_t* d_registers, unsigned long long* d_counts,
+                              hipStream_t stream);
 hipError_t launch_hll(const HllTask* d_tasks, int n_tasks, const DevColumn* d_cols,
                       const DevMask* d_masks, int64_t n_rows, int blocks_per_task,
                       uint32_t* d_registers, hipStream_t stream);

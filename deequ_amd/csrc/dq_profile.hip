@@ -18,6 +18,7 @@
 //    |10-exponent| <= 22 -- and any other well-formed number is counted as "unsupported" so
 //    the caller routes the column to Spark instead of returning an inexact value.
 #include "dq_parse.h"
+#include "dq_strhash.h"
 
 namespace dq {
 
@@ -67,11 +68,8 @@ __device__ inline uint64_t swar_bytes_below(int32_t m) {  // bytes [0, m) of a w
   return m <= 0 ? 0ull : m >= 8 ? all : (all & ((1ull << (8 * m)) - 1ull));
 }
 
-__device__ int classify_utf8_words(const WordSrc& ws, int32_t n) {
-  const uint32_t sh = ws.sh * 8u;
-  // the string's bytes 8k..8k+7 as one word (funnel shift of the aligned words); words past the
-  // string's length are not formed (a branch uniform across a column of similar lengths)
-  const uint64_t s0 = sh ? (ws.w0 >> sh) | (ws.w1 << (64u - sh)) : ws.w0;
+// s0, s1, s2: the string's bytes 0..7, 8..15, 16..23 (s1 / s2 read only when n > 8 / 16).
+__device__ int classify_shifted(uint64_t s0, uint64_t s1, uint64_t s2, int32_t n) {
   const uint32_t b0 = (uint32_t)s0 & 0xffu;
   int32_t pos = (n > 0 && (b0 == '+' || b0 == '-')) ? 1 : 0;
   if (pos < n && (((uint32_t)(s0 >> (8 * pos))) & 0xffu) == ' ') ++pos;
@@ -81,13 +79,11 @@ __device__ int classify_utf8_words(const WordSrc& ws, int32_t n) {
   uint64_t bad = swar_nondigit(s0) & in & ~dot;
   int dots = __builtin_popcountll(dot);
   if (n > 8 && bad == 0) {  // (a failed first word decides: String or Boolean from word 0)
-    const uint64_t s1 = sh ? (ws.w1 >> sh) | (ws.w2 << (64u - sh)) : ws.w1;
     in = swar_bytes_below(n - 8);
     dot = swar_is(s1, 0x2e2e2e2e2e2e2e2eull) & in;
     bad |= swar_nondigit(s1) & in & ~dot;
     dots += __builtin_popcountll(dot);
     if (n > 16) {
-      const uint64_t s2 = sh ? (ws.w2 >> sh) | (ws.w3 << (64u - sh)) : ws.w2;
       in = swar_bytes_below(n - 16);
       dot = swar_is(s2, 0x2e2e2e2e2e2e2e2eull) & in;
       bad |= swar_nondigit(s2) & in & ~dot;
@@ -98,6 +94,16 @@ __device__ int classify_utf8_words(const WordSrc& ws, int32_t n) {
   if (n == 4 && (uint32_t)s0 == 0x65757274u) return DT_BOOLEAN;                       // "true"
   if (n == 5 && (s0 & 0xffffffffffull) == 0x65736c6166ull) return DT_BOOLEAN;          // "false"
   return DT_STRING;
+}
+
+// The string's bytes 8k..8k+7 as one word (funnel shift of the aligned words).
+__device__ inline uint64_t funnel(uint64_t lo, uint64_t hi, uint32_t sh_bits) {
+  return sh_bits ? (lo >> sh_bits) | (hi << (64u - sh_bits)) : lo;
+}
+
+__device__ int classify_utf8_words(const WordSrc& ws, int32_t n) {
+  const uint32_t sh = ws.sh * 8u;
+  return classify_shifted(funnel(ws.w0, ws.w1, sh), funnel(ws.w1, ws.w2, sh), funnel(ws.w2, ws.w3, sh), n);
 }
 
 template <typename F>
@@ -209,7 +215,101 @@ __global__ __launch_bounds__(kBlock) void dq_datatype_kernel(const HllTask* __re
   if (threadIdx.x < 5) {
     uint64_t s = 0;
     for (int w = 0; w < kBlock / 64; ++w) s += part[w][threadIdx.x];
-    if (s) atomicAdd(&counts[(int64_t)blockIdx.y * 5 + threadIdx.x], (unsigned long long)s);
+    if (s) atomicAdd(&counts[(int64_t)task.reg_set * 5 + threadIdx.x], (unsigned long long)s);  // (reg_set = the task's count index)
+  }
+}
+
+// Profiler pass 1 on utf8 columns: DataType (DataType.scala:152-183) and ApproxCountDistinct
+// (StatefulHyperloglogPlus.scala:89-115) of the same (column, where) from ONE read of the
+// strings -- the offsets, then four aligned 8-byte words per row through a buffer descriptor
+// (unconditional: out of range reads 0), U rows per lane in flight; the words feed both the
+// SWAR classifier and the word-form XXH64 (strings of <= 24 bytes; longer ones take the
+// byte-pointer paths).  Every row is hashed and counted (rank 0 / DT_NULL when not selected),
+// so lanes diverge only on the length.  Counts are integers and registers maxima: the result
+// does not depend on the schedule.
+__global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* __restrict__ tasks,
+                                                                const DevColumn* __restrict__ cols,
+                                                                const DevMask* __restrict__ masks, int64_t n_rows,
+                                                                uint32_t* registers, unsigned long long* counts) {
+  __shared__ uint32_t regs[kHllM];
+  __shared__ uint64_t part[kBlock / 64][5];
+  const StrTask task = tasks[blockIdx.y];
+  for (int r = threadIdx.x; r < kHllM; r += kBlock) regs[r] = 0u;
+  __syncthreads();
+  const int64_t n_chunks = (n_rows + kScanRowAlign - 1) / kScanRowAlign;
+  const int64_t per_block = (n_chunks + gridDim.x - 1) / gridDim.x;
+  const int64_t r0 = min((int64_t)blockIdx.x * per_block * kScanRowAlign, n_rows);
+  const int64_t r1 = min(r0 + per_block * kScanRowAlign, n_rows);
+  const DevColumn& col = cols[task.column];
+  const uint8_t* wt = task.where_mask >= 0 ? reinterpret_cast<const uint8_t*>(masks[task.where_mask].t) : nullptr;
+  const uint8_t* vals = static_cast<const uint8_t*>(col.values);
+  const uintptr_t al = (uintptr_t)vals & ~(uintptr_t)7;
+  const uint32_t delta = (uint32_t)((uintptr_t)vals - al);
+  const uint32_t span = (delta + (uint32_t)col.offsets[n_rows] + 7u) & ~7u;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(al), 0, (int)span, 0x00020000);
+  uint64_t c[5] = {0, 0, 0, 0, 0};
+  constexpr int U = 4;
+  for (int64_t base = r0 + threadIdx.x; base < r1; base += U * kBlock) {
+    int32_t ob[U], oe[U];
+    uint32_t sel[U];
+    uint64_t w[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = base + (int64_t)u * kBlock;
+      const bool in = row < r1;
+      const int64_t rr = in ? row : r0;
+      ob[u] = col.offsets[rr];
+      oe[u] = col.offsets[rr + 1];
+      sel[u] = (in && (col.validity == nullptr || bit_at(col.validity, rr)) && (wt == nullptr || bit_at(wt, rr))) ? 1u : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t a = (delta + (uint32_t)ob[u]) & ~7u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(a + 8u * k), 0, 0);
+        w[u][k] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = base + (int64_t)u * kBlock;
+      if (row >= r1) break;
+      const int32_t n = oe[u] - ob[u];
+      int k;
+      W64 h;
+      if (n <= 24) {
+        const uint32_t sh = ((delta + (uint32_t)ob[u]) & 7u) * 8u;
+        const uint64_t s[3] = {funnel(w[u][0], w[u][1], sh), funnel(w[u][1], w[u][2], sh), funnel(w[u][2], w[u][3], sh)};
+        k = sel[u] ? classify_shifted(s[0], s[1], s[2], n) : DT_NULL;
+        h = xxh64_words_dev(s, (uint32_t)n);
+      } else {
+        k = sel[u] ? classify_utf8(PtrSrc{vals + ob[u]}, n) : DT_NULL;
+        h = xxh64_utf8_dev(vals + ob[u], (uint32_t)n);
+      }
+#pragma unroll
+      for (int i = 0; i < 5; ++i) c[i] += (k == i) ? 1u : 0u;
+      uint32_t idx, nlz, r;
+      hll_slot(h, idx, nlz);
+      asm("v_mad_u32_u24 %0, %1, %2, %2" : "=v"(r) : "v"(nlz), "v"(sel[u]));  // rank * sel
+      __hip_atomic_fetch_max(&regs[idx], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const uint64_t s = wave_sum(c[i]);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6][i] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < 5) {
+    uint64_t s = 0;
+    for (int wv = 0; wv < kBlock / 64; ++wv) s += part[wv][threadIdx.x];
+    if (s) atomicAdd(&counts[(int64_t)task.dt_index * 5 + threadIdx.x], (unsigned long long)s);
+  }
+  uint32_t* out = registers + (int64_t)task.reg_set * kHllM;
+  for (int r = threadIdx.x; r < kHllM; r += kBlock) {
+    const uint32_t v = regs[r];
+    if (v) atomicMax(&out[r], v);
   }
 }
 
@@ -308,6 +408,15 @@ __global__ __launch_bounds__(kBlock) void dq_cast_utf8_kernel(DevColumn src, int
     }
   }
   if (unsup) atomicAdd(n_unsupported, (unsigned long long)unsup);
+}
+
+hipError_t launch_string_pass(const StrTask* d_tasks, int n_tasks, const DevColumn* d_cols, const DevMask* d_masks,
+                              int64_t n_rows, int blocks_per_task, uint32_t* d_registers, unsigned long long* d_counts,
+                              hipStream_t stream) {
+  if (n_tasks <= 0 || n_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(dq_string_pass_kernel, dim3(blocks_per_task, n_tasks), dim3(kBlock), 0, stream, d_tasks, d_cols,
+                     d_masks, n_rows, d_registers, d_counts);
+  return hipGetLastError();
 }
 
 hipError_t launch_datatype(const HllTask* d_tasks, int n_tasks, const DevColumn* d_cols, const DevMask* d_masks,

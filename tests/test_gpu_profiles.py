@@ -266,3 +266,35 @@ def test_bool_histograms_fused_scan(gpu):
         assert got.numberOfBins == len(want), c
         assert {k: v.absolute for k, v in got.values.items()} == want, c
         assert all(v.ratio == v.absolute / n for v in got.values.values())
+
+
+@pytest.mark.parametrize("n", [63, 2049, 20000])
+def test_string_pass_datatype_and_hll_match_oracle(gpu, monkeypatch, n):
+    """DataType + ApproxCountDistinct of the same string column in one run take the fused string
+    pass (dq_string_pass_kernel: one read, word-form classifier and XXH64): DataType counts and
+    HLL register words bit-exact against the oracle and against the separate kernels
+    (DQ_NO_STRING_PASS=1), for strings of 0..40 bytes (word form <= 24, byte paths above, the
+    >= 32-byte XXH64 path), NULLs and a `where` filter."""
+    rng = np.random.default_rng(41 + n)
+    vals = []
+    for i in range(n):
+        if rng.random() < 0.07:
+            vals.append(None)
+            continue
+        k = int(rng.integers(0, 41))
+        pool = "0123456789.-+ truefalsxyz" if rng.random() < 0.7 else "0123456789"
+        vals.append("".join(pool[int(j)] for j in rng.integers(0, len(pool), k)))
+    spec = {"s": ["string", vals], "w": ["int32", [int(x) for x in rng.integers(0, 3, n)]]}
+    table, ot = product_table(spec), oracle_table(spec)
+    states = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("DQ_NO_STRING_PASS", "0" if fused == "1" else "1")
+        for where in (None, "w > 0"):
+            prov = d.InMemoryStateProvider()
+            an = [d.DataType("s", where), d.ApproxCountDistinct("s", where), d.Completeness("s", where)]
+            d.AnalysisRunner.onData(table).addAnalyzers(an).saveStatesWith(prov).run()
+            dt, hll = prov.load(an[0]), prov.load(an[1])
+            assert dt.counts() == O.datatype_state(ot, "s", where), (fused, where)
+            assert hll.words == O.approx_count_distinct_state(ot, "s", where).words, (fused, where)
+            states[(fused, where)] = (dt.counts(), hll.words)
+    assert states[("1", None)] == states[("0", None)] and states[("1", "w > 0")] == states[("0", "w > 0")]
