@@ -703,7 +703,7 @@ struct dq_plan : Stager {
   std::vector<HllTask> dtype_tasks;  // DataType: {column, type, where, count index}
   // HLL + DataType of the same utf8 (column, where): one fused string pass (dq_string_pass_kernel);
   // the HLL and DataType kernels launch only the tasks not fused here
-  std::vector<StrTask> str_tasks;
+  std::vector<StrTask> str_tasks, str_hll_tasks;  // (str_hll_tasks: utf8 HLL without a DataType)
   std::vector<HllTask> hll_launch, dtype_launch;
   std::vector<HllTask> len_tasks;    // MinLength / MaxLength: {column, type, where}
   std::vector<CorrTask> corr_tasks;  // Correlation: {x, y, where}
@@ -712,7 +712,7 @@ struct dq_plan : Stager {
   DevBuf d_unsup;  // per generic program: a row hit DQ_P_CAST_DOUBLE off its exact fast path
   std::vector<dq_status> op_status;  // per op, after dq_plan_finish
   DevBuf d_tasks, d_groups, d_ranges, d_hll, d_progs, d_insns, d_pool, d_acc, d_partials, d_regs,
-      d_cols, d_masks, d_mask_words, d_dtype, d_dtype_counts, d_len, d_len_out, d_corr, d_corr_part, d_corr_acc, d_str;
+      d_cols, d_masks, d_mask_words, d_dtype, d_dtype_counts, d_len, d_len_out, d_corr, d_corr_part, d_corr_acc, d_str, d_str_hll;
   int64_t mask_words = 0;
   // pinned descriptor staging (DevColumn + DevMask arrays) guarded by an event
   void* h_desc = nullptr;
@@ -1025,6 +1025,7 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
   // HLL and DataType of the same utf8 (column, where) -- every string column of the profiler's
   // pass 1 -- run as one string pass (one read of the strings); the rest keep their own kernels
   plan->str_tasks.clear();
+  plan->str_hll_tasks.clear();
   plan->hll_launch.clear();
   plan->dtype_launch.clear();
   {
@@ -1038,6 +1039,8 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
       if (dt >= 0) {
         dt_fused[dt] = true;
         plan->str_tasks.push_back(StrTask{h.column, h.where_mask, h.reg_set, dt});
+      } else if (h.ctype == DQ_T_UTF8 && getenv_flag("DQ_STRING_PASS_HLL")) {
+        plan->str_hll_tasks.push_back(StrTask{h.column, h.where_mask, h.reg_set, -1});
       } else {
         plan->hll_launch.push_back(h);
       }
@@ -1052,6 +1055,7 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
       (s = upload(plan->d_hll, plan->hll_launch.data(), plan->hll_launch.size() * sizeof(HllTask))) != DQ_OK ||
       (s = upload(plan->d_dtype, plan->dtype_launch.data(), plan->dtype_launch.size() * sizeof(HllTask))) != DQ_OK ||
       (s = upload(plan->d_str, plan->str_tasks.data(), plan->str_tasks.size() * sizeof(StrTask))) != DQ_OK ||
+      (s = upload(plan->d_str_hll, plan->str_hll_tasks.data(), plan->str_hll_tasks.size() * sizeof(StrTask))) != DQ_OK ||
       (s = plan->d_dtype_counts.ensure(std::max<size_t>(1, plan->dtype_tasks.size()) * 5 * sizeof(uint64_t))) != DQ_OK ||
       (s = upload(plan->d_len, plan->len_tasks.data(), plan->len_tasks.size() * sizeof(HllTask))) != DQ_OK ||
       (s = plan->d_len_out.ensure(std::max<size_t>(1, plan->len_tasks.size()) * 3 * sizeof(uint64_t))) != DQ_OK ||
@@ -1382,6 +1386,13 @@ extern "C" dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, in
     DQ_HIP(launch_string_pass(static_cast<const StrTask*>(plan->d_str.ptr), n_str, d_cols, d_masks, n_rows, (int)bpt,
                               static_cast<uint32_t*>(plan->d_regs.ptr),
                               static_cast<unsigned long long*>(plan->d_dtype_counts.ptr), plan->stream));
+  }
+  const int n_str_hll = (int)plan->str_hll_tasks.size();
+  if (n_str_hll > 0) {
+    int64_t bpt = std::max<int64_t>(1, plan->target_blocks / n_str_hll);
+    bpt = std::min<int64_t>(bpt, chunks);
+    DQ_HIP(launch_string_pass(static_cast<const StrTask*>(plan->d_str_hll.ptr), n_str_hll, d_cols, d_masks, n_rows,
+                              (int)bpt, static_cast<uint32_t*>(plan->d_regs.ptr), nullptr, plan->stream));
   }
   const int n_hll = (int)plan->hll_launch.size();
   if (n_hll > 0) {

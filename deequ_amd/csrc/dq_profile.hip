@@ -227,6 +227,12 @@ __global__ __launch_bounds__(kBlock) void dq_datatype_kernel(const HllTask* __re
 // byte-pointer paths).  Every row is hashed and counted (rank 0 / DT_NULL when not selected),
 // so lanes diverge only on the length.  Counts are integers and registers maxima: the result
 // does not depend on the schedule.
+#ifndef DQ_STR_U
+#define DQ_STR_U 4
+#endif
+// DT = false: the HLL alone (an ApproxCountDistinct without a DataType on the column), through
+// the same batched word loads.
+template <bool DT>
 __global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* __restrict__ tasks,
                                                                 const DevColumn* __restrict__ cols,
                                                                 const DevMask* __restrict__ masks, int64_t n_rows,
@@ -248,7 +254,7 @@ __global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* _
   const uint32_t span = (delta + (uint32_t)col.offsets[n_rows] + 7u) & ~7u;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(al), 0, (int)span, 0x00020000);
   uint64_t c[5] = {0, 0, 0, 0, 0};
-  constexpr int U = 4;
+  constexpr int U = DQ_STR_U;
   for (int64_t base = r0 + threadIdx.x; base < r1; base += U * kBlock) {
     int32_t ob[U], oe[U];
     uint32_t sel[U];
@@ -281,27 +287,31 @@ __global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* _
       if (n <= 24) {
         const uint32_t sh = ((delta + (uint32_t)ob[u]) & 7u) * 8u;
         const uint64_t s[3] = {funnel(w[u][0], w[u][1], sh), funnel(w[u][1], w[u][2], sh), funnel(w[u][2], w[u][3], sh)};
-        k = sel[u] ? classify_shifted(s[0], s[1], s[2], n) : DT_NULL;
+        k = (DT && sel[u]) ? classify_shifted(s[0], s[1], s[2], n) : DT_NULL;
         h = xxh64_words_dev(s, (uint32_t)n);
       } else {
-        k = sel[u] ? classify_utf8(PtrSrc{vals + ob[u]}, n) : DT_NULL;
+        k = (DT && sel[u]) ? classify_utf8(PtrSrc{vals + ob[u]}, n) : DT_NULL;
         h = xxh64_utf8_dev(vals + ob[u], (uint32_t)n);
       }
+      if constexpr (DT) {
 #pragma unroll
-      for (int i = 0; i < 5; ++i) c[i] += (k == i) ? 1u : 0u;
+        for (int i = 0; i < 5; ++i) c[i] += (k == i) ? 1u : 0u;
+      }
       uint32_t idx, nlz, r;
       hll_slot(h, idx, nlz);
       asm("v_mad_u32_u24 %0, %1, %2, %2" : "=v"(r) : "v"(nlz), "v"(sel[u]));  // rank * sel
       __hip_atomic_fetch_max(&regs[idx], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
+  if constexpr (DT) {
 #pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    const uint64_t s = wave_sum(c[i]);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6][i] = s;
+    for (int i = 0; i < 5; ++i) {
+      const uint64_t s = wave_sum(c[i]);
+      if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6][i] = s;
+    }
   }
   __syncthreads();
-  if (threadIdx.x < 5) {
+  if (DT && threadIdx.x < 5) {
     uint64_t s = 0;
     for (int wv = 0; wv < kBlock / 64; ++wv) s += part[wv][threadIdx.x];
     if (s) atomicAdd(&counts[(int64_t)task.dt_index * 5 + threadIdx.x], (unsigned long long)s);
@@ -414,8 +424,12 @@ hipError_t launch_string_pass(const StrTask* d_tasks, int n_tasks, const DevColu
                               int64_t n_rows, int blocks_per_task, uint32_t* d_registers, unsigned long long* d_counts,
                               hipStream_t stream) {
   if (n_tasks <= 0 || n_rows <= 0) return hipSuccess;
-  hipLaunchKernelGGL(dq_string_pass_kernel, dim3(blocks_per_task, n_tasks), dim3(kBlock), 0, stream, d_tasks, d_cols,
-                     d_masks, n_rows, d_registers, d_counts);
+  if (d_counts)
+    hipLaunchKernelGGL(dq_string_pass_kernel<true>, dim3(blocks_per_task, n_tasks), dim3(kBlock), 0, stream, d_tasks,
+                       d_cols, d_masks, n_rows, d_registers, d_counts);
+  else
+    hipLaunchKernelGGL(dq_string_pass_kernel<false>, dim3(blocks_per_task, n_tasks), dim3(kBlock), 0, stream, d_tasks,
+                       d_cols, d_masks, n_rows, d_registers, d_counts);
   return hipGetLastError();
 }
 

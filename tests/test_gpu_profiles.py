@@ -298,3 +298,23 @@ def test_string_pass_datatype_and_hll_match_oracle(gpu, monkeypatch, n):
             assert hll.words == O.approx_count_distinct_state(ot, "s", where).words, (fused, where)
             states[(fused, where)] = (dt.counts(), hll.words)
     assert states[("1", None)] == states[("0", None)] and states[("1", "w > 0")] == states[("0", "w > 0")]
+
+
+@pytest.mark.parametrize("knob", ["0", "1"])
+def test_string_hll_only_paths_match_oracle(gpu, monkeypatch, knob):
+    """ApproxCountDistinct of string columns alone: the HLL kernel (knob 0) and the string pass
+    without DataType (DQ_STRING_PASS_HLL=1) give the oracle's register words bit for bit."""
+    monkeypatch.setenv("DQ_STRING_PASS_HLL", knob)
+    rng = np.random.default_rng(77)
+    n = 30000
+    vals = [None if rng.random() < 0.05 else
+            "".join("0123456789abcdef"[int(j)] for j in rng.integers(0, 16, int(rng.integers(0, 40))))
+            for _ in range(n)]
+    spec = {"s": ["string", vals], "t": ["string", [v[:6] if v else v for v in vals]],
+            "w": ["int32", [int(x) for x in rng.integers(0, 3, n)]]}
+    table, ot = product_table(spec), oracle_table(spec)
+    prov = d.InMemoryStateProvider()
+    an = [d.ApproxCountDistinct("s"), d.ApproxCountDistinct("t"), d.ApproxCountDistinct("s", "w > 0")]
+    d.AnalysisRunner.onData(table).addAnalyzers(an).saveStatesWith(prov).run()
+    for a in an:
+        assert prov.load(a).words == O.approx_count_distinct_state(ot, a.column, a.where).words, str(a)
