@@ -718,6 +718,35 @@ constexpr unsigned long long kRecLenShift = 56;
 constexpr unsigned long long kRecKeyMask = (1ull << kRecLenShift) - 1;
 constexpr uint32_t kRecHole = 0xFFu;  // length byte of a record that holds no row
 
+#ifndef DQ_NT_RECORDS
+#define DQ_NT_RECORDS 0  // A/B: non-temporal records cost C4 3-4 ms (the next pass re-reads them from L2/MALL)
+#endif
+// Staged records are written once and read once by the next pass: optionally non-temporal.
+typedef unsigned int RecVec __attribute__((ext_vector_type(4)));
+__device__ inline FreqRec ld_rec(const FreqRec* p) {
+#if DQ_NT_RECORDS
+  const RecVec v = __builtin_nontemporal_load(reinterpret_cast<const RecVec*>(p));
+  FreqRec r;
+  r.k0 = (unsigned long long)v.x | ((unsigned long long)v.y << 32);
+  r.k1 = (unsigned long long)v.z | ((unsigned long long)v.w << 32);
+  return r;
+#else
+  return *p;
+#endif
+}
+__device__ inline void st_rec(FreqRec* p, const FreqRec& r) {
+#if DQ_NT_RECORDS
+  RecVec v;
+  v.x = (unsigned int)r.k0;
+  v.y = (unsigned int)(r.k0 >> 32);
+  v.z = (unsigned int)r.k1;
+  v.w = (unsigned int)(r.k1 >> 32);
+  __builtin_nontemporal_store(v, reinterpret_cast<RecVec*>(p));
+#else
+  *p = r;
+#endif
+}
+
 __device__ inline void rec_unpack(const FreqRec& r, unsigned long long* k1, uint32_t* len) {
   *len = (uint32_t)(r.k1 >> kRecLenShift);
   *k1 = r.k1 & kRecKeyMask;
@@ -1017,7 +1046,7 @@ __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restric
 #pragma unroll
         for (int j = 0; j < kAggBatch; ++j) {
           const uint64_t i = base + (uint64_t)j * NT + threadIdx.x;
-          if (i < r1) rb[j] = recs[i];
+          if (i < r1) rb[j] = ld_rec(recs + i);
         }
       }
 #pragma unroll
@@ -1237,7 +1266,7 @@ __device__ inline void part_tile(PartLdsT<MAXB>& L, const FreqRec (&rec)[PER], u
       const uint64_t o = L.gbase[b] + (r0 + j - L.start[b]);
       const FreqRec r = L.rec[j];
       if (o < out_cap) {
-        out[(base_id + b) * out_cap + o] = r;
+        st_rec(out + (base_id + b) * out_cap + o, r);
       } else {  // the region is full: the overflow list (aggregated by the sort path)
         const unsigned long long k = atomicAdd(ovf_n, 1ull);
         if (k < ovf_cap) ovf[k] = r;
@@ -1279,7 +1308,7 @@ __global__ __launch_bounds__(kPartThreads) void dq_freq_part_kernel(
 #pragma unroll
   for (int i = 0; i < kPartPerThread; ++i) {
     const uint32_t j = (uint32_t)i * kPartThreads + t;
-    if (j < count) rec[i] = in[begin + j];
+    if (j < count) rec[i] = ld_rec(in + begin + j);
   }
 #pragma unroll
   for (int i = 0; i < kPartPerThread; ++i) {
