@@ -939,6 +939,9 @@ __device__ inline void track_count(AggLds& L, const AggTrack& tr, uint32_t c) {
 #ifndef DQ_AGG_BATCH
 #define DQ_AGG_BATCH 8
 #endif
+#ifndef DQ_AGG_PB
+#define DQ_AGG_PB 0  // records probed together (0 = one at a time; A/B: 4 and 8 cost C4 3.5-4.5 ms)
+#endif
 #ifndef DQ_LDS_READ_PROBE
 #define DQ_LDS_READ_PROBE 0
 #endif
@@ -1049,6 +1052,80 @@ __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restric
           if (i < r1) rb[j] = ld_rec(recs + i);
         }
       }
+#if DQ_AGG_PB
+      // PB records at a time through ONE probing loop: each round issues the PB compare-and-swaps
+      // together, publishes the claims, then checks the candidate keys together -- the LDS
+      // round trips of the PB records overlap instead of running one record after another.
+      // (A claimer publishes in the round it claims; a record that met BUSY retries next round.)
+#pragma unroll
+      for (int g = 0; g < kAggBatch; g += DQ_AGG_PB) {
+        constexpr int PB = DQ_AGG_PB;
+        uint64_t hh[PB];
+        uint32_t sl[PB], probes[PB], pend = 0u;
+#pragma unroll
+        for (int q = 0; q < PB; ++q) {
+          const uint64_t i = base + (uint64_t)(g + q) * NT + threadIdx.x;
+          unsigned long long k1;
+          uint32_t len;
+          rec_unpack(rb[g + q], &k1, &len);
+          hh[q] = 0;
+          sl[q] = 0;
+          probes[q] = 0;
+          if (i < r1 && len != kRecHole) {
+            hh[q] = hash_inline(rb[g + q].k0, k1, len);
+            sl[q] = (uint32_t)(hh[q] & (S - 1));
+            pend |= 1u << q;
+          }
+        }
+        while (pend) {
+          unsigned long long c[PB];
+#pragma unroll
+          for (int q = 0; q < PB; ++q) c[q] = ((pend >> q) & 1u) ? atomicCAS(&K1[sl[q]], kLdsEmpty, kLdsBusy) : kLdsBusy;
+          uint32_t claimed = 0u;
+#pragma unroll
+          for (int q = 0; q < PB; ++q)
+            if (((pend >> q) & 1u) && c[q] == kLdsEmpty) {
+              K0[sl[q]] = rb[g + q].k0;
+              L.G[sl[q]] = tag_of(hh[q]);
+              claimed |= 1u << q;
+            }
+          if (claimed) {
+            __threadfence_block();
+#pragma unroll
+            for (int q = 0; q < PB; ++q)
+              if ((claimed >> q) & 1u) {
+                atomicExch(&K1[sl[q]], rb[g + q].k1);
+                atomicAdd(&C[sl[q]], 1u);
+              }
+            pend &= ~claimed;
+          }
+          unsigned long long k0v[PB];
+#pragma unroll
+          for (int q = 0; q < PB; ++q)
+            k0v[q] = (((pend >> q) & 1u) && c[q] == rb[g + q].k1)
+                         ? __hip_atomic_load(&K0[sl[q]], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)
+                         : ~rb[g + q].k0;
+#pragma unroll
+          for (int q = 0; q < PB; ++q) {
+            if (!((pend >> q) & 1u) || c[q] == kLdsBusy) continue;  // (BUSY: look at the slot again)
+            if (c[q] == rb[g + q].k1 && k0v[q] == rb[g + q].k0) {
+              atomicAdd(&C[sl[q]], 1u);
+              pend &= ~(1u << q);
+            } else {
+              sl[q] = (sl[q] + 1) & (S - 1);
+              if (++probes[q] >= S) {  // the LDS image is full
+                pend &= ~(1u << q);
+                unsigned long long k1;
+                uint32_t len;
+                rec_unpack(rb[g + q], &k1, &len);
+                if (OWNER_ONLY || owner) overflow = 1;
+                else piece_spill(T, rb[g + q], k1, len, hh[q], retry, n_retry);
+              }
+            }
+          }
+        }
+      }
+#else
 #pragma unroll
       for (int j = 0; j < kAggBatch; ++j) {
         const uint64_t i = base + (uint64_t)j * NT + threadIdx.x;
@@ -1064,6 +1141,7 @@ __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restric
           else piece_spill(T, r, k1, len, h, retry, n_retry);
         }
       }
+#endif
     }
     __syncthreads();
     if (!OWNER_ONLY && !owner) {  // merge the piece's counts into the shared slice

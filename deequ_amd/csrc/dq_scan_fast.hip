@@ -273,9 +273,11 @@ constexpr int kFastUnroll = DQ_FAST_UNROLL;  // 16-byte loads (2 rows) per lane 
 #define DQ_FAST_PREFETCH 1
 #endif
 
-#ifndef DQ_FAST_AUX
-#define DQ_FAST_AUX 2  // cache-policy bits of the streaming loads: nt (read once; A/B 13.11 vs 13.22 ms on C2)
-#endif
+// Streaming loads of a large pass go non-temporal (aux = 2: the bytes are read once and are far
+// larger than the 256 MiB Infinity Cache; A/B 13.11 vs 13.22 ms on C2); a small table (C1's 10M
+// rows) keeps the default policy, so a repeated pass over it is served from the Infinity Cache
+// (nt there doubled C1's step, 0.5 -> 1.0 ms).
+constexpr int64_t kNtMinRows = (int64_t)1 << 24;  // 128 MiB of 8-byte values per column
 // The loads of iteration `it`: 4 x 16 B of values and the 4 validity bytes of the same rows;
 // with SCNT also, on the scalar unit, the 16 bitmap bytes of each of the wave's 128-row groups,
 // whose popcount is the wave's selected-row count (no per-row VALU op for it).
@@ -289,7 +291,7 @@ struct FastLoad {
 
 template <bool SCNT>
 __device__ inline void fast_load(FastLoad& L, __amdgpu_buffer_rsrc_t rv, __amdgpu_buffer_rsrc_t rvalid,
-                                 BitmapWords vwords, uint32_t it) {
+                                 BitmapWords vwords, uint32_t it, bool nt) {
   constexpr uint32_t ROWS_PER_ITER = (uint32_t)kBlock * 2 * kFastUnroll;
   const uint32_t tid = threadIdx.x;
 #pragma unroll
@@ -297,8 +299,13 @@ __device__ inline void fast_load(FastLoad& L, __amdgpu_buffer_rsrc_t rv, __amdgp
     // (a load past the chunk -- the pipelined form's look-ahead -- reads 0 through the
     // descriptor's range check and is never used)
     const uint32_t r0 = it * ROWS_PER_ITER + ((uint32_t)u * kBlock + tid) * 2u;
-    L.vec[u] = __builtin_amdgcn_raw_buffer_load_b128(rv, (int)(r0 * 8u), 0, DQ_FAST_AUX);
-    L.vb[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rvalid, (int)(r0 >> 3), 0, DQ_FAST_AUX);
+    if (nt) {  // (wave-uniform)
+      L.vec[u] = __builtin_amdgcn_raw_buffer_load_b128(rv, (int)(r0 * 8u), 0, 2);
+      L.vb[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rvalid, (int)(r0 >> 3), 0, 2);
+    } else {
+      L.vec[u] = __builtin_amdgcn_raw_buffer_load_b128(rv, (int)(r0 * 8u), 0, 0);
+      L.vb[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rvalid, (int)(r0 >> 3), 0, 0);
+    }
     if constexpr (SCNT) {
       const uint32_t g = __builtin_amdgcn_readfirstlane((it * ROWS_PER_ITER + (uint32_t)u * kBlock * 2u) / 128u +
                                                         (tid >> 6));
@@ -376,18 +383,18 @@ __device__ inline void fast_main_loop(FastAcc& a, __amdgpu_buffer_rsrc_t rv, __a
                                       BitmapWords vwords,
                                       uint32_t no_valid, uint32_t full_iters, uint32_t sh_lo, uint32_t sh_hi,
                                       double shift, double cshift, int64_t lit_i, double lit_f, uint32_t* lregs,
-                                      uint32_t* s_nan) {
+                                      uint32_t* s_nan, bool nt) {
 #if DQ_FAST_PREFETCH
   // two-stage pipeline: iteration it + 1's loads are in flight while iteration it computes
   // (two register sets, the loop unrolled by two so no copies are needed)
   FastLoad A, B;
   uint32_t it = 0;
-  if (full_iters > 0) fast_load<SCNT>(A, rv, rvalid, vwords, 0);
+  if (full_iters > 0) fast_load<SCNT>(A, rv, rvalid, vwords, 0, nt);
 #pragma unroll 1
   for (; it + 1 < full_iters; it += 2) {
-    fast_load<SCNT>(B, rv, rvalid, vwords, it + 1);
+    fast_load<SCNT>(B, rv, rvalid, vwords, it + 1, nt);
     fast_compute<T, PK, STATS, HLL, MEMBER, SCNT>(a, A, no_valid, sh_lo, sh_hi, shift, cshift, lit_i, lit_f, lregs, s_nan);
-    fast_load<SCNT>(A, rv, rvalid, vwords, it + 2);
+    fast_load<SCNT>(A, rv, rvalid, vwords, it + 2, nt);
     fast_compute<T, PK, STATS, HLL, MEMBER, SCNT>(a, B, no_valid, sh_lo, sh_hi, shift, cshift, lit_i, lit_f, lregs, s_nan);
   }
   if (it < full_iters) fast_compute<T, PK, STATS, HLL, MEMBER, SCNT>(a, A, no_valid, sh_lo, sh_hi, shift, cshift, lit_i, lit_f, lregs, s_nan);
@@ -395,7 +402,7 @@ __device__ inline void fast_main_loop(FastAcc& a, __amdgpu_buffer_rsrc_t rv, __a
 #pragma unroll 1
   for (uint32_t it = 0; it < full_iters; ++it) {
     FastLoad L;
-    fast_load<SCNT>(L, rv, rvalid, vwords, it);
+    fast_load<SCNT>(L, rv, rvalid, vwords, it, nt);
     fast_compute<T, PK, STATS, HLL, MEMBER, SCNT>(a, L, no_valid, sh_lo, sh_hi, shift, cshift, lit_i, lit_f, lregs, s_nan);
   }
 #endif
@@ -454,6 +461,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DQ_FAST_
   const ScanTask& task = tasks[group[blockIdx.y]];
   int64_t row_begin, row_end;
   chunk_of_block(n_rows, row_begin, row_end);
+  const bool nt = n_rows >= kNtMinRows;
   const uint32_t span = (uint32_t)(row_end - row_begin);  // host keeps span * 8 < 4 GiB
   __shared__ uint32_t lregs[kHllM];
   __shared__ uint32_t lflag[kHllM / 32];
@@ -545,17 +553,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DQ_FAST_
   const bool scnt = DQ_FAST_SCNT && has_valid && (((uintptr_t)vwords & 3u) == 0u);
   if (member && scnt) {
     fast_main_loop<T, PK, STATS, HLL, true, true>(a, rv, rvalid, vwords, no_valid, full_iters, sh_lo, sh_hi, shift,
-                                                  cshift, lit_i, lit_f, lregs, &s_nan);
+                                                  cshift, lit_i, lit_f, lregs, &s_nan, nt);
     fast_tail<T, PK, STATS, HLL, true>(a, rv, rvalid, no_valid, full_iters * ROWS_PER_ITER, span, sh_lo, sh_hi,
                                        shift, cshift, lit_i, lit_f, lregs, &s_nan);
   } else if (member) {
     fast_main_loop<T, PK, STATS, HLL, true, false>(a, rv, rvalid, vwords, no_valid, full_iters, sh_lo, sh_hi, shift,
-                                                   cshift, lit_i, lit_f, lregs, &s_nan);
+                                                   cshift, lit_i, lit_f, lregs, &s_nan, nt);
     fast_tail<T, PK, STATS, HLL, true>(a, rv, rvalid, no_valid, full_iters * ROWS_PER_ITER, span, sh_lo, sh_hi,
                                        shift, cshift, lit_i, lit_f, lregs, &s_nan);
   } else {
     fast_main_loop<T, PK, STATS, HLL, false, false>(a, rv, rvalid, vwords, no_valid, full_iters, sh_lo, sh_hi,
-                                                    shift, cshift, lit_i, lit_f, lregs, &s_nan);
+                                                    shift, cshift, lit_i, lit_f, lregs, &s_nan, nt);
     fast_tail<T, PK, STATS, HLL, false>(a, rv, rvalid, no_valid, full_iters * ROWS_PER_ITER, span, sh_lo, sh_hi,
                                         shift, cshift, lit_i, lit_f, lregs, &s_nan);
   }
