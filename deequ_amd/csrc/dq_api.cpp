@@ -717,6 +717,8 @@ struct dq_plan : Stager {
   // pinned descriptor staging (DevColumn + DevMask arrays) guarded by an event
   void* h_desc = nullptr;
   size_t h_desc_size = 0;
+  void* h_back = nullptr;  // pinned bounce buffer of dq_plan_finish's readback
+  size_t h_back_size = 0;
   hipEvent_t desc_done = nullptr;
   bool desc_pending = false;
   int64_t total_rows = 0;
@@ -739,6 +741,7 @@ struct dq_plan : Stager {
     if (copy_stream) StreamPool::get().release(device, copy_stream);
     if (desc_done) (void)hipEventDestroy(desc_done);
     if (h_desc) PinnedPool::get().release(h_desc);
+    if (h_back) PinnedPool::get().release(h_back);
     if (stream) StreamPool::get().release(device, stream);
   }
 };
@@ -1461,24 +1464,42 @@ extern "C" dq_status dq_plan_finish(dq_plan* plan, dq_state* out, int n_out) {
   std::vector<uint64_t> dtc(plan->dtype_tasks.size() * 5);
   std::vector<uint64_t> lens(plan->len_tasks.size() * 3);
   std::vector<CorrAcc> corr(plan->corr_tasks.size());
-  if (!lens.empty())
-    DQ_HIP(hipMemcpyAsync(lens.data(), plan->d_len_out.ptr, lens.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
-                          plan->stream));
-  if (!corr.empty())
-    DQ_HIP(hipMemcpyAsync(corr.data(), plan->d_corr_acc.ptr, corr.size() * sizeof(CorrAcc), hipMemcpyDeviceToHost,
-                          plan->stream));
-  if (!dtc.empty())
-    DQ_HIP(hipMemcpyAsync(dtc.data(), plan->d_dtype_counts.ptr, dtc.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
-                          plan->stream));
-  if (!acc.empty())
-    DQ_HIP(hipMemcpyAsync(acc.data(), plan->d_acc.ptr, acc.size() * sizeof(ScanAcc), hipMemcpyDeviceToHost, plan->stream));
-  if (!regs.empty())
-    DQ_HIP(hipMemcpyAsync(regs.data(), plan->d_regs.ptr, regs.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, plan->stream));
   std::vector<uint32_t> unsup(plan->programs.size());
-  if (!unsup.empty())
-    DQ_HIP(hipMemcpyAsync(unsup.data(), plan->d_unsup.ptr, unsup.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                          plan->stream));
+  // every result array comes back in ONE pass through a pinned bounce buffer (pageable copies
+  // are staged by the runtime, tens of microseconds each), then one synchronize
+  struct Back {
+    void* dst;
+    const void* src;
+    size_t bytes;
+  };
+  const Back backs[] = {{lens.data(), plan->d_len_out.ptr, lens.size() * sizeof(uint64_t)},
+                        {corr.data(), plan->d_corr_acc.ptr, corr.size() * sizeof(CorrAcc)},
+                        {dtc.data(), plan->d_dtype_counts.ptr, dtc.size() * sizeof(uint64_t)},
+                        {acc.data(), plan->d_acc.ptr, acc.size() * sizeof(ScanAcc)},
+                        {regs.data(), plan->d_regs.ptr, regs.size() * sizeof(uint32_t)},
+                        {unsup.data(), plan->d_unsup.ptr, unsup.size() * sizeof(uint32_t)}};
+  size_t total = 0;
+  for (const Back& b : backs) total += (b.bytes + 255) & ~(size_t)255;
+  if (total > plan->h_back_size) {
+    PinnedPool::get().release(plan->h_back);
+    plan->h_back = nullptr;
+    plan->h_back_size = 0;
+    DQ_HIP(PinnedPool::get().alloc(total, &plan->h_back));
+    plan->h_back_size = total;
+  }
+  size_t at = 0;
+  for (const Back& b : backs) {
+    if (b.bytes)
+      DQ_HIP(hipMemcpyAsync(static_cast<uint8_t*>(plan->h_back) + at, b.src, b.bytes, hipMemcpyDeviceToHost,
+                            plan->stream));
+    at += (b.bytes + 255) & ~(size_t)255;
+  }
   DQ_HIP(hipStreamSynchronize(plan->stream));
+  at = 0;
+  for (const Back& b : backs) {
+    if (b.bytes) std::memcpy(b.dst, static_cast<uint8_t*>(plan->h_back) + at, b.bytes);
+    at += (b.bytes + 255) & ~(size_t)255;
+  }
   plan->op_status.assign(plan->slots.size(), DQ_OK);
   for (size_t i = 0; i < plan->slots.size(); ++i) {
     const OpSlot& s = plan->slots[i];
