@@ -1040,12 +1040,14 @@ __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restric
     __syncthreads();
     // records are loaded kAggBatch per thread at a time, all loads in flight together (one
     // dependent load per record made the loop latency-bound)
-    for (uint64_t base = r0; base < r1; base += (uint64_t)NT * kAggBatch) {
-      FreqRec rb[kAggBatch];
-      if (pre && base == r0) {
+    // (rb outside the loop, filled from `pre` before it: the caller's copy is dead from here on)
+    FreqRec rb[kAggBatch];
+    if (pre) {
 #pragma unroll
-        for (int j = 0; j < kAggBatch; ++j) rb[j] = (*pre)[j];
-      } else {
+      for (int j = 0; j < kAggBatch; ++j) rb[j] = (*pre)[j];
+    }
+    for (uint64_t base = r0; base < r1; base += (uint64_t)NT * kAggBatch) {
+      if (!pre || base != r0) {
 #pragma unroll
         for (int j = 0; j < kAggBatch; ++j) {
           const uint64_t i = base + (uint64_t)j * NT + threadIdx.x;
@@ -1401,6 +1403,9 @@ __global__ __launch_bounds__(kPartThreads) void dq_freq_part_kernel(
   part_tile(L, rec, bin, nb, base_id, out, out_cap, out_fill, ovf, ovf_n, ovf_cap, flag, nullptr);
 }
 
+#ifndef DQ_STAGE_TOUCH
+#define DQ_STAGE_TOUCH 0  // measured: no gain on C4 (31.4-32.0 vs 31.5-33.2 ms); =2 also touches key bytes (spills)
+#endif
 // Stage + level-1 partition fused: the rows of one batch become records written straight into
 // their level-1 regions (top b1 bits of the table hash), so the staging is not written and read
 // back in row order.  Tiles of kPartTile rows, grid-stride.  The sketch, the staged count and
@@ -1425,6 +1430,25 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(4)
     FreqRec rec[kStagePer];
     uint32_t bin[kStagePer];
     uint32_t too_long = 0u;
+#if DQ_STAGE_TOUCH
+    // the block's NEXT tile is touched while this one is built (one dword per 128-B line of its
+    // offsets, with DQ_STAGE_TOUCH=2 also of its key bytes), so its dependent offset -> bytes
+    // loads hit L2 / MALL instead of HBM; the touched values are consumed after the tile
+    uint32_t touch = 0u;
+    int32_t nb0 = 0, nb1 = 0;
+    if constexpr (ONE_STRING) {
+      const int64_t nrow0 = row0 + (int64_t)gridDim.x * kStageTile;
+      if (nrow0 < n_rows) {
+        const int64_t nrow1 = min(nrow0 + (int64_t)kStageTile, n_rows);
+        const int64_t orow = nrow0 + (int64_t)t * 32;  // 32 offsets per 128-B line
+        if (orow <= nrow1) touch ^= (uint32_t)c0.offsets[orow];
+        if (DQ_STAGE_TOUCH >= 2) {
+          nb0 = c0.offsets[nrow0];
+          nb1 = c0.offsets[nrow1];
+        }
+      }
+    }
+#endif
     if constexpr (ONE_STRING) {
       // groups of kStageGroup rows: their offsets, then their key words, all in flight together
       // (the whole tile at once would not fit the register file)
@@ -1473,7 +1497,20 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(4)
       }
     }
     if (too_long) atomicMax(long_key, (unsigned long long)too_long);
+#if DQ_STAGE_TOUCH >= 2
+    if constexpr (ONE_STRING) {
+      const uint8_t* bytes = static_cast<const uint8_t*>(c0.values);
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int64_t o = (int64_t)nb0 + ((int64_t)t + k * kPartThreads) * 128;
+        if (o < (int64_t)nb1) touch ^= bytes[o];
+      }
+    }
+#endif
     part_tile(L, rec, bin, nb, 0, out, cap1, fill1, ovf, ovf_n, ovf_cap, flag, staged);
+#if DQ_STAGE_TOUCH
+    asm volatile("" ::"v"(touch));
+#endif
   }
   __syncthreads();
   for (uint32_t i = t; i < (uint32_t)kHllM; i += kPartThreads)
@@ -1506,6 +1543,9 @@ constexpr int kAggRegionThreads = DQ_AGG_THREADS;
 #ifndef DQ_AGG_WAVES
 #define DQ_AGG_WAVES 4
 #endif
+#ifndef DQ_AGG_EARLY
+#define DQ_AGG_EARLY 1
+#endif
 __global__ __launch_bounds__(kAggRegionThreads) __attribute__((amdgpu_waves_per_eu(DQ_AGG_WAVES))) void dq_freq_agg_region_kernel(FreqTable T, const FreqRec* __restrict__ recs,
                                                                     const unsigned long long* __restrict__ fill,
                                                                     uint64_t cap, uint64_t n_slices, int table_empty,
@@ -1522,6 +1562,7 @@ __global__ __launch_bounds__(kAggRegionThreads) __attribute__((amdgpu_waves_per_
     const unsigned long long f = fill[b];
     return b * cap + (f < cap ? f : cap);
   };
+#if DQ_AGG_PREFETCH
   auto load_first = [&](uint64_t b, FreqRec (&out)[kAggBatch]) {
     const uint64_t r0 = b * cap, r1 = item_end(b);
 #pragma unroll
@@ -1530,13 +1571,31 @@ __global__ __launch_bounds__(kAggRegionThreads) __attribute__((amdgpu_waves_per_
       if (i < r1) out[j] = recs[i];
     }
   };
+#endif
+#if DQ_AGG_PREFETCH
   FreqRec cur[kAggBatch];
-  if (DQ_AGG_PREFETCH && blockIdx.x < n_slices) load_first(blockIdx.x, cur);
+  if (blockIdx.x < n_slices) load_first(blockIdx.x, cur);
+#endif
   for (uint64_t b = blockIdx.x; b < n_slices; b += gridDim.x) {
     const uint64_t r0 = b * cap;
     const uint64_t r1 = item_end(b);
+#if DQ_AGG_PREFETCH
     FreqRec nxt[kAggBatch];
-    if (DQ_AGG_PREFETCH && b + gridDim.x < n_slices) load_first(b + gridDim.x, nxt);
+    if (b + gridDim.x < n_slices) load_first(b + gridDim.x, nxt);
+#elif DQ_AGG_EARLY
+    // the item's records are touched (one dword per 128-B line, one per thread) before the LDS
+    // image is initialised, so their HBM latency overlaps the init and the barrier and the
+    // item's loads then hit L2; one register, consumed after the item
+    uint32_t touch = 0u;
+    {
+      const uint64_t i = r0 + (uint64_t)threadIdx.x * 8u;
+      if (i < r1) touch = *reinterpret_cast<const uint32_t*>(recs + i);
+    }
+    if (DQ_AGG_EARLY >= 2 && b + gridDim.x < n_slices) {  // and the next item's, from its region start
+      const uint64_t i = (b + gridDim.x) * cap + (uint64_t)threadIdx.x * 8u;
+      if (i < (b + gridDim.x + 1) * cap) touch ^= *reinterpret_cast<const uint32_t*>(recs + i);
+    }
+#endif
     if (r1 == r0) {
       if (tr.write_all) {
         FreqSlot* slice = T.slots + (b << kFreqSliceLog);
@@ -1545,10 +1604,19 @@ __global__ __launch_bounds__(kAggRegionThreads) __attribute__((amdgpu_waves_per_
       if (tr.smax && threadIdx.x == 0) tr.smax[b] = 0u;
     } else {
       agg_item<kAggRegionThreads, true>(L, T, recs, r0, r1, b, true, table_empty, retry, n_retry, new_groups,
-                                        track || tr.write_all ? &tr : nullptr, DQ_AGG_PREFETCH ? &cur : nullptr);
+                                        track || tr.write_all ? &tr : nullptr,
+#if DQ_AGG_PREFETCH
+                                        &cur);
+#else
+                                        nullptr);
+#endif
     }
+#if DQ_AGG_PREFETCH
 #pragma unroll
     for (int j = 0; j < kAggBatch; ++j) cur[j] = nxt[j];
+#elif DQ_AGG_EARLY
+    asm volatile("" ::"v"(touch));
+#endif
   }
   if (track) {
     __syncthreads();
