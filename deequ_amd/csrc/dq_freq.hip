@@ -1543,6 +1543,9 @@ constexpr int kAggRegionThreads = DQ_AGG_THREADS;
 #ifndef DQ_AGG_WAVES
 #define DQ_AGG_WAVES 4
 #endif
+#ifndef DQ_AGG_FILL_AHEAD
+#define DQ_AGG_FILL_AHEAD 0  // read the next item's fill one item ahead (A/B pending)
+#endif
 #ifndef DQ_AGG_EARLY
 #define DQ_AGG_EARLY 1  // 1: touch the item's records before its LDS init (-1 ms on C4); 2: also the next item's (measured +4 ms)
 #endif
@@ -1576,9 +1579,18 @@ __global__ __launch_bounds__(kAggRegionThreads) __attribute__((amdgpu_waves_per_
   FreqRec cur[kAggBatch];
   if (blockIdx.x < n_slices) load_first(blockIdx.x, cur);
 #endif
+#if DQ_AGG_FILL_AHEAD
+  // the next item's fill is read one item ahead (its latency hides behind the current item)
+  uint64_t r1_next = blockIdx.x < n_slices ? item_end(blockIdx.x) : 0;
+#endif
   for (uint64_t b = blockIdx.x; b < n_slices; b += gridDim.x) {
     const uint64_t r0 = b * cap;
+#if DQ_AGG_FILL_AHEAD
+    const uint64_t r1 = r1_next;
+    if (b + gridDim.x < n_slices) r1_next = item_end(b + gridDim.x);
+#else
     const uint64_t r1 = item_end(b);
+#endif
 #if DQ_AGG_PREFETCH
     FreqRec nxt[kAggBatch];
     if (b + gridDim.x < n_slices) load_first(b + gridDim.x, nxt);
