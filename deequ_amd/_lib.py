@@ -103,6 +103,7 @@ ArrowArray._fields_ = [("length", c_int64), ("null_count", c_int64), ("offset", 
 # measurement entry points (include/deequ_amd_diag.h; not part of the drop-in boundary)
 DIAG_SIGNATURES = {
     "dq_diag_hash_rate": (c_int, [c_int, c_int, c_int, POINTER(c_double)]),
+    "dq_diag_freq_paths": (c_int, [c_void_p, POINTER(c_int64)]),
 }
 
 
@@ -167,6 +168,8 @@ SIGNATURES = {
     "dq_states_merge_ranks": (c_int, [POINTER(DqState), c_int, c_int, POINTER(DqState)]),
     "dq_group_freq_exchange": (c_int, [c_void_p, c_void_p, c_void_p, POINTER(c_int64)]),
     "dq_group_freq_summary": (c_int, [c_void_p, c_void_p, c_int64, POINTER(DqFreqSummary)]),
+    "dq_group_freq_top": (c_int, [c_void_p, c_void_p, c_int, POINTER(DqFreqGroup), c_int64, c_void_p, c_int64,
+                                  POINTER(c_int64), POINTER(c_int64)]),
 }
 
 _lib = None

@@ -508,6 +508,36 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu((NP <= 3
     }
   }
   a.shift = shift;
+  if (stats_on) {  // (block-uniform) the cancellation guard of the shifted moments
+    const uint64_t n_w = wave_sum_u64((uint64_t)a.n_sel) + a.n_sel_w;  // lane 0
+    const double S1 = wave_sum_f64(a.s1), S2 = wave_sum_f64(a.s2);
+    double wn = 0.0, wmean = 0.0;
+    bool cancel = false;
+    if (lane == 0 && n_w > 0) {
+      wn = (double)n_w;
+      wmean = shift + S1 / wn;
+      cancel = moments_cancel(wn, S1, S2);
+    }
+    if (__syncthreads_or(cancel)) {
+      // redo Σd, Σd² of the chunk about its mean, one row per lane; the lanes' selected counts
+      // move with them (the block's total is unchanged)
+      const double m = block_mean_of_waves(wn, wmean);
+      if (fabs(m) <= 0x1p1000) {
+        a.shift = m;
+        a.s1 = a.s2 = 0.0;
+        a.n_sel = 0u;
+        a.n_sel_w = 0u;
+        for (uint32_t r = tid; r < span; r += kBlock) {
+          const double x = (double)buf_elem<T>(rv, r);
+          const uint32_t s = (buf_bits<1>(rvalid, r) | no_valid) & (buf_bits<1>(rwt, r) | no_where) & 1u;
+          const double dd = s ? (x - m) : 0.0;
+          a.s1 += dd;
+          a.s2 = fma(dd, dd, a.s2);
+          a.n_sel += s;
+        }
+      }
+    }
+  }
   thread_finish<T, NP>(a, NP, &partials[(int64_t)blockIdx.y * gridDim.x + blockIdx.x]);
 }
 

@@ -240,6 +240,41 @@ __device__ inline double wave_sum_f64(double v) {
   return v;
 }
 
+// Cancellation guard of the shifted moments.  Both value scans take a wave's Σd, Σd² about a
+// shift c (a value of the column the wave saw first) and form m2 = S2 - S1²/n, whose relative
+// rounding is about eps * S2 / m2: harmless while c lies near the data, but when c is an outlier
+// (a 1e8 sentinel among N(0, 1) values) S1²/n is nearly all of S2 and the difference cancels.
+// Spark's per-row update has no such mode (CentralMomentAgg, StandardDeviation.scala:37-44
+// merge), so a wave whose S1²/n exceeds kMomentCancel * m2 makes its workgroup redo the moments
+// of its chunk about the chunk's mean (then S1 ~ 0 and S2 ~ m2).  Ordinary data never comes close:
+// a uniform column gives at most 3, a normal one needs c beyond 4 sigma.
+constexpr double kMomentCancel = 16.0;
+__device__ inline bool moments_cancel(double n, double S1, double S2) {
+  const double q = S1 * S1 / n;
+  return q > kMomentCancel * (S2 - q);  // (NaN / Inf moments: false, nothing to rescue)
+}
+
+// The workgroup's mean from its waves' (n, mean) (lane 0 of each wave supplies them), merged in
+// wave order; every thread gets the same value.  Called at most once per kernel.
+__device__ inline double block_mean_of_waves(double n_w, double mean_w) {
+  __shared__ double s_n[kBlock / 64], s_m[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) {
+    s_n[threadIdx.x >> 6] = n_w;
+    s_m[threadIdx.x >> 6] = mean_w;
+  }
+  __syncthreads();
+  double n = 0.0, m = 0.0;
+#pragma unroll
+  for (int w = 0; w < kBlock / 64; ++w) {
+    if (s_n[w] > 0.0) {
+      const double nn = n + s_n[w];
+      m += (s_m[w] - m) * (s_n[w] / nn);
+      n = nn;
+    }
+  }
+  return m;
+}
+
 __device__ inline void chunk_of_block(int64_t n_rows, int64_t& row_begin, int64_t& row_end) {
   const int64_t n_chunks = (n_rows + kScanRowAlign - 1) / kScanRowAlign;
   const int64_t per_block = (n_chunks + gridDim.x - 1) / gridDim.x;

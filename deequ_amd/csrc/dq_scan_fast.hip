@@ -59,36 +59,12 @@ __device__ inline double uniform_f64(double v) {  // a wave-uniform double into 
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
-__device__ inline uint32_t ffbh32(uint32_t v) {  // leading zeros, ~0u for 0
-  uint32_t r;
-  asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(v));
-  return r;
-}
-__device__ inline uint32_t add1_sat(uint32_t v) {  // v + 1, clamped at 0xFFFFFFFF
-  uint32_t r;
-  asm("v_add_u32_e64 %0, %1, 1 clamp" : "=v"(r) : "v"(v));
-  return r;
-}
-
-// Register byte offset and rank of the pre-final hash `h` (xxh64_*_dev):
-// x = h ^ (h >> 32), idx = x >>> 55, rank = nlz((x << 9) | W_PADDING) + 1
-// (StatefulHyperloglogPlus.scala:96-99).  w_hi = top word of x << 9; when it is zero the rank
-// needs the low word too, and the marker is returned instead.
-__device__ inline void hll_rank_fast(W64 h, uint32_t& byte_off, uint32_t& rank) {
-  byte_off = (h.hi >> 21) & 0x7fcu;
-  const uint32_t xlo = h.lo ^ h.hi;
-  const uint32_t w_hi = __builtin_amdgcn_alignbit(h.hi, xlo, 23);
-  rank = add1_sat(ffbh32(w_hi));
-}
-
-#ifndef DQ_FAST_MIN_HLL
-#define DQ_FAST_MIN_HLL 1
-#endif
-// The min form of the register update (DQ_FAST_MIN_HLL): a register's rank is nlz(w) + 1 of its
+// The register update in min form: a register's rank is nlz(w) + 1 of its
 // smallest w = (x << 9) | W_PADDING, so the workgroup keeps, per register, the MINIMUM of
 // s = bits 54..24 of x (in bits 30..0; one alignbit and one and from the hash halves) with
 // ds_min_u32, and turns it into a rank once, when folding: rank = nlz32(s) for s != 0 (s = 0:
-// rank >= 32, the exact re-rank below).  That drops the per-row v_ffbh and +1 of the max form.
+// rank >= 32, the exact re-rank below).  No per-row v_ffbh and +1 (the max form measured
+// 12.94 vs 12.93 ms on C2: kept for the shorter instruction stream).
 // An untouched register keeps 0xFFFFFFFF, which no s reaches (bit 31 is clear).
 __device__ inline void hll_key_min(W64 h, uint32_t& byte_off, uint32_t& s) {
   byte_off = (h.hi >> 21) & 0x7fcu;
@@ -115,25 +91,17 @@ __device__ inline bool is_nan_rare(double x) {
   return r != 0u;
 }
 
-__device__ inline void lds_max(uint32_t* regs, uint32_t byte_off, uint32_t v) {
-  __hip_atomic_fetch_max(reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(regs) + byte_off), v,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 __device__ inline void lds_min(uint32_t* regs, uint32_t byte_off, uint32_t v) {
   __hip_atomic_fetch_min(reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(regs) + byte_off), v,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-#ifndef DQ_FAST_MADTRICK
-#define DQ_FAST_MADTRICK 1
-#endif
 // a * C + A (mod 2^64) on 32-bit halves with the cross terms as mul_lo -> mad_u64 (the mad adds
 // the first cross term as its 64-bit addend, whose low half is a scratch register) -> add, i.e.
 // v_mad_u64_u32 + v_mul_lo_u32 + v_mad_u64_u32 + v_add_u32 instead of the compiler's
 // v_mad_u64_u32 + 2 v_mul_lo_u32 + v_add3_u32 (one full-rate add in place of a half-rate add3).
 template <uint64_t C, uint64_t A = 0>
 __device__ inline W64 w64_mul_fast(W64 a) {
-#if DQ_FAST_MADTRICK
   const uint64_t p = (uint64_t)a.lo * (uint32_t)C + A;
   uint32_t hi;
   asm("v_mul_lo_u32 v2, %1, %2\n\t"
@@ -143,9 +111,6 @@ __device__ inline W64 w64_mul_fast(W64 a) {
       : "v"(a.lo), "s"((uint32_t)(C >> 32)), "v"(a.hi), "s"((uint32_t)C), "v"((uint32_t)(p >> 32))
       : "v2", "v3", "vcc");
   return {(uint32_t)p, hi};
-#else
-  return w64_mul<C, A>(a);
-#endif
 }
 
 // xxh64_8_dev (dq_internal.h) with the multiplies above: Spark XXH64.hashLong, seed 42, the hash
@@ -178,7 +143,6 @@ struct FastAcc {
   double s1, s2;       // Σd, Σd² with d = xm - c
   double fs, fc;       // compensated Σxm (fp64): the Sum, stand-ins included (removed at the end)
   double fmin, fmax;   // fp64: of x; int64: of d = x - c (exact, see fast_row), x = d + c at the end
-  uint32_t sel_w;      // wave-uniform: selected rows counted from the bitmap on the scalar unit (SCNT)
   uint64_t pc;         // wave-uniform: Σ over visited rows of cmp(xm) (before negation)
 };
 
@@ -246,17 +210,10 @@ __device__ inline void fast_row(FastAcc& a, uint32_t lo, uint32_t hi, uint32_t m
         hhi = 0x7ff80000u;
       }
     }
-#if DQ_FAST_MIN_HLL
     uint32_t off, s;
     hll_key_min(hash_halves<T>(hlo, hhi), off, s);
     if constexpr (!MEMBER) s |= ~m;  // an unselected row leaves the minimum alone
     lds_min(lregs, off, s);
-#else
-    uint32_t off, rank;
-    hll_rank_fast(hash_halves<T>(hlo, hhi), off, rank);
-    if constexpr (!MEMBER) rank &= m;
-    lds_max(lregs, off, rank);
-#endif
   }
 }
 
@@ -269,29 +226,22 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 #define DQ_FAST_WAVES 1  // amdgpu_waves_per_eu minimum (register budget: 8 -> 64 VGPRs, 6 -> 80)
 #endif
 constexpr int kFastUnroll = DQ_FAST_UNROLL;  // 16-byte loads (2 rows) per lane per iteration
-#ifndef DQ_FAST_PREFETCH
-#define DQ_FAST_PREFETCH 1
-#endif
 
 // Streaming loads of a large pass go non-temporal (aux = 2: the bytes are read once and are far
 // larger than the 256 MiB Infinity Cache; A/B 13.11 vs 13.22 ms on C2); a small table (C1's 10M
 // rows) keeps the default policy, so a repeated pass over it is served from the Infinity Cache
 // (nt there doubled C1's step, 0.5 -> 1.0 ms).
 constexpr int64_t kNtMinRows = (int64_t)1 << 24;  // 128 MiB of 8-byte values per column
-// The loads of iteration `it`: 4 x 16 B of values and the 4 validity bytes of the same rows;
-// with SCNT also, on the scalar unit, the 16 bitmap bytes of each of the wave's 128-row groups,
-// whose popcount is the wave's selected-row count (no per-row VALU op for it).
-typedef const __attribute__((address_space(4))) v4u* BitmapWords;  // s_load_dwordx4 of a uniform index
-
+// The loads of iteration `it`: 4 x 16 B of values and the 4 validity bytes of the same rows.
+// (Counting the selected rows from 16-byte bitmap words on the scalar unit instead of one VALU
+// op per row measured slower: the words cost SGPRs and VGPRs, i.e. occupancy.)
 struct FastLoad {
   v4u vec[kFastUnroll];
   uint32_t vb[kFastUnroll];
-  v4u sw[kFastUnroll];
 };
 
-template <bool SCNT>
-__device__ inline void fast_load(FastLoad& L, __amdgpu_buffer_rsrc_t rv, __amdgpu_buffer_rsrc_t rvalid,
-                                 BitmapWords vwords, uint32_t it, bool nt) {
+__device__ inline void fast_load(FastLoad& L, __amdgpu_buffer_rsrc_t rv, __amdgpu_buffer_rsrc_t rvalid, uint32_t it,
+                                 bool nt) {
   constexpr uint32_t ROWS_PER_ITER = (uint32_t)kBlock * 2 * kFastUnroll;
   const uint32_t tid = threadIdx.x;
 #pragma unroll
@@ -306,15 +256,10 @@ __device__ inline void fast_load(FastLoad& L, __amdgpu_buffer_rsrc_t rv, __amdgp
       L.vec[u] = __builtin_amdgcn_raw_buffer_load_b128(rv, (int)(r0 * 8u), 0, 0);
       L.vb[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rvalid, (int)(r0 >> 3), 0, 0);
     }
-    if constexpr (SCNT) {
-      const uint32_t g = __builtin_amdgcn_readfirstlane((it * ROWS_PER_ITER + (uint32_t)u * kBlock * 2u) / 128u +
-                                                        (tid >> 6));
-      L.sw[u] = vwords[g];
-    }
   }
 }
 
-template <typename T, int PK, bool STATS, bool HLL, bool MEMBER, bool SCNT>
+template <typename T, int PK, bool STATS, bool HLL, bool MEMBER>
 __device__ inline void fast_compute(FastAcc& a, const FastLoad& L, uint32_t no_valid, uint32_t sh_lo, uint32_t sh_hi,
                                     double shift, double cshift, int64_t lit_i, double lit_f, uint32_t* lregs,
                                     uint32_t* s_nan) {
@@ -331,11 +276,8 @@ __device__ inline void fast_compute(FastAcc& a, const FastLoad& L, uint32_t no_v
       m[j] = (uint32_t)__builtin_amdgcn_sbfe((int32_t)bits, bp + (uint32_t)k, 1);
       lo[j] = sel32(L.vec[u][2 * k], m[j], sh_lo);
       hi[j] = sel32(L.vec[u][2 * k + 1], m[j], sh_hi);
-      if constexpr (!SCNT) a.n_sel -= m[j];
+      a.n_sel -= m[j];
     }
-    if constexpr (SCNT)
-      a.sel_w += __builtin_popcount(L.sw[u][0]) + __builtin_popcount(L.sw[u][1]) + __builtin_popcount(L.sw[u][2]) +
-                 __builtin_popcount(L.sw[u][3]);
   }
   double dsum = -0.0;
   // statistics + predicate of all rows first: for fp64 the iteration's Σx tells whether a
@@ -378,34 +320,24 @@ __device__ inline void fast_compute(FastAcc& a, const FastLoad& L, uint32_t no_v
   }
 }
 
-template <typename T, int PK, bool STATS, bool HLL, bool MEMBER, bool SCNT>
+template <typename T, int PK, bool STATS, bool HLL, bool MEMBER>
 __device__ inline void fast_main_loop(FastAcc& a, __amdgpu_buffer_rsrc_t rv, __amdgpu_buffer_rsrc_t rvalid,
-                                      BitmapWords vwords,
                                       uint32_t no_valid, uint32_t full_iters, uint32_t sh_lo, uint32_t sh_hi,
                                       double shift, double cshift, int64_t lit_i, double lit_f, uint32_t* lregs,
                                       uint32_t* s_nan, bool nt) {
-#if DQ_FAST_PREFETCH
   // two-stage pipeline: iteration it + 1's loads are in flight while iteration it computes
   // (two register sets, the loop unrolled by two so no copies are needed)
   FastLoad A, B;
   uint32_t it = 0;
-  if (full_iters > 0) fast_load<SCNT>(A, rv, rvalid, vwords, 0, nt);
+  if (full_iters > 0) fast_load(A, rv, rvalid, 0, nt);
 #pragma unroll 1
   for (; it + 1 < full_iters; it += 2) {
-    fast_load<SCNT>(B, rv, rvalid, vwords, it + 1, nt);
-    fast_compute<T, PK, STATS, HLL, MEMBER, SCNT>(a, A, no_valid, sh_lo, sh_hi, shift, cshift, lit_i, lit_f, lregs, s_nan);
-    fast_load<SCNT>(A, rv, rvalid, vwords, it + 2, nt);
-    fast_compute<T, PK, STATS, HLL, MEMBER, SCNT>(a, B, no_valid, sh_lo, sh_hi, shift, cshift, lit_i, lit_f, lregs, s_nan);
+    fast_load(B, rv, rvalid, it + 1, nt);
+    fast_compute<T, PK, STATS, HLL, MEMBER>(a, A, no_valid, sh_lo, sh_hi, shift, cshift, lit_i, lit_f, lregs, s_nan);
+    fast_load(A, rv, rvalid, it + 2, nt);
+    fast_compute<T, PK, STATS, HLL, MEMBER>(a, B, no_valid, sh_lo, sh_hi, shift, cshift, lit_i, lit_f, lregs, s_nan);
   }
-  if (it < full_iters) fast_compute<T, PK, STATS, HLL, MEMBER, SCNT>(a, A, no_valid, sh_lo, sh_hi, shift, cshift, lit_i, lit_f, lregs, s_nan);
-#else
-#pragma unroll 1
-  for (uint32_t it = 0; it < full_iters; ++it) {
-    FastLoad L;
-    fast_load<SCNT>(L, rv, rvalid, vwords, it, nt);
-    fast_compute<T, PK, STATS, HLL, MEMBER, SCNT>(a, L, no_valid, sh_lo, sh_hi, shift, cshift, lit_i, lit_f, lregs, s_nan);
-  }
-#endif
+  if (it < full_iters) fast_compute<T, PK, STATS, HLL, MEMBER>(a, A, no_valid, sh_lo, sh_hi, shift, cshift, lit_i, lit_f, lregs, s_nan);
   a.n_rows += full_iters * kFastUnroll * 2;
 }
 
@@ -445,7 +377,6 @@ __device__ inline void fast_acc_init(FastAcc& a) {
   a.fs = a.fc = 0.0;
   a.fmin = __builtin_huge_val();
   a.fmax = -__builtin_huge_val();
-  a.sel_w = 0u;
   a.pc = 0u;
 }
 
@@ -467,7 +398,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DQ_FAST_
   __shared__ uint32_t lflag[kHllM / 32];
   __shared__ uint32_t s_nan;  // a selected NaN seen (fp64 statistics)
   if constexpr (HLL) {
-    for (int r = threadIdx.x; r < kHllM; r += kBlock) lregs[r] = DQ_FAST_MIN_HLL ? 0xFFFFFFFFu : 0u;
+    for (int r = threadIdx.x; r < kHllM; r += kBlock) lregs[r] = 0xFFFFFFFFu;
   }
   if (threadIdx.x == 0) s_nan = 0u;
   __syncthreads();
@@ -544,26 +475,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DQ_FAST_
   fast_acc_init(a);
   constexpr uint32_t ROWS_PER_ITER = (uint32_t)kBlock * 2u * kFastUnroll;
   const uint32_t full_iters = span / ROWS_PER_ITER;
-  // the wave's selected rows are counted from 16-byte bitmap words on the scalar unit when the
-  // chunk's bitmap is dword aligned (Arrow buffers are; a sliced device column may not be)
-  const BitmapWords vwords = (BitmapWords)(uintptr_t)(has_valid ? col.validity + (row_begin >> 3) : nullptr);
-#ifndef DQ_FAST_SCNT
-#define DQ_FAST_SCNT 0  // measured slower: the bitmap words cost SGPRs and VGPRs (occupancy)
-#endif
-  const bool scnt = DQ_FAST_SCNT && has_valid && (((uintptr_t)vwords & 3u) == 0u);
-  if (member && scnt) {
-    fast_main_loop<T, PK, STATS, HLL, true, true>(a, rv, rvalid, vwords, no_valid, full_iters, sh_lo, sh_hi, shift,
-                                                  cshift, lit_i, lit_f, lregs, &s_nan, nt);
-    fast_tail<T, PK, STATS, HLL, true>(a, rv, rvalid, no_valid, full_iters * ROWS_PER_ITER, span, sh_lo, sh_hi,
-                                       shift, cshift, lit_i, lit_f, lregs, &s_nan);
-  } else if (member) {
-    fast_main_loop<T, PK, STATS, HLL, true, false>(a, rv, rvalid, vwords, no_valid, full_iters, sh_lo, sh_hi, shift,
-                                                   cshift, lit_i, lit_f, lregs, &s_nan, nt);
+  if (member) {
+    fast_main_loop<T, PK, STATS, HLL, true>(a, rv, rvalid, no_valid, full_iters, sh_lo, sh_hi, shift, cshift, lit_i,
+                                            lit_f, lregs, &s_nan, nt);
     fast_tail<T, PK, STATS, HLL, true>(a, rv, rvalid, no_valid, full_iters * ROWS_PER_ITER, span, sh_lo, sh_hi,
                                        shift, cshift, lit_i, lit_f, lregs, &s_nan);
   } else {
-    fast_main_loop<T, PK, STATS, HLL, false, false>(a, rv, rvalid, vwords, no_valid, full_iters, sh_lo, sh_hi,
-                                                    shift, cshift, lit_i, lit_f, lregs, &s_nan, nt);
+    fast_main_loop<T, PK, STATS, HLL, false>(a, rv, rvalid, no_valid, full_iters, sh_lo, sh_hi, shift, cshift, lit_i,
+                                             lit_f, lregs, &s_nan, nt);
     fast_tail<T, PK, STATS, HLL, false>(a, rv, rvalid, no_valid, full_iters * ROWS_PER_ITER, span, sh_lo, sh_hi,
                                         shift, cshift, lit_i, lit_f, lregs, &s_nan);
   }
@@ -601,12 +520,57 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DQ_FAST_
     }
   }
 
+  // The moments' cancellation guard (moments_cancel, dq_scan_common.h): a wave whose shift was an
+  // outlier makes the workgroup redo Σd, Σd² of its chunk about the chunk's mean.  The re-run's
+  // stand-in for unselected rows is that mean itself (as int64 bits / fp64 bits), so their d is
+  // exactly 0; its min / max are not used (they saw the stand-in).
+  const bool lane0 = lane == 0;
+  double mom_shift = (INT_STATS && exact_stats) ? (found_any ? shift_any : 0.0) : shift;
+  uint64_t mom_w = 0u;  // lane 0: the wave's rows behind S1, S2
+  double S1 = 0.0, S2 = 0.0;
+  if constexpr (STATS) {
+    mom_w = wave_sum_u64(mom_sel);
+    S1 = wave_sum_f64(a.s1);
+    S2 = wave_sum_f64(a.s2);
+    double wn = 0.0, wmean = 0.0;
+    bool cancel = false;
+    if (lane0 && mom_w > 0) {
+      wn = (double)mom_w;
+      wmean = mom_shift + S1 / wn;
+      cancel = moments_cancel(wn, S1, S2);
+    }
+    if (__syncthreads_or(cancel)) {
+      const double m = block_mean_of_waves(wn, wmean);
+      if (fabs(m) < (FP ? 0x1p1000 : 0x1p62)) {
+        uint32_t m_lo, m_hi;
+        double m_shift;
+        if constexpr (FP) {
+          m_shift = m;
+          const uint64_t b = __builtin_bit_cast(uint64_t, m);
+          m_lo = (uint32_t)b;
+          m_hi = (uint32_t)(b >> 32);
+        } else {
+          const uint64_t b = (uint64_t)(int64_t)rint(m);
+          m_lo = (uint32_t)b;
+          m_hi = (uint32_t)(b >> 32);
+          m_shift = i64_to_f64(m_lo, m_hi);  // what the re-run converts a stand-in row to
+        }
+        FastAcc e;
+        fast_acc_init(e);
+        fast_tail<T, PK_NONE, true, false, true, true>(e, rv, rvalid, no_valid, 0u, span, m_lo, m_hi, m_shift, cshift,
+                                                       lit_i, lit_f, lregs, &s_nan);
+        mom_shift = m_shift;
+        mom_w = wave_sum_u64(e.n_sel);
+        S1 = wave_sum_f64(e.s1);
+        S2 = wave_sum_f64(e.s2);
+      }
+    }
+  }
+
   if constexpr (HLL) {
     __syncthreads();
-#if DQ_FAST_MIN_HLL
     for (int r = threadIdx.x; r < kHllM; r += kBlock) lregs[r] = hll_min_to_rank(lregs[r]);
     __syncthreads();
-#endif
     // Registers holding the marker: re-rank them exactly over this workgroup's rows (rare).
     bool mine = false;
     if (threadIdx.x < kHllM / 32) lflag[threadIdx.x] = 0u;
@@ -647,17 +611,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DQ_FAST_
 
   // ---- lane accumulators -> the block's ScanAcc partial (same layout as dq_scan_values_kernel;
   // block_reduce_store sums / merges the lanes, so lane 0 carries the wave-level terms)
-  const bool lane0 = lane == 0;
   const uint64_t rows_w = wave_sum_u64(a.n_rows);  // lane 0
-  const uint64_t sel_w = wave_sum_u64(a.n_sel) + a.sel_w;  // lane 0 (lane counts + scalar counts)
+  const uint64_t sel_w = wave_sum_u64(a.n_sel);    // lane 0
   const uint64_t unsel_w = rows_w - sel_w;
-  const uint64_t mom_w = exact_stats ? wave_sum_u64(mom_sel) : sel_w;  // lane 0
   const uint64_t sh_bits = ((uint64_t)sh_hi << 32) | sh_lo;
   uint64_t isum = 0u;
   double mean = 0.0, m2 = 0.0, fs = 0.0, fc = 0.0;
   if constexpr (STATS) {
-    const double S1 = wave_sum_f64(a.s1);  // lane 0
-    const double S2 = wave_sum_f64(a.s2);
     isum = a.isum;
     fs = a.fs;
     fc = a.fc;
@@ -665,7 +625,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DQ_FAST_
       if constexpr (!FP) isum -= unsel_w * sh_bits;  // the stand-in copies of unselected rows (wrapping)
       if (mom_w > 0) {
         const double n = (double)mom_w;
-        mean = (exact_stats ? (found_any ? shift_any : 0.0) : shift) + S1 / n;
+        mean = mom_shift + S1 / n;
         m2 = S2 - S1 * S1 / n;
         m2 = (m2 < 0.0) ? 0.0 : m2;  // rounding; NaN/Inf propagate
       }

@@ -143,6 +143,18 @@ def merge_scan_results(local, error, kinds, group=None):
     return out
 
 
+def agree(error: Optional[BaseException], what: str, group=None) -> None:
+    """Every rank learns whether any rank's local step failed (collective), before the next data
+    collective: a failed rank re-raises its own error, the others raise naming the step, so no
+    rank is left blocked in a collective its peer never enters (the all-fail scope of
+    AnalysisRunner.scala:320-323 over the ranks)."""
+    failed = allreduce_flag(error is not None, group)
+    if error is not None:
+        raise error
+    if failed:
+        raise L.DeequAmdError(L.DQ_ERR_STATE, "%s failed on another rank" % what)
+
+
 def allreduce_flag(flag: bool, group=None) -> bool:
     """True on every rank if `flag` is true on any rank (collective)."""
     import torch
@@ -184,11 +196,16 @@ def exchange_frequencies(table, group=None):
     dev = table.torch_device
     comm = dev if _comm_device(group) == "cuda" else torch.device("cpu")
     W = table.WIRE_BYTES
-    part_g, part_k = table.partition_sizes(world)
-    send_g = torch.empty(max(1, sum(part_g)) * W, dtype=torch.uint8, device=dev)
-    send_k = torch.empty(max(8, sum(part_k)), dtype=torch.uint8, device=dev)
-    if sum(part_g):
-        table.partition_into(world, send_g, send_k)
+    part_g, part_k, err = [0] * world, [0] * world, None
+    try:
+        part_g, part_k = table.partition_sizes(world)
+        send_g = torch.empty(max(1, sum(part_g)) * W, dtype=torch.uint8, device=dev)
+        send_k = torch.empty(max(8, sum(part_k)), dtype=torch.uint8, device=dev)
+        if sum(part_g):
+            table.partition_into(world, send_g, send_k)
+    except Exception as e:  # noqa: BLE001 -- agreed on below, then re-raised
+        err = e
+    agree(err, "partitioning the frequency table by owner", group)
     sizes = torch.tensor([[g, k] for g, k in zip(part_g, part_k)], dtype=torch.int64).reshape(-1).to(comm)
     recv_sizes = torch.empty_like(sizes)
     dist.all_to_all_single(recv_sizes, sizes, group=group)
@@ -204,14 +221,19 @@ def exchange_frequencies(table, group=None):
     if comm.type == "cuda":
         torch.cuda.current_stream(dev).synchronize()  # the library reads them on its own stream
     recv_g, recv_k = _to(recv_g, dev), _to(recv_k, dev)
-    owned = type(table).like(table)
-    og = ok = 0
-    for s in range(world):
-        n = recv[s][0]
-        if n:
-            owned.import_wire(recv_g[og:og + n * W], n, recv_k[ok:ok + max(1, recv[s][1])], recv[s][1], 0)
-        og += n * W
-        ok += recv[s][1]
+    owned, err = None, None
+    try:
+        owned = type(table).like(table)
+        og = ok = 0
+        for s in range(world):
+            n = recv[s][0]
+            if n:
+                owned.import_wire(recv_g[og:og + n * W], n, recv_k[ok:ok + max(1, recv[s][1])], recv[s][1], 0)
+            og += n * W
+            ok += recv[s][1]
+    except Exception as e:  # noqa: BLE001
+        err = e
+    agree(err, "merging the received frequency parts", group)
     return owned
 
 
@@ -309,10 +331,17 @@ def compute_frequencies_distributed(data, grouping_columns, histogram: bool = Fa
     from .frequencies import FrequencyTable
     make = table_factory or FrequencyTable
     schema = data.schema
-    local = make(grouping_columns, {c: schema[c] for c in schema}, histogram)
-    for batch in data.batches():
-        local.consume(batch)
-    n_local = local.summary().num_rows
+    local, n_local, err = None, 0, None
+    try:
+        local = make(grouping_columns, {c: schema[c] for c in schema}, histogram)
+        for batch in data.batches():
+            local.consume(batch)
+        n_local = local.summary().num_rows
+    except Exception as e:  # noqa: BLE001 -- every rank fails together (agree)
+        err = e
+    if err is not None and local is not None:
+        local.close()
+    agree(err, "the frequency group-by", group)
     owned = exchange_frequencies(local, group)
     local.close()
     n = torch.tensor([n_local], dtype=torch.int64)

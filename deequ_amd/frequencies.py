@@ -225,6 +225,12 @@ class FrequencyTable:
         import torch
         return torch.device("cuda", self.device)
 
+    def paths(self) -> Dict[str, int]:
+        """Which group-by paths this table's groupings took (dq_diag_freq_paths; tests)."""
+        out = (ctypes.c_int64 * 4)()
+        L.check(L.lib().dq_diag_freq_paths(self.handle, out))
+        return {"slots": out[0], "partition_runs": out[1], "slice_bits": out[2], "sort_records": out[3]}
+
     def merge_from(self, other: "FrequencyTable") -> None:
         """self += other, device to device."""
         L.check(L.lib().dq_freq_merge(self.handle, other.handle))

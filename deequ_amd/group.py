@@ -56,6 +56,24 @@ class DqGroup:
         L.check(L.lib().dq_group_freq_summary(self.handle, owned.handle, int(num_rows), ctypes.byref(s)))
         return s
 
+    def freq_top(self, owned, n: int):
+        """Histogram's top-n over the dataset from the owned tables (collective): (counts, keys),
+        count descending then key ascending, ties at the cut kept -- FrequencyTable.top's
+        contract over the union of the ranks' rows."""
+        from .frequencies import _unpack_groups
+        cap_g, cap_k = max(16, 2 * n), max(4096, 64 * n)
+        while True:
+            groups = (L.DqFreqGroup * cap_g)()
+            keys = ctypes.create_string_buffer(cap_k)
+            got, kb = ctypes.c_int64(), ctypes.c_int64()
+            st = L.lib().dq_group_freq_top(self.handle, owned.handle, int(n), groups, cap_g, keys, cap_k,
+                                           ctypes.byref(got), ctypes.byref(kb))
+            if st == L.DQ_ERR_SPACE:  # (the same sizes on every rank: every rank retries)
+                cap_g, cap_k = max(cap_g, got.value), max(cap_k, kb.value)
+                continue
+            L.check(st)
+            return _unpack_groups(groups, got.value, keys.raw)
+
     def close(self) -> None:
         if self.handle:
             L.lib().dq_group_destroy(self.handle)

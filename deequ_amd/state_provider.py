@@ -152,33 +152,52 @@ class HdfsStateProvider:
             raise ValueError("Unable to persist state for analyzer %s." % analyzer)
 
     def _persist_frequencies(self, ident: str, state) -> None:
-        import pyarrow as pa
-        import pyarrow.parquet as pq
-        from .javafmt import spark_cast_to_string
+        from .distributed import DistributedFrequencies
         directory = self._path(ident, "-frequencies.pqt")
+        if isinstance(state, DistributedFrequencies):
+            self._persist_frequencies_sharded(ident, directory, state)
+            return
         if os.path.exists(directory):
             if not self.allowOverwrite:
                 raise FileExistsError("path %s already exists." % directory)
             shutil.rmtree(directory)
-        table = state.table
-        freqs = state.frequencies()
-        columns = list(table.key_columns)
-        if table.histogram:  # Histogram's state groups the column cast to string (Histogram.scala:63-66)
-            dtype = table.dtypes[0]
-            names, types = columns, ["string"]
-            rows = [((("NullValue" if k[0] is None else (k[0] if dtype == "string" else
-                                                         spark_cast_to_string(k[0], dtype))),), c)
-                    for k, c in freqs.items()]
-        else:
-            names, types = columns, list(table.dtypes)
-            rows = list(freqs.items())
-        arrays = [pa.array([r[0][i] for r in rows], type=getattr(pa, _PA_TYPES[t])()) for i, t in enumerate(types)]
-        arrays.append(pa.array([r[1] for r in rows], type=pa.int64()))
         os.makedirs(directory)
-        count_col = HISTOGRAM_COUNT_COL if table.histogram else COUNT_COL
-        pq.write_table(pa.Table.from_arrays(arrays, names=names + [count_col]),
-                       os.path.join(directory, "part-00000.snappy.parquet"))
+        _write_frequency_part(os.path.join(directory, "part-00000.snappy.parquet"), state.table, state.frequencies())
         self._write(self._path(ident, "-num_rows.bin"), struct.pack(">q", state.numRows))
+
+    def _persist_frequencies_sharded(self, ident: str, directory: str, state) -> None:
+        """A frequency state held by the ranks of a process group (each owns disjoint keys after
+        the key-hash exchange) is written as the reference's Spark job writes its partitions:
+        rank r writes part-%05d with the groups it owns, rank 0 the numRows file -- no rank
+        gathers the table (StateProvider.scala:222-240 writes the state DataFrame partition by
+        partition).  Collective; the ranks share the filesystem (one node)."""
+        import torch.distributed as dist
+        from .distributed import agree, allreduce_flag
+        from .frequencies import decode_key
+        group = state.group
+        rank = dist.get_rank(group)
+        exists = rank == 0 and os.path.exists(directory)
+        if allreduce_flag(exists and not self.allowOverwrite, group):
+            raise FileExistsError("path %s already exists." % directory)
+        err = None
+        if rank == 0:
+            try:
+                if exists:
+                    shutil.rmtree(directory)
+                os.makedirs(directory)
+            except Exception as e:  # noqa: BLE001 -- agreed on, then re-raised
+                err = e
+        agree(err, "creating %s" % directory, group)
+        try:
+            owned = state.owned
+            counts, keys = owned.export()
+            freqs = {decode_key(k, owned.dtypes, owned.histogram): int(c) for k, c in zip(keys, counts.tolist())}
+            _write_frequency_part(os.path.join(directory, "part-%05d.snappy.parquet" % rank), state.table, freqs)
+            if rank == 0:
+                self._write(self._path(ident, "-num_rows.bin"), struct.pack(">q", state.numRows))
+        except Exception as e:  # noqa: BLE001
+            err = e
+        agree(err, "writing the frequency state's parts", group)
 
     # ------------------------------------------------------------ load
     def load(self, analyzer):
@@ -240,6 +259,28 @@ class HdfsStateProvider:
             freqs[key] = freqs.get(key, 0) + int(c)
         return FrequenciesAndNumRows.from_frequencies(names, dtypes, freqs, num_rows,
                                                       histogram=isinstance(analyzer, Histogram))
+
+
+def _write_frequency_part(path: str, table, freqs: Dict[tuple, int]) -> None:
+    """One parquet part of a frequency state: the grouping columns + the count column (Histogram:
+    the column cast to string, Histogram.scala:63-66, NULL -> "NullValue")."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from .javafmt import spark_cast_to_string
+    columns = list(table.key_columns)
+    if table.histogram:
+        dtype = table.dtypes[0]
+        names, types = columns, ["string"]
+        rows = [((("NullValue" if k[0] is None else (k[0] if dtype == "string" else
+                                                     spark_cast_to_string(k[0], dtype))),), c)
+                for k, c in freqs.items()]
+    else:
+        names, types = columns, list(table.dtypes)
+        rows = list(freqs.items())
+    arrays = [pa.array([r[0][i] for r in rows], type=getattr(pa, _PA_TYPES[t])()) for i, t in enumerate(types)]
+    arrays.append(pa.array([r[1] for r in rows], type=pa.int64()))
+    count_col = HISTOGRAM_COUNT_COL if table.histogram else COUNT_COL
+    pq.write_table(pa.Table.from_arrays(arrays, names=names + [count_col]), path)
 
 
 def _concat(tables):

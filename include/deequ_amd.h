@@ -467,7 +467,10 @@ dq_status dq_group_allgather_merge(dq_group* g, dq_state* states, int n_ops);
  * (State.sum per kind, Analyzer.scala:367-386; e.g. StandardDeviation.scala:37-44). */
 dq_status dq_states_merge_ranks(const dq_state* gathered, int n_ranks, int n_ops, dq_state* out);
 
-/* The key-hash exchange: every rank partitions `local` by owner (dq_freq_partition), the parts
+/* Every dq_group_* call is collective; a failure of any rank's local step fails the call on
+ * every rank (agreed on before data moves), so no rank is left blocked in a collective.
+ *
+ * The key-hash exchange: every rank partitions `local` by owner (dq_freq_partition), the parts
  * travel in one RCCL all-to-all (grouped send/recv), and each rank merges what it receives into
  * `owned` (an empty table with the same key columns) -- which then holds the keys this rank owns,
  * disjoint across ranks.  *num_rows = the dataset's numRows (sum over ranks). */
@@ -477,6 +480,14 @@ dq_status dq_group_freq_exchange(dq_group* g, dq_freq* local, dq_freq* owned, in
  * all-reduced (sum) over RCCL, counts beyond the histogram all-gathered, then the fixed-order
  * dq_freq_summary_from_histogram -- equal, bit for bit, to a single table over all rows. */
 dq_status dq_group_freq_summary(dq_group* g, dq_freq* owned, int64_t num_rows, dq_freq_summary* out);
+
+/* Histogram's top-maxDetailBins over the whole dataset (Histogram.scala:78-79, rdd.top + the
+ * groupBy's exchange): the union of every owner's dq_freq_top(owned, n), cut at the n-th largest
+ * count with all ties kept, count descending then encoded key ascending -- dq_freq_top's contract
+ * over the union of the ranks' rows.  Same buffer protocol as dq_freq_top: on DQ_ERR_SPACE
+ * *n_out / *key_bytes_out hold the sizes and every rank retries with larger buffers. */
+dq_status dq_group_freq_top(dq_group* g, dq_freq* owned, int n, dq_freq_group* groups, int64_t max_groups,
+                            uint8_t* key_bytes, int64_t key_cap, int64_t* n_out, int64_t* key_bytes_out);
 
 #ifdef __cplusplus
 }

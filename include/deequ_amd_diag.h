@@ -20,6 +20,12 @@ extern "C" {
  * (hashes per second, best launch) to *hashes_per_sec. */
 dq_status dq_diag_hash_rate(int device, int with_hll, int reps, double* hashes_per_sec);
 
+/* Aggregates what `f` has staged, then reports which paths its groupings took (tests assert
+ * that a workload exercised the path it is meant to): out[0] = table slots (2048 per slice),
+ * out[1] = partition-path aggregations, out[2] = hash bits (log2 slices) of the last one,
+ * out[3] = records that went through the sort path (small stagings, retries, skew fallbacks). */
+dq_status dq_diag_freq_paths(dq_freq* f, int64_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -196,6 +196,59 @@ def test_run_on_aggregated_states_over_gpu_states(gpu):
     assert partial.metric(d.Sum("i")).value.get() == first.metric(d.Sum("i")).value.get()
 
 
+def test_run_on_aggregated_states_vs_oracle(gpu):
+    """runOnAggregatedStates over GPU-computed partition states against the ORACLE's states of
+    the same partitions merged with `Analyzers.merge` (Analyzer.scala:367-386, State.sum of each
+    state class; oracle.merge_options), in the same partition order.  Bit-exact for counts,
+    integral sums, Min/Max, HLL counts and the frequency metrics; fp64 within 1e-12."""
+    rng = np.random.default_rng(29)
+    n = 24000
+    spec = {"i": ["int64", [None if rng.random() < 0.05 else int(x) for x in rng.integers(-1000, 10 ** 6, n)]],
+            "f": ["float64", [None if rng.random() < 0.05 else float(x) for x in rng.normal(5e2, 50, n)]],
+            "s": ["string", [None if rng.random() < 0.02 else "k%d" % x for x in rng.integers(0, 4000, n)]]}
+    analyzers = [d.Size(), d.Completeness("i"), d.Compliance("pos", "i >= 0"), d.Sum("i"), d.Mean("f"),
+                 d.StandardDeviation("f"), d.Minimum("i"), d.Maximum("f"), d.ApproxCountDistinct("s"),
+                 d.ApproxCountDistinct("i"), d.Uniqueness(["s"]), d.Distinctness(["s"]), d.Entropy("s"),
+                 d.CountDistinct(["s"]), d.UniqueValueRatio(["s"])]
+    cuts = [0, 5003, 5004, 16000, n]
+    providers, parts = [], []
+    for a0, b0 in zip(cuts, cuts[1:]):
+        sub = {k: [t, v[a0:b0]] for k, (t, v) in spec.items()}
+        prov = d.InMemoryStateProvider()
+        d.AnalysisRunner.onData(product_table(sub)).addAnalyzers(analyzers).saveStatesWith(prov).run()
+        providers.append(prov)
+        parts.append(oracle_table(sub))
+    schema = {"i": "int64", "f": "float64", "s": "string"}
+    agg = d.AnalysisRunner.runOnAggregatedStates(schema, d.Analysis(analyzers), providers)
+
+    def merged(fn, *args):
+        return O.merge_options(*[fn(p, *args) for p in parts])
+
+    want = {
+        d.Size(): merged(O.size_state).metric_value(),
+        d.Completeness("i"): merged(O.completeness_state, "i").metric_value(),
+        d.Compliance("pos", "i >= 0"): merged(O.compliance_state, "i >= 0").metric_value(),
+        d.Sum("i"): merged(O.sum_state, "i").metric_value(),
+        d.Minimum("i"): merged(O.min_state, "i").metric_value(),
+        d.Maximum("f"): merged(O.max_state, "f").metric_value(),
+        d.ApproxCountDistinct("s"): merged(O.approx_count_distinct_state, "s").metric_value(),
+        d.ApproxCountDistinct("i"): merged(O.approx_count_distinct_state, "i").metric_value(),
+    }
+    freq = merged(O.frequencies_state, ["s"])
+    want[d.Uniqueness(["s"])] = O.uniqueness_metric(freq)
+    want[d.Distinctness(["s"])] = O.distinctness_metric(freq)
+    want[d.CountDistinct(["s"])] = O.count_distinct_metric(freq)
+    want[d.UniqueValueRatio(["s"])] = O.unique_value_ratio_metric(freq)
+    close = {d.Mean("f"): merged(O.mean_state, "f").metric_value(),
+             d.StandardDeviation("f"): merged(O.stddev_state, "f").metric_value(),
+             d.Entropy("s"): O.entropy_exact(freq)}
+    for a, w in want.items():
+        assert agg.metric(a).value.get() == w, (a, agg.metric(a).value.get(), w)
+    for a, w in close.items():
+        got = agg.metric(a).value.get()
+        assert abs(got - w) <= 1e-12 * abs(w), (a, got, w)
+
+
 class _ExtractionFailingMean(d.Mean):
     """AnalysisTest.scala:228-253: fromAggregationResult throws."""
 

@@ -127,9 +127,42 @@ def _run(world, bad_rank):
     return results
 
 
+def _oracle_metrics(d):
+    """The oracle's metric of every analyzer with an oracle restatement, over the whole table."""
+    from helpers import oracle_metric, oracle_state, oracle_table
+    ot = oracle_table(_spec(0, N))
+    out = {}
+    for a in _analyzers(d):
+        name = type(a).__name__
+        if name in ("Size",):
+            args = [a.where]
+        elif name == "Compliance":
+            args = [a.instance_name, a.predicate, a.where]
+        elif name == "Correlation":
+            args = [a.firstColumn, a.secondColumn, a.where]
+        elif name == "Entropy":
+            args = [a.column]
+        elif name in ("Uniqueness", "Distinctness", "CountDistinct", "UniqueValueRatio"):
+            args = [list(a.columns)]
+        elif name in ("Histogram", "DataType"):
+            continue
+        else:
+            args = [a.column, a.where]
+        out[str(a)] = oracle_metric(oracle_state(name, args, ot), name, args)
+    return out
+
+
 def test_sharded_runner_and_profiler_equal_whole_table(gpu):
+    import deequ_amd as d
     res = _run(2, False)
     whole = res[0]["whole"]
+    # the sharded result against the ORACLE too, not only against the one-rank GPU run
+    for name, want in _oracle_metrics(d).items():
+        got = res[0]["metrics"][name]
+        if want == "failure":
+            assert got[0] == "failure", (name, got)
+        else:
+            assert _close(got, want), (name, got, want)
     for r in (0, 1):
         assert res[r]["count"] == N
         assert res[r]["metrics"] == res[0]["metrics"]  # every rank holds the same metrics
@@ -186,6 +219,9 @@ def test_c_abi_group_world_one(gpu):
         counts, keys = owned.export()
         c2, k2 = local.export()
         assert dict(zip(keys, counts.tolist())) == dict(zip(k2, c2.tolist()))
+        tc, tk = g.freq_top(owned, 7)
+        lc, lk = local.top(7)
+        assert tc.tolist() == lc.tolist() and tk == lk
         local.close()
         owned.close()
     finally:

@@ -170,3 +170,32 @@ def test_oracle_profiles_known_answers(case):
     if e["kind"] == "numeric":
         for f in ("mean", "maximum", "minimum", "sum", "stdDev"):
             assert p[f] == e[f], (case["source"], f)
+
+
+@pytest.mark.parametrize("dtype", ["int64", "float64", "string"])
+def test_c_oracle_hll_registers_equal_python_oracle(dtype):
+    """The C restatement's HLL registers (oracle/dq_oracle.c, used by the large GPU parity
+    tests) == the Python oracle's, NULLs skipped, NaN / -0.0 / empty strings included."""
+    import numpy as np
+    import cdq_oracle as C
+    rnd = random.Random(7)
+    n = 4000
+    if dtype == "int64":
+        vals = [rnd.getrandbits(64) - (1 << 63) for _ in range(n)]
+    elif dtype == "float64":
+        vals = [rnd.uniform(-1e6, 1e6) for _ in range(n)] + [float("nan"), -0.0, 0.0, math.inf]
+    else:
+        vals = ["%016x" % rnd.getrandbits(64) for _ in range(n)] + ["", "é", "a" * 70]
+    valid = [rnd.random() >= 0.1 for _ in vals]
+    bitmap = np.packbits(np.array(valid, dtype=bool), bitorder="little")
+    bitmap = np.concatenate([bitmap, np.zeros(8, np.uint8)])
+    if dtype == "string":
+        data = [v.encode() for v in vals]
+        offs = np.zeros(len(data) + 1, dtype=np.int32)
+        np.cumsum([len(b) for b in data], out=offs[1:])
+        buf = np.frombuffer(b"".join(data) + b"\0" * 8, dtype=np.uint8)
+        regs = C.hll_registers("string", buf, bitmap, offs)
+    else:
+        regs = C.hll_registers(dtype, np.array(vals, dtype=np.int64 if dtype == "int64" else np.float64), bitmap)
+    want = O.hll_registers([v for v, ok in zip(vals, valid) if ok], dtype)
+    assert regs.tolist() == list(want)
