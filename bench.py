@@ -391,17 +391,40 @@ def _column_bytes(col) -> float:
     return float(n * col.values.element_size()) + valid
 
 
+def kernel_source_digest() -> str:
+    """sha256 (16 hex) of the library's sources (deequ_amd/csrc, include/): the build a PMC
+    traffic file was collected on must have exactly these kernels for its bytes to be quoted."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "deequ_amd", "csrc", "*")) + glob.glob(os.path.join(ROOT, "include", "*.h")))
+    for f in files:
+        if os.path.isfile(f) and not f.endswith((".o", ".so")):
+            h.update(os.path.relpath(f, ROOT).encode())
+            with open(f, "rb") as fh:
+                h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def _pmc_traffic(workload: str):
-    """HBM bytes per step of `workload` at its default size, from the PMC pass committed under
+    """HBM bytes per step of `workload` at its default size, from a PMC pass committed under
     profiles/ (tools/pmc_traffic.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE of this same bench,
     read = 2 x FETCH_SIZE on gfx950).  Counters cannot be read inside an unprofiled run, so this
-    is a COPIED profile value, labelled as such in the line (traffic_source); None if absent."""
-    path = os.path.join(ROOT, "profiles", "r02_traffic_%s_r02.json" % workload)
-    try:
-        with open(path) as f:
-            return json.load(f)["hbm_bytes_per_step"], os.path.relpath(path, ROOT)
-    except Exception:  # noqa: BLE001
-        return None, None
+    is a COPIED profile value, labelled as such in the line (traffic_source).  Only a file whose
+    `kernel_src_digest` equals this tree's kernel_source_digest() is used: traffic measured on
+    other kernels is never quoted (None, with the reason in traffic_source)."""
+    import glob
+    digest = kernel_source_digest()
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic_%s*.json" % workload)), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except Exception:  # noqa: BLE001
+            continue
+        if d.get("kernel_src_digest") == digest:
+            return d["hbm_bytes_per_step"], "copied from %s (PMC pass of this bench at its default size, kernel " \
+                "sources %s)" % (os.path.relpath(path, ROOT), digest)
+    return None, "null: no PMC traffic file in profiles/ was collected on these kernel sources (%s)" % digest
 
 
 def _step_roofline(bytes_per_step: float, step_s: float, what: str, traffic=None, workload=None,
@@ -414,7 +437,7 @@ def _step_roofline(bytes_per_step: float, step_s: float, what: str, traffic=None
            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel_ms": step_s * 1e3,
            "algorithmic_bytes_per_launch": bytes_per_step, "timed_unit": what}
     if src:
-        out["traffic_source"] = "copied from %s (PMC pass of this bench at its default size)" % src
+        out["traffic_source"] = src
     return out
 
 
@@ -618,13 +641,14 @@ def run_c5(args, world, rank, local):
     n_hist = sum(1 for c in p.values() if c.histogram is not None)
     step_s = elapsed / args.steps
     cols = shard.columns
+    # pass 1 reads every column once: Completeness, HLL, DataType and -- for schema-numeric columns
+    # -- the statistics too (profiles.py computes them in pass 1's fused scan, never re-reading)
     pass1 = sum(_column_bytes(c) for c in cols.values())
-    numeric = [n for n, c in cols.items() if c.dtype in ("int64", "float64")]
     cast = [n for n, c in cols.items() if c.dtype == "string" and p[n].dataType in (1, 2)]
     rows = args.c5_rows
-    # pass 2: numeric columns + each cast string column read once, cast written (8 B + bit) and scanned
-    pass2 = sum(_column_bytes(cols[n]) for n in numeric) + sum(_column_bytes(cols[n]) + 2 * rows * (8 + 1 / 8.0)
-                                                                for n in cast)
+    # pass 2 reads only the strings pass 1 typed numeric: the cast kernel reads the string column
+    # and writes 8 B + a validity bit per row, the statistics scan reads that back
+    pass2 = sum(_column_bytes(cols[n]) + 2 * rows * (8 + 1 / 8.0) for n in cast)
     pass3 = sum(_column_bytes(cols[n]) for n, c in p.items() if c.histogram is not None)
     return {
         "metric": "rows/sec for ColumnProfilerRunner (C5)", "value": args.c5_rows * world * args.steps / elapsed,
@@ -635,7 +659,7 @@ def run_c5(args, world, rank, local):
                                "utf8, 10 bool); ColumnProfilerRunner, 3 passes, KLL off (reference default)"
                                % args.c5_rows},
         "roofline": _step_roofline(pass1 + pass2 + pass3, step_s,
-                                   "one whole profile per GPU (3 passes; bytes = every column read by each pass)",
+                                   "one whole profile per GPU (3 passes; bytes = what each pass must read: pass 1 every column once, pass 2 the numeric-typed strings cast + re-scanned, pass 3 the histogram columns)",
                                    workload="c5" if world == 1 else None, default_size=args.c5_rows == 100_000_000),
         "check": {"columns": len(p), "histograms": n_hist,
                   "s00_distinct": p["s00"].approximateNumDistinctValues,
@@ -792,8 +816,7 @@ def main():
                           "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                           "kernel_ms": kernel_ms,
                           "algorithmic_bytes_per_launch": BYTES_PER_ROW * args.rows},
-                         **({"traffic_source": "copied from %s (PMC pass of this bench at its default size)"
-                             % traffic_src} if traffic_src else {})),
+                         **({"traffic_source": traffic_src} if traffic_src else {})),
         "valu_roofline": valu_roofline(local, float(args.rows) * n_hll, kernel_ms) if n_hll else None,
         "cpu_baseline": None,
     }

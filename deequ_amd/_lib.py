@@ -104,6 +104,7 @@ ArrowArray._fields_ = [("length", c_int64), ("null_count", c_int64), ("offset", 
 DIAG_SIGNATURES = {
     "dq_diag_hash_rate": (c_int, [c_int, c_int, c_int, POINTER(c_double)]),
     "dq_diag_freq_paths": (c_int, [c_void_p, POINTER(c_int64)]),
+    "dq_diag_parse_double": (c_int, [c_char_p, c_int64, POINTER(c_double), POINTER(c_int32)]),
 }
 
 

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "dq_internal.h"
+#include "dq_numparse.h"
 #include "../../include/deequ_amd_diag.h"
 #include "hll_p9_tables.h"
 
@@ -703,16 +704,15 @@ struct dq_plan : Stager {
   std::vector<HllTask> dtype_tasks;  // DataType: {column, type, where, count index}
   // HLL + DataType of the same utf8 (column, where): one fused string pass (dq_string_pass_kernel);
   // the HLL and DataType kernels launch only the tasks not fused here
-  std::vector<StrTask> str_tasks, str_hll_tasks;  // (str_hll_tasks: utf8 HLL without a DataType)
+  std::vector<StrTask> str_tasks;
   std::vector<HllTask> hll_launch, dtype_launch;
   std::vector<HllTask> len_tasks;    // MinLength / MaxLength: {column, type, where}
   std::vector<CorrTask> corr_tasks;  // Correlation: {x, y, where}
   std::vector<Program> programs;  // generic predicate programs -> batch masks
   // device state
-  DevBuf d_unsup;  // per generic program: a row hit DQ_P_CAST_DOUBLE off its exact fast path
   std::vector<dq_status> op_status;  // per op, after dq_plan_finish
   DevBuf d_tasks, d_groups, d_ranges, d_hll, d_progs, d_insns, d_pool, d_acc, d_partials, d_regs,
-      d_cols, d_masks, d_mask_words, d_dtype, d_dtype_counts, d_len, d_len_out, d_corr, d_corr_part, d_corr_acc, d_str, d_str_hll;
+      d_cols, d_masks, d_mask_words, d_dtype, d_dtype_counts, d_len, d_len_out, d_corr, d_corr_part, d_corr_acc, d_str;
   int64_t mask_words = 0;
   // pinned descriptor staging (DevColumn + DevMask arrays) guarded by an event
   void* h_desc = nullptr;
@@ -1028,7 +1028,6 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
   // HLL and DataType of the same utf8 (column, where) -- every string column of the profiler's
   // pass 1 -- run as one string pass (one read of the strings); the rest keep their own kernels
   plan->str_tasks.clear();
-  plan->str_hll_tasks.clear();
   plan->hll_launch.clear();
   plan->dtype_launch.clear();
   {
@@ -1042,8 +1041,6 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
       if (dt >= 0) {
         dt_fused[dt] = true;
         plan->str_tasks.push_back(StrTask{h.column, h.where_mask, h.reg_set, dt});
-      } else if (h.ctype == DQ_T_UTF8 && getenv_flag("DQ_STRING_PASS_HLL")) {
-        plan->str_hll_tasks.push_back(StrTask{h.column, h.where_mask, h.reg_set, -1});
       } else {
         plan->hll_launch.push_back(h);
       }
@@ -1058,7 +1055,6 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
       (s = upload(plan->d_hll, plan->hll_launch.data(), plan->hll_launch.size() * sizeof(HllTask))) != DQ_OK ||
       (s = upload(plan->d_dtype, plan->dtype_launch.data(), plan->dtype_launch.size() * sizeof(HllTask))) != DQ_OK ||
       (s = upload(plan->d_str, plan->str_tasks.data(), plan->str_tasks.size() * sizeof(StrTask))) != DQ_OK ||
-      (s = upload(plan->d_str_hll, plan->str_hll_tasks.data(), plan->str_hll_tasks.size() * sizeof(StrTask))) != DQ_OK ||
       (s = plan->d_dtype_counts.ensure(std::max<size_t>(1, plan->dtype_tasks.size()) * 5 * sizeof(uint64_t))) != DQ_OK ||
       (s = upload(plan->d_len, plan->len_tasks.data(), plan->len_tasks.size() * sizeof(HllTask))) != DQ_OK ||
       (s = plan->d_len_out.ensure(std::max<size_t>(1, plan->len_tasks.size()) * 3 * sizeof(uint64_t))) != DQ_OK ||
@@ -1067,7 +1063,6 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
       (s = upload(plan->d_progs, progs.data(), progs.size() * sizeof(PredProgram))) != DQ_OK ||
       (s = upload(plan->d_insns, insns.data(), insns.size() * sizeof(PredInsn))) != DQ_OK ||
       (s = upload(plan->d_pool, pool.data(), pool.size())) != DQ_OK ||
-      (s = plan->d_unsup.ensure(std::max<size_t>(1, plan->programs.size()) * sizeof(uint32_t))) != DQ_OK ||
       (s = plan->d_acc.ensure(std::max<size_t>(1, plan->scan_tasks.size()) * sizeof(ScanAcc))) != DQ_OK ||
       (s = plan->d_regs.ensure(std::max<size_t>(1, plan->hll_sets.size()) * kHllM * sizeof(uint32_t))) != DQ_OK ||
       (s = plan->d_cols.ensure(std::max(1, n_columns) * sizeof(DevColumn))) != DQ_OK ||
@@ -1140,8 +1135,6 @@ extern "C" dq_status dq_plan_reset(dq_plan* plan) {
   if (!plan) return fail(DQ_ERR_INVALID, "plan is NULL");
   DQ_HIP(hipSetDevice(plan->ctx->device));
   DQ_HIP(launch_init_acc(static_cast<ScanAcc*>(plan->d_acc.ptr), (int)plan->scan_tasks.size(), plan->stream));
-  DQ_HIP(hipMemsetAsync(plan->d_unsup.ptr, 0, std::max<size_t>(1, plan->programs.size()) * sizeof(uint32_t),
-                        plan->stream));
   if (!plan->hll_sets.empty())
     DQ_HIP(hipMemsetAsync(plan->d_regs.ptr, 0, plan->hll_sets.size() * kHllM * sizeof(uint32_t), plan->stream));
   if (!plan->dtype_tasks.empty())
@@ -1361,8 +1354,7 @@ extern "C" dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, in
     DQ_HIP(launch_predicates(static_cast<const PredProgram*>(plan->d_progs.ptr), n_progs,
                              static_cast<const PredInsn*>(plan->d_insns.ptr),
                              static_cast<const uint8_t*>(plan->d_pool.ptr), d_cols, n_rows,
-                             static_cast<uint64_t*>(plan->d_mask_words.ptr), plan->mask_words,
-                             static_cast<uint32_t*>(plan->d_unsup.ptr), plan->stream));
+                             static_cast<uint64_t*>(plan->d_mask_words.ptr), plan->mask_words, plan->stream));
 
   if (n_scan > 0) {
     ScanAcc* parts = static_cast<ScanAcc*>(plan->d_partials.ptr);
@@ -1389,13 +1381,6 @@ extern "C" dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, in
     DQ_HIP(launch_string_pass(static_cast<const StrTask*>(plan->d_str.ptr), n_str, d_cols, d_masks, n_rows, (int)bpt,
                               static_cast<uint32_t*>(plan->d_regs.ptr),
                               static_cast<unsigned long long*>(plan->d_dtype_counts.ptr), plan->stream));
-  }
-  const int n_str_hll = (int)plan->str_hll_tasks.size();
-  if (n_str_hll > 0) {
-    int64_t bpt = std::max<int64_t>(1, plan->target_blocks / n_str_hll);
-    bpt = std::min<int64_t>(bpt, chunks);
-    DQ_HIP(launch_string_pass(static_cast<const StrTask*>(plan->d_str_hll.ptr), n_str_hll, d_cols, d_masks, n_rows,
-                              (int)bpt, static_cast<uint32_t*>(plan->d_regs.ptr), nullptr, plan->stream));
   }
   const int n_hll = (int)plan->hll_launch.size();
   if (n_hll > 0) {
@@ -1464,7 +1449,6 @@ extern "C" dq_status dq_plan_finish(dq_plan* plan, dq_state* out, int n_out) {
   std::vector<uint64_t> dtc(plan->dtype_tasks.size() * 5);
   std::vector<uint64_t> lens(plan->len_tasks.size() * 3);
   std::vector<CorrAcc> corr(plan->corr_tasks.size());
-  std::vector<uint32_t> unsup(plan->programs.size());
   // every result array comes back in ONE pass through a pinned bounce buffer (pageable copies
   // are staged by the runtime, tens of microseconds each), then one synchronize
   struct Back {
@@ -1476,8 +1460,7 @@ extern "C" dq_status dq_plan_finish(dq_plan* plan, dq_state* out, int n_out) {
                         {corr.data(), plan->d_corr_acc.ptr, corr.size() * sizeof(CorrAcc)},
                         {dtc.data(), plan->d_dtype_counts.ptr, dtc.size() * sizeof(uint64_t)},
                         {acc.data(), plan->d_acc.ptr, acc.size() * sizeof(ScanAcc)},
-                        {regs.data(), plan->d_regs.ptr, regs.size() * sizeof(uint32_t)},
-                        {unsup.data(), plan->d_unsup.ptr, unsup.size() * sizeof(uint32_t)}};
+                        {regs.data(), plan->d_regs.ptr, regs.size() * sizeof(uint32_t)}};
   size_t total = 0;
   for (const Back& b : backs) total += (b.bytes + 255) & ~(size_t)255;
   if (total > plan->h_back_size) {
@@ -1501,11 +1484,6 @@ extern "C" dq_status dq_plan_finish(dq_plan* plan, dq_state* out, int n_out) {
     at += (b.bytes + 255) & ~(size_t)255;
   }
   plan->op_status.assign(plan->slots.size(), DQ_OK);
-  for (size_t i = 0; i < plan->slots.size(); ++i) {
-    const OpSlot& s = plan->slots[i];
-    if ((s.prog_pred >= 0 && unsup[s.prog_pred]) || (s.prog_where >= 0 && unsup[s.prog_where]))
-      plan->op_status[i] = DQ_ERR_UNSUPPORTED;
-  }
   plan->desc_pending = false;
   plan->host_tmp.clear();
 
@@ -1830,6 +1808,21 @@ extern "C" dq_status dq_state_metric(const dq_state* s, double* out) {
 }
 
 // ------------------------------------------------------------------------------ casts
+namespace {
+struct HostBytes {  // a byte source for the host build of dq_numparse.h
+  const uint8_t* p;
+  uint32_t operator[](int32_t i) const { return p[i]; }
+};
+}  // namespace
+
+extern "C" dq_status dq_diag_parse_double(const uint8_t* s, int64_t n, double* out, int32_t* ok) {
+  if ((!s && n > 0) || !out || !ok || n < 0 || n > INT32_MAX) return fail(DQ_ERR_INVALID, "bad argument");
+  double v = 0.0;
+  *ok = numparse::parse_double(HostBytes{s}, (int32_t)n, &v);
+  *out = v;
+  return DQ_OK;
+}
+
 extern "C" dq_status dq_cast_utf8(dq_ctx* ctx, const dq_column* src, int64_t n_rows, int32_t to_type,
                                   void* d_values, uint8_t* d_validity, int64_t* n_unsupported) {
   if (!ctx || !src || !n_unsupported || (n_rows > 0 && (!d_values || !d_validity)))
@@ -1845,22 +1838,14 @@ extern "C" dq_status dq_cast_utf8(dq_ctx* ctx, const dq_column* src, int64_t n_r
   st.col_types.assign(1, DQ_T_UTF8);
   st.resize_stage(1);
   DevColumn dc;
-  DevBuf d_unsup;
   dq_status s = prepare_column(&st, 0, *src, n_rows, &dc);
-  if (s == DQ_OK) s = d_unsup.ensure(sizeof(unsigned long long));
-  unsigned long long h_unsup = 0;
   hipError_t e = hipSuccess;
-  if (s == DQ_OK) e = hipMemsetAsync(d_unsup.ptr, 0, sizeof(unsigned long long), st.stream);
-  if (s == DQ_OK && e == hipSuccess)
-    e = launch_cast_utf8(dc, n_rows, to_type, d_values, d_validity, static_cast<unsigned long long*>(d_unsup.ptr), st.stream);
-  if (s == DQ_OK && e == hipSuccess)
-    e = hipMemcpyAsync(&h_unsup, d_unsup.ptr, sizeof(h_unsup), hipMemcpyDeviceToHost, st.stream);
+  if (s == DQ_OK) e = launch_cast_utf8(dc, n_rows, to_type, d_values, d_validity, st.stream);
   if (s == DQ_OK && e == hipSuccess) e = hipStreamSynchronize(st.stream);
   StreamPool::get().release(ctx->device, st.stream);
   st.stream = nullptr;
   if (s != DQ_OK) return s;
   if (e != hipSuccess) return fail(DQ_ERR_DEVICE, std::string("dq_cast_utf8: ") + hipGetErrorString(e));
-  *n_unsupported = (int64_t)h_unsup;
   return DQ_OK;
 }
 

@@ -86,13 +86,20 @@ __device__ uint64_t xxh64_any(const uint8_t* p, uint32_t len, uint64_t seed) {
   return xxh_avalanche(h);
 }
 
+// The table hash of an inline key (len <= 16).  It only places groups (slice, first probe, tag,
+// owner rank) -- keys are always compared exactly -- so it is the table's own function, not
+// Spark's: three 64-bit multiplies (each key word once, then one finalising multiply) instead
+// of XXH64's eight, since the stage, the level-2 split and the slice aggregation each hash every
+// record.  Its bins measured Poisson-spread (std/sqrt(mean) 0.97-1.0) over the slice, slot and
+// region bits for C4's 12-digit keys, sequential decimal strings and small / shifted integers.
+// (The length goes into k1's top byte, which an inline key of <= 15 bytes leaves zero.)
 __device__ inline uint64_t hash_inline(uint64_t k0, uint64_t k1, uint32_t len) {
-  uint64_t h = (uint64_t)len * kP5 + 42u;
-  h ^= xxh_round(0, k0);
-  h = rotl64(h, 27) * kP1 + kP4;
-  h ^= xxh_round(0, k1);
-  h = rotl64(h, 27) * kP1 + kP4;
-  return xxh_avalanche(h);
+  const uint64_t a = (k0 + 0x165667B19E3779F9ull) * 0x9E3779B97F4A7C15ull;
+  const uint64_t b = (k1 ^ ((uint64_t)len << 56) ^ 0x27D4EB2F165667C5ull) * 0xC2B2AE3D27D4EB4Full;
+  uint64_t h = a ^ ((b << 32) | (b >> 32));
+  h ^= h >> 29;
+  h *= 0xD6E8FEB86659FD93ull;
+  return h ^ (h >> 32);
 }
 
 // One row's grouping key.  Inline (len <= 16) keys live in k0/k1; longer keys point at their
@@ -718,34 +725,10 @@ constexpr unsigned long long kRecLenShift = 56;
 constexpr unsigned long long kRecKeyMask = (1ull << kRecLenShift) - 1;
 constexpr uint32_t kRecHole = 0xFFu;  // length byte of a record that holds no row
 
-#ifndef DQ_NT_RECORDS
-#define DQ_NT_RECORDS 0  // A/B: non-temporal records cost C4 3-4 ms (the next pass re-reads them from L2/MALL)
-#endif
-// Staged records are written once and read once by the next pass: optionally non-temporal.
-typedef unsigned int RecVec __attribute__((ext_vector_type(4)));
-__device__ inline FreqRec ld_rec(const FreqRec* p) {
-#if DQ_NT_RECORDS
-  const RecVec v = __builtin_nontemporal_load(reinterpret_cast<const RecVec*>(p));
-  FreqRec r;
-  r.k0 = (unsigned long long)v.x | ((unsigned long long)v.y << 32);
-  r.k1 = (unsigned long long)v.z | ((unsigned long long)v.w << 32);
-  return r;
-#else
-  return *p;
-#endif
-}
-__device__ inline void st_rec(FreqRec* p, const FreqRec& r) {
-#if DQ_NT_RECORDS
-  RecVec v;
-  v.x = (unsigned int)r.k0;
-  v.y = (unsigned int)(r.k0 >> 32);
-  v.z = (unsigned int)r.k1;
-  v.w = (unsigned int)(r.k1 >> 32);
-  __builtin_nontemporal_store(v, reinterpret_cast<RecVec*>(p));
-#else
-  *p = r;
-#endif
-}
+// Staged records are written once and read once by the next pass (plain loads/stores: measured,
+// non-temporal records cost C4 3-4 ms because the next pass re-reads them from L2 / MALL).
+__device__ inline FreqRec ld_rec(const FreqRec* p) { return *p; }
+__device__ inline void st_rec(FreqRec* p, const FreqRec& r) { *p = r; }
 
 __device__ inline void rec_unpack(const FreqRec& r, unsigned long long* k1, uint32_t* len) {
   *len = (uint32_t)(r.k1 >> kRecLenShift);
@@ -939,12 +922,6 @@ __device__ inline void track_count(AggLds& L, const AggTrack& tr, uint32_t c) {
 #ifndef DQ_AGG_BATCH
 #define DQ_AGG_BATCH 8
 #endif
-#ifndef DQ_AGG_PB
-#define DQ_AGG_PB 0  // records probed together (0 = one at a time; A/B: 4 and 8 cost C4 3.5-4.5 ms)
-#endif
-#ifndef DQ_LDS_READ_PROBE
-#define DQ_LDS_READ_PROBE 0
-#endif
 constexpr int kAggBatch = DQ_AGG_BATCH;  // records per thread loaded together
 
 // Count record r (table hash h) in the LDS slice image; false if the image is full.  (The
@@ -957,13 +934,7 @@ __device__ inline bool lds_count(unsigned long long* K0, unsigned long long* K1,
   uint32_t s = (uint32_t)(h & (S - 1));
   bool done = false;
   for (uint32_t probe = 0; probe < S && !done;) {
-#if DQ_LDS_READ_PROBE
-    // a plain read first: only an EMPTY slot is worth a compare-and-swap
-    unsigned long long c = __hip_atomic_load(&K1[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (c == kLdsEmpty) c = atomicCAS(&K1[s], kLdsEmpty, kLdsBusy);
-#else
     const unsigned long long c = atomicCAS(&K1[s], kLdsEmpty, kLdsBusy);
-#endif
     if (c == kLdsEmpty) {  // claimed: publish the key, then count
       K0[s] = r.k0;
       G[s] = tag_of(h);  // (written back with the slot: no second hash of the key)
@@ -999,13 +970,10 @@ __device__ __noinline__ void piece_spill(const FreqTable& T, const FreqRec& r, u
 // Aggregate records [r0, r1) of slice b.  owner: the work item holds the slice's whole bucket
 // (load the slice, count in LDS, write it back with plain stores); otherwise it is one piece of a
 // split bucket (count in LDS, merge into the slice with device-scope atomics).
-// pre (optional): the item's first NT * kAggBatch records, already loaded by the caller (thread
-// t holds records r0 + j * NT + t), so they were in flight during the previous item.
 template <int NT, bool OWNER_ONLY>
 __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restrict__ recs, uint64_t r0, uint64_t r1,
                          uint64_t b, bool owner, int table_empty, FreqRec* retry, unsigned long long* n_retry,
-                         unsigned long long* new_groups, const AggTrack* tr = nullptr,
-                         const FreqRec (*pre)[kAggBatch] = nullptr) {
+                         unsigned long long* new_groups, const AggTrack* tr = nullptr) {
   constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
   unsigned long long* K0 = L.K0;
   unsigned long long* K1 = L.K1;
@@ -1040,94 +1008,13 @@ __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restric
     __syncthreads();
     // records are loaded kAggBatch per thread at a time, all loads in flight together (one
     // dependent load per record made the loop latency-bound)
-    // (rb outside the loop, filled from `pre` before it: the caller's copy is dead from here on)
     FreqRec rb[kAggBatch];
-    if (pre) {
-#pragma unroll
-      for (int j = 0; j < kAggBatch; ++j) rb[j] = (*pre)[j];
-    }
     for (uint64_t base = r0; base < r1; base += (uint64_t)NT * kAggBatch) {
-      if (!pre || base != r0) {
 #pragma unroll
-        for (int j = 0; j < kAggBatch; ++j) {
-          const uint64_t i = base + (uint64_t)j * NT + threadIdx.x;
-          if (i < r1) rb[j] = ld_rec(recs + i);
-        }
+      for (int j = 0; j < kAggBatch; ++j) {
+        const uint64_t i = base + (uint64_t)j * NT + threadIdx.x;
+        if (i < r1) rb[j] = ld_rec(recs + i);
       }
-#if DQ_AGG_PB
-      // PB records at a time through ONE probing loop: each round issues the PB compare-and-swaps
-      // together, publishes the claims, then checks the candidate keys together -- the LDS
-      // round trips of the PB records overlap instead of running one record after another.
-      // (A claimer publishes in the round it claims; a record that met BUSY retries next round.)
-#pragma unroll
-      for (int g = 0; g < kAggBatch; g += DQ_AGG_PB) {
-        constexpr int PB = DQ_AGG_PB;
-        uint64_t hh[PB];
-        uint32_t sl[PB], probes[PB], pend = 0u;
-#pragma unroll
-        for (int q = 0; q < PB; ++q) {
-          const uint64_t i = base + (uint64_t)(g + q) * NT + threadIdx.x;
-          unsigned long long k1;
-          uint32_t len;
-          rec_unpack(rb[g + q], &k1, &len);
-          hh[q] = 0;
-          sl[q] = 0;
-          probes[q] = 0;
-          if (i < r1 && len != kRecHole) {
-            hh[q] = hash_inline(rb[g + q].k0, k1, len);
-            sl[q] = (uint32_t)(hh[q] & (S - 1));
-            pend |= 1u << q;
-          }
-        }
-        while (pend) {
-          unsigned long long c[PB];
-#pragma unroll
-          for (int q = 0; q < PB; ++q) c[q] = ((pend >> q) & 1u) ? atomicCAS(&K1[sl[q]], kLdsEmpty, kLdsBusy) : kLdsBusy;
-          uint32_t claimed = 0u;
-#pragma unroll
-          for (int q = 0; q < PB; ++q)
-            if (((pend >> q) & 1u) && c[q] == kLdsEmpty) {
-              K0[sl[q]] = rb[g + q].k0;
-              L.G[sl[q]] = tag_of(hh[q]);
-              claimed |= 1u << q;
-            }
-          if (claimed) {
-            __threadfence_block();
-#pragma unroll
-            for (int q = 0; q < PB; ++q)
-              if ((claimed >> q) & 1u) {
-                atomicExch(&K1[sl[q]], rb[g + q].k1);
-                atomicAdd(&C[sl[q]], 1u);
-              }
-            pend &= ~claimed;
-          }
-          unsigned long long k0v[PB];
-#pragma unroll
-          for (int q = 0; q < PB; ++q)
-            k0v[q] = (((pend >> q) & 1u) && c[q] == rb[g + q].k1)
-                         ? __hip_atomic_load(&K0[sl[q]], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)
-                         : ~rb[g + q].k0;
-#pragma unroll
-          for (int q = 0; q < PB; ++q) {
-            if (!((pend >> q) & 1u) || c[q] == kLdsBusy) continue;  // (BUSY: look at the slot again)
-            if (c[q] == rb[g + q].k1 && k0v[q] == rb[g + q].k0) {
-              atomicAdd(&C[sl[q]], 1u);
-              pend &= ~(1u << q);
-            } else {
-              sl[q] = (sl[q] + 1) & (S - 1);
-              if (++probes[q] >= S) {  // the LDS image is full
-                pend &= ~(1u << q);
-                unsigned long long k1;
-                uint32_t len;
-                rec_unpack(rb[g + q], &k1, &len);
-                if (OWNER_ONLY || owner) overflow = 1;
-                else piece_spill(T, rb[g + q], k1, len, hh[q], retry, n_retry);
-              }
-            }
-          }
-        }
-      }
-#else
 #pragma unroll
       for (int j = 0; j < kAggBatch; ++j) {
         const uint64_t i = base + (uint64_t)j * NT + threadIdx.x;
@@ -1143,7 +1030,6 @@ __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restric
           else piece_spill(T, r, k1, len, h, retry, n_retry);
         }
       }
-#endif
     }
     __syncthreads();
     if (!OWNER_ONLY && !owner) {  // merge the piece's counts into the shared slice
@@ -1403,9 +1289,6 @@ __global__ __launch_bounds__(kPartThreads) void dq_freq_part_kernel(
   part_tile(L, rec, bin, nb, base_id, out, out_cap, out_fill, ovf, ovf_n, ovf_cap, flag, nullptr);
 }
 
-#ifndef DQ_STAGE_TOUCH
-#define DQ_STAGE_TOUCH 0  // measured: no gain on C4 (31.4-32.0 vs 31.5-33.2 ms); =2 also touches key bytes (spills)
-#endif
 // Stage + level-1 partition fused: the rows of one batch become records written straight into
 // their level-1 regions (top b1 bits of the table hash), so the staging is not written and read
 // back in row order.  Tiles of kPartTile rows, grid-stride.  The sketch, the staged count and
@@ -1430,25 +1313,6 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(4)
     FreqRec rec[kStagePer];
     uint32_t bin[kStagePer];
     uint32_t too_long = 0u;
-#if DQ_STAGE_TOUCH
-    // the block's NEXT tile is touched while this one is built (one dword per 128-B line of its
-    // offsets, with DQ_STAGE_TOUCH=2 also of its key bytes), so its dependent offset -> bytes
-    // loads hit L2 / MALL instead of HBM; the touched values are consumed after the tile
-    uint32_t touch = 0u;
-    int32_t nb0 = 0, nb1 = 0;
-    if constexpr (ONE_STRING) {
-      const int64_t nrow0 = row0 + (int64_t)gridDim.x * kStageTile;
-      if (nrow0 < n_rows) {
-        const int64_t nrow1 = min(nrow0 + (int64_t)kStageTile, n_rows);
-        const int64_t orow = nrow0 + (int64_t)t * 32;  // 32 offsets per 128-B line
-        if (orow <= nrow1) touch ^= (uint32_t)c0.offsets[orow];
-        if (DQ_STAGE_TOUCH >= 2) {
-          nb0 = c0.offsets[nrow0];
-          nb1 = c0.offsets[nrow1];
-        }
-      }
-    }
-#endif
     if constexpr (ONE_STRING) {
       // groups of kStageGroup rows: their offsets, then their key words, all in flight together
       // (the whole tile at once would not fit the register file)
@@ -1497,20 +1361,7 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(4)
       }
     }
     if (too_long) atomicMax(long_key, (unsigned long long)too_long);
-#if DQ_STAGE_TOUCH >= 2
-    if constexpr (ONE_STRING) {
-      const uint8_t* bytes = static_cast<const uint8_t*>(c0.values);
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int64_t o = (int64_t)nb0 + ((int64_t)t + k * kPartThreads) * 128;
-        if (o < (int64_t)nb1) touch ^= bytes[o];
-      }
-    }
-#endif
     part_tile(L, rec, bin, nb, 0, out, cap1, fill1, ovf, ovf_n, ovf_cap, flag, staged);
-#if DQ_STAGE_TOUCH
-    asm volatile("" ::"v"(touch));
-#endif
   }
   __syncthreads();
   for (uint32_t i = t; i < (uint32_t)kHllM; i += kPartThreads)
@@ -1537,17 +1388,8 @@ __global__ __launch_bounds__(kBlock) void dq_freq_compact_kernel(const FreqRec* 
 #define DQ_AGG_THREADS 512
 #endif
 constexpr int kAggRegionThreads = DQ_AGG_THREADS;
-#ifndef DQ_AGG_PREFETCH
-#define DQ_AGG_PREFETCH 0  // measured: the extra registers cost more than the overlap gains (C4 33.2 vs 34.9-39.2 ms)
-#endif
 #ifndef DQ_AGG_WAVES
 #define DQ_AGG_WAVES 4
-#endif
-#ifndef DQ_AGG_FILL_AHEAD
-#define DQ_AGG_FILL_AHEAD 0  // read the next item's fill one item ahead (A/B pending)
-#endif
-#ifndef DQ_AGG_EARLY
-#define DQ_AGG_EARLY 1  // 1: touch the item's records before its LDS init (-1 ms on C4); 2: also the next item's (measured +4 ms)
 #endif
 __global__ __launch_bounds__(kAggRegionThreads) __attribute__((amdgpu_waves_per_eu(DQ_AGG_WAVES))) void dq_freq_agg_region_kernel(FreqTable T, const FreqRec* __restrict__ recs,
                                                                     const unsigned long long* __restrict__ fill,
@@ -1560,41 +1402,10 @@ __global__ __launch_bounds__(kAggRegionThreads) __attribute__((amdgpu_waves_per_
     for (int i = threadIdx.x; i < kAggLdsHist; i += kAggRegionThreads) L.hist[i] = 0u;
     __syncthreads();
   }
-  // software pipeline: the next item's first records are loaded while this item is counted
-  auto item_end = [&](uint64_t b) -> uint64_t {
-    const unsigned long long f = fill[b];
-    return b * cap + (f < cap ? f : cap);
-  };
-#if DQ_AGG_PREFETCH
-  auto load_first = [&](uint64_t b, FreqRec (&out)[kAggBatch]) {
-    const uint64_t r0 = b * cap, r1 = item_end(b);
-#pragma unroll
-    for (int j = 0; j < kAggBatch; ++j) {
-      const uint64_t i = r0 + (uint64_t)j * kAggRegionThreads + threadIdx.x;
-      if (i < r1) out[j] = recs[i];
-    }
-  };
-#endif
-#if DQ_AGG_PREFETCH
-  FreqRec cur[kAggBatch];
-  if (blockIdx.x < n_slices) load_first(blockIdx.x, cur);
-#endif
-#if DQ_AGG_FILL_AHEAD
-  // the next item's fill is read one item ahead (its latency hides behind the current item)
-  uint64_t r1_next = blockIdx.x < n_slices ? item_end(blockIdx.x) : 0;
-#endif
   for (uint64_t b = blockIdx.x; b < n_slices; b += gridDim.x) {
     const uint64_t r0 = b * cap;
-#if DQ_AGG_FILL_AHEAD
-    const uint64_t r1 = r1_next;
-    if (b + gridDim.x < n_slices) r1_next = item_end(b + gridDim.x);
-#else
-    const uint64_t r1 = item_end(b);
-#endif
-#if DQ_AGG_PREFETCH
-    FreqRec nxt[kAggBatch];
-    if (b + gridDim.x < n_slices) load_first(b + gridDim.x, nxt);
-#elif DQ_AGG_EARLY
+    const unsigned long long f = fill[b];
+    const uint64_t r1 = r0 + (f < cap ? f : cap);
     // the item's records are touched (one dword per 128-B line, one per thread) before the LDS
     // image is initialised, so their HBM latency overlaps the init and the barrier and the
     // item's loads then hit L2; one register, consumed after the item
@@ -1603,11 +1414,6 @@ __global__ __launch_bounds__(kAggRegionThreads) __attribute__((amdgpu_waves_per_
       const uint64_t i = r0 + (uint64_t)threadIdx.x * 8u;
       if (i < r1) touch = *reinterpret_cast<const uint32_t*>(recs + i);
     }
-    if (DQ_AGG_EARLY >= 2 && b + gridDim.x < n_slices) {  // and the next item's, from its region start
-      const uint64_t i = (b + gridDim.x) * cap + (uint64_t)threadIdx.x * 8u;
-      if (i < (b + gridDim.x + 1) * cap) touch ^= *reinterpret_cast<const uint32_t*>(recs + i);
-    }
-#endif
     if (r1 == r0) {
       if (tr.write_all) {
         FreqSlot* slice = T.slots + (b << kFreqSliceLog);
@@ -1616,19 +1422,9 @@ __global__ __launch_bounds__(kAggRegionThreads) __attribute__((amdgpu_waves_per_
       if (tr.smax && threadIdx.x == 0) tr.smax[b] = 0u;
     } else {
       agg_item<kAggRegionThreads, true>(L, T, recs, r0, r1, b, true, table_empty, retry, n_retry, new_groups,
-                                        track || tr.write_all ? &tr : nullptr,
-#if DQ_AGG_PREFETCH
-                                        &cur);
-#else
-                                        nullptr);
-#endif
+                                        track || tr.write_all ? &tr : nullptr);
     }
-#if DQ_AGG_PREFETCH
-#pragma unroll
-    for (int j = 0; j < kAggBatch; ++j) cur[j] = nxt[j];
-#elif DQ_AGG_EARLY
     asm volatile("" ::"v"(touch));
-#endif
   }
   if (track) {
     __syncthreads();

@@ -307,8 +307,7 @@ hipError_t launch_hll(const HllTask* d_tasks, int n_tasks, const DevColumn* d_co
                       uint32_t* d_registers, hipStream_t stream);
 hipError_t launch_predicates(const PredProgram* d_progs, int n_progs, const PredInsn* d_insns,
                              const uint8_t* d_pool, const DevColumn* d_cols, int64_t n_rows,
-                             uint64_t* d_mask_words, int64_t words_per_mask, uint32_t* d_unsup,
-                             hipStream_t stream);
+                             uint64_t* d_mask_words, int64_t words_per_mask, hipStream_t stream);
 hipError_t launch_rebase_offsets(int32_t* d_offs, int64_t n, int32_t first, hipStream_t stream);
 hipError_t launch_realign_bitmap(const uint8_t* src, int64_t bit_offset, int64_t n_bits,
                                  uint8_t* dst, hipStream_t stream);
@@ -325,7 +324,7 @@ hipError_t launch_corr(const CorrTask* d_tasks, int n_tasks, const DevColumn* d_
                        int64_t n_rows, int blocks_per_task, CorrAcc* d_partials, CorrAcc* d_acc,
                        hipStream_t stream);
 hipError_t launch_cast_utf8(const DevColumn& src, int64_t n_rows, int to_type, void* d_values, uint8_t* d_validity,
-                            unsigned long long* d_unsupported, hipStream_t stream);
+                            hipStream_t stream);
 
 // ---------------------------------------------------------------- XXH64 (host + device)
 constexpr uint64_t kP1 = 0x9E3779B185EBCA87ull;

@@ -90,7 +90,7 @@ __device__ inline bool cmp_result(int opcode, int ord) {
 }
 
 __device__ void eval_program(const PredInsn* code, int n, const uint8_t* pool, const DevColumn* cols, int64_t row,
-                             bool& t, bool& nn, bool& unsup) {
+                             bool& t, bool& nn) {
   Val st[kMaxStack];
   int sp = 0;
   for (int pc = 0; pc < n; ++pc) {
@@ -106,7 +106,6 @@ __device__ void eval_program(const PredInsn* code, int n, const uint8_t* pool, c
         if (a.type == VT_STR) {
           double v = 0.0;
           const int r = a.null ? 0 : parse_double(PtrSrc{a.s}, (int32_t)a.i, &v);
-          if (r == 2) unsup = true;  // well formed, but not exactly convertible here
           a.null = (r == 1) ? a.null : 1;
           a.f = v;
         } else {
@@ -187,7 +186,7 @@ __global__ __launch_bounds__(kBlock) void dq_pred_kernel(const PredProgram* __re
                                                          const uint8_t* __restrict__ pool,
                                                          const DevColumn* __restrict__ cols,
                                                          int64_t n_rows, uint64_t* out,
-                                                         int64_t words_per_mask, uint32_t* unsup_flags) {
+                                                         int64_t words_per_mask) {
   const PredProgram prog = progs[blockIdx.y];
   const PredInsn* code = insns + prog.first;
   const int lane = threadIdx.x & 63;
@@ -197,9 +196,8 @@ __global__ __launch_bounds__(kBlock) void dq_pred_kernel(const PredProgram* __re
   for (int64_t w = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); w < n_words;
        w += (int64_t)gridDim.x * (kBlock / 64)) {
     const int64_t row = (w << 6) + lane;
-    bool t = false, nn = false, unsup = false;
-    if (row < n_rows) eval_program(code, prog.n, pool, cols, row, t, nn, unsup);
-    if (__ballot(unsup) && lane == 0) atomicOr(&unsup_flags[blockIdx.y], 1u);
+    bool t = false, nn = false;
+    if (row < n_rows) eval_program(code, prog.n, pool, cols, row, t, nn);
     const uint64_t bt = __ballot(t);
     const uint64_t bn = __ballot(nn);
     if (lane == 0) {
@@ -228,14 +226,13 @@ __global__ void dq_realign_kernel(const uint8_t* __restrict__ src, int64_t bit_o
 
 hipError_t launch_predicates(const PredProgram* d_progs, int n_progs, const PredInsn* d_insns,
                              const uint8_t* d_pool, const DevColumn* d_cols, int64_t n_rows,
-                             uint64_t* d_mask_words, int64_t words_per_mask, uint32_t* d_unsup,
-                             hipStream_t stream) {
+                             uint64_t* d_mask_words, int64_t words_per_mask, hipStream_t stream) {
   if (n_progs <= 0 || n_rows <= 0) return hipSuccess;
   const int64_t n_words = (n_rows + 63) >> 6;
   int64_t blocks = (n_words + 3) / 4;
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(dq_pred_kernel, dim3((unsigned)blocks, n_progs), dim3(kBlock), 0, stream,
-                     d_progs, d_insns, d_pool, d_cols, n_rows, d_mask_words, words_per_mask, d_unsup);
+                     d_progs, d_insns, d_pool, d_cols, n_rows, d_mask_words, words_per_mask);
   return hipGetLastError();
 }
 

@@ -13,10 +13,9 @@
 //    Fractional (ColumnProfiler.castNumericStringColumns, :427-445), Spark 2.2.2 semantics:
 //    long = UTF8String.toLong (optional sign, digits, optional '.' + digits truncated, no
 //    whitespace, overflow -> NULL); double = java.lang.Double.parseDouble (whitespace trimmed,
-//    sign, digits, '.', exponent, f/d suffix, NaN/Infinity).  Doubles are produced exactly
-//    (correctly rounded) on the Clinger fast path -- <= 19 significant digits, value < 2^53,
-//    |10-exponent| <= 22 -- and any other well-formed number is counted as "unsupported" so
-//    the caller routes the column to Spark instead of returning an inexact value.
+//    sign, digits, '.', exponent, f/d suffix, NaN/Infinity, hexadecimal), correctly rounded for
+//    every input (dq_numparse.h: Clinger's fast path, Eisel-Lemire, an exact big-integer
+//    comparison near rounding boundaries).
 #include "dq_parse.h"
 #include "dq_strhash.h"
 
@@ -366,20 +365,15 @@ __device__ bool parse_long_words(const WordSrc& ws, int32_t n, int64_t* out) {
   return parse_long(ws, n, out);
 }
 
-__device__ inline bool cast_one(const WordSrc& p, int32_t n, int to_type, int64_t* lv, double* dv,
-                                uint32_t* unsup) {
+__device__ inline bool cast_one(const WordSrc& p, int32_t n, int to_type, int64_t* lv, double* dv) {
   if (to_type == DQ_T_INT64) return parse_long_words(p, n, lv);
-  const int r = parse_double(p, n, dv);
-  *unsup += r == 2;
-  return r == 1;
+  return parse_double(p, n, dv) == 1;
 }
 
 template <typename Src>
-__device__ inline bool cast_one(const Src& p, int32_t n, int to_type, int64_t* lv, double* dv, uint32_t* unsup) {
+__device__ inline bool cast_one(const Src& p, int32_t n, int to_type, int64_t* lv, double* dv) {
   if (to_type == DQ_T_INT64) return parse_long(p, n, lv);
-  const int r = parse_double(p, n, dv);
-  *unsup += r == 2;
-  return r == 1;
+  return parse_double(p, n, dv) == 1;
 }
 
 }  // namespace
@@ -387,10 +381,8 @@ __device__ inline bool cast_one(const Src& p, int32_t n, int to_type, int64_t* l
 // One row per lane: values are written coalesced, and each wave's 64 validity bits (a ballot)
 // are stored by its first lane -- one 8-byte word when the wave's rows are all in range.
 __global__ __launch_bounds__(kBlock) void dq_cast_utf8_kernel(DevColumn src, int64_t n_rows, int to_type,
-                                                              void* values, uint8_t* validity,
-                                                              unsigned long long* n_unsupported) {
+                                                              void* values, uint8_t* validity) {
   const uint32_t lane = threadIdx.x & 63u;
-  uint32_t unsup = 0u;
   for (int64_t base = (int64_t)blockIdx.x * kBlock; base < n_rows; base += (int64_t)gridDim.x * kBlock) {
     const int64_t row = base + threadIdx.x;
     int64_t lv = 0;
@@ -399,8 +391,8 @@ __global__ __launch_bounds__(kBlock) void dq_cast_utf8_kernel(DevColumn src, int
     if (row < n_rows && (src.validity == nullptr || bit_at(src.validity, row))) {
       const int32_t b = src.offsets[row], e = src.offsets[row + 1];
       const uint8_t* p = static_cast<const uint8_t*>(src.values) + b;
-      if (e - b <= 24) ok = cast_one(WordSrc(p, e - b), e - b, to_type, &lv, &dv, &unsup);
-      else ok = cast_one(PtrSrc{p}, e - b, to_type, &lv, &dv, &unsup);
+      if (e - b <= 24) ok = cast_one(WordSrc(p, e - b), e - b, to_type, &lv, &dv);
+      else ok = cast_one(PtrSrc{p}, e - b, to_type, &lv, &dv);
     }
     if (row < n_rows) {
       if (to_type == DQ_T_INT64) static_cast<int64_t*>(values)[row] = ok ? lv : 0;
@@ -417,7 +409,6 @@ __global__ __launch_bounds__(kBlock) void dq_cast_utf8_kernel(DevColumn src, int
       }
     }
   }
-  if (unsup) atomicAdd(n_unsupported, (unsigned long long)unsup);
 }
 
 hipError_t launch_string_pass(const StrTask* d_tasks, int n_tasks, const DevColumn* d_cols, const DevMask* d_masks,
@@ -442,12 +433,12 @@ hipError_t launch_datatype(const HllTask* d_tasks, int n_tasks, const DevColumn*
 }
 
 hipError_t launch_cast_utf8(const DevColumn& src, int64_t n_rows, int to_type, void* d_values, uint8_t* d_validity,
-                            unsigned long long* d_unsupported, hipStream_t stream) {
+                            hipStream_t stream) {
   if (n_rows <= 0) return hipSuccess;
   int64_t blocks = (n_rows + kBlock - 1) / kBlock;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(dq_cast_utf8_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, src, n_rows, to_type,
-                     d_values, d_validity, d_unsupported);
+                     d_values, d_validity);
   return hipGetLastError();
 }
 

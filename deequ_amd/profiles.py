@@ -219,8 +219,8 @@ def _extract_generic_statistics(columns, schema, ctx, predefined) -> GenericColu
 
 def cast_string_column(col, to_dtype: str, device: Optional[int] = None):
     """Spark 2.2.2 Cast(StringType -> LongType | DoubleType) of one utf8 column on the GPU
-    (dq_cast_utf8); the result is a device-resident column.  Raises UnsupportedOnGpu when a value
-    needs the exact slow-path double parse (the reference would run that column on Spark)."""
+    (dq_cast_utf8); the result is a device-resident column.  Doubles are Java's parseDouble,
+    correctly rounded for every input (dq_numparse.h)."""
     import torch
     from .engine import current_device
     from .table import Column
@@ -233,9 +233,6 @@ def cast_string_column(col, to_dtype: str, device: Optional[int] = None):
     src = col.to_dq()
     L.check(L.lib().dq_cast_utf8(L.Context.get(dev_idx).handle, ctypes.byref(src), n, L.TYPE_CODES[to_dtype],
                                  vals.data_ptr(), valid.data_ptr(), ctypes.byref(unsupported)))
-    if unsupported.value:
-        raise L.UnsupportedOnGpu(L.DQ_ERR_UNSUPPORTED, "%d values need Spark's exact (slow-path) string to "
-                                 "double parse" % unsupported.value)
     return Column(to_dtype, n, vals, valid, device=True)
 
 
@@ -255,16 +252,14 @@ def _cast_numeric_string_columns(columns, data, generic):
             targets[c] = "float64"
     if not targets:
         return data
-    from .distributed import allreduce_flag, is_sharded
-    if is_sharded(data):  # every rank casts its shard; a rank's unsupported value fails them all
+    from .distributed import agree, is_sharded
+    if is_sharded(data):  # every rank casts its shard; a failure on any rank fails them all
         local, error = None, None
         try:
             local = _cast_batches(data.local, targets)
-        except L.UnsupportedOnGpu as e:
+        except L.DeequAmdError as e:
             error = e
-        if allreduce_flag(error is not None, data.group):
-            raise error or L.UnsupportedOnGpu(L.DQ_ERR_UNSUPPORTED, "another rank's shard needs Spark's exact "
-                                                                  "(slow-path) string to double parse")
+        agree(error, "the string cast of pass 2", data.group)
         return data.with_local(local)
     return _cast_batches(data, targets)
 

@@ -109,9 +109,8 @@ typedef enum dq_pred_opcode {
   DQ_P_CAST_DOUBLE = 7, /* pop value; push it as fp64: Spark 2.2 Cast(-> DoubleType), which a
                            comparison of a string with a number inserts (PromoteStrings): a string
                            through java.lang.Double.parseDouble of its trimmed text, NULL when
-                           unparsable.  A well-formed string off the exact fast path (> 19
-                           significant digits, |exponent| > 22, hex) makes the op report
-                           DQ_ERR_UNSUPPORTED from dq_plan_op_status (route it to Spark).    */
+                           unparsable; correctly rounded for every input (decimal of any
+                           length and exponent, hexadecimal, NaN / Infinity, f/d suffix).   */
   DQ_P_EQ = 10, DQ_P_NE = 11, DQ_P_LT = 12, DQ_P_LE = 13, DQ_P_GT = 14, DQ_P_GE = 15,
   DQ_P_EQ_NULLSAFE = 16, /* <=>                                                             */
   DQ_P_IS_NULL = 20,   /* pop value; push boolean (never NULL)                              */
@@ -230,9 +229,10 @@ dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, int n_columns
 /* Wait for all consumed batches and write one dq_state per op (in op order). */
 dq_status dq_plan_finish(dq_plan* plan, dq_state* out, int n_out);
 
-/* Status of op `op` after dq_plan_finish: DQ_OK, or DQ_ERR_UNSUPPORTED when a batch held input
- * the GPU could not evaluate exactly for that op (DQ_P_CAST_DOUBLE off its fast path); the JNI
- * layer then fails or reroutes that analyzer only (AnalysisRunner.scala:340-353 scope). */
+/* Status of op `op` after dq_plan_finish: DQ_OK, or an error the op alone failed with (the
+ * per-analyzer scope of AnalysisRunner.scala:340-353: the JNI layer fails or reroutes that
+ * analyzer only).  Every op this library plans evaluates exactly, so it reports DQ_OK today;
+ * the entry point keeps the per-op scope in the ABI. */
 dq_status dq_plan_op_status(dq_plan* plan, int op);
 
 /* ---------------------------------------------------------------- Arrow C Data Interface
@@ -330,9 +330,10 @@ uint64_t dq_xxh64(const void* data, size_t len, uint64_t seed);
 /* Spark 2.2.2 Cast(StringType -> LongType | DoubleType) of one utf8 column, as
  * ColumnProfiler.castNumericStringColumns does before pass 2 (ColumnProfiler.scala:346-355,
  * 427-445).  Writes n_rows values and a validity bitmap (LSB-first, NULL = unparsable) into
- * DEVICE buffers on ctx's GPU.  Doubles are exact (correctly rounded); a well-formed number
- * outside the exact fast path (> 19 significant digits, |exponent| > 22, hex) is counted in
- * *n_unsupported and its row left NULL -- the caller routes the column to Spark when > 0. */
+ * DEVICE buffers on ctx's GPU.  Doubles are java.lang.Double.parseDouble, correctly rounded
+ * for every input (Clinger's fast path, Eisel-Lemire over a 128-bit power-of-five table, an
+ * exact big-integer comparison near rounding boundaries; hexadecimal literals rounded half-even).
+ * *n_unsupported is always set to 0 (kept for ABI stability: nothing is routed back). */
 dq_status dq_cast_utf8(dq_ctx* ctx, const dq_column* src, int64_t n_rows, int32_t to_type,
                        void* d_values, uint8_t* d_validity, int64_t* n_unsupported);
 

@@ -26,6 +26,12 @@ dq_status dq_diag_hash_rate(int device, int with_hll, int reps, double* hashes_p
  * out[3] = records that went through the sort path (small stagings, retries, skew fallbacks). */
 dq_status dq_diag_freq_paths(dq_freq* f, int64_t* out);
 
+/* Host build of the library's java.lang.Double.parseDouble (the parser dq_cast_utf8 and the
+ * predicate IR's string -> double cast run on the device, compiled from the same source):
+ * *ok = 1 and *out = the correctly rounded value, or *ok = 0 (NumberFormatException, NULL in
+ * Spark).  Lets CPU tests check it against a reference parser on millions of strings. */
+dq_status dq_diag_parse_double(const uint8_t* s, int64_t n, double* out, int32_t* ok);
+
 #ifdef __cplusplus
 }
 #endif

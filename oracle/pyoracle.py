@@ -611,7 +611,7 @@ def java_parse_double(s: str) -> Optional[float]:
         t = t[1:]
     while t and ord(t[-1]) <= 0x20:
         t = t[:-1]
-    m = re.fullmatch(r"([+-]?)(NaN|Infinity|((\d+\.?\d*|\.\d+)([eE][+-]?\d+)?)[fFdD]?)", t)
+    m = re.fullmatch(r"([+-]?)(NaN|Infinity|((\d+\.?\d*|\.\d+)([eE][+-]?\d+)?)[fFdD]?)", t, re.ASCII)
     if m:
         sign, body = m.group(1), m.group(2)
         if body == "NaN":
@@ -620,9 +620,12 @@ def java_parse_double(s: str) -> Optional[float]:
             return float("-inf") if sign == "-" else float("inf")
         num = body.rstrip("fFdD")
         return float(sign + num)
-    hm = re.fullmatch(r"([+-]?)0[xX]([0-9a-fA-F]*\.?[0-9a-fA-F]*)[pP]([+-]?\d+)[fFdD]?", t)
+    hm = re.fullmatch(r"([+-]?)0[xX]([0-9a-fA-F]*\.?[0-9a-fA-F]*)[pP]([+-]?\d+)[fFdD]?", t, re.ASCII)
     if hm and hm.group(2).strip("."):
-        return float.fromhex(hm.group(1) + "0x" + hm.group(2) + "p" + hm.group(3))
+        try:
+            return float.fromhex(hm.group(1) + "0x" + hm.group(2) + "p" + hm.group(3))
+        except OverflowError:  # rounds past Double.MAX_VALUE: Java gives Infinity
+            return float("-inf") if hm.group(1) == "-" else float("inf")
     return None
 
 

@@ -176,3 +176,48 @@ def test_c_abi_rank_fold_rejects_bad_arguments():
     assert L.lib().dq_states_merge_ranks(arr, 0, 2, out) == L.DQ_ERR_INVALID
     arr[0].kind, arr[1].kind = L.DQ_OP_SUM, L.DQ_OP_MEAN  # kinds differ across ranks
     assert L.lib().dq_states_merge_ranks(arr, 2, 1, out) != L.DQ_OK
+
+
+def _scope_worker(rank, world, port, q):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+    import torch.distributed as dist
+    from deequ_amd import _lib as L
+    from deequ_amd.distributed import merge_scan_results
+    from deequ_amd.engine import OpUnsupported
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    local = _states_for(_table(rank * 100, (rank + 1) * 100))
+    kinds = [k for k, _ in local]
+    states = [_to_dq(k, st) for k, st in local]
+    # rank 1 could not evaluate op 2 on its shard (dq_plan_op_status): that op fails on every
+    # rank, the others merge as usual (AnalysisRunner.scala:340-353 over the whole dataset)
+    if rank == 1:
+        states[2] = OpUnsupported(L.UnsupportedOnGpu(L.DQ_ERR_UNSUPPORTED, "injected"))
+    out = merge_scan_results(states, None, kinds)
+    q.put((rank, [isinstance(o, OpUnsupported) for o in out]))
+    # and an aggregation failure on rank 0 fails every rank (the all-fail scope, :320-323)
+    err = None
+    try:
+        merge_scan_results(None if rank == 0 else states, RuntimeError("boom") if rank == 0 else None, kinds)
+    except Exception as e:  # noqa: BLE001
+        err = type(e).__name__
+    q.put((rank + 100, err))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_failure_scopes_span_ranks():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 2
+    procs = [ctx.Process(target=_scope_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2 * world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert res[r][2] and sum(res[r]) == 1, res[r]
+    assert res[100] == "RuntimeError" and res[101] == "DeequAmdError"

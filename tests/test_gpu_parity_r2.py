@@ -5,7 +5,7 @@
   Double.toString), run on the GPU against the oracle;
 * Spark 2.2's implicit string -> double cast in comparisons (PromoteStrings), e.g. `item > 3`
   on a string column (CheckTest.scala:193) and `unique < 4` (AnalyzerTests.scala:551-558), on
-  the device through DQ_P_CAST_DOUBLE; a number off the exact parse path is reported per op;
+  the device through DQ_P_CAST_DOUBLE, correctly rounded for every input (no fall-back);
 * FloatType comparisons with integer literals above 2^24 (float vs int -> FloatType);
 * fp64 sums of values of opposite sign near DBL_MAX, in both scan kernels;
 * runOnAggregatedStates over loaders holding GPU-computed partition states
@@ -90,20 +90,22 @@ def test_string_to_double_cast_in_predicates(gpu):
             _check_state(b, d.run_scan([b], pt)[b], ot)
 
 
-def test_string_to_double_off_fast_path_is_reported_per_op(gpu):
-    """A number the device cannot convert exactly (> 19 significant digits) fails that op only
-    (dq_plan_op_status): the other analyzers of the same fused pass still succeed."""
-    spec = {"item": ["string", ["1", "2", "12345678901234567890123", "4"]], "v": ["int32", [1, 2, 3, 4]]}
-    pt = product_table(spec)
+def test_string_to_double_beyond_fast_path_is_exact(gpu):
+    """Numbers off Clinger's fast path (> 19 significant digits, |exponent| > 22, hexadecimal,
+    halfway points) cast exactly on the device (Eisel-Lemire + the big-integer comparison), so
+    the op succeeds and matches the oracle's Java parseDouble (the fused pass's other analyzers
+    are unaffected)."""
+    vals = ["1", "2", "12345678901234567890123", "4", "3.0000000000000000000000001", "2.9999999999999999999999",
+            "0x1.8p1", "3e-400", "1e400", "3.000000000000000444089209850062616169452667236328125"]
+    spec = {"item": ["string", vals], "v": ["int32", list(range(1, len(vals) + 1))]}
+    pt, ot = product_table(spec), oracle_table(spec)
     cast_op = d.Compliance("cast", "item > 3")
     others = [d.Size(), d.Sum("v"), d.Compliance("plain", "v > 2")]
     ctx = d.AnalysisRunner.onData(pt).addAnalyzers([cast_op] + others).run()
-    m = ctx.metric(cast_op)
-    assert isinstance(m.value, Failure), m
-    assert "fast path" in str(m.value.exception), m
-    assert ctx.metric(d.Size()).value.get() == 4.0
-    assert ctx.metric(d.Sum("v")).value.get() == 10.0
-    assert ctx.metric(d.Compliance("plain", "v > 2")).value.get() == 0.5
+    assert ctx.metric(cast_op).value.get() == O.compliance_state(ot, "item > 3").metric_value()
+    assert ctx.metric(d.Size()).value.get() == float(len(vals))
+    assert ctx.metric(d.Sum("v")).value.get() == float(sum(range(1, len(vals) + 1)))
+    assert ctx.metric(d.Compliance("plain", "v > 2")).value.get() == (len(vals) - 2) / len(vals)
 
 
 def test_reference_string_cast_known_answers(gpu):

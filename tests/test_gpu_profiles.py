@@ -197,11 +197,37 @@ def test_cast_to_double_matches_java(gpu):
             assert g is not None and struct.pack("<d", g) == struct.pack("<d", want), (v, g, want)
 
 
-def test_cast_off_fast_path_is_unsupported(gpu):
-    col = d.Column.from_pylist(["1.25", "3.14159265358979323846264"], "string")
-    from deequ_amd._lib import UnsupportedOnGpu
-    with pytest.raises(UnsupportedOnGpu):
-        cast_string_column(col, "float64")
+def test_cast_to_double_full_range_on_device(gpu):
+    """dq_cast_utf8 on the device, bit for bit against the oracle's Java parseDouble, for the
+    inputs off Clinger's fast path (the CPU test of the host build, tests/test_numparse.py, uses
+    the same generators): > 19 significant digits, exponents across the whole range, exact
+    halfway points and one digit either side, 700-1200-digit strings, subnormals, overflow,
+    hexadecimal literals, malformed strings.  Strings of <= 24 bytes take the word-loaded path,
+    longer ones the pointer path."""
+    import random
+    from test_numparse import halfway_strings, random_decimal
+    rng = random.Random(2024)
+    vals = [random_decimal(rng) for _ in range(20000)] + halfway_strings(rng, 1500)
+    vals += ["3.14159265358979323846264", "1.7976931348623158e308", "2.4703282292062328e-324", "0x1.8p1",
+             "0x1.fffffffffffff8p1023", "1" + "0" * 400 + "e-400", "-0.0", "1e-400", "1e400", "x", "", None]
+    for _ in range(50):
+        n = rng.randint(700, 1200)
+        dg = "".join(rng.choice("0123456789") for _ in range(n))
+        vals.append(dg[0] + "." + dg[1:] + "e" + str(rng.randint(-330, 300)))
+    col = d.Column.from_pylist(vals, "string")
+    got = cast_string_column(col, "float64").to_pylist()
+    bad = []
+    for v, g in zip(vals, got):
+        want = None if v is None else O.java_parse_double(v)
+        if want is None or g is None:
+            ok = want is None and g is None
+        elif math.isnan(want):
+            ok = math.isnan(g)
+        else:
+            ok = struct.pack("<d", g) == struct.pack("<d", want)
+        if not ok:
+            bad.append((v, g, want))
+    assert not bad, bad[:5]
 
 
 # ---- ColumnProfiler known answers
@@ -300,11 +326,9 @@ def test_string_pass_datatype_and_hll_match_oracle(gpu, monkeypatch, n):
     assert states[("1", None)] == states[("0", None)] and states[("1", "w > 0")] == states[("0", "w > 0")]
 
 
-@pytest.mark.parametrize("knob", ["0", "1"])
-def test_string_hll_only_paths_match_oracle(gpu, monkeypatch, knob):
-    """ApproxCountDistinct of string columns alone: the HLL kernel (knob 0) and the string pass
-    without DataType (DQ_STRING_PASS_HLL=1) give the oracle's register words bit for bit."""
-    monkeypatch.setenv("DQ_STRING_PASS_HLL", knob)
+def test_string_hll_only_matches_oracle(gpu):
+    """ApproxCountDistinct of string columns alone (the HLL kernel) gives the oracle's register
+    words bit for bit."""
     rng = np.random.default_rng(77)
     n = 30000
     vals = [None if rng.random() < 0.05 else

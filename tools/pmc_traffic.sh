@@ -20,10 +20,14 @@ for C in FETCH_SIZE WRITE_SIZE; do
   if [ $st -ne 0 ]; then echo "STOP: pmc $C exit $st"; tail -5 "$D.log"; exit $st; fi
 done
 python - <<PY
-import csv, glob, json, re, collections
+import csv, glob, json, re, collections, sys
+sys.path.insert(0, ".")
+import bench
 pat = re.compile(r"""$KERNEL""")
 out = {"workload": "$WL", "kernel_regex": r"""$KERNEL""", "steps_profiled": $STEPS + 1,
-       "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, one pass each; read = 2 x FETCH_SIZE (gfx950)"}
+       "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, one pass each; read = 2 x FETCH_SIZE (gfx950)",
+       "kernel_src_digest": bench.kernel_source_digest(), "commit": "${COMMIT:-unknown}",
+       "bench_args": "${BENCH_ARGS:-}"}
 per_kernel = collections.defaultdict(lambda: {"FETCH_SIZE": 0.0, "WRITE_SIZE": 0.0, "dispatches": set()})
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     for f in glob.glob("$OUT/pmct_${WL}_%s_$TAG/**/*counter_collection.csv" % c, recursive=True):
