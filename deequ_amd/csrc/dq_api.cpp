@@ -72,7 +72,8 @@ static bool valid_type(int t) { return t >= DQ_T_BOOL && t <= DQ_T_UTF8; }
 // every hipFree synchronises the device -- a profiler run creates and drops dozens of small
 // tables and plans, each free a device-wide stall.  Freed blocks are therefore kept per device
 // and handed out again (best fit within 2x of the request).  A block may still be in use by a
-// stream when it is freed: it is reused only after a device synchronisation.  On an allocation
+// stream when it is freed: it is reused only after a device synchronisation (taken outside the
+// pool's lock; one sync fences every block released before it began).  On an allocation
 // failure the device's cached blocks are released and the allocation retried.
 class BlockPool {
  public:
@@ -86,7 +87,7 @@ class BlockPool {
 
   hipError_t alloc(int dev, size_t bytes, void** out) {
     if (bytes >= kPoolMin) {
-      std::lock_guard<std::mutex> g(mu_);
+      std::unique_lock<std::mutex> g(mu_);
       int best = -1;
       for (size_t i = 0; i < blocks_.size(); ++i) {
         const Blk& b = blocks_[i];
@@ -95,15 +96,26 @@ class BlockPool {
           best = (int)i;
       }
       if (best >= 0) {
-        if (!blocks_[best].fenced) {
-          hipError_t e = hipDeviceSynchronize();
-          if (e != hipSuccess) return e;
-          for (Blk& b : blocks_)
-            if (b.dev == dev) b.fenced = true;
-        }
-        *out = blocks_[best].ptr;
-        cached_ -= blocks_[best].bytes;
+        // claim the block, then (if work on it may still be queued) synchronise the device
+        // OUTSIDE the lock: other threads' allocations and releases proceed meanwhile (the
+        // profiler runs several group-bys on their own streams at once)
+        const Blk blk = blocks_[best];
+        cached_ -= blk.bytes;
         blocks_.erase(blocks_.begin() + best);
+        if (!blk.fenced) {
+          const uint64_t upto = seq_;  // every block released so far is fenced by this sync
+          g.unlock();
+          hipError_t e = hipDeviceSynchronize();
+          g.lock();
+          if (e != hipSuccess) {
+            blocks_.push_back(blk);
+            cached_ += blk.bytes;
+            return e;
+          }
+          for (Blk& b : blocks_)
+            if (b.dev == dev && b.seq <= upto) b.fenced = true;
+        }
+        *out = blk.ptr;
         return hipSuccess;
       }
     }
@@ -122,7 +134,7 @@ class BlockPool {
       return;
     }
     std::lock_guard<std::mutex> g(mu_);
-    blocks_.push_back(Blk{ptr, bytes, dev, false});
+    blocks_.push_back(Blk{ptr, bytes, dev, false, ++seq_});
     cached_ += bytes;
     while (cached_ > kPoolMaxCached && !blocks_.empty()) {  // drop the oldest
       cached_ -= blocks_.front().bytes;
@@ -150,10 +162,12 @@ class BlockPool {
     size_t bytes;
     int dev;
     bool fenced;
+    uint64_t seq;  // release order
   };
   std::mutex mu_;
   std::vector<Blk> blocks_;
   size_t cached_ = 0;
+  uint64_t seq_ = 0;
 };
 
 // Streams and pinned host blocks are recycled too: the profiler creates dozens of plans and
