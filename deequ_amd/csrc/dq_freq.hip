@@ -709,11 +709,12 @@ __global__ __launch_bounds__(kBlock) void dq_freq_part_scatter_kernel(FreqTable 
 
 // ---- sorted-bucket path ---------------------------------------------------------------------
 // High-cardinality group-by without a device-scope atomic per row:
-//  1. stage (one streaming pass): every selected row becomes a 16-B record plus a 32-bit sort
-//     key (the top hash bits), and feeds an HLL sketch of the hashes that sizes the table.  A
-//     workgroup owns a contiguous row range and reserves its output with ONE atomic (its rows
-//     are counted from the validity bitmaps first), so no address takes an atomic per wave;
-//  2. sort: rocPRIM radix sort of (key, record) on the top log2(#slices) key bits (dq_sort.hip);
+//  1. stage (one streaming pass): every selected row becomes a 16-B record and feeds an HLL
+//     sketch of the hashes that sizes the table.  A workgroup owns a contiguous row range and
+//     reserves its output with ONE atomic (its rows are counted from the validity bitmaps
+//     first), so no address takes an atomic per wave;
+//  2. bucket split: the records grouped by slice (the top log2(#slices) hash bits) with exact
+//     counts, two LDS multi-split levels (dq_freq_split_kernel below);
 //  3. agg: one work item per slice's bucket.  A bucket of at most kFreqAggPiece records is one work
 //     item: its slice is loaded into LDS, the records are counted there and the slice is written
 //     back with plain stores (the workgroup owns it).  A larger bucket (a hot key, or Histogram's
@@ -736,7 +737,8 @@ __device__ inline void rec_unpack(const FreqRec& r, unsigned long long* k1, uint
 }
 
 // HLL sketch of the staged hashes (p = 9): an estimate of the number of distinct keys, used
-// only to size the table before aggregation.
+// only to size the table before aggregation.  (Sketching a 1/8 hash-based sample instead
+// measured no faster on C4: 1.341 vs 1.341 ms per stage launch.)
 __device__ inline void sketch_update(uint32_t* regs, uint64_t h) {
   uint32_t idx, pw;
   hll_idx_rank(h, &idx, &pw);
@@ -757,7 +759,7 @@ __device__ inline bool row_selected(const FreqKeySpec& ks, const DevColumn* cols
 // rows (validity only), one atomicAdd per block reserves the block's records, and the second
 // pass writes every selected row at its ballot prefix -- no block barrier inside either loop.
 __global__ __launch_bounds__(kBlock) void dq_freq_stage_kernel(FreqKeySpec ks, const DevColumn* __restrict__ cols,
-                                                               int64_t n_rows, FreqRec* out, uint32_t* sort_keys,
+                                                               int64_t n_rows, FreqRec* out,
                                                                unsigned long long* cursor, uint32_t* hll,
                                                                unsigned long long* long_key) {
   __shared__ uint32_t regs[kHllM];
@@ -797,11 +799,9 @@ __global__ __launch_bounds__(kBlock) void dq_freq_stage_kernel(FreqKeySpec ks, c
       Key k;
       bool too_long;
       FreqRec r;
-      uint32_t key32 = 0xFFFFFFFFu;
       if (make_key(ks, cols, row, k, scratch, too_long) && k.len <= 15 && k.ptr == nullptr) {
         r.k0 = k.k0;
         r.k1 = k.k1 | ((unsigned long long)k.len << kRecLenShift);
-        key32 = (uint32_t)(k.hash >> 32);
         sketch_update(regs, k.hash);
       } else {  // a key longer than 15 bytes: the host rolls this batch back to the general path
         r.k0 = 0;
@@ -809,62 +809,12 @@ __global__ __launch_bounds__(kBlock) void dq_freq_stage_kernel(FreqKeySpec ks, c
         atomicMax(long_key, (unsigned long long)(k.len > 15 ? k.len : 16));
       }
       out[pos] = r;
-      sort_keys[pos] = key32;
     }
     w += (unsigned long long)__popcll(m);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < kHllM; i += kBlock)
     if (regs[i]) atomicMax(&hll[i], regs[i]);
-}
-
-// Slice ids to sort by.  Round 0: the staged keys (top 32 hash bits) shifted down to the slice
-// id in place; retry rounds: recomputed from the records a full slice handed back.  (The sort
-// then runs on bits [0, bits): rocPRIM's radix sort with begin_bit > 0 left small inputs
-// unsorted on gfx950 / ROCm 7.2, measured.)
-__global__ __launch_bounds__(kBlock) void dq_freq_slice_keys_kernel(const FreqRec* __restrict__ recs, uint64_t n,
-                                                                    int bits, int from_records, uint32_t* keys) {
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
-    uint32_t key;
-    if (from_records) {
-      const FreqRec r = recs[i];
-      unsigned long long k1;
-      uint32_t len;
-      rec_unpack(r, &k1, &len);
-      key = len == kRecHole ? 0xFFFFFFFFu : (uint32_t)(hash_inline(r.k0, k1, len) >> 32);
-    } else {
-      key = keys[i];
-    }
-    keys[i] = bits ? key >> (32 - bits) : 0u;
-  }
-}
-
-__device__ inline uint64_t key_slice(uint32_t key, int /*bits*/) { return key; }  // keys hold slice ids
-
-__device__ inline uint64_t first_at_or_above(const uint32_t* keys, uint64_t n, int bits, uint64_t b) {
-  uint64_t lo = 0, hi = n;
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (key_slice(keys[mid], bits) < b) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
-
-// off[b] = first sorted position of slice b (b = 0 .. n_buckets); pieces[b] = work items of b.
-__global__ __launch_bounds__(kBlock) void dq_freq_bounds_kernel(const uint32_t* __restrict__ keys, uint64_t n,
-                                                                int bits, uint64_t n_buckets, uint64_t* off,
-                                                                uint32_t* pieces) {
-  for (uint64_t b = (uint64_t)blockIdx.x * kBlock + threadIdx.x; b <= n_buckets; b += (uint64_t)gridDim.x * kBlock) {
-    const uint64_t lo = first_at_or_above(keys, n, bits, b);
-    off[b] = lo;
-    if (b < n_buckets) {
-      const uint64_t hi = first_at_or_above(keys, n, bits, b + 1);
-      pieces[b] = (uint32_t)((hi - lo + kFreqAggPiece - 1) / kFreqAggPiece);
-    } else {
-      pieces[b] = 0u;
-    }
-  }
 }
 
 // LDS slot words: K1 = EMPTY / BUSY (being published) / FOREIGN (a group this path cannot hold:
@@ -1115,7 +1065,7 @@ __global__ __launch_bounds__(kBlock) void dq_freq_agg_kernel(FreqTable T, const 
   }
 }
 
-// ---- partition path (replaces the radix sort for large stagings) --------------------------
+// ---- partition path (large stagings: no counting pass, fixed-capacity regions) -------------
 // Two passes of an LDS multi-split put every staged record into the region of its slice:
 //  P1: stage array -> 2^b1 level-1 regions (top b1 bits of the table hash);
 //  P2: each level-1 region -> the 2^(bits-b1) slice regions under it.
@@ -1172,7 +1122,10 @@ template <int PER, int MAXB>
 __device__ inline void part_tile(PartLdsT<MAXB>& L, const FreqRec (&rec)[PER], uint32_t (&bin)[PER],
                                  uint32_t nb, uint64_t base_id, FreqRec* __restrict__ out, uint64_t out_cap,
                                  unsigned long long* out_fill, FreqRec* ovf, unsigned long long* ovf_n,
-                                 uint64_t ovf_cap, unsigned int* flag, unsigned long long* staged) {
+                                 uint64_t ovf_cap, unsigned int* flag, unsigned long long* staged,
+                                 const unsigned long long* region_start = nullptr) {
+  // region_start != nullptr: exact regions -- output region id starts at record region_start[id]
+  // of `out` (sizes counted beforehand: nothing can overflow), out_fill is its cursor
   const uint32_t t = threadIdx.x;
   for (uint32_t i = t; i < nb; i += kPartThreads) L.hist[i] = 0u;
   __syncthreads();
@@ -1211,6 +1164,7 @@ __device__ inline void part_tile(PartLdsT<MAXB>& L, const FreqRec (&rec)[PER], u
   for (uint32_t b = t; b < nb; b += kPartThreads) {
     const uint32_t c = L.hist[b];
     L.gbase[b] = c ? atomicAdd(&out_fill[base_id + b], (unsigned long long)c) : 0ull;
+    if (region_start && c) L.gbase[b] += region_start[base_id + b];
   }
   const uint32_t total = L.total;
   __syncthreads();
@@ -1231,7 +1185,9 @@ __device__ inline void part_tile(PartLdsT<MAXB>& L, const FreqRec (&rec)[PER], u
       const uint32_t b = L.bin[j];
       const uint64_t o = L.gbase[b] + (r0 + j - L.start[b]);
       const FreqRec r = L.rec[j];
-      if (o < out_cap) {
+      if (region_start) {
+        st_rec(out + o, r);
+      } else if (o < out_cap) {
         st_rec(out + (base_id + b) * out_cap + o, r);
       } else {  // the region is full: the overflow list (aggregated by the sort path)
         const unsigned long long k = atomicAdd(ovf_n, 1ull);
@@ -1287,6 +1243,166 @@ __global__ __launch_bounds__(kPartThreads) void dq_freq_part_kernel(
     }
   }
   part_tile(L, rec, bin, nb, base_id, out, out_cap, out_fill, ovf, ovf_n, ovf_cap, flag, nullptr);
+}
+
+// ---- bucket split: the sort path's grouping of staged records by slice (small stagings, and the
+// partition path's retry / skew fall-backs), hand-written on the same LDS multi-split: a slice id
+// of `bits` (<= 22) hash bits is split in two levels, b1 = min(bits, 11) high bits, then the low
+// b2 = bits - b1 bits inside each level-1 region.  Each level COUNTS first (one device atomic per
+// (tile, non-empty bin)), the counts are scanned into exact region starts, and the SCATTER pass
+// writes every record inside its region (one atomic cursor add per (tile, bin)): nothing can
+// overflow, a hot key costs one atomic per tile, and level 2's counts are the per-slice record
+// counts the aggregation's work items come from.  Holes (length byte 0xFF) are dropped.
+//   level 1 (in_off == nullptr): tile blockIdx.x of in[0, n), bin = slice >> b2, id = bin;
+//   level 2: tile blockIdx.x of region y = blockIdx.y, in[in_off[y], in_off[y + 1]),
+//            bin = slice & (2^b2 - 1), id = (y << b2) | bin = the slice.
+// count != nullptr: add the bins' counts to count[id]; else scatter to out (region_start, cursor).
+__global__ __launch_bounds__(kPartThreads) void dq_freq_split_kernel(
+    const FreqRec* __restrict__ in, uint64_t n, const unsigned long long* __restrict__ in_off, int bits, int b2,
+    unsigned long long* count, FreqRec* __restrict__ out, const unsigned long long* __restrict__ region_start,
+    unsigned long long* cursor) {
+  __shared__ PartLdsT<(1 << kPartMaxBinBits)> L;
+  const uint32_t t = threadIdx.x;
+  const bool level2 = in_off != nullptr;
+  const uint32_t nb = level2 ? (1u << b2) : (1u << (bits - b2));
+  uint64_t begin, end, base_id = 0;
+  if (level2) {
+    begin = in_off[blockIdx.y] + (uint64_t)blockIdx.x * kPartTile;
+    end = in_off[blockIdx.y + 1];
+    base_id = (uint64_t)blockIdx.y << b2;
+  } else {
+    begin = (uint64_t)blockIdx.x * kPartTile;
+    end = n;
+  }
+  if (begin >= end) return;
+  const uint64_t cnt_in = min((uint64_t)kPartTile, end - begin);
+  FreqRec rec[kPartPerThread];
+  uint32_t bin[kPartPerThread];
+#pragma unroll
+  for (int i = 0; i < kPartPerThread; ++i) {
+    const uint32_t j = (uint32_t)i * kPartThreads + t;
+    if (j < cnt_in) rec[i] = ld_rec(in + begin + j);
+  }
+#pragma unroll
+  for (int i = 0; i < kPartPerThread; ++i) {
+    const uint32_t j = (uint32_t)i * kPartThreads + t;
+    bin[i] = kPartNoBin;
+    if (j < cnt_in) {
+      bool hole;
+      const uint64_t h = rec_hash(rec[i], &hole);
+      const uint32_t slice = bits ? (uint32_t)(h >> (64 - bits)) : 0u;
+      if (!hole) bin[i] = level2 ? (slice & (nb - 1u)) : (slice >> b2);
+    }
+  }
+  if (count) {  // counting pass: LDS histogram, one device atomic per non-empty bin
+    for (uint32_t i = t; i < nb; i += kPartThreads) L.hist[i] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kPartPerThread; ++i)
+      if (bin[i] != kPartNoBin) atomicAdd(&L.hist[bin[i]], 1u);
+    __syncthreads();
+    for (uint32_t b = t; b < nb; b += kPartThreads) {
+      const uint32_t c = L.hist[b];
+      if (c) atomicAdd(&count[base_id + b], (unsigned long long)c);
+    }
+    return;
+  }
+  part_tile(L, rec, bin, nb, base_id, out, ~0ull, cursor, nullptr, nullptr, 0, nullptr, nullptr, region_start);
+}
+
+// Exclusive scan of n counts (in place, 64-bit): chunks of kScanChunk by one block each, the chunk
+// sums scanned by one block, then added back.  (The bucket split's region starts and the
+// aggregation's work-item numbering.)
+constexpr int kScanThreads = 1024;
+constexpr int kScanPer = 4;
+constexpr uint32_t kScanChunk = (uint32_t)kScanThreads * kScanPer;
+
+template <typename T>
+__device__ inline T block_exclusive_scan(T v, T* warp_sums, T* total) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  T incl = v;
+  for (int d = 1; d < 64; d <<= 1) {
+    const T o = __shfl_up(incl, d, 64);
+    if ((int)lane >= d) incl += o;
+  }
+  if (lane == 63) warp_sums[wave] = incl;
+  __syncthreads();
+  if (wave == 0) {
+    const uint32_t nw = blockDim.x >> 6;
+    T w = lane < nw ? warp_sums[lane] : (T)0;
+    T wi = w;
+    for (int d = 1; d < 64; d <<= 1) {
+      const T o = __shfl_up(wi, d, 64);
+      if ((int)lane >= d) wi += o;
+    }
+    if (lane < nw) warp_sums[lane] = wi - w;
+    if (lane == nw - 1) *total = wi;
+  }
+  __syncthreads();
+  return warp_sums[wave] + incl - v;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kScanThreads) void dq_scan_chunks_kernel(T* data, uint64_t n, T* sums) {
+  __shared__ T ws[kScanThreads / 64];
+  __shared__ T total;
+  const uint64_t base = (uint64_t)blockIdx.x * kScanChunk + (uint64_t)threadIdx.x * kScanPer;
+  T v[kScanPer];
+  T s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    v[k] = base + k < n ? data[base + k] : (T)0;
+    s += v[k];
+  }
+  T run = block_exclusive_scan<T>(s, ws, &total);
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    if (base + k < n) data[base + k] = run;
+    run += v[k];
+  }
+  if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+// one block: exclusive scan of the m chunk sums (in place), in rounds of kScanChunk with a carry
+template <typename T>
+__global__ __launch_bounds__(kScanThreads) void dq_scan_sums_kernel(T* sums, uint64_t m) {
+  __shared__ T ws[kScanThreads / 64];
+  __shared__ T total;
+  T carry = 0;
+  for (uint64_t r = 0; r < m; r += kScanChunk) {
+    const uint64_t base = r + (uint64_t)threadIdx.x * kScanPer;
+    T v[kScanPer];
+    T s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      v[k] = base + k < m ? sums[base + k] : (T)0;
+      s += v[k];
+    }
+    T run = carry + block_exclusive_scan<T>(s, ws, &total);
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      if (base + k < m) sums[base + k] = run;
+      run += v[k];
+    }
+    carry += total;
+    __syncthreads();  // ws / total are rewritten by the next round
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kScanThreads) void dq_scan_add_kernel(T* data, uint64_t n, const T* sums) {
+  const T add = sums[blockIdx.x];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanChunk + (uint64_t)threadIdx.x * kScanPer;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k)
+    if (base + k < n) data[base + k] += add;
+}
+
+// pieces[b] = work items of slice b's bucket (its count cut into kFreqAggPiece records), b < n
+__global__ __launch_bounds__(kBlock) void dq_freq_pieces_kernel(const unsigned long long* __restrict__ counts,
+                                                                uint64_t n, uint32_t* pieces) {
+  for (uint64_t b = (uint64_t)blockIdx.x * kBlock + threadIdx.x; b <= n; b += (uint64_t)gridDim.x * kBlock)
+    pieces[b] = b < n ? (uint32_t)((counts[b] + kFreqAggPiece - 1) / kFreqAggPiece) : 0u;
 }
 
 // Stage + level-1 partition fused: the rows of one batch become records written straight into
@@ -1478,32 +1594,58 @@ hipError_t launch_freq_part_scatter(const FreqTable& T, int n_parts, const unsig
 }
 
 hipError_t launch_freq_stage(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, FreqRec* d_out,
-                             uint32_t* d_sort_keys, unsigned long long* d_cursor, uint32_t* d_hll,
+                             unsigned long long* d_cursor, uint32_t* d_hll,
                              unsigned long long* d_long_key, hipStream_t stream) {
   if (n_rows <= 0) return hipSuccess;
   int64_t blocks = (n_rows + kBlock * 16 - 1) / (kBlock * 16);
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(dq_freq_stage_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, ks, d_cols, n_rows, d_out,
-                     d_sort_keys, d_cursor, d_hll, d_long_key);
+                     d_cursor, d_hll, d_long_key);
   return hipGetLastError();
 }
 
-hipError_t launch_freq_slice_keys(const FreqRec* d_recs, uint64_t n, int bits, int from_records, uint32_t* d_keys,
-                                  hipStream_t stream) {
+hipError_t launch_freq_split(const FreqRec* d_in, uint64_t n, const unsigned long long* d_in_off, uint64_t n_regions,
+                             uint64_t max_region, int bits, int b2, unsigned long long* d_count, FreqRec* d_out,
+                             const unsigned long long* d_region_start, unsigned long long* d_cursor, hipStream_t stream) {
+  if (bits < 0 || bits > 2 * kPartMaxBinBits || b2 < 0 || bits - b2 > kPartMaxBinBits || b2 > kPartMaxBinBits)
+    return hipErrorInvalidValue;
+  dim3 grid;
+  if (d_in_off) {
+    if (n_regions == 0 || n_regions > 65535) return hipErrorInvalidValue;
+    if (max_region == 0) return hipSuccess;
+    grid = dim3((unsigned)((max_region + kPartTile - 1) / kPartTile), (unsigned)n_regions);
+  } else {
+    if (n == 0) return hipSuccess;
+    grid = dim3((unsigned)((n + kPartTile - 1) / kPartTile));
+  }
+  hipLaunchKernelGGL(dq_freq_split_kernel, grid, dim3(kPartThreads), 0, stream, d_in, n, d_in_off, bits, b2, d_count,
+                     d_out, d_region_start, d_cursor);
+  return hipGetLastError();
+}
+
+template <typename T>
+static hipError_t exclusive_scan(T* d_data, uint64_t n, T* d_sums, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  uint64_t blocks = (n + kBlock * 8 - 1) / (kBlock * 8);
-  if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(dq_freq_slice_keys_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, d_recs, n, bits,
-                     from_records, d_keys);
+  const uint64_t chunks = (n + kScanChunk - 1) / kScanChunk;
+  hipLaunchKernelGGL(dq_scan_chunks_kernel<T>, dim3((unsigned)chunks), dim3(kScanThreads), 0, stream, d_data, n, d_sums);
+  if (chunks > 1) {
+    hipLaunchKernelGGL(dq_scan_sums_kernel<T>, dim3(1), dim3(kScanThreads), 0, stream, d_sums, chunks);
+    hipLaunchKernelGGL(dq_scan_add_kernel<T>, dim3((unsigned)chunks), dim3(kScanThreads), 0, stream, d_data, n,
+                       static_cast<const T*>(d_sums));
+  }
   return hipGetLastError();
 }
+hipError_t scan_exclusive_u64(unsigned long long* d_data, uint64_t n, unsigned long long* d_sums, hipStream_t stream) {
+  return exclusive_scan<unsigned long long>(d_data, n, d_sums, stream);
+}
+hipError_t scan_exclusive_u32(uint32_t* d_data, uint64_t n, uint32_t* d_sums, hipStream_t stream) {
+  return exclusive_scan<uint32_t>(d_data, n, d_sums, stream);
+}
 
-hipError_t launch_freq_bounds(const uint32_t* d_sorted_keys, uint64_t n, int bits, uint64_t n_buckets,
-                              uint64_t* d_off, uint32_t* d_pieces, hipStream_t stream) {
-  uint64_t blocks = (n_buckets + 1 + kBlock - 1) / kBlock;
+hipError_t launch_freq_pieces(const unsigned long long* d_counts, uint64_t n, uint32_t* d_pieces, hipStream_t stream) {
+  uint64_t blocks = (n + 1 + kBlock - 1) / kBlock;
   if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(dq_freq_bounds_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, d_sorted_keys, n, bits,
-                     n_buckets, d_off, d_pieces);
+  hipLaunchKernelGGL(dq_freq_pieces_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, d_counts, n, d_pieces);
   return hipGetLastError();
 }
 

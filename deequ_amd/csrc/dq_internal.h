@@ -232,20 +232,24 @@ hipError_t launch_freq_part_count(const FreqTable& T, int n_parts, unsigned long
 hipError_t launch_freq_part_scatter(const FreqTable& T, int n_parts, const unsigned long long* d_base,
                                     unsigned long long* d_cursor, FreqSlot* out_groups, uint8_t* out_keys,
                                     hipStream_t stream);
-// Sorted-bucket path (dq_freq.hip, dq_sort.hip): stage rows as FreqRec + a 32-bit sort key (top
-// hash bits) + an HLL sketch of their hashes (to size the table), sort by the key's top `bits`
-// bits (the slice), then aggregate every slice's bucket in LDS (split buckets merge atomically).
+// Sorted-bucket path (dq_freq.hip): stage rows as FreqRec + an HLL sketch of their hashes (to size
+// the table), group them by slice (the bucket split below), then aggregate every slice's bucket
+// in LDS (split buckets merge atomically).
 hipError_t launch_freq_stage(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, FreqRec* d_out,
-                             uint32_t* d_sort_keys, unsigned long long* d_cursor, uint32_t* d_hll, unsigned long long* d_long_key,
+                             unsigned long long* d_cursor, uint32_t* d_hll, unsigned long long* d_long_key,
                              hipStream_t stream);
-hipError_t launch_freq_slice_keys(const FreqRec* d_recs, uint64_t n, int bits, int from_records, uint32_t* d_keys,
-                                  hipStream_t stream);
-hipError_t sort_freq_records(void* d_tmp, size_t& tmp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
-                             const FreqRec* recs_in, FreqRec* recs_out, uint64_t n, int bits, hipStream_t stream);
-hipError_t scan_freq_pieces(void* d_tmp, size_t& tmp_bytes, const uint32_t* pieces, uint32_t* piece_start,
-                            uint64_t n, hipStream_t stream);
-hipError_t launch_freq_bounds(const uint32_t* d_sorted_keys, uint64_t n, int bits, uint64_t n_buckets,
-                              uint64_t* d_off, uint32_t* d_pieces, hipStream_t stream);
+// The bucket split (dq_freq.hip): level 1 (d_in_off == nullptr) over d_in[0, n) by the top
+// bits - b2 slice bits, level 2 over the n_regions exact regions of d_in_off by the low b2 bits;
+// d_count != nullptr counts (adds to d_count[id]), else scatters into d_out at d_region_start[id]
+// + cursor.  max_region: the largest level-2 input region.
+hipError_t launch_freq_split(const FreqRec* d_in, uint64_t n, const unsigned long long* d_in_off, uint64_t n_regions,
+                             uint64_t max_region, int bits, int b2, unsigned long long* d_count, FreqRec* d_out,
+                             const unsigned long long* d_region_start, unsigned long long* d_cursor, hipStream_t stream);
+// In-place exclusive scans (d_sums: ceil(n / 4096) scratch words).
+hipError_t scan_exclusive_u64(unsigned long long* d_data, uint64_t n, unsigned long long* d_sums, hipStream_t stream);
+hipError_t scan_exclusive_u32(uint32_t* d_data, uint64_t n, uint32_t* d_sums, hipStream_t stream);
+// pieces[b] = aggregation work items of slice b (b < n), pieces[n] = 0
+hipError_t launch_freq_pieces(const unsigned long long* d_counts, uint64_t n, uint32_t* d_pieces, hipStream_t stream);
 hipError_t launch_freq_agg(const FreqTable& T, const FreqRec* d_recs, const uint64_t* d_off,
                            const uint32_t* d_piece_start, uint64_t n_buckets, uint64_t max_items, int table_empty,
                            FreqRec* d_retry, unsigned long long* d_n_retry, unsigned long long* d_new_groups,
