@@ -141,3 +141,31 @@ def test_few_group_hint_single_launch_and_fallback(gpu, distinct, hint):
     u, c = np.unique(vals[valid], return_counts=True)
     assert s.num_groups == len(u)
     assert got == dict(zip(u.tolist(), c.tolist()))
+
+
+@pytest.mark.parametrize("hot_frac", [0.0, 0.3])
+def test_bucket_split_two_levels(gpu, monkeypatch, hot_frac):
+    """The sort path's hand-written bucket split at > 2^11 slices (two multi-split levels: the
+    top 11 slice bits, then the rest inside each level-1 region), with and without a hot key
+    (one atomic per tile, not per record): exact group counts against numpy."""
+    monkeypatch.setenv("DQ_FREQ_PART", "0")  # every record through the sort path
+    rng = np.random.default_rng(11)
+    n = 9_000_000
+    vals = rng.integers(0, 6_000_000, n)
+    if hot_frac:
+        vals[rng.random(n) < hot_frac] = 987_654_321
+    table = d.Table({"v": d.Column.from_numpy(vals, None, "int64")})
+    t = FrequencyTable(["v"], {"v": "int64"})
+    t.consume(table)
+    s = t.summary()
+    p = t.paths()
+    u, c = np.unique(vals, return_counts=True)
+    assert p["slots"] >= (1 << 23) and p["sort_records"] >= n, p  # >= 2^12 slices: two levels
+    assert s.num_groups == len(u)
+    assert s.num_unique == int((c == 1).sum())
+    assert s.grouped_rows == n
+    hist = np.bincount(c)
+    ent = -sum(float(k) * (cc / n) * np.log(cc / n) for cc, k in enumerate(hist) if k and cc)
+    assert abs(s.entropy - ent) <= 1e-12 * abs(ent)
+    counts, keys = t.top(3)
+    assert sorted(counts.tolist(), reverse=True)[:3] == sorted(c.tolist(), reverse=True)[:3]

@@ -358,6 +358,45 @@ __global__ __launch_bounds__(256) void k_mx_ds_alignbit(Stamp* st, uint32_t* sin
   if (regs[threadIdx.x] + r == 0x5a5a5a5au) sink[0] = 1;
 }
 
+// Dependent-issue latency: ONE chain per wave (each instruction waits for the previous one), run
+// with one wave per SIMD (see main: "lat" rows) -- cycles per instruction = the latency seen by a
+// dependent instruction of the same wave.
+#define L64(NAME, ASM)                                                                      \
+  __global__ __launch_bounds__(256) void k_##NAME(Stamp* st, uint32_t* sink, uint32_t seed) { \
+    uint64_t a0 = threadIdx.x ^ seed;                                                         \
+    uint64_t b = seed * 3ull + 0x9e3779b97f4a7c15ull, c = seed + 0x123456789ull;              \
+    unsigned long long t0, r0;                                                                \
+    stamp_begin(st, t0, r0);                                                                  \
+    for (int i = 0; i < kIters; ++i) {                                                        \
+      _Pragma("unroll") for (int u = 0; u < kUnroll * 8; ++u)                                 \
+        asm volatile(ASM : "+v"(a0) : "v"(b), "v"(c));                                        \
+    }                                                                                         \
+    stamp_end(st, t0, r0);                                                                    \
+    if (a0 == 0x5a5a5a5aull) sink[0] = (uint32_t)a0;                                          \
+  }
+#define L32(NAME, ASM)                                                                      \
+  __global__ __launch_bounds__(256) void k_##NAME(Stamp* st, uint32_t* sink, uint32_t seed) { \
+    uint32_t a0 = threadIdx.x ^ seed;                                                         \
+    uint32_t b = seed * 3u + 0x9e3779b9u, c = seed + 0x12345u;                                \
+    unsigned long long t0, r0;                                                                \
+    stamp_begin(st, t0, r0);                                                                  \
+    for (int i = 0; i < kIters; ++i) {                                                        \
+      _Pragma("unroll") for (int u = 0; u < kUnroll * 8; ++u)                                 \
+        asm volatile(ASM : "+v"(a0) : "v"(b), "v"(c));                                        \
+    }                                                                                         \
+    stamp_end(st, t0, r0);                                                                    \
+    if (a0 == 0x5a5a5a5au) sink[0] = a0;                                                      \
+  }
+L64(lat_add_f64, "v_add_f64 %0, %0, %1")
+L64(lat_fma_f64, "v_fma_f64 %0, %0, %1, %2")
+L64(lat_min_f64, "v_min_f64 %0, %0, %1")
+L64(lat_lshl_add_u64, "v_lshl_add_u64 %0, %0, 0, %1")
+L32(lat_add_u32, "v_add_u32 %0, %0, %1")
+L32(lat_xor_b32, "v_xor_b32 %0, %0, %1")
+L32(lat_mul_lo_u32, "v_mul_lo_u32 %0, %0, %1")
+L32(lat_alignbit_b32, "v_alignbit_b32 %0, %0, %1, 7")
+L32(lat_bitop3_b32, "v_bitop3_b32 %0, %0, %1, %2 bitop3:0x36")
+
 typedef void (*KFn)(Stamp*, uint32_t*, uint32_t);
 struct Entry { const char* name; KFn fn; };
 #define E(n) {#n, k_##n}
@@ -456,6 +495,23 @@ int main() {
     const double cpi_wall = (ms * 1e-3) * clk[blocks / 2] * 1e9 * (cus * 4.0) / wave_insts;
     printf("%s  {\"insn\": \"%s\", \"cyc_per_wave_insn_per_simd\": %.3f, \"wall_based\": %.3f, \"ghz\": %.3f, \"ms\": %.3f}",
            first ? "" : ",\n", en.name, cpi, cpi_wall, clk[blocks / 2], ms);
+    first = false;
+  }
+  printf("\n], \"latency\": [\n");
+  // one wave per SIMD (64-thread blocks, 4 per CU), one dependency chain per wave
+  static const Entry kLat[] = {E(lat_add_f64), E(lat_fma_f64), E(lat_min_f64), E(lat_lshl_add_u64), E(lat_add_u32),
+                               E(lat_xor_b32), E(lat_mul_lo_u32), E(lat_alignbit_b32), E(lat_bitop3_b32)};
+  const int lblocks = cus * 4;
+  first = true;
+  for (const Entry& en : kLat) {
+    for (int rep = 0; rep < 2; ++rep) hipLaunchKernelGGL(en.fn, dim3(lblocks), dim3(64), 0, 0, d_st, d_sink, 7u + rep);
+    CHK(hipDeviceSynchronize());
+    CHK(hipMemcpy(st.data(), d_st, sizeof(Stamp) * lblocks, hipMemcpyDeviceToHost));
+    std::vector<double> cyc(lblocks);
+    for (int b = 0; b < lblocks; ++b) cyc[b] = (double)(st[b].t1 - st[b].t0);
+    std::sort(cyc.begin(), cyc.end());
+    printf("%s  {\"insn\": \"%s\", \"dependent_cycles\": %.3f}", first ? "" : ",\n", en.name,
+           cyc[lblocks / 2] / insts_per_wave);
     first = false;
   }
   printf("\n]}\n");
