@@ -222,7 +222,10 @@ def cpu_baseline(sample_rows: int, threads: int):
                 "sample": "unavailable: %s" % e}
     secs = cdq_oracle.time_c2_scan(sample_rows, threads)
     return {"value": sample_rows / secs, "unit": "rows/s", "cores": threads, "kind": "port",
-            "host_cpus": os.cpu_count(),
+            "host_cpus": os.cpu_count(), "value_per_core": sample_rows / secs / threads,
+            "cores_policy": "the CPUs this process may use: affinity mask capped by OMP_NUM_THREADS (the GPU "
+                            "pool gives each GPU 16 of the host's %d; os.cpu_count() counts all 8 GPUs' share)"
+                            % (os.cpu_count() or 0),
             "sample": "%d rows x 8 cols (C2 distributions, 5%% NULL), 65 analyzers (8 HLL), C restatement "
                       "of Spark 2.2.2 aggregation (oracle/dq_oracle.c), %d threads, %.2f s"
                       % (sample_rows, threads, secs)}

@@ -105,6 +105,8 @@ DIAG_SIGNATURES = {
     "dq_diag_hash_rate": (c_int, [c_int, c_int, c_int, POINTER(c_double)]),
     "dq_diag_freq_paths": (c_int, [c_void_p, POINTER(c_int64)]),
     "dq_diag_parse_double": (c_int, [c_char_p, c_int64, POINTER(c_double), POINTER(c_int32)]),
+    "dq_diag_table_hash": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
+    "dq_diag_key_pack": (c_int, [c_char_p, c_int32, POINTER(c_uint64), c_char_p, POINTER(c_int32), POINTER(c_int32)]),
 }
 
 
@@ -205,6 +207,8 @@ def lib():
             pass
         l = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in list(SIGNATURES.items()) + list(DIAG_SIGNATURES.items()):
+            if name in DIAG_SIGNATURES and os.environ.get("DEEQU_AMD_LIB") and not hasattr(l, name):
+                continue  # (an older A/B build may lack a newer diagnostic export)
             fn = getattr(l, name)
             fn.restype = res
             fn.argtypes = args

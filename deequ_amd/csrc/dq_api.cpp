@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "dq_internal.h"
+#include "dq_keypack.h"
 #include "dq_numparse.h"
 #include "../../include/deequ_amd_diag.h"
 #include "hll_p9_tables.h"
@@ -338,6 +339,29 @@ extern "C" dq_status dq_diag_hash_rate(int device, int with_hll, int reps, doubl
   if (sink) (void)hipFree(sink);
   if (e != hipSuccess) return fail(DQ_ERR_DEVICE, std::string("dq_diag_hash_rate: ") + hipGetErrorString(e));
   *hashes_per_sec = (double)blocks * kBlock * 4.0 * iters / (best * 1e-3);
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_diag_table_hash(int device, const uint64_t* k0, const uint64_t* k1, const uint32_t* len,
+                                        int64_t n, uint64_t* out) {
+  if (n < 0 || (n > 0 && (!k0 || !k1 || !len || !out))) return fail(DQ_ERR_INVALID, "bad argument");
+  if (n == 0) return DQ_OK;
+  DQ_HIP(hipSetDevice(device));
+  void* d = nullptr;
+  const size_t bytes = (size_t)n * (8 + 8 + 4 + 16);
+  DQ_HIP(hipMalloc(&d, bytes));
+  uint8_t* b = static_cast<uint8_t*>(d);
+  uint64_t* d_k0 = reinterpret_cast<uint64_t*>(b);
+  uint64_t* d_k1 = d_k0 + n;
+  uint64_t* d_out = d_k1 + n;
+  uint32_t* d_len = reinterpret_cast<uint32_t*>(d_out + 2 * n);
+  hipError_t e = hipMemcpy(d_k0, k0, n * 8, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d_k1, k1, n * 8, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d_len, len, n * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = launch_freq_hash(d_k0, d_k1, d_len, n, d_out, nullptr);
+  if (e == hipSuccess) e = hipMemcpy(out, d_out, n * 16, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(DQ_ERR_DEVICE, std::string("dq_diag_table_hash: ") + hipGetErrorString(e));
   return DQ_OK;
 }
 
@@ -1834,6 +1858,27 @@ extern "C" dq_status dq_diag_parse_double(const uint8_t* s, int64_t n, double* o
   double v = 0.0;
   *ok = numparse::parse_double(HostBytes{s}, (int32_t)n, &v);
   *out = v;
+  return DQ_OK;
+}
+
+// Host build of the group-by's digit-key packing (dq_keypack.h): the record word of a key of
+// <= 15 bytes, and the key bytes it unpacks to.
+extern "C" dq_status dq_diag_key_pack(const uint8_t* key, int32_t len, uint64_t* packed, uint8_t* back,
+                                      int32_t* back_len, int32_t* ok) {
+  if ((!key && len > 0) || !packed || !back || !back_len || !ok || len < 0) return fail(DQ_ERR_INVALID, "bad argument");
+  *ok = 0;
+  if (len > 15) return DQ_OK;
+  uint64_t k[2] = {0, 0};
+  std::memcpy(k, key, (size_t)len);
+  uint64_t p = 0;
+  if (!dq::kp_pack_record(k[0], k[1], (uint32_t)len, &p)) return DQ_OK;
+  uint64_t u[2];
+  uint32_t n = 0;
+  dq::kp_unpack(p, &u[0], &u[1], &n);
+  std::memcpy(back, u, n);
+  *back_len = (int32_t)n;
+  *packed = p;
+  *ok = 1;
   return DQ_OK;
 }
 

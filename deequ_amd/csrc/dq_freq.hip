@@ -21,6 +21,9 @@
 // find room there go straight to the global table.  Low-cardinality / skewed columns therefore
 // cost one global atomic per (workgroup, key) instead of one per row.
 #include "dq_internal.h"
+#include "dq_keypack.h"
+
+#include <type_traits>
 
 namespace dq {
 
@@ -93,7 +96,7 @@ __device__ uint64_t xxh64_any(const uint8_t* p, uint32_t len, uint64_t seed) {
 // record.  Its bins measured Poisson-spread (std/sqrt(mean) 0.97-1.0) over the slice, slot and
 // region bits for C4's 12-digit keys, sequential decimal strings and small / shifted integers.
 // (The length goes into k1's top byte, which an inline key of <= 15 bytes leaves zero.)
-__device__ inline uint64_t hash_inline(uint64_t k0, uint64_t k1, uint32_t len) {
+__device__ inline uint64_t hash_raw(uint64_t k0, uint64_t k1, uint32_t len) {
   const uint64_t a = (k0 + 0x165667B19E3779F9ull) * 0x9E3779B97F4A7C15ull;
   const uint64_t b = (k1 ^ ((uint64_t)len << 56) ^ 0x27D4EB2F165667C5ull) * 0xC2B2AE3D27D4EB4Full;
   uint64_t h = a ^ ((b << 32) | (b >> 32));
@@ -101,6 +104,20 @@ __device__ inline uint64_t hash_inline(uint64_t k0, uint64_t k1, uint32_t len) {
   h *= 0xD6E8FEB86659FD93ull;
   return h ^ (h >> 32);
 }
+
+// The table hash of a packed digit record (dq_keypack.h): the key's bytes are unpacked (a few
+// shifts and masks) and hashed like every other inline key, so the table and every other path
+// are unchanged by the record format.
+__device__ inline uint64_t hash_record_packed(uint64_t p) {
+  uint64_t k0, k1;
+  uint32_t len;
+  kp_unpack(p, &k0, &k1, &len);
+  return hash_raw(k0, k1, len);
+}
+
+// The table hash of an inline key, wherever a key is hashed (stage, splits, aggregations,
+// inserts, imports, lookups, rehash, owner ranks).
+__device__ inline uint64_t hash_inline(uint64_t k0, uint64_t k1, uint32_t len) { return hash_raw(k0, k1, len); }
 
 // One row's grouping key.  Inline (len <= 16) keys live in k0/k1; longer keys point at their
 // bytes (`ptr`, in the batch or in thread-local scratch).
@@ -320,16 +337,23 @@ __device__ bool heap_equal(const FreqTable& T, uint64_t off, const uint8_t* p, u
 // hands such rows back for a retry after the table grows).
 template <bool kFlagOverflow = true>
 __device__ bool global_insert(const FreqTable& T, const Key& k, unsigned long long cnt) {
+  // Every action happens inside the loop iteration and the loop ends only through `state`: a
+  // lane that waits for another lane of its own wave to publish a slot must see that publish in
+  // its next iteration.  (With the publish on an exit path -- `return` right after it -- the
+  // compiler may move it behind the loop, after the lanes that wait for it.)
   const uint32_t tag = tag_of(k.hash);
   const bool inl = k.len <= 16;
   const unsigned long long want = ((unsigned long long)tag << 32) | (inl ? 0ull : kHeapKey) | k.len;
   uint64_t probes = 0;
   uint64_t slot = probe_slot(T, k.hash, 0);
   uint32_t waits = 0;
-  while (probes < kFreqSliceSlots) {
+  int state = 0;  // 0 = probing, 1 = counted, 2 = no room in the slice, 3 = key heap full
+  while (state == 0) {
     FreqSlot* e = &T.slots[slot];
-    unsigned long long c = atomicCAS(&e->ctrl, 0ull, want);
+    const unsigned long long c = atomicCAS(&e->ctrl, 0ull, want);
+    bool next = false;
     if (c == 0ull) {  // claimed: publish key, count, then READY
+      bool heap_ok = true;
       if (inl) {
         atomicExch(&e->k0, (unsigned long long)k.k0);
         atomicExch(&e->k1, (unsigned long long)k.k1);
@@ -339,44 +363,49 @@ __device__ bool global_insert(const FreqTable& T, const Key& k, unsigned long lo
         if (off + bytes > T.heap_cap) {  // publish anyway so that no reader waits on the slot
           atomicOr(T.overflow, 2u);
           atomicExch(&e->k0, ~0ull);
-          atomicAdd(&e->count, cnt);
-          __hip_atomic_fetch_or(&e->ctrl, kReady, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-          return false;
+          heap_ok = false;
+        } else {
+          unsigned long long* hw = reinterpret_cast<unsigned long long*>(T.heap) + (off >> 3);
+          for (uint32_t i = 0; i < k.len; i += 8) {
+            const uint32_t n = k.len - i < 8 ? k.len - i : 8;
+            atomicExch(hw + (i >> 3), (unsigned long long)ld_partial(k.ptr + i, n));
+          }
+          atomicExch(&e->k0, off);
         }
-        unsigned long long* hw = reinterpret_cast<unsigned long long*>(T.heap) + (off >> 3);
-        for (uint32_t i = 0; i < k.len; i += 8) {
-          const uint32_t n = k.len - i < 8 ? k.len - i : 8;
-          atomicExch(hw + (i >> 3), (unsigned long long)ld_partial(k.ptr + i, n));
-        }
-        atomicExch(&e->k0, off);
       }
       atomicAdd(&e->count, cnt);
-      atomicAdd(T.n_groups, 1ull);
+      if (heap_ok) atomicAdd(T.n_groups, 1ull);
       __hip_atomic_fetch_or(&e->ctrl, kReady, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      return true;
-    }
-    if ((uint32_t)(c >> 32) == tag && (c & (kLenMask | kHeapKey)) == (want & (kLenMask | kHeapKey))) {
-      if (!(c & kReady)) {  // being published by another lane/wave: re-read this slot
-        if (++waits > (1u << 24)) break;
-        __builtin_amdgcn_s_sleep(1);
-        continue;
-      }
-      bool eq;
-      if (inl) {
-        eq = atom_read(&e->k0) == k.k0 && atom_read(&e->k1) == k.k1;
+      state = heap_ok ? 1 : 3;  // (3: heap full, flagged above with bit 2 only)
+    } else if ((uint32_t)(c >> 32) == tag && (c & (kLenMask | kHeapKey)) == (want & (kLenMask | kHeapKey))) {
+      if (!(c & kReady)) {  // being published by another lane/wave: look at this slot again
+        if (++waits > (1u << 24)) state = 2;
+        else __builtin_amdgcn_s_sleep(1);
       } else {
-        const unsigned long long off = atom_read(&e->k0);
-        eq = off + k.len <= T.heap_cap && heap_equal(T, off, k.ptr, k.len);
+        bool eq;
+        if (inl) {
+          eq = atom_read(&e->k0) == k.k0 && atom_read(&e->k1) == k.k1;
+        } else {
+          const unsigned long long off = atom_read(&e->k0);
+          eq = off + k.len <= T.heap_cap && heap_equal(T, off, k.ptr, k.len);
+        }
+        if (eq) {
+          atomicAdd(&e->count, cnt);
+          state = 1;
+        } else {
+          next = true;
+        }
       }
-      if (eq) {
-        atomicAdd(&e->count, cnt);
-        return true;
-      }
+    } else {
+      next = true;
     }
-    slot = probe_slot(T, k.hash, ++probes);
+    if (next) {
+      if (++probes < kFreqSliceSlots) slot = probe_slot(T, k.hash, probes);
+      else state = 2;
+    }
   }
-  if (kFlagOverflow) atomicOr(T.overflow, 1u);
-  return false;
+  if (state == 2 && kFlagOverflow) atomicOr(T.overflow, 1u);
+  return state == 1;
 }
 
 // Slot and tag of an inline key in a workgroup's LDS table: a 32-bit mix (two 32-bit multiplies
@@ -729,7 +758,6 @@ constexpr uint32_t kRecHole = 0xFFu;  // length byte of a record that holds no r
 // Staged records are written once and read once by the next pass (plain loads/stores: measured,
 // non-temporal records cost C4 3-4 ms because the next pass re-reads them from L2 / MALL).
 __device__ inline FreqRec ld_rec(const FreqRec* p) { return *p; }
-__device__ inline void st_rec(FreqRec* p, const FreqRec& r) { *p = r; }
 
 __device__ inline void rec_unpack(const FreqRec& r, unsigned long long* k1, uint32_t* len) {
   *len = (uint32_t)(r.k1 >> kRecLenShift);
@@ -1096,9 +1124,11 @@ constexpr int kStageGroup = 4;  // rows per thread whose loads the fused stage i
 constexpr int kStagePer = 12;   // rows per thread per fused-stage tile (register budget)
 constexpr uint32_t kStageTile = (uint32_t)kPartThreads * kStagePer;
 
-template <int MAXB>
+// R: the record type of the regions -- FreqRec (16 B: key bytes + length) or, for a staging of
+// digit keys, its packed word (uint64_t, dq_keypack.h).
+template <int MAXB, typename R = FreqRec>
 struct PartLdsT {
-  FreqRec rec[kPartSub];
+  R rec[kPartSub];
   uint16_t bin[kPartSub];
   uint32_t hist[MAXB];
   uint32_t start[MAXB];
@@ -1113,14 +1143,30 @@ __device__ inline uint64_t rec_hash(const FreqRec& r, bool* hole) {
   *hole = len == kRecHole;
   return hash_inline(r.k0, k1, len);
 }
+__device__ inline uint64_t rec_hash(uint64_t p, bool* hole) {
+  *hole = false;
+  return hash_record_packed(p);
+}
+
+// A record in the 16-byte form (what the overflow and retry lists and the sort path hold).
+__device__ inline FreqRec rec_raw(const FreqRec& r) { return r; }
+__device__ inline FreqRec rec_raw(uint64_t p) {
+  uint64_t k0, k1;
+  uint32_t len;
+  kp_unpack(p, &k0, &k1, &len);
+  FreqRec r;
+  r.k0 = k0;
+  r.k1 = k1 | ((unsigned long long)len << kRecLenShift);
+  return r;
+}
 
 // One tile's multi-split: each thread holds kPartPerThread records and their LDS bins (bin <
 // 2^bin_bits, or kPartNoBin for none); output region of a bin = base_id + bin.  Ranks come from
 // LDS atomics, the room in each region from ONE device atomic per (tile, non-empty bin), and the
 // records are written from an LDS image sorted by bin, kPartSub at a time (coalesced runs).
-template <int PER, int MAXB>
-__device__ inline void part_tile(PartLdsT<MAXB>& L, const FreqRec (&rec)[PER], uint32_t (&bin)[PER],
-                                 uint32_t nb, uint64_t base_id, FreqRec* __restrict__ out, uint64_t out_cap,
+template <int PER, int MAXB, typename R>
+__device__ inline void part_tile(PartLdsT<MAXB, R>& L, const R (&rec)[PER], uint32_t (&bin)[PER],
+                                 uint32_t nb, uint64_t base_id, R* __restrict__ out, uint64_t out_cap,
                                  unsigned long long* out_fill, FreqRec* ovf, unsigned long long* ovf_n,
                                  uint64_t ovf_cap, unsigned int* flag, unsigned long long* staged,
                                  const unsigned long long* region_start = nullptr) {
@@ -1184,14 +1230,14 @@ __device__ inline void part_tile(PartLdsT<MAXB>& L, const FreqRec (&rec)[PER], u
     for (uint32_t j = t; j < m; j += kPartThreads) {
       const uint32_t b = L.bin[j];
       const uint64_t o = L.gbase[b] + (r0 + j - L.start[b]);
-      const FreqRec r = L.rec[j];
+      const R r = L.rec[j];
       if (region_start) {
-        st_rec(out + o, r);
+        out[o] = r;
       } else if (o < out_cap) {
-        st_rec(out + (base_id + b) * out_cap + o, r);
-      } else {  // the region is full: the overflow list (aggregated by the sort path)
+        out[(base_id + b) * out_cap + o] = r;
+      } else {  // the region is full: the overflow list (16-B records, aggregated by the sort path)
         const unsigned long long k = atomicAdd(ovf_n, 1ull);
-        if (k < ovf_cap) ovf[k] = r;
+        if (k < ovf_cap) ovf[k] = rec_raw(r);
         else atomicOr(flag, 1u);
       }
     }
@@ -1203,11 +1249,12 @@ __device__ inline void part_tile(PartLdsT<MAXB>& L, const FreqRec (&rec)[PER], u
 // blockIdx.x of region blockIdx.y (in + y * in_cap, min(in_fill[y], in_cap) records).
 // A record's output region = the top id_bits of its hash; its LDS bin = the low bin_bits of
 // that id (the higher id bits are the input region's, uniform over the tile).
+template <typename R>
 __global__ __launch_bounds__(kPartThreads) void dq_freq_part_kernel(
-    const FreqRec* __restrict__ in, uint64_t in_n, const unsigned long long* __restrict__ in_fill, uint64_t in_cap,
-    int id_bits, int bin_bits, FreqRec* __restrict__ out, uint64_t out_cap, unsigned long long* out_fill,
+    const R* __restrict__ in, uint64_t in_n, const unsigned long long* __restrict__ in_fill, uint64_t in_cap,
+    int id_bits, int bin_bits, R* __restrict__ out, uint64_t out_cap, unsigned long long* out_fill,
     FreqRec* ovf, unsigned long long* ovf_n, uint64_t ovf_cap, unsigned int* flag) {
-  __shared__ PartLdsT<(1 << kPartMaxBinBits)> L;
+  __shared__ PartLdsT<(1 << kPartMaxBinBits), R> L;
   const uint32_t t = threadIdx.x;
   const uint32_t nb = 1u << bin_bits;
   uint64_t base_id = 0, begin, count;
@@ -1225,12 +1272,12 @@ __global__ __launch_bounds__(kPartThreads) void dq_freq_part_kernel(
     if (begin >= in_n) return;
     count = min((uint64_t)kPartTile, in_n - begin);
   }
-  FreqRec rec[kPartPerThread];
+  R rec[kPartPerThread];
   uint32_t bin[kPartPerThread];
 #pragma unroll
   for (int i = 0; i < kPartPerThread; ++i) {
     const uint32_t j = (uint32_t)i * kPartThreads + t;
-    if (j < count) rec[i] = ld_rec(in + begin + j);
+    if (j < count) rec[i] = in[begin + j];
   }
 #pragma unroll
   for (int i = 0; i < kPartPerThread; ++i) {
@@ -1410,12 +1457,19 @@ __global__ __launch_bounds__(kBlock) void dq_freq_pieces_kernel(const unsigned l
 // back in row order.  Tiles of kPartTile rows, grid-stride.  The sketch, the staged count and
 // the long-key flag are kept as by dq_freq_stage_kernel.  Single-string keys (the common case)
 // load their offsets, then their bytes, for all of a thread's rows at once.
-template <bool ONE_STRING>
+// PACK (single string key only): the regions hold packed digit records (uint64_t, dq_keypack.h);
+// a key that is not a digit string goes to the overflow list as a 16-B record (counted there and
+// in `staged`), and a batch with more of them than the list holds raises `flag` (the host then
+// rolls it back and stages the table's keys as 16-B records from then on).
+template <bool ONE_STRING, bool PACK>
 __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(4))) void dq_freq_stage_part_kernel(
-    FreqKeySpec ks, const DevColumn* __restrict__ cols, int64_t n_rows, int b1, FreqRec* __restrict__ out,
-    uint64_t cap1, unsigned long long* fill1, FreqRec* ovf, unsigned long long* ovf_n, uint64_t ovf_cap,
-    unsigned int* flag, uint32_t* hll, unsigned long long* long_key, unsigned long long* staged) {
-  __shared__ PartLdsT<(1 << kStageBinBits)> L;
+    FreqKeySpec ks, const DevColumn* __restrict__ cols, int64_t n_rows, int b1,
+    typename std::conditional<PACK, uint64_t, FreqRec>::type* __restrict__ out, uint64_t cap1,
+    unsigned long long* fill1, FreqRec* ovf, unsigned long long* ovf_n, uint64_t ovf_cap, unsigned int* flag,
+    uint32_t* hll, unsigned long long* long_key, unsigned long long* staged) {
+  static_assert(ONE_STRING || !PACK, "packed records are staged from one string key column");
+  using R = typename std::conditional<PACK, uint64_t, FreqRec>::type;
+  __shared__ PartLdsT<(1 << kStageBinBits), R> L;
   __shared__ uint32_t regs[kHllM];
   const uint32_t t = threadIdx.x;
   const uint32_t nb = 1u << b1;
@@ -1424,9 +1478,10 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(4)
   const DevColumn& c0 = cols[ks.key_cols[0]];
   alignas(8) uint8_t scratch[kMaxLocalKey];
   const int64_t n_tiles = (n_rows + kStageTile - 1) / kStageTile;
+  uint32_t n_side = 0;  // PACK: this thread's keys put on the overflow list (not digit strings)
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     const int64_t row0 = tile * (int64_t)kStageTile;
-    FreqRec rec[kStagePer];
+    R rec[kStagePer];
     uint32_t bin[kStagePer];
     uint32_t too_long = 0u;
     if constexpr (ONE_STRING) {
@@ -1447,9 +1502,28 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(4)
             too_long = max(too_long, len[i]);
             continue;
           }
-          const uint64_t h = hash_inline(k0[i], k1[i], len[i]);
-          rec[g + i].k0 = k0[i];
-          rec[g + i].k1 = k1[i] | ((unsigned long long)len[i] << kRecLenShift);
+          uint64_t h;
+          if constexpr (PACK) {
+            uint64_t p;
+            h = hash_raw(k0[i], k1[i], len[i]);
+            if (kp_pack_record(k0[i], k1[i], len[i], &p)) {
+              rec[g + i] = p;
+            } else {  // not a digit key: a 16-B record on the overflow list
+              sketch_update(regs, h);
+              FreqRec r;
+              r.k0 = k0[i];
+              r.k1 = k1[i] | ((unsigned long long)len[i] << kRecLenShift);
+              const unsigned long long k = atomicAdd(ovf_n, 1ull);
+              if (k < ovf_cap) ovf[k] = r;
+              else atomicOr(flag, 1u);
+              ++n_side;
+              continue;
+            }
+          } else {
+            h = hash_inline(k0[i], k1[i], len[i]);
+            rec[g + i].k0 = k0[i];
+            rec[g + i].k1 = k1[i] | ((unsigned long long)len[i] << kRecLenShift);
+          }
           bin[g + i] = (uint32_t)(h >> (64 - b1)) & (nb - 1u);
           sketch_update(regs, h);
         }
@@ -1470,8 +1544,10 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(4)
           too_long = max(too_long, k.len > 15 ? k.len : 16u);
           continue;
         }
-        rec[i].k0 = k.k0;
-        rec[i].k1 = k.k1 | ((unsigned long long)k.len << kRecLenShift);
+        if constexpr (!PACK) {
+          rec[i].k0 = k.k0;
+          rec[i].k1 = k.k1 | ((unsigned long long)k.len << kRecLenShift);
+        }
         bin[i] = (uint32_t)(k.hash >> (64 - b1)) & (nb - 1u);
         sketch_update(regs, k.hash);
       }
@@ -1479,6 +1555,7 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(4)
     if (too_long) atomicMax(long_key, (unsigned long long)too_long);
     part_tile(L, rec, bin, nb, 0, out, cap1, fill1, ovf, ovf_n, ovf_cap, flag, staged);
   }
+  if (PACK && n_side) atomicAdd(staged, (unsigned long long)n_side);
   __syncthreads();
   for (uint32_t i = t; i < (uint32_t)kHllM; i += kPartThreads)
     if (regs[i]) atomicMax(&hll[i], regs[i]);
@@ -1486,7 +1563,9 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(4)
 
 // Copy regions (min(fill, cap) records each) to out[prefix[r] ..]: the partitioned staging
 // laid out contiguously again for the sort path (rare: skew, or a table of few slices).
-__global__ __launch_bounds__(kBlock) void dq_freq_compact_kernel(const FreqRec* __restrict__ in,
+// (R = uint64_t: packed digit records, written out as 16-B records.)
+template <typename R>
+__global__ __launch_bounds__(kBlock) void dq_freq_compact_kernel(const R* __restrict__ in,
                                                                  const unsigned long long* __restrict__ fill,
                                                                  uint64_t cap, const unsigned long long* __restrict__ prefix,
                                                                  FreqRec* __restrict__ out) {
@@ -1494,7 +1573,7 @@ __global__ __launch_bounds__(kBlock) void dq_freq_compact_kernel(const FreqRec* 
   const unsigned long long f = fill[r];
   const uint64_t have = f < cap ? f : cap;
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < have; i += (uint64_t)gridDim.x * kBlock)
-    out[prefix[r] + i] = in[r * cap + i];
+    out[prefix[r] + i] = rec_raw(in[r * cap + i]);
 }
 
 // Aggregate slice region b (records b * cap .. + min(fill[b], cap)) as its slice's owner.
@@ -1545,6 +1624,167 @@ __global__ __launch_bounds__(kAggRegionThreads) __attribute__((amdgpu_waves_per_
   if (track) {
     __syncthreads();
     for (int i = threadIdx.x; i < kAggLdsHist; i += kAggRegionThreads)
+      if (L.hist[i]) atomicAdd(&tr.hist[i], (unsigned long long)L.hist[i]);
+  }
+}
+
+// The owner aggregation of slice regions of packed digit records (dq_keypack.h).  The LDS image
+// holds one word per slot -- the packed key -- so a slot is claimed AND published by one CAS
+// (no separate key publish, no busy state), and a record is counted with at most one CAS per
+// probe plus one add.  The image is unpacked into the table's key bytes once per group, at
+// write-out.  Same contract as dq_freq_agg_region_kernel (owner only; tr as there); a slice whose
+// keys overflow the image returns all of its records to the retry list as 16-B records.
+struct AggLdsP {
+  unsigned long long K[kFreqSliceSlots];
+  uint32_t C[kFreqSliceSlots];
+  int overflow;
+  uint32_t fresh;
+  uint32_t cmax;
+  unsigned long long retry_base;
+  uint32_t hist[kAggLdsHist];
+};
+
+__device__ inline bool lds_count_packed(unsigned long long* K, uint32_t* C, uint64_t p, uint64_t h) {
+  constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
+  uint32_t s = (uint32_t)(h & (S - 1));
+  for (uint32_t probe = 0; probe < S; ++probe) {
+    const unsigned long long c = atomicCAS(&K[s], kPackEmpty, (unsigned long long)p);
+    if (c == kPackEmpty || c == p) {
+      atomicAdd(&C[s], 1u);
+      return true;
+    }
+    s = (s + 1) & (S - 1);
+  }
+  return false;
+}
+
+#ifndef DQ_AGGP_BATCH
+#define DQ_AGGP_BATCH 8
+#endif
+constexpr int kAggPBatch = DQ_AGGP_BATCH;  // packed records per thread loaded together
+
+__global__ __launch_bounds__(kAggRegionThreads) __attribute__((amdgpu_waves_per_eu(DQ_AGG_WAVES))) void dq_freq_agg_packed_kernel(
+    FreqTable T, const uint64_t* __restrict__ recs, const unsigned long long* __restrict__ fill, uint64_t cap,
+    uint64_t n_slices, int table_empty, FreqRec* retry, unsigned long long* n_retry, unsigned long long* new_groups,
+    AggTrack tr) {
+  constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
+  constexpr int NT = kAggRegionThreads;
+  __shared__ AggLdsP L;
+  const bool track = tr.hist != nullptr;
+  if (track) {
+    for (int i = threadIdx.x; i < kAggLdsHist; i += NT) L.hist[i] = 0u;
+    __syncthreads();
+  }
+  for (uint64_t b = blockIdx.x; b < n_slices; b += gridDim.x) {
+    const uint64_t r0 = b * cap;
+    const unsigned long long f = fill[b];
+    const uint64_t r1 = r0 + (f < cap ? f : cap);
+    FreqSlot* slice = T.slots + (b << kFreqSliceLog);
+    // touch the item's records (one dword per 128-B line) before the image is initialised, so
+    // their HBM latency overlaps the init and the barrier (as dq_freq_agg_region_kernel)
+    uint32_t touch = 0u;
+    {
+      const uint64_t i = r0 + (uint64_t)threadIdx.x * 16u;
+      if (i < r1) touch = *reinterpret_cast<const uint32_t*>(recs + i);
+    }
+    if (r1 == r0) {
+      if (tr.write_all)
+        for (uint32_t s = threadIdx.x; s < S; s += NT) slice[s] = FreqSlot{0ull, 0ull, 0ull, 0ull};
+      if (tr.smax && threadIdx.x == 0) tr.smax[b] = 0u;
+      asm volatile("" ::"v"(touch));
+      continue;
+    }
+    for (uint32_t s = threadIdx.x; s < S; s += NT) {
+      unsigned long long k = kPackEmpty;
+      if (!table_empty) {
+        const FreqSlot e = slice[s];
+        const uint32_t len = (uint32_t)(e.ctrl & kLenMask);
+        if (e.ctrl & kReady) {
+          uint64_t p;
+          k = !(e.ctrl & kHeapKey) && len <= 15 && kp_pack_record(e.k0, e.k1, len, &p) ? p : kPackForeign;
+        }
+      }
+      L.K[s] = k;
+      L.C[s] = 0u;
+    }
+    if (threadIdx.x == 0) {
+      L.overflow = 0;
+      L.fresh = 0u;
+      L.cmax = 0u;
+    }
+    __syncthreads();
+    uint64_t rb[kAggPBatch];
+    for (uint64_t base = r0; base < r1; base += (uint64_t)NT * kAggPBatch) {
+#pragma unroll
+      for (int j = 0; j < kAggPBatch; ++j) {
+        const uint64_t i = base + (uint64_t)j * NT + threadIdx.x;
+        if (i < r1) rb[j] = recs[i];
+      }
+#pragma unroll
+      for (int j = 0; j < kAggPBatch; ++j) {
+        const uint64_t i = base + (uint64_t)j * NT + threadIdx.x;
+        if (i >= r1) continue;
+        if (!lds_count_packed(L.K, L.C, rb[j], hash_record_packed(rb[j]))) L.overflow = 1;
+      }
+    }
+    __syncthreads();
+    if (L.overflow) {  // the slice is full: leave it untouched, hand the region's rows back
+      if (threadIdx.x == 0) L.retry_base = atomicAdd(n_retry, (unsigned long long)(r1 - r0));
+      __syncthreads();
+      for (uint64_t i = r0 + threadIdx.x; i < r1; i += NT) retry[L.retry_base + (i - r0)] = rec_raw(recs[i]);
+      if (tr.write_all)  // (the table was not cleared: the slice starts out empty)
+        for (uint32_t s = threadIdx.x; s < S; s += NT) slice[s] = FreqSlot{0ull, 0ull, 0ull, 0ull};
+      if (tr.smax && threadIdx.x == 0) tr.smax[b] = 0xFFFFFFFFu;  // unknown: never skipped
+    } else {
+      for (uint32_t s = threadIdx.x; s < S; s += NT) {
+        const uint32_t c = L.C[s];
+        if (!c) {
+          if (tr.write_all) slice[s] = FreqSlot{0ull, 0ull, 0ull, 0ull};
+          continue;
+        }
+        if (track || tr.smax) {
+          atomicMax(&L.cmax, c);
+          if (track) {
+            if (c < (uint32_t)kAggLdsHist) {
+              atomicAdd(&L.hist[c], 1u);
+            } else if (c < (uint32_t)kFreqHist) {
+              atomicAdd(&tr.hist[c], 1ull);
+            } else {
+              const unsigned long long i = atomicAdd(tr.n_big, 1ull);
+              if (i < tr.big_cap) tr.big[i] = c;
+            }
+          }
+        }
+        FreqSlot& e = slice[s];
+        bool is_new = false;
+        if (!table_empty && (e.ctrl & kReady)) {
+          e.count += c;
+        } else {
+          const uint64_t p = L.K[s];
+          uint64_t k0, k1;
+          uint32_t len;
+          kp_unpack(p, &k0, &k1, &len);
+          FreqSlot n;
+          n.ctrl = ((unsigned long long)tag_of(hash_record_packed(p)) << 32) | kReady | len;
+          n.count = c;
+          n.k0 = k0;
+          n.k1 = k1;
+          e = n;
+          is_new = true;
+        }
+        const uint64_t nb = __ballot(is_new);  // one LDS add per wave, not one per new group
+        if (nb && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(nb)) atomicAdd(&L.fresh, (uint32_t)__popcll(nb));
+      }
+      __syncthreads();
+      if (threadIdx.x == 0 && L.fresh) atomicAdd(new_groups, (unsigned long long)L.fresh);
+      if (tr.smax && threadIdx.x == 0) tr.smax[b] = L.cmax;
+    }
+    __syncthreads();  // LDS is reused by the next slice
+    asm volatile("" ::"v"(touch));
+  }
+  if (track) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < kAggLdsHist; i += NT)
       if (L.hist[i]) atomicAdd(&tr.hist[i], (unsigned long long)L.hist[i]);
   }
 }
@@ -1660,10 +1900,10 @@ hipError_t launch_freq_agg(const FreqTable& T, const FreqRec* d_recs, const uint
   return hipGetLastError();
 }
 
-hipError_t launch_freq_part(const FreqRec* d_in, uint64_t in_n, const unsigned long long* d_in_fill, uint64_t in_cap,
-                            uint64_t n_in_regions, int id_bits, int bin_bits, FreqRec* d_out, uint64_t out_cap,
+hipError_t launch_freq_part(const void* d_in, uint64_t in_n, const unsigned long long* d_in_fill, uint64_t in_cap,
+                            uint64_t n_in_regions, int id_bits, int bin_bits, void* d_out, uint64_t out_cap,
                             unsigned long long* d_out_fill, FreqRec* d_ovf, unsigned long long* d_ovf_n,
-                            uint64_t ovf_cap, unsigned int* d_flag, hipStream_t stream) {
+                            uint64_t ovf_cap, unsigned int* d_flag, bool packed, hipStream_t stream) {
   if (bin_bits < 0 || bin_bits > kPartMaxBinBits || id_bits < bin_bits || id_bits > 32) return hipErrorInvalidValue;
   dim3 grid;
   if (d_in_fill) {
@@ -1673,44 +1913,60 @@ hipError_t launch_freq_part(const FreqRec* d_in, uint64_t in_n, const unsigned l
     if (in_n == 0) return hipSuccess;
     grid = dim3((unsigned)((in_n + kPartTile - 1) / kPartTile));
   }
-  hipLaunchKernelGGL(dq_freq_part_kernel, grid, dim3(kPartThreads), 0, stream, d_in, in_n, d_in_fill, in_cap, id_bits,
-                     bin_bits, d_out, out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag);
+  if (packed)
+    hipLaunchKernelGGL(dq_freq_part_kernel<uint64_t>, grid, dim3(kPartThreads), 0, stream,
+                       static_cast<const uint64_t*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
+                       static_cast<uint64_t*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag);
+  else
+    hipLaunchKernelGGL(dq_freq_part_kernel<FreqRec>, grid, dim3(kPartThreads), 0, stream,
+                       static_cast<const FreqRec*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
+                       static_cast<FreqRec*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag);
   return hipGetLastError();
 }
 
-hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, const DevColumn* d_cols, int64_t n_rows, int b1,
-                                  FreqRec* d_out,
+hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, bool packed, const DevColumn* d_cols,
+                                  int64_t n_rows, int b1, void* d_out,
                                   uint64_t cap1, unsigned long long* d_fill1, FreqRec* d_ovf, unsigned long long* d_ovf_n,
                                   uint64_t ovf_cap, unsigned int* d_flag, uint32_t* d_hll, unsigned long long* d_long_key,
                                   unsigned long long* d_staged, hipStream_t stream) {
   if (n_rows <= 0) return hipSuccess;
-  if (b1 < 1 || b1 > kStageBinBits) return hipErrorInvalidValue;
+  if (b1 < 1 || b1 > kStageBinBits || (packed && !one_string)) return hipErrorInvalidValue;
   const int64_t tiles = (n_rows + kStageTile - 1) / kStageTile;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int64_t blocks = tiles < (int64_t)cus * 4 ? tiles : (int64_t)cus * 4;
-  if (one_string)
-    hipLaunchKernelGGL(dq_freq_stage_part_kernel<true>, dim3((unsigned)blocks), dim3(kPartThreads), 0, stream, ks, d_cols,
-                       n_rows, b1, d_out, cap1, d_fill1, d_ovf, d_ovf_n, ovf_cap, d_flag, d_hll, d_long_key, d_staged);
+  if (packed)
+    hipLaunchKernelGGL((dq_freq_stage_part_kernel<true, true>), dim3((unsigned)blocks), dim3(kPartThreads), 0, stream, ks,
+                       d_cols, n_rows, b1, static_cast<uint64_t*>(d_out), cap1, d_fill1, d_ovf, d_ovf_n, ovf_cap, d_flag,
+                       d_hll, d_long_key, d_staged);
+  else if (one_string)
+    hipLaunchKernelGGL((dq_freq_stage_part_kernel<true, false>), dim3((unsigned)blocks), dim3(kPartThreads), 0, stream, ks,
+                       d_cols, n_rows, b1, static_cast<FreqRec*>(d_out), cap1, d_fill1, d_ovf, d_ovf_n, ovf_cap, d_flag,
+                       d_hll, d_long_key, d_staged);
   else
-    hipLaunchKernelGGL(dq_freq_stage_part_kernel<false>, dim3((unsigned)blocks), dim3(kPartThreads), 0, stream, ks, d_cols,
-                       n_rows, b1, d_out, cap1, d_fill1, d_ovf, d_ovf_n, ovf_cap, d_flag, d_hll, d_long_key, d_staged);
+    hipLaunchKernelGGL((dq_freq_stage_part_kernel<false, false>), dim3((unsigned)blocks), dim3(kPartThreads), 0, stream, ks,
+                       d_cols, n_rows, b1, static_cast<FreqRec*>(d_out), cap1, d_fill1, d_ovf, d_ovf_n, ovf_cap, d_flag,
+                       d_hll, d_long_key, d_staged);
   return hipGetLastError();
 }
 
-hipError_t launch_freq_compact(const FreqRec* d_in, const unsigned long long* d_fill, uint64_t cap, uint64_t n_regions,
-                               const unsigned long long* d_prefix, FreqRec* d_out, hipStream_t stream) {
+hipError_t launch_freq_compact(const void* d_in, bool packed, const unsigned long long* d_fill, uint64_t cap,
+                               uint64_t n_regions, const unsigned long long* d_prefix, FreqRec* d_out, hipStream_t stream) {
   if (n_regions == 0) return hipSuccess;
   if (n_regions > 65535) return hipErrorInvalidValue;
   uint64_t bx = (cap + kBlock * 8 - 1) / (kBlock * 8);
   if (bx > 64) bx = 64;
   if (bx < 1) bx = 1;
-  hipLaunchKernelGGL(dq_freq_compact_kernel, dim3((unsigned)bx, (unsigned)n_regions), dim3(kBlock),
-                     0, stream, d_in, d_fill, cap, d_prefix, d_out);
+  if (packed)
+    hipLaunchKernelGGL(dq_freq_compact_kernel<uint64_t>, dim3((unsigned)bx, (unsigned)n_regions), dim3(kBlock), 0, stream,
+                       static_cast<const uint64_t*>(d_in), d_fill, cap, d_prefix, d_out);
+  else
+    hipLaunchKernelGGL(dq_freq_compact_kernel<FreqRec>, dim3((unsigned)bx, (unsigned)n_regions), dim3(kBlock), 0, stream,
+                       static_cast<const FreqRec*>(d_in), d_fill, cap, d_prefix, d_out);
   return hipGetLastError();
 }
 
-hipError_t launch_freq_agg_region(const FreqTable& T, const FreqRec* d_recs, const unsigned long long* d_fill,
+hipError_t launch_freq_agg_region(const FreqTable& T, const void* d_recs, bool packed, const unsigned long long* d_fill,
                                   uint64_t cap, uint64_t n_slices, int table_empty, FreqRec* d_retry,
                                   unsigned long long* d_n_retry, unsigned long long* d_new_groups,
                                   unsigned long long* d_hist, unsigned long long* d_big, unsigned long long* d_n_big,
@@ -1719,8 +1975,14 @@ hipError_t launch_freq_agg_region(const FreqTable& T, const FreqRec* d_recs, con
   if (blocks < 1) blocks = 1;
   if (!table_empty && (d_hist || d_smax || write_all)) return hipErrorInvalidValue;
   AggTrack tr{d_hist, d_big, d_n_big, big_cap, d_smax, write_all};
-  hipLaunchKernelGGL(dq_freq_agg_region_kernel, dim3((unsigned)blocks), dim3(kAggRegionThreads), 0, stream, T, d_recs, d_fill, cap,
-                     n_slices, table_empty, d_retry, d_n_retry, d_new_groups, tr);
+  if (packed)
+    hipLaunchKernelGGL(dq_freq_agg_packed_kernel, dim3((unsigned)blocks), dim3(kAggRegionThreads), 0, stream, T,
+                       static_cast<const uint64_t*>(d_recs), d_fill, cap, n_slices, table_empty, d_retry, d_n_retry,
+                       d_new_groups, tr);
+  else
+    hipLaunchKernelGGL(dq_freq_agg_region_kernel, dim3((unsigned)blocks), dim3(kAggRegionThreads), 0, stream, T,
+                       static_cast<const FreqRec*>(d_recs), d_fill, cap, n_slices, table_empty, d_retry, d_n_retry,
+                       d_new_groups, tr);
   return hipGetLastError();
 }
 
@@ -1799,6 +2061,29 @@ hipError_t launch_freq_export(const FreqTable& T, unsigned long long min_count, 
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(dq_freq_export_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, min_count, out);
+  return hipGetLastError();
+}
+
+// Diagnostics: the table hash and the packed word (or ~0) of n inline keys (tests compare them
+// with a host restatement: every path must place a key with this one function).
+__global__ __launch_bounds__(kBlock) void dq_freq_hash_kernel(const uint64_t* __restrict__ k0, const uint64_t* __restrict__ k1,
+                                                              const uint32_t* __restrict__ len, int64_t n, uint64_t* out) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    uint64_t p;
+    const uint64_t h = hash_inline(k0[i], k1[i], len[i]);
+    const bool pk = kp_pack_record(k0[i], k1[i], len[i], &p);
+    // (a packed record must hash like its key: a disagreement shows up as a wrong hash)
+    out[2 * i] = pk && hash_record_packed(p) != h ? ~h : h;
+    out[2 * i + 1] = pk ? p : ~0ull;
+  }
+}
+
+hipError_t launch_freq_hash(const uint64_t* d_k0, const uint64_t* d_k1, const uint32_t* d_len, int64_t n, uint64_t* d_out,
+                            hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  int64_t blocks = (n + kBlock - 1) / kBlock;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(dq_freq_hash_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, d_k0, d_k1, d_len, n, d_out);
   return hipGetLastError();
 }
 

@@ -221,6 +221,8 @@ hipError_t launch_freq_hist(const FreqTable& T, unsigned long long* d_hist, unsi
 hipError_t launch_freq_export(const FreqTable& T, unsigned long long min_count, const FreqOut& out,
                               hipStream_t stream, const uint32_t* d_smax = nullptr);
 hipError_t launch_freq_import(const FreqTable& T, const FreqIn& in, hipStream_t stream);
+hipError_t launch_freq_hash(const uint64_t* d_k0, const uint64_t* d_k1, const uint32_t* d_len, int64_t n, uint64_t* d_out,
+                            hipStream_t stream);
 hipError_t launch_freq_lookup(const FreqTable& T, const uint8_t* d_key, uint32_t len, unsigned long long* d_out,
                               hipStream_t stream);
 hipError_t launch_freq_heap_need(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
@@ -256,25 +258,28 @@ hipError_t launch_freq_agg(const FreqTable& T, const FreqRec* d_recs, const uint
                            hipStream_t stream);
 // Partition path (dq_freq.hip): stage array (d_in_fill == nullptr) or regions -> regions of
 // out_cap records by the top id_bits of the table hash; overflow -> d_ovf (d_flag bit 0 when
-// that is full too).  Then one owner work item per slice region.
-hipError_t launch_freq_part(const FreqRec* d_in, uint64_t in_n, const unsigned long long* d_in_fill, uint64_t in_cap,
-                            uint64_t n_in_regions, int id_bits, int bin_bits, FreqRec* d_out, uint64_t out_cap,
+// that is full too).  Then one owner work item per slice region.  packed: the records are
+// packed digit keys (uint64_t, dq_keypack.h), else FreqRec; the overflow / retry lists always
+// hold FreqRec.
+hipError_t launch_freq_part(const void* d_in, uint64_t in_n, const unsigned long long* d_in_fill, uint64_t in_cap,
+                            uint64_t n_in_regions, int id_bits, int bin_bits, void* d_out, uint64_t out_cap,
                             unsigned long long* d_out_fill, FreqRec* d_ovf, unsigned long long* d_ovf_n,
-                            uint64_t ovf_cap, unsigned int* d_flag, hipStream_t stream);
+                            uint64_t ovf_cap, unsigned int* d_flag, bool packed, hipStream_t stream);
 // With an empty table it can also produce the count-of-counts histogram (d_hist, counts >=
 // kFreqHist into d_big), each slice's largest count (d_smax) and write every slot (write_all:
 // the table needs no clearing).
 // Stage + level-1 partition in one pass (records straight into their 2^b1 level-1 regions);
 // regions -> contiguous (prefix = exclusive sum of the clamped fills) for the sort path.
-// one_string: the only key column is utf8 (the kernel's batched-load fast path).
-hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, const DevColumn* d_cols, int64_t n_rows, int b1,
-                                  FreqRec* d_out,
+// one_string: the only key column is utf8 (the kernel's batched-load fast path); packed (needs
+// one_string): digit keys staged as packed words, other keys onto the overflow list.
+hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, bool packed, const DevColumn* d_cols,
+                                  int64_t n_rows, int b1, void* d_out,
                                   uint64_t cap1, unsigned long long* d_fill1, FreqRec* d_ovf, unsigned long long* d_ovf_n,
                                   uint64_t ovf_cap, unsigned int* d_flag, uint32_t* d_hll, unsigned long long* d_long_key,
                                   unsigned long long* d_staged, hipStream_t stream);
-hipError_t launch_freq_compact(const FreqRec* d_in, const unsigned long long* d_fill, uint64_t cap, uint64_t n_regions,
-                               const unsigned long long* d_prefix, FreqRec* d_out, hipStream_t stream);
-hipError_t launch_freq_agg_region(const FreqTable& T, const FreqRec* d_recs, const unsigned long long* d_fill,
+hipError_t launch_freq_compact(const void* d_in, bool packed, const unsigned long long* d_fill, uint64_t cap,
+                               uint64_t n_regions, const unsigned long long* d_prefix, FreqRec* d_out, hipStream_t stream);
+hipError_t launch_freq_agg_region(const FreqTable& T, const void* d_recs, bool packed, const unsigned long long* d_fill,
                                   uint64_t cap, uint64_t n_slices, int table_empty, FreqRec* d_retry,
                                   unsigned long long* d_n_retry, unsigned long long* d_new_groups,
                                   unsigned long long* d_hist, unsigned long long* d_big, unsigned long long* d_n_big,

@@ -227,9 +227,10 @@ class FrequencyTable:
 
     def paths(self) -> Dict[str, int]:
         """Which group-by paths this table's groupings took (dq_diag_freq_paths; tests)."""
-        out = (ctypes.c_int64 * 4)()
+        out = (ctypes.c_int64 * 5)()
         L.check(L.lib().dq_diag_freq_paths(self.handle, out))
-        return {"slots": out[0], "partition_runs": out[1], "slice_bits": out[2], "sort_records": out[3]}
+        return {"slots": out[0], "partition_runs": out[1], "slice_bits": out[2], "sort_records": out[3],
+                "packed_runs": out[4]}
 
     def merge_from(self, other: "FrequencyTable") -> None:
         """self += other, device to device."""

@@ -23,7 +23,8 @@ dq_status dq_diag_hash_rate(int device, int with_hll, int reps, double* hashes_p
 /* Aggregates what `f` has staged, then reports which paths its groupings took (tests assert
  * that a workload exercised the path it is meant to): out[0] = table slots (2048 per slice),
  * out[1] = partition-path aggregations, out[2] = hash bits (log2 slices) of the last one,
- * out[3] = records that went through the sort path (small stagings, retries, skew fallbacks). */
+ * out[3] = records that went through the sort path (small stagings, retries, skew fallbacks),
+ * out[4] = partition-path aggregations of packed digit-key records.  `out` holds 5 values. */
 dq_status dq_diag_freq_paths(dq_freq* f, int64_t* out);
 
 /* Host build of the library's java.lang.Double.parseDouble (the parser dq_cast_utf8 and the
@@ -31,6 +32,18 @@ dq_status dq_diag_freq_paths(dq_freq* f, int64_t* out);
  * *ok = 1 and *out = the correctly rounded value, or *ok = 0 (NumberFormatException, NULL in
  * Spark).  Lets CPU tests check it against a reference parser on millions of strings. */
 dq_status dq_diag_parse_double(const uint8_t* s, int64_t n, double* out, int32_t* ok);
+
+/* Host build of the group-by's record packing of digit-string keys (<= 15 ASCII digits, or
+ * Histogram's "NullValue"; deequ_amd/csrc/dq_keypack.h): *ok = 1, *packed = the 8-byte record
+ * word and back[0 .. *back_len) = the key bytes it unpacks to; *ok = 0 for any other key. */
+/* The group-by's table hash of n inline keys (k0/k1 = key bytes little-endian, len <= 16) as the
+ * device computes it: out[2i] = the hash, out[2i+1] = the packed record word or ~0 (tests check
+ * both against a host restatement). */
+dq_status dq_diag_table_hash(int device, const uint64_t* k0, const uint64_t* k1, const uint32_t* len, int64_t n,
+                             uint64_t* out);
+
+dq_status dq_diag_key_pack(const uint8_t* key, int32_t len, uint64_t* packed, uint8_t* back, int32_t* back_len,
+                           int32_t* ok);
 
 #ifdef __cplusplus
 }

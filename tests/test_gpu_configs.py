@@ -97,6 +97,7 @@ def test_c4_scale_partition_group_by(gpu):
     u, c = np.unique(ids_h[valid_h], return_counts=True)
     assert paths["slots"] >= 1 << 28, paths            # >= 2^17 slices
     assert paths["partition_runs"] >= 1, paths
+    assert paths["packed_runs"] >= 1, paths            # 12-digit keys: 8-byte records
     assert paths["sort_records"] <= n // 100, paths    # retries only
     assert s.num_rows == n
     assert s.grouped_rows == int(valid_h.sum())

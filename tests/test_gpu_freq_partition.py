@@ -145,3 +145,104 @@ def test_region_staging_batches_and_rollback(gpu, part, long_frac):
             want[kb] = want.get(kb, 0) + 1
         assert got == want, hist
         t.close()
+
+
+# ---- packed digit-key records (dq_keypack.h) -------------------------------------------------
+
+def _count(keys, hist):
+    want = {}
+    for k in keys:
+        if k is None and not hist:
+            continue
+        kb = b"NullValue" if k is None else k.encode()
+        want[kb] = want.get(kb, 0) + 1
+    return want
+
+
+def _consume_batches(keys, hist, batches, **kw):
+    t = FrequencyTable(["key"], {"key": "string"}, histogram=hist, **kw)
+    step = (len(keys) + batches - 1) // batches
+    for s in range(0, len(keys), step):
+        t.consume(d.Table.from_pydict({"key": ("string", keys[s:s + step])}))
+    return t
+
+
+@pytest.mark.parametrize("other_frac", [0.0, 0.02])
+@pytest.mark.parametrize("hist", [False, True])
+def test_packed_digit_keys(gpu, part, hist, other_frac):
+    """Digit keys of every length 0..15 (leading zeros kept), NULLs ("NullValue" for Histogram,
+    its own packed code), and a few keys that are not digit strings (16-B records on the
+    overflow list, aggregated after the packed regions): exact groups and counts."""
+    rng = np.random.default_rng(21)
+    n = 600_000  # ~350k groups: a 2^20-slot table, one slice per level-1 region
+    a = rng.integers(0, 500_000, n)
+    ln = rng.integers(0, 16, n)
+    keys = []
+    for i in range(n):
+        if i % 37 == 0:
+            keys.append(None)
+        elif rng.random() < other_frac:
+            keys.append("id-%d" % (a[i] % 500))
+        else:
+            keys.append(("%015d" % a[i])[15 - ln[i]:] if ln[i] else "")
+    t = _consume_batches(keys, hist, 3)
+    assert _export(t) == _count(keys, hist)
+    paths = t.paths()
+    assert paths["packed_runs"] >= 1, paths
+    s = t.summary()
+    want = _count(keys, hist)
+    assert s.num_groups == len(want)
+    assert s.num_unique == sum(1 for c in want.values() if c == 1)
+    t.close()
+
+
+def test_packed_then_other_keys(gpu, part):
+    """Digit batches staged packed, then a batch of hex keys overflows the overflow list: the
+    packed regions are aggregated, the table switches to 16-B records, and the result is exact."""
+    rng = np.random.default_rng(22)
+    n = 400_000  # ~330k digit groups: the packed regions are aggregated on the partition path
+    digits = ["%012d" % v for v in rng.integers(0, 1_000_000, n)]
+    hexes = ["%012x" % v for v in rng.integers(0, 2**40, n)]  # 99.6 % not digit strings
+    keys = digits + hexes + digits[: n // 2]
+    t = _consume_batches(keys, False, 5)  # batches 1-2 digits, 3 hex (the switch), 4-5 mixed
+    assert _export(t) == _count(keys, False)
+    assert t.paths()["packed_runs"] >= 1
+    t.close()
+
+
+@pytest.mark.parametrize("mode", ["budget", "load", "few"])
+def test_packed_paths_equal_unpacked(gpu, part, monkeypatch, mode):
+    """The same digit keys with DQ_FREQ_PACK=0 (16-B records) and packed: identical tables.
+    budget: early aggregations into a non-empty table (existing digit and non-digit groups
+    loaded into the packed LDS image); load: a table of fewer slots than groups, whose slices
+    overflow the LDS image (their records return to the retry list as 16-B records); few: fewer slices than
+    level-1 regions (the packed regions are unpacked to a contiguous staging for the sort path)."""
+    rng = np.random.default_rng(23)
+    batches = 4
+    if mode == "few":
+        n, distinct = 100_000, 300
+    else:  # ~700k groups: 2^21 slots, level-2 split on
+        n, distinct = 1_600_000, 1_000_000
+    vals = rng.integers(0, distinct, n)
+    keys = ["%010d" % v if i % 11 else "k%d" % (v % 97) for i, v in enumerate(vals)]
+    if mode == "budget":  # the second batch is aggregated into the first one's table
+        monkeypatch.setenv("DQ_FREQ_STAGE_BUDGET", "700000")
+        batches = 2
+    if mode == "load":  # 2^20 slots for ~1.1M groups: most slices overflow their LDS image
+        monkeypatch.setenv("DQ_FREQ_PART_SLOTS", str(1 << 20))
+        n, distinct = 1_500_000, 2_000_000
+        vals = rng.integers(0, distinct, n)
+        keys = ["%010d" % v if i % 11 else "k%d" % (v % 97) for i, v in enumerate(vals)]
+    res = {}
+    for pack in ("0", "1"):
+        monkeypatch.setenv("DQ_FREQ_PACK", pack)
+        t = _consume_batches(keys, True, batches)
+        res[pack] = _export(t)
+        res[pack + "paths"] = t.paths()
+        t.close()
+    assert res["1"] == res["0"] == _count(keys, True)
+    assert res["0paths"]["packed_runs"] == 0
+    if mode != "few":
+        assert res["1paths"]["packed_runs"] >= (2 if mode == "budget" else 1), res["1paths"]
+    if mode == "load":
+        assert res["1paths"]["sort_records"] > 0, res["1paths"]  # slices overflowed LDS
