@@ -419,12 +419,14 @@ __device__ inline uint32_t lds_hash(uint64_t k0, uint64_t k1, uint32_t len) {
   return h ^ (h >> 13);
 }
 
-struct LdsSlot {
-  unsigned long long ctrl;  // as the global ctrl (READY unused: LDS keys are written before ctrl)
-  unsigned long long k0, k1;
-  unsigned int count;
-  unsigned int pad;
+// Structure of arrays: a wave's 64 random slots spread over all 64 LDS banks (32-byte slot
+// records put every slot of a wave on 8 of them).
+struct LdsTable {
+  unsigned long long ctrl[kLdsSlots];  // as the global ctrl (READY unused: LDS keys are written before ctrl)
+  unsigned long long k0[kLdsSlots], k1[kLdsSlots];
+  unsigned int count[kLdsSlots];
 };
+#define DQ_LDS(f, i) lds.f[i]
 
 }  // namespace
 
@@ -432,11 +434,11 @@ struct LdsSlot {
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void dq_freq_insert_kernel(FreqKeySpec ks,
                                                                 const DevColumn* __restrict__ cols,
                                                                 int64_t n_rows, FreqTable T) {
-  __shared__ LdsSlot lds[kLdsSlots];
+  __shared__ LdsTable lds;
   __shared__ int lds_open;
   for (int i = threadIdx.x; i < kLdsSlots; i += kBlock) {
-    lds[i].ctrl = 0;
-    lds[i].count = 0;
+    DQ_LDS(ctrl, i) = 0;
+    DQ_LDS(count, i) = 0;
   }
   if (threadIdx.x == 0) lds_open = 1;
   __syncthreads();
@@ -460,20 +462,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       const unsigned long long want = ((unsigned long long)lh << 32) | kReady | k.len;
       uint32_t s = lh & (kLdsSlots - 1);
       for (int probe = 0; probe < kLdsProbe * 4 && !done; ) {
-        unsigned long long c = __hip_atomic_load(&lds[s].ctrl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (c == 0ull) c = atomicCAS(&lds[s].ctrl, 0ull, 1ull);  // 1 = BUSY
+        unsigned long long c = __hip_atomic_load(&DQ_LDS(ctrl, s), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (c == 0ull) c = atomicCAS(&DQ_LDS(ctrl, s), 0ull, 1ull);  // 1 = BUSY
         if (c == 0ull) {
-          lds[s].k0 = k.k0;
-          lds[s].k1 = k.k1;
-          atomicAdd(&lds[s].count, 1u);
+          DQ_LDS(k0, s) = k.k0;
+          DQ_LDS(k1, s) = k.k1;
+          atomicAdd(&DQ_LDS(count, s), 1u);
           __threadfence_block();
-          atomicExch(&lds[s].ctrl, want);
+          atomicExch(&DQ_LDS(ctrl, s), want);
           done = true;
         } else if (c == 1ull) {
           ++probe;  // another lane is publishing this slot: look again
-        } else if (c == want && __hip_atomic_load(&lds[s].k0, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == k.k0 &&
-                   __hip_atomic_load(&lds[s].k1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == k.k1) {
-          atomicAdd(&lds[s].count, 1u);
+        } else if (c == want && __hip_atomic_load(&DQ_LDS(k0, s), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == k.k0 &&
+                   __hip_atomic_load(&DQ_LDS(k1, s), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == k.k1) {
+          atomicAdd(&DQ_LDS(count, s), 1u);
           done = true;
         } else {
           s = (s + 1) & (kLdsSlots - 1);
@@ -529,15 +531,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       }
 #pragma unroll
       for (int j = 0; j < R; ++j)
-        c[j] = want[j] ? __hip_atomic_load(&lds[slot[j]].ctrl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0ull;
+        c[j] = want[j] ? __hip_atomic_load(&DQ_LDS(ctrl, slot[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0ull;
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the keys published before those ctrl words
 #pragma unroll
       for (int j = 0; j < R; ++j) {
         bool hit = false;
         if (want[j] && c[j] == want[j])
-          hit = __hip_atomic_load(&lds[slot[j]].k0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == k[j].k0 &&
-                __hip_atomic_load(&lds[slot[j]].k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == k[j].k1;
-        if (hit) atomicAdd(&lds[slot[j]].count, 1u);
+          hit = __hip_atomic_load(&DQ_LDS(k0, slot[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == k[j].k0 &&
+                __hip_atomic_load(&DQ_LDS(k1, slot[j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == k[j].k1;
+        if (hit) atomicAdd(&DQ_LDS(count, slot[j]), 1u);
         else if (ok[j] && !insert_row(k[j])) overflowed = true;
       }
     }
@@ -555,15 +557,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   __syncthreads();
   // flush the LDS groups
   for (int i = threadIdx.x; i < kLdsSlots; i += kBlock) {
-    const unsigned long long c = lds[i].ctrl;
-    if (c > 1ull && lds[i].count) {
+    const unsigned long long c = DQ_LDS(ctrl, i);
+    if (c > 1ull && DQ_LDS(count, i)) {
       Key k;
-      k.k0 = lds[i].k0;
-      k.k1 = lds[i].k1;
+      k.k0 = DQ_LDS(k0, i);
+      k.k1 = DQ_LDS(k1, i);
       k.len = (uint32_t)(c & kLenMask);
       k.ptr = nullptr;
       k.hash = hash_inline(k.k0, k.k1, k.len);
-      global_insert(T, k, lds[i].count);
+      global_insert(T, k, DQ_LDS(count, i));
     }
   }
 }
@@ -1117,19 +1119,34 @@ constexpr int kPartThreads = DQ_PART_NT;
 constexpr int kPartPerThread = 16;
 constexpr uint32_t kPartTile = (uint32_t)kPartThreads * kPartPerThread;  // records per tile
 constexpr uint32_t kPartSub = DQ_PART_SUB;                               // records per LDS round
+#ifndef DQ_PARTP_PER
+#define DQ_PARTP_PER 16
+#endif
+#ifndef DQ_PARTP_SUB
+#define DQ_PARTP_SUB 6144
+#endif
+// packed (8-byte) records: per thread and per LDS round of the level-2 split
+constexpr int kPartPerThreadP = DQ_PARTP_PER;
+constexpr uint32_t kPartTileP = (uint32_t)kPartThreads * kPartPerThreadP;
+constexpr uint32_t kPartSubP = DQ_PARTP_SUB;
 constexpr int kPartMaxBinBits = kPartMaxBits;
 constexpr int kStageBinBits = 9;  // the level-1 split of the fused stage (dq_freq_api.inc kRegionBits)
 constexpr uint32_t kPartNoBin = 0xFFFFu;
 constexpr int kStageGroup = 4;  // rows per thread whose loads the fused stage issues together
 constexpr int kStagePer = 12;   // rows per thread per fused-stage tile (register budget)
 constexpr uint32_t kStageTile = (uint32_t)kPartThreads * kStagePer;
+#ifndef DQ_STAGEP_SUB
+#define DQ_STAGEP_SUB 6144
+#endif
+constexpr uint32_t kStageSubP = DQ_STAGEP_SUB;  // packed records per LDS round of the fused stage
 
 // R: the record type of the regions -- FreqRec (16 B: key bytes + length) or, for a staging of
 // digit keys, its packed word (uint64_t, dq_keypack.h).
-template <int MAXB, typename R = FreqRec>
+template <int MAXB, typename R = FreqRec, uint32_t SUBN = (sizeof(R) == 8 ? kPartSubP : kPartSub)>
 struct PartLdsT {
-  R rec[kPartSub];
-  uint16_t bin[kPartSub];
+  static constexpr uint32_t SUB = SUBN;
+  R rec[SUB];
+  uint16_t bin[SUB];
   uint32_t hist[MAXB];
   uint32_t start[MAXB];
   unsigned long long gbase[MAXB];
@@ -1164,14 +1181,15 @@ __device__ inline FreqRec rec_raw(uint64_t p) {
 // 2^bin_bits, or kPartNoBin for none); output region of a bin = base_id + bin.  Ranks come from
 // LDS atomics, the room in each region from ONE device atomic per (tile, non-empty bin), and the
 // records are written from an LDS image sorted by bin, kPartSub at a time (coalesced runs).
-template <int PER, int MAXB, typename R>
-__device__ inline void part_tile(PartLdsT<MAXB, R>& L, const R (&rec)[PER], uint32_t (&bin)[PER],
+template <int PER, int MAXB, typename R, uint32_t SUBN>
+__device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER], uint32_t (&bin)[PER],
                                  uint32_t nb, uint64_t base_id, R* __restrict__ out, uint64_t out_cap,
                                  unsigned long long* out_fill, FreqRec* ovf, unsigned long long* ovf_n,
                                  uint64_t ovf_cap, unsigned int* flag, unsigned long long* staged,
                                  const unsigned long long* region_start = nullptr) {
   // region_start != nullptr: exact regions -- output region id starts at record region_start[id]
   // of `out` (sizes counted beforehand: nothing can overflow), out_fill is its cursor
+  constexpr uint32_t SUB = SUBN;
   const uint32_t t = threadIdx.x;
   for (uint32_t i = t; i < nb; i += kPartThreads) L.hist[i] = 0u;
   __syncthreads();
@@ -1214,19 +1232,19 @@ __device__ inline void part_tile(PartLdsT<MAXB, R>& L, const R (&rec)[PER], uint
   }
   const uint32_t total = L.total;
   __syncthreads();
-  for (uint32_t r0 = 0; r0 < total; r0 += kPartSub) {
+  for (uint32_t r0 = 0; r0 < total; r0 += SUB) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       if ((bin[i] & 0xFFFFu) == kPartNoBin) continue;
       const uint32_t b = bin[i] & 0xFFFFu;
       const uint32_t p = L.start[b] + (bin[i] >> 16) - r0;
-      if (p < kPartSub) {
+      if (p < SUB) {
         L.rec[p] = rec[i];
         L.bin[p] = (uint16_t)b;
       }
     }
     __syncthreads();
-    const uint32_t m = min(kPartSub, total - r0);
+    const uint32_t m = min(SUB, total - r0);
     for (uint32_t j = t; j < m; j += kPartThreads) {
       const uint32_t b = L.bin[j];
       const uint64_t o = L.gbase[b] + (r0 + j - L.start[b]);
@@ -1249,12 +1267,17 @@ __device__ inline void part_tile(PartLdsT<MAXB, R>& L, const R (&rec)[PER], uint
 // blockIdx.x of region blockIdx.y (in + y * in_cap, min(in_fill[y], in_cap) records).
 // A record's output region = the top id_bits of its hash; its LDS bin = the low bin_bits of
 // that id (the higher id bits are the input region's, uniform over the tile).
-template <typename R>
-__global__ __launch_bounds__(kPartThreads) void dq_freq_part_kernel(
+#ifndef DQ_PARTP_WAVES
+#define DQ_PARTP_WAVES 4
+#endif
+// MAXB: LDS bin arrays for up to that many bins (512 when bin_bits <= 9: more LDS for the image).
+template <typename R, int MAXB>
+__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(sizeof(R) == 8 ? DQ_PARTP_WAVES : 1))) void dq_freq_part_kernel(
     const R* __restrict__ in, uint64_t in_n, const unsigned long long* __restrict__ in_fill, uint64_t in_cap,
     int id_bits, int bin_bits, R* __restrict__ out, uint64_t out_cap, unsigned long long* out_fill,
     FreqRec* ovf, unsigned long long* ovf_n, uint64_t ovf_cap, unsigned int* flag) {
-  __shared__ PartLdsT<(1 << kPartMaxBinBits), R> L;
+  __shared__ PartLdsT<MAXB, R> L;
+  constexpr uint32_t TILE = sizeof(R) == 8 ? kPartTileP : kPartTile;
   const uint32_t t = threadIdx.x;
   const uint32_t nb = 1u << bin_bits;
   uint64_t base_id = 0, begin, count;
@@ -1262,25 +1285,26 @@ __global__ __launch_bounds__(kPartThreads) void dq_freq_part_kernel(
     const uint64_t r = blockIdx.y;
     const unsigned long long f = in_fill[r];
     const uint64_t have = f < in_cap ? f : in_cap;
-    begin = (uint64_t)blockIdx.x * kPartTile;
+    begin = (uint64_t)blockIdx.x * TILE;
     if (begin >= have) return;
-    count = min((uint64_t)kPartTile, have - begin);
+    count = min((uint64_t)TILE, have - begin);
     begin += r * in_cap;
     base_id = r << bin_bits;
   } else {
-    begin = (uint64_t)blockIdx.x * kPartTile;
+    begin = (uint64_t)blockIdx.x * TILE;
     if (begin >= in_n) return;
-    count = min((uint64_t)kPartTile, in_n - begin);
+    count = min((uint64_t)TILE, in_n - begin);
   }
-  R rec[kPartPerThread];
-  uint32_t bin[kPartPerThread];
+  constexpr int PER = sizeof(R) == 8 ? kPartPerThreadP : kPartPerThread;
+  R rec[PER];
+  uint32_t bin[PER];
 #pragma unroll
-  for (int i = 0; i < kPartPerThread; ++i) {
+  for (int i = 0; i < PER; ++i) {
     const uint32_t j = (uint32_t)i * kPartThreads + t;
     if (j < count) rec[i] = in[begin + j];
   }
 #pragma unroll
-  for (int i = 0; i < kPartPerThread; ++i) {
+  for (int i = 0; i < PER; ++i) {
     const uint32_t j = (uint32_t)i * kPartThreads + t;
     bin[i] = kPartNoBin;
     if (j < count) {
@@ -1461,15 +1485,18 @@ __global__ __launch_bounds__(kBlock) void dq_freq_pieces_kernel(const unsigned l
 // a key that is not a digit string goes to the overflow list as a 16-B record (counted there and
 // in `staged`), and a batch with more of them than the list holds raises `flag` (the host then
 // rolls it back and stages the table's keys as 16-B records from then on).
+#ifndef DQ_STAGEP_WAVES
+#define DQ_STAGEP_WAVES 4
+#endif
 template <bool ONE_STRING, bool PACK>
-__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(4))) void dq_freq_stage_part_kernel(
+__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(PACK ? DQ_STAGEP_WAVES : 4))) void dq_freq_stage_part_kernel(
     FreqKeySpec ks, const DevColumn* __restrict__ cols, int64_t n_rows, int b1,
     typename std::conditional<PACK, uint64_t, FreqRec>::type* __restrict__ out, uint64_t cap1,
     unsigned long long* fill1, FreqRec* ovf, unsigned long long* ovf_n, uint64_t ovf_cap, unsigned int* flag,
     uint32_t* hll, unsigned long long* long_key, unsigned long long* staged) {
   static_assert(ONE_STRING || !PACK, "packed records are staged from one string key column");
   using R = typename std::conditional<PACK, uint64_t, FreqRec>::type;
-  __shared__ PartLdsT<(1 << kStageBinBits), R> L;
+  __shared__ PartLdsT<(1 << kStageBinBits), R, (PACK ? kStageSubP : kPartSub)> L;
   __shared__ uint32_t regs[kHllM];
   const uint32_t t = threadIdx.x;
   const uint32_t nb = 1u << b1;
@@ -1663,12 +1690,19 @@ __device__ inline bool lds_count_packed(unsigned long long* K, uint32_t* C, uint
 #endif
 constexpr int kAggPBatch = DQ_AGGP_BATCH;  // packed records per thread loaded together
 
-__global__ __launch_bounds__(kAggRegionThreads) __attribute__((amdgpu_waves_per_eu(DQ_AGG_WAVES))) void dq_freq_agg_packed_kernel(
+#ifndef DQ_AGGP_WAVES
+#define DQ_AGGP_WAVES 8
+#endif
+#ifndef DQ_AGGP_THREADS
+#define DQ_AGGP_THREADS 256
+#endif
+constexpr int kAggPThreads = DQ_AGGP_THREADS;
+__global__ __launch_bounds__(kAggPThreads) __attribute__((amdgpu_waves_per_eu(DQ_AGGP_WAVES))) void dq_freq_agg_packed_kernel(
     FreqTable T, const uint64_t* __restrict__ recs, const unsigned long long* __restrict__ fill, uint64_t cap,
     uint64_t n_slices, int table_empty, FreqRec* retry, unsigned long long* n_retry, unsigned long long* new_groups,
     AggTrack tr) {
   constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
-  constexpr int NT = kAggRegionThreads;
+  constexpr int NT = kAggPThreads;
   __shared__ AggLdsP L;
   const bool track = tr.hist != nullptr;
   if (track) {
@@ -1905,20 +1939,25 @@ hipError_t launch_freq_part(const void* d_in, uint64_t in_n, const unsigned long
                             unsigned long long* d_out_fill, FreqRec* d_ovf, unsigned long long* d_ovf_n,
                             uint64_t ovf_cap, unsigned int* d_flag, bool packed, hipStream_t stream) {
   if (bin_bits < 0 || bin_bits > kPartMaxBinBits || id_bits < bin_bits || id_bits > 32) return hipErrorInvalidValue;
+  const uint64_t tile = packed ? kPartTileP : kPartTile;  // (the kernel's records per workgroup)
   dim3 grid;
   if (d_in_fill) {
     if (n_in_regions == 0 || n_in_regions > 65535) return hipErrorInvalidValue;
-    grid = dim3((unsigned)((in_cap + kPartTile - 1) / kPartTile), (unsigned)n_in_regions);
+    grid = dim3((unsigned)((in_cap + tile - 1) / tile), (unsigned)n_in_regions);
   } else {
     if (in_n == 0) return hipSuccess;
-    grid = dim3((unsigned)((in_n + kPartTile - 1) / kPartTile));
+    grid = dim3((unsigned)((in_n + tile - 1) / tile));
   }
-  if (packed)
-    hipLaunchKernelGGL(dq_freq_part_kernel<uint64_t>, grid, dim3(kPartThreads), 0, stream,
+  if (packed && bin_bits <= kStageBinBits)
+    hipLaunchKernelGGL((dq_freq_part_kernel<uint64_t, (1 << kStageBinBits)>), grid, dim3(kPartThreads), 0, stream,
+                       static_cast<const uint64_t*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
+                       static_cast<uint64_t*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag);
+  else if (packed)
+    hipLaunchKernelGGL((dq_freq_part_kernel<uint64_t, (1 << kPartMaxBinBits)>), grid, dim3(kPartThreads), 0, stream,
                        static_cast<const uint64_t*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
                        static_cast<uint64_t*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag);
   else
-    hipLaunchKernelGGL(dq_freq_part_kernel<FreqRec>, grid, dim3(kPartThreads), 0, stream,
+    hipLaunchKernelGGL((dq_freq_part_kernel<FreqRec, (1 << kPartMaxBinBits)>), grid, dim3(kPartThreads), 0, stream,
                        static_cast<const FreqRec*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
                        static_cast<FreqRec*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag);
   return hipGetLastError();
@@ -1976,7 +2015,7 @@ hipError_t launch_freq_agg_region(const FreqTable& T, const void* d_recs, bool p
   if (!table_empty && (d_hist || d_smax || write_all)) return hipErrorInvalidValue;
   AggTrack tr{d_hist, d_big, d_n_big, big_cap, d_smax, write_all};
   if (packed)
-    hipLaunchKernelGGL(dq_freq_agg_packed_kernel, dim3((unsigned)blocks), dim3(kAggRegionThreads), 0, stream, T,
+    hipLaunchKernelGGL(dq_freq_agg_packed_kernel, dim3((unsigned)blocks), dim3(kAggPThreads), 0, stream, T,
                        static_cast<const uint64_t*>(d_recs), d_fill, cap, n_slices, table_empty, d_retry, d_n_retry,
                        d_new_groups, tr);
   else

@@ -29,42 +29,49 @@ constexpr uint64_t kPackForeign = ~0ull - 1ull;
 constexpr uint64_t kNullK0 = 0x756c61566c6c754eull;  // "NullValu"
 constexpr uint64_t kNullK1 = 0x65ull;                // "e"
 
-// The bytes of x below n (n <= 8; the rest ignored): all ASCII digits?  *nib = their values as
-// 8 nibbles (byte i -> bits 4i..4i+3; bytes >= n -> 0).
-DQ_KP_FN bool kp_digits8(uint64_t x, uint32_t n, uint32_t* nib) {
-  const uint64_t m = n >= 8 ? ~0ull : ((1ull << (8u * n)) - 1ull);
-  const uint64_t y = (x & m) | (0x3030303030303030ull & ~m);  // pad with '0'
-  if (y & 0x8080808080808080ull) return false;                 // not ASCII (the adds below carry)
-  // per byte b < 0x80: (b | 0x80) - 0x30 has bit 7 iff b >= '0'; b + 0x46 has bit 7 iff b > '9'
-  const uint64_t ge0 = (y | 0x8080808080808080ull) - 0x3030303030303030ull;
-  const uint64_t gt9 = y + 0x4646464646464646ull;
-  if ((ge0 & ~gt9 & 0x8080808080808080ull) != 0x8080808080808080ull) return false;
-  const uint64_t d = y - 0x3030303030303030ull;                // bytes 0..9
-  uint64_t t = (d | (d >> 4)) & 0x00FF00FF00FF00FFull;         // byte pairs -> one byte each
-  t = (t | (t >> 8)) & 0x0000FFFF0000FFFFull;
-  t = (t | (t >> 16)) & 0x00000000FFFFFFFFull;
-  *nib = (uint32_t)t;
-  return true;
+// 32-bit halves throughout: the VALU is 32 bits wide, so the work is done per 4-byte word.
+// Low n bytes of a word (n clamped to 0..4), the rest '0'.
+DQ_KP_FN uint32_t kp_pad4(uint32_t w, int32_t n) {
+  const uint32_t m = n >= 4 ? 0xFFFFFFFFu : (n <= 0 ? 0u : (1u << (8 * n)) - 1u);
+  return (w & m) | (0x30303030u & ~m);
 }
 
-// 8 nibbles -> 8 digit bytes, the bytes from n on zero.
-DQ_KP_FN uint64_t kp_spread8(uint32_t nib, uint32_t n) {
-  uint64_t x = nib;
-  x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
-  x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
-  x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
-  x += 0x3030303030303030ull;
-  return n >= 8 ? x : (n ? x & ((1ull << (8u * n)) - 1ull) : 0ull);
+// 0 if every byte of y (padded) is an ASCII digit, else bit 7 of some byte.
+DQ_KP_FN uint32_t kp_nondigit4(uint32_t y) {
+  // per byte b < 0x80: (b | 0x80) - 0x30 keeps bit 7 iff b >= '0'; b + 0x46 sets it iff b > '9'
+  const uint32_t ge0 = (y | 0x80808080u) - 0x30303030u;
+  const uint32_t gt9 = y + 0x46464646u;  // (a byte >= 0x80 carries; it is caught by y itself)
+  return (~ge0 | gt9 | y) & 0x80808080u;
+}
+
+// 4 digit bytes -> 4 nibbles (byte i -> bits 4i..4i+3).
+DQ_KP_FN uint32_t kp_nib4(uint32_t y) {
+  const uint32_t d = y - 0x30303030u;  // bytes 0..9, no borrow
+  const uint32_t t = d | (d >> 4);      // bytes 0 and 2 hold the pairs
+  return (t & 0xFFu) | ((t >> 8) & 0xFF00u);
+}
+
+// 4 nibbles -> 4 digit bytes, the bytes from n on zero.
+DQ_KP_FN uint32_t kp_spread4(uint32_t nib, int32_t n) {
+  uint32_t x = nib & 0xFFFFu;
+  x = (x | (x << 8)) & 0x00FF00FFu;
+  x = (x | (x << 4)) & 0x0F0F0F0Fu;
+  x += 0x30303030u;
+  const uint32_t m = n >= 4 ? 0xFFFFFFFFu : (n <= 0 ? 0u : (1u << (8 * n)) - 1u);
+  return x & m;
 }
 
 // The packed word of an inline key (k0/k1 little-endian key bytes, len <= 15), if it is a digit
 // string (false otherwise; "NullValue" is not one -- see kp_pack_record).
 DQ_KP_FN bool kp_pack(uint64_t k0, uint64_t k1, uint32_t len, uint64_t* p) {
   if (len > 15) return false;
-  uint32_t a, b;
-  if (!kp_digits8(k0, len < 8 ? len : 8, &a)) return false;
-  if (!kp_digits8(k1, len > 8 ? len - 8 : 0, &b)) return false;
-  *p = (uint64_t)a | ((uint64_t)b << 32) | ((uint64_t)len << 60);
+  const int32_t n = (int32_t)len;
+  const uint32_t y0 = kp_pad4((uint32_t)k0, n), y1 = kp_pad4((uint32_t)(k0 >> 32), n - 4);
+  const uint32_t y2 = kp_pad4((uint32_t)k1, n - 8), y3 = kp_pad4((uint32_t)(k1 >> 32), n - 12);
+  if (kp_nondigit4(y0) | kp_nondigit4(y1) | kp_nondigit4(y2) | kp_nondigit4(y3)) return false;
+  const uint32_t lo = kp_nib4(y0) | (kp_nib4(y1) << 16);
+  const uint32_t hi = kp_nib4(y2) | (kp_nib4(y3) << 16) | (len << 28);  // (nibble 15 is 0: len <= 15)
+  *p = (uint64_t)lo | ((uint64_t)hi << 32);
   return true;
 }
 
@@ -85,10 +92,11 @@ DQ_KP_FN void kp_unpack(uint64_t p, uint64_t* k0, uint64_t* k1, uint32_t* len) {
     *len = 9;
     return;
   }
-  const uint32_t n = (uint32_t)(p >> 60);
-  *len = n;
-  *k0 = kp_spread8((uint32_t)p, n < 8 ? n : 8);
-  *k1 = kp_spread8((uint32_t)(p >> 32) & 0x0FFFFFFFu, n > 8 ? n - 8 : 0);
+  const uint32_t lo = (uint32_t)p, hi = (uint32_t)(p >> 32);
+  const int32_t n = (int32_t)(hi >> 28);
+  *len = (uint32_t)n;
+  *k0 = (uint64_t)kp_spread4(lo, n) | ((uint64_t)kp_spread4(lo >> 16, n - 4) << 32);
+  *k1 = (uint64_t)kp_spread4(hi, n - 8) | ((uint64_t)kp_spread4((hi >> 16) & 0x0FFFu, n - 12) << 32);
 }
 
 }  // namespace dq
