@@ -1272,11 +1272,12 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
 #endif
 // MAXB: LDS bin arrays for up to that many bins (512 when bin_bits <= 9: more LDS for the image).
 template <typename R, int MAXB>
-__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(sizeof(R) == 8 ? DQ_PARTP_WAVES : 1))) void dq_freq_part_kernel(
+__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(sizeof(R) == 8 && MAXB <= 512 ? DQ_PARTP_WAVES : 1))) void dq_freq_part_kernel(
     const R* __restrict__ in, uint64_t in_n, const unsigned long long* __restrict__ in_fill, uint64_t in_cap,
     int id_bits, int bin_bits, R* __restrict__ out, uint64_t out_cap, unsigned long long* out_fill,
     FreqRec* ovf, unsigned long long* ovf_n, uint64_t ovf_cap, unsigned int* flag) {
-  __shared__ PartLdsT<MAXB, R> L;
+  // (2048 bins: the smaller LDS rounds keep two workgroups per CU)
+  __shared__ PartLdsT<MAXB, R, (sizeof(R) == 8 && MAXB <= 512 ? kPartSubP : kPartSub)> L;
   constexpr uint32_t TILE = sizeof(R) == 8 ? kPartTileP : kPartTile;
   const uint32_t t = threadIdx.x;
   const uint32_t nb = 1u << bin_bits;
@@ -1691,7 +1692,7 @@ __device__ inline bool lds_count_packed(unsigned long long* K, uint32_t* C, uint
 constexpr int kAggPBatch = DQ_AGGP_BATCH;  // packed records per thread loaded together
 
 #ifndef DQ_AGGP_WAVES
-#define DQ_AGGP_WAVES 8
+#define DQ_AGGP_WAVES 8  // (registers allow 5: the compiler warns, the measured build)
 #endif
 #ifndef DQ_AGGP_THREADS
 #define DQ_AGGP_THREADS 256
