@@ -39,6 +39,9 @@ def lib():
                                ctypes.c_int, ctypes.POINTER(ColState)]
         l.dqo_time_c2_hll.restype = ctypes.c_double
         l.dqo_time_c2_hll.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        l.dqo_time_c2_hll_for.restype = ctypes.c_double
+        l.dqo_time_c2_hll_for.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_double, ctypes.POINTER(ctypes.c_int)]
         l.dqo_gen_c2.restype = None
         l.dqo_gen_c2.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int,
                                  ctypes.c_void_p, ctypes.c_void_p]
@@ -51,15 +54,17 @@ def lib():
     return _lib
 
 
-def time_c2_scan(rows: int, threads: int, hll: bool = True) -> float:
-    """Seconds for the Spark-semantics scan of a C2 sample of `rows` rows on `threads` threads
-    (data generation excluded); with `hll`, the 8 columns' HLL registers in the timed region."""
+def time_c2_scan(rows: int, threads: int, hll: bool = True, min_secs: float = 0.0):
+    """(seconds, passes): timed passes of the Spark-semantics scan over one C2 sample of `rows`
+    rows on `threads` threads (data generation excluded), repeated until `min_secs` have been
+    spent (one pass by default); with `hll`, the 8 columns' HLL registers in the timed region."""
     out = (ColState * 8)()
     regs = (ctypes.c_uint8 * (8 * 512))() if hll else None
-    secs = lib().dqo_time_c2_hll(rows, threads, out, regs)
+    passes = ctypes.c_int(0)
+    secs = lib().dqo_time_c2_hll_for(rows, threads, out, regs, float(min_secs), ctypes.byref(passes))
     if secs < 0:
         raise MemoryError("oracle could not allocate the C2 sample")
-    return secs
+    return secs, passes.value
 
 
 def gen_c2(rows: int, col: int, seed: int = 42):

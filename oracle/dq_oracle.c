@@ -259,13 +259,23 @@ static void* hll_thread(void* arg) {
 
 /* C2 with ApproxCountDistinct too: the scan, then the HLL registers of the 8 columns (row
  * partitions per thread, merged by register max = DeequHyperLogLogPlusPlusUtils.merge). */
-double dqo_time_c2_hll(int64_t rows, int threads, dqo_colstate* out8, uint8_t* regs8x512);
+double dqo_time_c2_hll_for(int64_t rows, int threads, dqo_colstate* out8, uint8_t* regs8x512, double min_secs,
+                           int* passes);
+
+double dqo_time_c2_hll(int64_t rows, int threads, dqo_colstate* out8, uint8_t* regs8x512) {
+  int passes = 0;
+  return dqo_time_c2_hll_for(rows, threads, out8, regs8x512, 0.0, &passes);
+}
 
 double dqo_time_c2(int64_t rows, int threads, dqo_colstate* out8) {
   return dqo_time_c2_hll(rows, threads, out8, NULL);
 }
 
-double dqo_time_c2_hll(int64_t rows, int threads, dqo_colstate* out8, uint8_t* regs8x512) {
+/* Timed passes over one generated sample until at least min_secs have been spent (1 pass when
+ * min_secs <= 0); returns the total seconds of the *passes passes (each pass = the whole scan and
+ * HLL; the results are those of the last pass -- every pass computes the same states). */
+double dqo_time_c2_hll_for(int64_t rows, int threads, dqo_colstate* out8, uint8_t* regs8x512, double min_secs,
+                           int* passes) {
   int types[8], pred_op[8], as_f64[8];
   int64_t lit_i[8];
   double lit_f[8];
@@ -295,6 +305,9 @@ double dqo_time_c2_hll(int64_t rows, int threads, dqo_colstate* out8, uint8_t* r
     for (int t = 0; t < ng; ++t) pthread_join(th[t], NULL);
   }
   struct timespec t0, t1;
+  double total = 0.0;
+  int done = 0;
+  do {
   clock_gettime(CLOCK_MONOTONIC, &t0);
   dqo_scan(rows, 8, types, (const void* const*)values, (const uint8_t* const*)validity, pred_op,
            as_f64, lit_i, lit_f, threads, out8);
@@ -319,11 +332,15 @@ double dqo_time_c2_hll(int64_t rows, int threads, dqo_colstate* out8, uint8_t* r
     free(jobs);
   }
   clock_gettime(CLOCK_MONOTONIC, &t1);
+  total += (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+  ++done;
+  } while (total < min_secs && done < 1000);
   for (int c = 0; c < 8; ++c) {
     free(values[c]);
     free(validity[c]);
   }
-  return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+  *passes = done;
+  return total;
 }
 
 /* ------------------------------------------------------------------ XXH64 + HLL registers */
