@@ -365,23 +365,28 @@ __device__ bool parse_long_words(const WordSrc& ws, int32_t n, int64_t* out) {
   return parse_long(ws, n, out);
 }
 
-__device__ inline bool cast_one(const WordSrc& p, int32_t n, int to_type, int64_t* lv, double* dv) {
-  if (to_type == DQ_T_INT64) return parse_long_words(p, n, lv);
-  return parse_double(p, n, dv) == 1;
+template <int TO>
+__device__ inline bool cast_one(const WordSrc& p, int32_t n, int64_t* lv, double* dv) {
+  if constexpr (TO == DQ_T_INT64) return parse_long_words(p, n, lv);
+  else return parse_double(p, n, dv) == 1;
 }
 
-template <typename Src>
-__device__ inline bool cast_one(const Src& p, int32_t n, int to_type, int64_t* lv, double* dv) {
-  if (to_type == DQ_T_INT64) return parse_long(p, n, lv);
-  return parse_double(p, n, dv) == 1;
+template <int TO, typename Src>
+__device__ inline bool cast_one(const Src& p, int32_t n, int64_t* lv, double* dv) {
+  if constexpr (TO == DQ_T_INT64) return parse_long(p, n, lv);
+  else return parse_double(p, n, dv) == 1;
 }
 
 }  // namespace
 
 // One row per lane: values are written coalesced, and each wave's 64 validity bits (a ballot)
-// are stored by its first lane -- one 8-byte word when the wave's rows are all in range.
-__global__ __launch_bounds__(kBlock) void dq_cast_utf8_kernel(DevColumn src, int64_t n_rows, int to_type,
-                                                              void* values, uint8_t* validity) {
+// are stored by its first lane -- one 8-byte word when the wave's rows are all in range.  One
+// instantiation per target type: the string -> long cast does not carry the double parser's
+// registers (its exact big-number path) into its occupancy.
+template <int TO>
+__global__ __launch_bounds__(kBlock) void dq_cast_utf8_kernel(DevColumn src, int64_t n_rows, void* values,
+                                                              uint8_t* validity) {
+  constexpr int to_type = TO;
   const uint32_t lane = threadIdx.x & 63u;
   for (int64_t base = (int64_t)blockIdx.x * kBlock; base < n_rows; base += (int64_t)gridDim.x * kBlock) {
     const int64_t row = base + threadIdx.x;
@@ -391,8 +396,8 @@ __global__ __launch_bounds__(kBlock) void dq_cast_utf8_kernel(DevColumn src, int
     if (row < n_rows && (src.validity == nullptr || bit_at(src.validity, row))) {
       const int32_t b = src.offsets[row], e = src.offsets[row + 1];
       const uint8_t* p = static_cast<const uint8_t*>(src.values) + b;
-      if (e - b <= 24) ok = cast_one(WordSrc(p, e - b), e - b, to_type, &lv, &dv);
-      else ok = cast_one(PtrSrc{p}, e - b, to_type, &lv, &dv);
+      if (e - b <= 24) ok = cast_one<TO>(WordSrc(p, e - b), e - b, &lv, &dv);
+      else ok = cast_one<TO>(PtrSrc{p}, e - b, &lv, &dv);
     }
     if (row < n_rows) {
       if (to_type == DQ_T_INT64) static_cast<int64_t*>(values)[row] = ok ? lv : 0;
@@ -437,8 +442,12 @@ hipError_t launch_cast_utf8(const DevColumn& src, int64_t n_rows, int to_type, v
   if (n_rows <= 0) return hipSuccess;
   int64_t blocks = (n_rows + kBlock - 1) / kBlock;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(dq_cast_utf8_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, src, n_rows, to_type,
-                     d_values, d_validity);
+  if (to_type == DQ_T_INT64)
+    hipLaunchKernelGGL(dq_cast_utf8_kernel<DQ_T_INT64>, dim3((unsigned)blocks), dim3(kBlock), 0, stream, src, n_rows,
+                       d_values, d_validity);
+  else
+    hipLaunchKernelGGL(dq_cast_utf8_kernel<DQ_T_FLOAT64>, dim3((unsigned)blocks), dim3(kBlock), 0, stream, src, n_rows,
+                       d_values, d_validity);
   return hipGetLastError();
 }
 
