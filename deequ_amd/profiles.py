@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import re
 import ctypes
+import os
 import json
 from collections import OrderedDict
 from dataclasses import dataclass, field
@@ -178,21 +179,42 @@ class ColumnProfiler:
 
         if printStatusUpdates:
             print("### PROFILING: Computing numeric column statistics in pass (2/3)...")
-        casted = _cast_numeric_string_columns(relevant, data, generic)
-        second = []
-        for c in relevant:
-            if c not in early and generic.typeOf(c) in numeric_types:
-                second += _stats(c)
-        numeric = _extract_numeric_statistics(ctx1)
-        if second:
-            ctx2 = AnalysisRunner.onData(casted).addAnalyzers(second).run()
-            for k, v in _extract_numeric_statistics(ctx2).items():
-                numeric[k].update(v)
+        # Pass 3 needs only pass 1's results (the inferred types and distinct estimates), so on
+        # one device its group-bys run beside pass 2's casts and scan (each on its own streams;
+        # the library releases the GIL).  Over a ShardedTable both passes are collective, so
+        # they stay in order there.  A pass-2 failure is raised as the sequential run would.
+        targets = _find_target_columns_for_histograms(schema, generic, lowCardinalityHistogramThreshold)
+        from concurrent.futures import ThreadPoolExecutor
+        from .distributed import is_sharded
+        overlap = os.environ.get("DEEQU_AMD_PROFILE_SERIAL", "0") != "1"  # (A/B and debugging knob)
+        side = ThreadPoolExecutor(max_workers=1) if overlap and targets and not is_sharded(data) else None
+        pending = (side.submit(compute_histograms, data, targets, generic.approximateNumDistincts)
+                   if side else None)
+        try:
+            casted = _cast_numeric_string_columns(relevant, data, generic)
+            second = []
+            for c in relevant:
+                if c not in early and generic.typeOf(c) in numeric_types:
+                    second += _stats(c)
+            numeric = _extract_numeric_statistics(ctx1)
+            if second:
+                ctx2 = AnalysisRunner.onData(casted).addAnalyzers(second).run()
+                for k, v in _extract_numeric_statistics(ctx2).items():
+                    numeric[k].update(v)
+        except BaseException:
+            if side:
+                side.shutdown(wait=True)
+            raise
 
         if printStatusUpdates:
             print("### PROFILING: Computing histograms of low-cardinality columns in pass (3/3)...")
-        targets = _find_target_columns_for_histograms(schema, generic, lowCardinalityHistogramThreshold)
-        histograms = compute_histograms(data, targets, generic.approximateNumDistincts)
+        if side:
+            try:
+                histograms = pending.result()
+            finally:
+                side.shutdown(wait=True)
+        else:
+            histograms = compute_histograms(data, targets, generic.approximateNumDistincts)
         return _create_profiles(relevant, generic, numeric, histograms)
 
 
