@@ -226,7 +226,7 @@ def cpu_baseline(sample_rows: int, threads: int):
     secs, passes = cdq_oracle.time_c2_scan(sample_rows, threads, min_secs=CPU_BASELINE_SECS)
     rows = sample_rows * passes
     return {"value": rows / secs, "unit": "rows/s", "cores": threads, "kind": "port",
-            "host_cpus": os.cpu_count(), "value_per_core": sample_rows / secs / threads,
+            "host_cpus": os.cpu_count(), "value_per_core": rows / secs / threads,
             "cores_policy": "the CPUs this process may use: affinity mask capped by OMP_NUM_THREADS (the GPU "
                             "pool gives each GPU 16 of the host's %d; os.cpu_count() counts all 8 GPUs' share)"
                             % (os.cpu_count() or 0),
