@@ -1120,7 +1120,7 @@ constexpr int kPartPerThread = 16;
 constexpr uint32_t kPartTile = (uint32_t)kPartThreads * kPartPerThread;  // records per tile
 constexpr uint32_t kPartSub = DQ_PART_SUB;                               // records per LDS round
 #ifndef DQ_PARTP_PER
-#define DQ_PARTP_PER 16
+#define DQ_PARTP_PER 24
 #endif
 #ifndef DQ_PARTP_SUB
 #define DQ_PARTP_SUB 6144
@@ -1687,7 +1687,7 @@ __device__ inline bool lds_count_packed(unsigned long long* K, uint32_t* C, uint
 }
 
 #ifndef DQ_AGGP_BATCH
-#define DQ_AGGP_BATCH 8
+#define DQ_AGGP_BATCH 4
 #endif
 constexpr int kAggPBatch = DQ_AGGP_BATCH;  // packed records per thread loaded together
 
