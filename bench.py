@@ -33,6 +33,9 @@ BYTES_PER_ROW = 8 * (8 + 1.0 / 8)  # 8 columns x (8 B value + 1 validity bit) = 
 def parse_args():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                   help="process-group backend for N > 1: nccl (= RCCL over xGMI, the measured path) or gloo "
+                        "(host collectives: the multi-rank path rehearsed on a one-GPU box, ranks sharing cuda:0)")
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--rows", type=int, default=1_000_000_000, help="rows per GPU")
@@ -58,6 +61,9 @@ def parse_args():
     p.add_argument("--c4-rows", type=int, default=1_000_000_000, help="rows per GPU")
     p.add_argument("--c4-batch", type=int, default=125_000_000, help="rows per string batch")
     p.add_argument("--c4-distinct", type=int, default=201_500_000)
+    p.add_argument("--c4-verify", action="store_true",
+                   help="after timing, check the C4 metrics against torch.unique over the integer ids on the "
+                        "device (an independent sort-based group-by; 1 rank); adds `verify` to the line")
     p.add_argument("--c5-rows", type=int, default=100_000_000, help="rows per GPU")
     return p.parse_args()
 
@@ -301,6 +307,65 @@ def make_c3_string_table(rows: int, n_cols: int, rank: int, device: int):
     return d.Table(cols)
 
 
+def c4_valid_ids(rows: int, batch: int, distinct: int, rank: int, device: int):
+    """The integer ids behind make_c4_batches' non-NULL keys, regenerated from the same generator
+    sequence (the keys are their 12-digit decimals), concatenated on the device."""
+    import torch
+    dev = torch.device("cuda", device)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(7 + 1000 * rank)
+    out = []
+    for b0 in range(0, rows, batch):
+        m = min(batch, rows - b0)
+        sub = 1 << 24
+        for s in range(0, m, sub):
+            e = min(m, s + sub)
+            keys = torch.randint(0, distinct, (e - s,), generator=gen, device=dev, dtype=torch.int64)
+            valid = torch.rand(e - s, generator=gen, device=dev) >= 0.01  # as _valid_bits draws them
+            out.append(keys[valid])
+    return torch.cat(out)
+
+
+def c4_verify(args, metrics, dist_metric, analyzers):
+    """The C4 metrics against torch.unique(return_counts=True) over the same ids on the device:
+    CountDistinct, Uniqueness, Distinctness exactly, Entropy within 1e-12 (same count-of-counts
+    summation order), Histogram's NULL bin and number of bins exactly, and every detail bin's
+    count plus the detail bins' count multiset (the top counts; ties at the cut are broken by key)."""
+    import math
+    import numpy as np
+    import torch
+    ids = c4_valid_ids(args.c4_rows, args.c4_batch, args.c4_distinct, 0, torch.cuda.current_device())
+    n_valid = int(ids.numel())
+    u, c = torch.unique(ids, sorted=True, return_counts=True)
+    del ids
+    n = float(args.c4_rows)
+    groups, unique = int(u.numel()), int((c == 1).sum())
+    hist = torch.bincount(c).cpu().tolist()
+    ent = 0.0
+    for k in range(1, len(hist)):  # dq_freq_api.inc summary_from_hist's order and terms
+        if hist[k]:
+            ent += float(hist[k]) * (-(k / n) * math.log(k / n))
+    got = {str(a): v for a, v in metrics.items()}
+    out = {"n_valid": n_valid, "groups": groups, "unique": unique,
+           "count_distinct_ok": got[str(analyzers[3])] == float(groups),
+           "uniqueness_ok": got[str(analyzers[0])] == unique / n,
+           "distinctness_ok": got[str(analyzers[1])] == groups / n,
+           "entropy_rel_err": abs(got[str(analyzers[2])] - ent) / ent}
+    uh, ch = u.cpu().numpy(), c.cpu().numpy()
+    vals = {k: v.absolute for k, v in dist_metric.values.items()}
+    nonnull = {k: a for k, a in vals.items() if k != "NullValue"}
+    idx = np.array([int(k) for k in nonnull], dtype=np.int64)
+    cnt = np.array(list(nonnull.values()), dtype=np.int64)
+    pos = np.clip(np.searchsorted(uh, idx), 0, len(uh) - 1)
+    out["detail_bins"] = len(nonnull)
+    out["detail_counts_ok"] = bool(np.all(uh[pos] == idx) and np.all(ch[pos] == cnt))
+    out["detail_multiset_ok"] = bool(np.array_equal(np.sort(cnt)[::-1], np.sort(ch)[::-1][:len(cnt)]))
+    out["null_bin_ok"] = vals.get("NullValue", 0) == args.c4_rows - n_valid
+    out["number_of_bins_ok"] = dist_metric.numberOfBins == groups + (1 if n_valid < args.c4_rows else 0)
+    out["ok"] = all(out[k] for k in out if k.endswith("_ok")) and out["entropy_rel_err"] <= 1e-12
+    return out
+
+
 def make_c4_batches(rows: int, batch: int, distinct: int, rank: int, device: int):
     """C4: a string key = 12-digit zero-padded decimal of a uniform int in [0, distinct), 1% NULL,
     as Arrow utf8 batches of `batch` rows (int32 offsets cap one batch at 2 GiB of chars)."""
@@ -327,6 +392,11 @@ def make_c4_batches(rows: int, batch: int, distinct: int, rank: int, device: int
         parts.append(d.Table({"key": d.Column("string", m, chars, valid, offsets=offsets, device=True)}))
     torch.cuda.synchronize(dev)
     return d.PartitionedTable(parts)
+
+
+def _comm_dev(args, local: int):
+    """allgather_merge's device argument: the GPU for RCCL, None (host tensors) for gloo."""
+    return local if args.backend == "nccl" else None
 
 
 def valu_roofline(device: int, hashes: float, kernel_ms: float):
@@ -367,7 +437,7 @@ def run_c3(args, world, rank, local):
             ev[1].record(stream)
         raw = plan.finish_raw()
         if world > 1:
-            raw = allgather_merge(raw, len(analyzers), device=local)
+            raw = allgather_merge(raw, len(analyzers), device=_comm_dev(args, local))
         return raw
     elapsed, kernel_ms, raw = _timed(args, world, step)
     est = d.ApproxCountDistinctState(list(raw[0].words)).metricValue()
@@ -390,7 +460,7 @@ def run_c3(args, world, rank, local):
             scan_ms += e0.elapsed_time(e1)
         fraw = plan.finish_raw()
         if world > 1:
-            fraw = allgather_merge(fraw, len(analyzers), device=local)
+            fraw = allgather_merge(fraw, len(analyzers), device=_comm_dev(args, local))
         rows_job = args.c3_rows * args.c3_batches
         full_job = {"batches": args.c3_batches, "rows_per_gpu": rows_job, "columns": args.c3_columns,
                     "scan_ms": scan_ms, "rows_per_s_per_gpu": rows_job / (scan_ms * 1e-3),
@@ -497,6 +567,10 @@ def run_c4(args, world, rank, local):
     elapsed, _, ctx = _timed(args, world, step)
     metrics = {str(a): ctx.metric(a).value.get() for a in analyzers[:4]}
     hist = ctx.metric(analyzers[4]).value.get()
+    verify = None
+    if args.c4_verify and world == 1:
+        del ctx
+        verify = c4_verify(args, {a: metrics[str(a)] for a in analyzers[:4]}, hist, analyzers)
     in_bytes = sum(_column_bytes(b.columns["key"]) for b in shard.batches())
     groups = metrics[str(analyzers[3])] / world  # the groups this rank's share of the table holds
     # input + one write of the final table (8 B hash + 8 B count + 8 B key ref)
@@ -527,6 +601,7 @@ def run_c4(args, world, rank, local):
         "table_access": {"record_passes_per_row": 3, "record_bytes": 8, "global_table_probes_per_row": 0,
                          "table_slots_written_per_row": _c4_table_slots(groups) / float(args.c4_rows)},
         "check": dict(metrics, histogram_bins=hist.numberOfBins),
+        **({"verify": verify} if verify is not None else {}),
     }
 
 
@@ -709,6 +784,16 @@ def run_c5(args, world, rank, local):
     }
 
 
+def _max_over_ranks(x: float) -> float:
+    """MAX over the ranks (the job's time), on the device the process group's backend uses."""
+    import torch
+    import torch.distributed as dist
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def _timed(args, world, step):
     """W warmup steps, then K timed steps between barriers + device syncs; max over ranks."""
     import torch
@@ -731,9 +816,7 @@ def _timed(args, world, step):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = _max_over_ranks(elapsed)
     try:
         kernel_ms = sum(a.elapsed_time(b) for a, b in events) / len(events)
     except (RuntimeError, ValueError):  # the step did not record the events
@@ -773,10 +856,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend == "gloo":  # a rehearsal of the multi-rank path: ranks may share a GPU
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     d.set_device(local)
-    if world > 1:
+    if world > 1 and args.backend == "nccl":
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    elif world > 1:
+        dist.init_process_group("gloo")
     if args.workload != "c2":
         result = {"c1": run_c1, "c3": run_c3, "c4": run_c4, "c5": run_c5}[args.workload](args, world, rank, local)
         if rank == 0:
@@ -801,7 +888,7 @@ def main():
             ev_pair[1].record(stream)
         raw = plan.finish_raw()
         if world > 1:
-            raw = allgather_merge(raw, n_ops, device=local)
+            raw = allgather_merge(raw, n_ops, device=_comm_dev(args, local))
         return raw
 
     for _ in range(args.warmup):
@@ -819,9 +906,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = _max_over_ranks(elapsed)
 
     kernel_ms = sum(a.elapsed_time(b) for a, b in events) / len(events)
     states = [state_from_dq(raw[i]) for i in range(n_ops)]
@@ -869,6 +954,13 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or host_cpu_share()
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample_rows, threads)
+        # beside the one-GPU share: every host CPU (nproc), as SURVEY §8(d) states the baseline
+        nproc = os.cpu_count() or threads
+        if nproc != threads and result["cpu_baseline"].get("value"):
+            allc = cpu_baseline(args.cpu_sample_rows, nproc)
+            result["cpu_baseline"]["all_host_cpus"] = {
+                "value": allc.get("value"), "unit": "rows/s", "cores": nproc, "nproc": nproc,
+                "value_per_core": allc.get("value_per_core"), "sample": allc.get("sample")}
     if rank == 0:
         print(json.dumps(result))
     if world > 1:

@@ -158,7 +158,9 @@ SIGNATURES = {
     "dq_freq_import": (c_int, [c_void_p, POINTER(DqFreqGroup), c_int64, c_void_p, c_int64]),
     "dq_cast_utf8": (c_int, [c_void_p, POINTER(DqColumn), c_int64, c_int32, c_void_p, c_void_p, POINTER(c_int64)]),
     "dq_freq_partition": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_void_p, c_int64, POINTER(c_int64),
-                                  POINTER(c_int64)]),
+                                  POINTER(c_int64), POINTER(c_int64)]),
+    "dq_freq_import_parts": (c_int, [c_void_p, c_int, c_void_p, POINTER(c_int64), POINTER(c_int64), c_void_p,
+                                     POINTER(c_int64), c_int64]),
     "dq_freq_import_wire": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_int64]),
     "dq_freq_count_histogram": (c_int, [c_void_p, POINTER(c_int64), c_int64, POINTER(c_int64), c_int64,
                                         POINTER(c_int64)]),

@@ -749,6 +749,7 @@ struct dq_plan : Stager {
   std::vector<Program> programs;  // generic predicate programs -> batch masks
   // device state
   std::vector<dq_status> op_status;  // per op, after dq_plan_finish
+  bool pred_cast = false;  // a predicate program casts a string to double (its own kernel: the parser's scratch)
   DevBuf d_tasks, d_groups, d_ranges, d_hll, d_progs, d_insns, d_pool, d_acc, d_partials, d_regs,
       d_cols, d_masks, d_mask_words, d_dtype, d_dtype_counts, d_len, d_len_out, d_corr, d_corr_part, d_corr_acc, d_str;
   int64_t mask_words = 0;
@@ -1054,10 +1055,12 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
   std::vector<PredProgram> progs;
   std::vector<PredInsn> insns;
   std::string pool;
+  plan->pred_cast = false;
   for (const auto& p : plan->programs) {
     progs.push_back(PredProgram{(int32_t)insns.size(), (int32_t)p.code.size()});
     for (PredInsn in : p.code) {
       if (in.opcode == DQ_P_LIT_STRING) in.i64 += (int64_t)pool.size();  // plan-wide pool offset
+      if (in.opcode == DQ_P_CAST_DOUBLE) plan->pred_cast = true;
       insns.push_back(in);
     }
     pool += p.pool;
@@ -1392,7 +1395,8 @@ extern "C" dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, in
     DQ_HIP(launch_predicates(static_cast<const PredProgram*>(plan->d_progs.ptr), n_progs,
                              static_cast<const PredInsn*>(plan->d_insns.ptr),
                              static_cast<const uint8_t*>(plan->d_pool.ptr), d_cols, n_rows,
-                             static_cast<uint64_t*>(plan->d_mask_words.ptr), plan->mask_words, plan->stream));
+                             static_cast<uint64_t*>(plan->d_mask_words.ptr), plan->mask_words, plan->pred_cast,
+                             plan->stream));
 
   if (n_scan > 0) {
     ScanAcc* parts = static_cast<ScanAcc*>(plan->d_partials.ptr);

@@ -23,6 +23,7 @@
 #include "dq_internal.h"
 #include "dq_keypack.h"
 
+#include <cstdio>
 #include <type_traits>
 
 namespace dq {
@@ -105,19 +106,29 @@ __device__ inline uint64_t hash_raw(uint64_t k0, uint64_t k1, uint32_t len) {
   return h ^ (h >> 32);
 }
 
-// The table hash of a packed digit record (dq_keypack.h): the key's bytes are unpacked (a few
-// shifts and masks) and hashed like every other inline key, so the table and every other path
-// are unchanged by the record format.
+// The table hash of a key that packs into one word (a digit string, or Histogram's NULL group;
+// dq_keypack.h): two 64-bit multiplies of the packed word, each followed by a fold of the high
+// half into the low one.  The partition path's level-2 split and its slice aggregation hash
+// every record, so a packed record is hashed as it is (round 3 unpacked it and ran hash_raw:
+// ~75 VALU instructions per record against ~13).  Bins measured Poisson-spread over the slice,
+// probe, tag and owner bits for C4's 12-digit keys and sequential decimal strings.
 __device__ inline uint64_t hash_record_packed(uint64_t p) {
-  uint64_t k0, k1;
-  uint32_t len;
-  kp_unpack(p, &k0, &k1, &len);
-  return hash_raw(k0, k1, len);
+  uint64_t x = p + 0x9E3779B97F4A7C15ull;
+  x ^= x >> 32;
+  x *= 0xD6E8FEB86659FD93ull;
+  x ^= x >> 32;
+  x *= 0xD6E8FEB86659FD93ull;
+  return x ^ (x >> 32);
 }
 
 // The table hash of an inline key, wherever a key is hashed (stage, splits, aggregations,
-// inserts, imports, lookups, rehash, owner ranks).
-__device__ inline uint64_t hash_inline(uint64_t k0, uint64_t k1, uint32_t len) { return hash_raw(k0, k1, len); }
+// inserts, imports, lookups, rehash, owner ranks): a key that packs is hashed as its packed
+// word, so a digit key hashes alike whether it travels as a packed or a 16-byte record.
+__device__ inline uint64_t hash_inline(uint64_t k0, uint64_t k1, uint32_t len) {
+  uint64_t p;
+  if (kp_pack_record(k0, k1, len, &p)) return hash_record_packed(p);
+  return hash_raw(k0, k1, len);
+}
 
 // One row's grouping key.  Inline (len <= 16) keys live in k0/k1; longer keys point at their
 // bytes (`ptr`, in the batch or in thread-local scratch).
@@ -347,7 +358,7 @@ __device__ bool global_insert(const FreqTable& T, const Key& k, unsigned long lo
   uint64_t probes = 0;
   uint64_t slot = probe_slot(T, k.hash, 0);
   uint32_t waits = 0;
-  int state = 0;  // 0 = probing, 1 = counted, 2 = no room in the slice, 3 = key heap full
+  int state = 0;  // 0 = probing, 1 = counted, 2 = no room in the slice, 3 = key heap full, 4 = wait timeout
   while (state == 0) {
     FreqSlot* e = &T.slots[slot];
     const unsigned long long c = atomicCAS(&e->ctrl, 0ull, want);
@@ -375,11 +386,14 @@ __device__ bool global_insert(const FreqTable& T, const Key& k, unsigned long lo
       }
       atomicAdd(&e->count, cnt);
       if (heap_ok) atomicAdd(T.n_groups, 1ull);
-      __hip_atomic_fetch_or(&e->ctrl, kReady, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      if (!(T.test_flags & kFreqTestNoPublish))
+        __hip_atomic_fetch_or(&e->ctrl, kReady, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       state = heap_ok ? 1 : 3;  // (3: heap full, flagged above with bit 2 only)
     } else if ((uint32_t)(c >> 32) == tag && (c & (kLenMask | kHeapKey)) == (want & (kLenMask | kHeapKey))) {
       if (!(c & kReady)) {  // being published by another lane/wave: look at this slot again
-        if (++waits > (1u << 24)) state = 2;
+        // (a wait that never ends is a failure -- its own overflow bit, reported as an error by
+        // every caller -- never a full slice that would send the rows to a retry)
+        if (++waits > (1u << 22)) state = 4;
         else __builtin_amdgcn_s_sleep(1);
       } else {
         bool eq;
@@ -405,6 +419,7 @@ __device__ bool global_insert(const FreqTable& T, const Key& k, unsigned long lo
     }
   }
   if (state == 2 && kFlagOverflow) atomicOr(T.overflow, 1u);
+  if (state == 4) atomicOr(T.overflow, kFreqWaitTimeout);
   return state == 1;
 }
 
@@ -692,50 +707,15 @@ __global__ void dq_freq_lookup_kernel(FreqTable T, const uint8_t* key, uint32_t 
 }
 
 // ---- multi-GPU key-hash partitioning (owner = a function of hash bits the table does not use
-// for its slot index, so every owner's keys still spread over its whole table)
+// for its slot index, so every owner's keys still spread over its whole table): bits 11..30,
+// above the first probe (bits 0..10) and below any slice index (the top <= 22 bits); they
+// overlap only the 32-bit tag, which then loses log2(n_parts) bits of its spread per owner.
 __device__ inline uint32_t freq_owner(uint64_t h, uint32_t n_parts) {
-  return (uint32_t)(((uint64_t)(uint32_t)(h >> 16) * n_parts) >> 32);
+  return (uint32_t)((((h >> 11) & 0xFFFFFull) * n_parts) >> 20);
 }
 
 __device__ inline uint64_t slot_hash(const FreqTable& T, const FreqSlot& e, uint32_t len) {
   return (e.ctrl & kHeapKey) ? xxh64_any(T.heap + e.k0, len, 42) : hash_inline(e.k0, e.k1, len);
-}
-
-__global__ __launch_bounds__(kBlock) void dq_freq_part_count_kernel(FreqTable T, int n_parts,
-                                                                    unsigned long long* cnt) {
-  const uint64_t n = T.mask + 1;
-  for (uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x; s < n; s += (uint64_t)gridDim.x * kBlock) {
-    const FreqSlot e = T.slots[s];  // launch boundary: every insert is visible
-    if (!(e.ctrl & kReady)) continue;
-    const uint32_t len = (uint32_t)(e.ctrl & kLenMask);
-    const uint32_t p = freq_owner(slot_hash(T, e, len), (uint32_t)n_parts);
-    atomicAdd(&cnt[2 * p], 1ull);
-    if (e.ctrl & kHeapKey) atomicAdd(&cnt[2 * p + 1], ((unsigned long long)len + 7ull) & ~7ull);
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void dq_freq_part_scatter_kernel(FreqTable T, int n_parts,
-                                                                      const unsigned long long* base,
-                                                                      unsigned long long* cursor,
-                                                                      FreqSlot* out, uint8_t* keys) {
-  const uint64_t n = T.mask + 1;
-  for (uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x; s < n; s += (uint64_t)gridDim.x * kBlock) {
-    FreqSlot e = T.slots[s];
-    if (!(e.ctrl & kReady)) continue;
-    const uint32_t len = (uint32_t)(e.ctrl & kLenMask);
-    const uint32_t p = freq_owner(slot_hash(T, e, len), (uint32_t)n_parts);
-    const unsigned long long i = atomicAdd(&cursor[2 * p], 1ull);
-    if (e.ctrl & kHeapKey) {
-      const unsigned long long bytes = ((unsigned long long)len + 7ull) & ~7ull;
-      const unsigned long long off = atomicAdd(&cursor[2 * p + 1], bytes);  // within part p's region
-      const uint64_t* src = reinterpret_cast<const uint64_t*>(T.heap + e.k0);
-      uint64_t* dst = reinterpret_cast<uint64_t*>(keys + base[2 * p + 1] + off);
-      for (unsigned long long w = 0; w < bytes / 8; ++w) dst[w] = src[w];
-      e.k0 = off;
-    }
-    e.ctrl &= ~kReady;  // wire form: READY is a table-internal flag
-    out[base[2 * p] + i] = e;
-  }
 }
 
 // ---- sorted-bucket path ---------------------------------------------------------------------
@@ -1132,8 +1112,10 @@ constexpr uint32_t kPartSubP = DQ_PARTP_SUB;
 constexpr int kPartMaxBinBits = kPartMaxBits;
 constexpr int kStageBinBits = 9;  // the level-1 split of the fused stage (dq_freq_api.inc kRegionBits)
 constexpr uint32_t kPartNoBin = 0xFFFFu;
-constexpr int kStageGroup = 4;  // rows per thread whose loads the fused stage issues together
-constexpr int kStagePer = 12;   // rows per thread per fused-stage tile (register budget)
+#ifndef DQ_STAGE_PER
+#define DQ_STAGE_PER 12
+#endif
+constexpr int kStagePer = DQ_STAGE_PER;   // rows per thread per fused-stage tile (register budget)
 constexpr uint32_t kStageTile = (uint32_t)kPartThreads * kStagePer;
 #ifndef DQ_STAGEP_SUB
 #define DQ_STAGEP_SUB 6144
@@ -1177,27 +1159,53 @@ __device__ inline FreqRec rec_raw(uint64_t p) {
   return r;
 }
 
+// Phase timing of the fused stage (a diagnostic build only, -DDQ_STAGE_PROF): thread 0 of every
+// workgroup adds the clock cycles of each phase of each tile to g_stage_prof (read back and
+// printed per launch by launch_freq_stage_part).
+#ifdef DQ_STAGE_PROF
+__device__ unsigned long long g_stage_prof[8];
+#define DQ_PROF_MARK(PROF, i)                                                        \
+  do {                                                                               \
+    if (PROF && threadIdx.x == 0) {                                                  \
+      const unsigned long long now_ = clock64();                                     \
+      if (i > 0) atomicAdd(&g_stage_prof[i - 1], now_ - prof_t_);                    \
+      prof_t_ = now_;                                                                \
+    }                                                                                \
+  } while (0)
+#else
+#define DQ_PROF_MARK(PROF, i) do { } while (0)
+#endif
+
 // One tile's multi-split: each thread holds kPartPerThread records and their LDS bins (bin <
 // 2^bin_bits, or kPartNoBin for none); output region of a bin = base_id + bin.  Ranks come from
 // LDS atomics, the room in each region from ONE device atomic per (tile, non-empty bin), and the
 // records are written from an LDS image sorted by bin, kPartSub at a time (coalesced runs).
-template <int PER, int MAXB, typename R, uint32_t SUBN>
+struct NoMid {
+  __device__ void operator()() const {}
+};
+// mid(): called once the tile's room is reserved, before its records are written (the fused
+// stage issues the next tile's offset loads there, so they arrive during the writes).
+template <int PER, int MAXB, typename R, uint32_t SUBN, bool PROF = false, int WOUT_UNROLL = 16, typename Mid = NoMid>
 __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER], uint32_t (&bin)[PER],
                                  uint32_t nb, uint64_t base_id, R* __restrict__ out, uint64_t out_cap,
                                  unsigned long long* out_fill, FreqRec* ovf, unsigned long long* ovf_n,
                                  uint64_t ovf_cap, unsigned int* flag, unsigned long long* staged,
-                                 const unsigned long long* region_start = nullptr) {
+                                 const unsigned long long* region_start = nullptr, unsigned long long prof_t_ = 0,
+                                 const Mid& mid = Mid()) {
   // region_start != nullptr: exact regions -- output region id starts at record region_start[id]
   // of `out` (sizes counted beforehand: nothing can overflow), out_fill is its cursor
   constexpr uint32_t SUB = SUBN;
   const uint32_t t = threadIdx.x;
+  DQ_PROF_MARK(PROF, 1);
   for (uint32_t i = t; i < nb; i += kPartThreads) L.hist[i] = 0u;
   __syncthreads();
+  DQ_PROF_MARK(PROF, 2);
   // rank of each record within its bin (LDS atomics), packed with the bin: rank << 16 | bin
 #pragma unroll
   for (int i = 0; i < PER; ++i)
     if (bin[i] != kPartNoBin) bin[i] |= atomicAdd(&L.hist[bin[i]], 1u) << 16;
   __syncthreads();
+  DQ_PROF_MARK(PROF, 3);
   // exclusive scan of the bins by wave 0 (nb / 64 consecutive bins per lane)
   if (t < 64) {
     const uint32_t per = (nb + 63u) / 64u;
@@ -1225,6 +1233,7 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
     }
   }
   __syncthreads();
+  DQ_PROF_MARK(PROF, 4);
   for (uint32_t b = t; b < nb; b += kPartThreads) {
     const uint32_t c = L.hist[b];
     L.gbase[b] = c ? atomicAdd(&out_fill[base_id + b], (unsigned long long)c) : 0ull;
@@ -1232,6 +1241,8 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
   }
   const uint32_t total = L.total;
   __syncthreads();
+  DQ_PROF_MARK(PROF, 5);
+  mid();
   for (uint32_t r0 = 0; r0 < total; r0 += SUB) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -1244,7 +1255,10 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
       }
     }
     __syncthreads();
+    DQ_PROF_MARK(PROF, 6);
     const uint32_t m = min(SUB, total - r0);
+    // (a bounded unroll: the fused stage holds the next tile's offsets across this loop)
+#pragma unroll WOUT_UNROLL
     for (uint32_t j = t; j < m; j += kPartThreads) {
       const uint32_t b = L.bin[j];
       const uint64_t o = L.gbase[b] + (r0 + j - L.start[b]);
@@ -1260,6 +1274,7 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
       }
     }
     __syncthreads();
+    DQ_PROF_MARK(PROF, 7);
   }
 }
 
@@ -1486,6 +1501,96 @@ __global__ __launch_bounds__(kBlock) void dq_freq_pieces_kernel(const unsigned l
 // a key that is not a digit string goes to the overflow list as a 16-B record (counted there and
 // in `staged`), and a batch with more of them than the list holds raises `flag` (the host then
 // rolls it back and stages the table's keys as 16-B records from then on).
+// A pointer every lane holds alike, in scalar registers (a buffer descriptor built from a value
+// the compiler cannot prove uniform is re-made per lane in a waterfall loop).
+template <typename T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<T*>(((uint64_t)hi << 32) | lo);
+}
+
+// The (begin, end) offsets of tile `tl`'s kStagePer rows of one utf8 column (row j of this thread
+// = tl * kStageTile + j * kPartThreads + threadIdx.x): one 8-byte load of each row's offset pair
+// through a descriptor of the tile's offsets (rows past the batch read 0).  The validity bits
+// come as ONE dword per lane: row j of lane l of wave w is bit l & 31 of tile dword
+// 16 j + 2 w + (l >> 5), which lane 2 j + (l >> 5) of the wave loads (stage_valid_mask).
+__device__ __forceinline__ void stage_offsets(const DevColumn& c0, int64_t n_rows, int64_t tl,
+                                              uint32_t (&pob)[kStagePer], uint32_t (&poe)[kStagePer],
+                                              uint32_t& vword) {
+  const int64_t r0 = tl * (int64_t)kStageTile;
+  const int64_t left = n_rows - r0;
+  const uint32_t m = (uint32_t)(left < (int64_t)kStageTile ? left : (int64_t)kStageTile);
+  const uint32_t t = threadIdx.x;
+  const __amdgpu_buffer_rsrc_t rs_off = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int32_t*>(uniform_ptr(c0.offsets) + r0), 0, (int)(4u * (m + 1u)), 0x00020000);
+#pragma unroll
+  for (int j = 0; j < kStagePer; ++j) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs_off, (int)(4u * ((uint32_t)j * kPartThreads + t)), 0, 0);
+    pob[j] = v[0];
+    poe[j] = v[1];
+  }
+  const uint8_t* validity = uniform_ptr(c0.validity);
+  if (validity != nullptr) {
+    const uint32_t l = t & 63u, w = t >> 6;
+    const __amdgpu_buffer_rsrc_t rs_v = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(validity + (r0 >> 3)), 0, (int)((m + 7u) >> 3), 0x00020000);
+    const uint32_t dw = 16u * (l >> 1) + 2u * w + (l & 1u);
+    const uint32_t nbytes = (m + 7u) >> 3;
+    vword = 0u;
+    if (l < 2u * kStagePer) {
+      if (4u * dw + 4u <= nbytes) {
+        vword = __builtin_amdgcn_raw_buffer_load_b32(rs_v, (int)(4u * dw), 0, 0);
+      } else {  // the bitmap's last, partial dword: byte by byte (a range check is per dword)
+        for (uint32_t k = 0; k < 4u; ++k)
+          if (4u * dw + k < nbytes)
+            vword |= (uint32_t)(uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rs_v, (int)(4u * dw + k), 0, 0) << (8u * k);
+      }
+    }
+  }
+}
+
+// The 16 bytes from a key's first byte (one unaligned buffer load), or -- for a key that ends
+// within 16 bytes of the heap's end -- its bytes from the aligned words that hold them.
+template <int N>
+__device__ __forceinline__ void stage_key_load(__amdgpu_buffer_rsrc_t rs_vals, const uint8_t* vals, uint32_t heap_end,
+                                               uint32_t ob, const uint32_t (&lens)[N], int j, uint32_t (&w)[4]) {
+  if (ob + 16u <= heap_end) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_vals, (int)ob, 0, 0);
+    w[0] = v[0];
+    w[1] = v[1];
+    w[2] = v[2];
+    w[3] = v[3];
+  } else {
+    uint32_t n = (lens[j / 4] >> (8 * (j % 4))) & 0xFFu;
+    n = n > 16u ? 0u : n;  // (NULL / too long: no key bytes are used)
+    n = ob + n <= heap_end ? n : 0u;
+    const uint64_t lo = ld_partial(vals + ob, n < 8u ? n : 8u);
+    const uint64_t hi = n > 8u ? ld_partial(vals + ob + 8, n - 8u) : 0ull;
+    w[0] = (uint32_t)lo;
+    w[1] = (uint32_t)(lo >> 32);
+    w[2] = (uint32_t)hi;
+    w[3] = (uint32_t)(hi >> 32);
+  }
+}
+
+// The validity of row j of every lane of this wave, as a lane mask (from stage_offsets' vword).
+__device__ __forceinline__ uint64_t stage_valid_mask(uint32_t vword, int j) {
+  const uint32_t lo = __builtin_amdgcn_readlane(vword, 2 * j), hi = __builtin_amdgcn_readlane(vword, 2 * j + 1);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+#ifndef DQ_STAGE_LOAD_A
+#define DQ_STAGE_LOAD_A 12
+#endif
+#ifndef DQ_STAGE_LOAD_B
+#define DQ_STAGE_LOAD_B 0
+#endif
+constexpr int kStageLoadA = DQ_STAGE_LOAD_A;  // key loads issued before the first row is processed
+constexpr int kStageLoadB = DQ_STAGE_LOAD_B;  // the rest after this many rows
+#ifndef DQ_STAGE_WOUT_UNROLL
+#define DQ_STAGE_WOUT_UNROLL 2
+#endif
 #ifndef DQ_STAGEP_WAVES
 #define DQ_STAGEP_WAVES 4
 #endif
@@ -1507,54 +1612,112 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(PA
   alignas(8) uint8_t scratch[kMaxLocalKey];
   const int64_t n_tiles = (n_rows + kStageTile - 1) / kStageTile;
   uint32_t n_side = 0;  // PACK: this thread's keys put on the overflow list (not digit strings)
+  // ONE_STRING: the key bytes through one buffer descriptor (a utf8 column's offsets are int32, so
+  // its heap is < 2 GiB); each tile's offsets through a descriptor of that tile's offsets (bounded,
+  // so rows past the batch read 0), as (begin, end) pairs: one 8-byte load per row.
+  const uint32_t heap_end = ONE_STRING ? __builtin_amdgcn_readfirstlane((uint32_t)uniform_ptr(c0.offsets)[n_rows]) : 0u;
+  const __amdgpu_buffer_rsrc_t rs_vals =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(uniform_ptr(c0.values)), 0, (int)heap_end, 0x00020000);
+  const bool has_validity = uniform_ptr(c0.validity) != nullptr;
+  const uint8_t* vals = static_cast<const uint8_t*>(uniform_ptr(c0.values));
+  uint32_t pob[kStagePer], poe[kStagePer], vword = 0u;
+  if (ONE_STRING && (int64_t)blockIdx.x < n_tiles) stage_offsets(c0, n_rows, blockIdx.x, pob, poe, vword);
+  // PACK: once the overflow list has filled up (a column of keys that are not digit strings) the
+  // batch will be rolled back, so the workgroups stop: thread 0 reads `flag` while each tile's
+  // records are written (abort_v) and the workgroup leaves at the next tile's top.
+  __shared__ unsigned int abort_s;
+  unsigned int abort_v = 0u;
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    if constexpr (PACK) {
+      if (tile != (int64_t)blockIdx.x) {
+        if (t == 0) abort_s = abort_v;
+        __syncthreads();
+        if (abort_s) break;
+      }
+    }
     const int64_t row0 = tile * (int64_t)kStageTile;
+    unsigned long long prof_t_ = 0;
+    (void)prof_t_;
+    DQ_PROF_MARK(true, 0);
     R rec[kStagePer];
     uint32_t bin[kStagePer];
     uint32_t too_long = 0u;
     if constexpr (ONE_STRING) {
-      // groups of kStageGroup rows: their offsets, then their key words, all in flight together
-      // (the whole tile at once would not fit the register file)
-      constexpr int G = kStageGroup;
+      // This tile's offsets (and validity bits) were loaded during the previous tile's
+      // multi-split (pob / poe / vword); the keys of all kStagePer rows are loaded now, 16 bytes
+      // each from the key's first byte (one unaligned buffer load; bytes past the heap read 0),
+      // all in flight together, and the NEXT tile's offsets are issued before this tile's split.
+      // key lengths as bytes, 4 to a register (kLenNull = Histogram's NULL, "NullValue"; lengths
+      // above 15 are clamped to 255: such a batch is rolled back, only "too long" matters)
+      constexpr uint32_t kLenNull = 254u;
+      uint32_t lens[(kStagePer + 3) / 4] = {}, sel = 0u;
 #pragma unroll
-      for (int g = 0; g < kStagePer; g += G) {
-        uint64_t k0[G], k1[G];
-        uint32_t len[G], sel, lng;
-        string_keys<G>(c0, ks.null_as_key != 0, row0 + g * kPartThreads + t, kPartThreads, n_rows, k0, k1, len, sel,
-                       lng);
+      for (int j = 0; j < kStagePer; ++j) {
+        const int64_t row = row0 + j * kPartThreads + t;
+        const uint32_t n = poe[j] - pob[j];
+        const bool valid = !has_validity || ((stage_valid_mask(vword, j) >> (t & 63u)) & 1u);
+        if (row < n_rows && (valid || ks.null_as_key)) sel |= 1u << j;
+        const uint32_t nb8 = (row < n_rows && !valid) ? kLenNull : (n < 254u ? n : 255u);
+        lens[j / 4] |= nb8 << (8 * (j % 4));
+      }
+      // rows [0, kStageLoadA) are loaded first; the rest once row kStageLoadB - 1 is processed
+      // (all twelve in flight at once would not leave registers for four waves per SIMD)
+      // (the keys that end within 16 bytes of the heap's end are read word by word instead: a
+      // buffer range check is per dword, and a wider read could leave the allocation)
+      uint32_t kw[kStagePer][4];
 #pragma unroll
-        for (int i = 0; i < G; ++i) {
-          bin[g + i] = kPartNoBin;
-          if (!((sel >> i) & 1u)) continue;
-          if ((lng >> i) & 1u) {
-            too_long = max(too_long, len[i]);
+      for (int j = 0; j < kStageLoadA; ++j) stage_key_load(rs_vals, vals, heap_end, pob[j], lens, j, kw[j]);
+#pragma unroll
+      for (int j = 0; j < kStagePer; ++j) {
+        if (j == kStageLoadB) {
+#pragma unroll
+          for (int q = kStageLoadA; q < kStagePer; ++q) stage_key_load(rs_vals, vals, heap_end, pob[q], lens, q, kw[q]);
+        }
+        bin[j] = kPartNoBin;
+        if (!((sel >> j) & 1u)) continue;
+        uint64_t k0, k1;
+        uint32_t n = (lens[j / 4] >> (8 * (j % 4))) & 0xFFu;
+        if (n == kLenNull) {
+          n = 9;
+          k0 = kNullK0;
+          k1 = kNullK1;
+        } else if (n > 15) {
+          too_long = max(too_long, n);
+          continue;
+        } else {
+          const uint64_t lo = (uint64_t)kw[j][0] | ((uint64_t)kw[j][1] << 32);
+          const uint64_t hi = (uint64_t)kw[j][2] | ((uint64_t)kw[j][3] << 32);
+          k0 = n >= 8 ? lo : (lo & ((1ull << (8u * n)) - 1ull));
+          k1 = n > 8 ? (hi & ((1ull << (8u * (n - 8u))) - 1ull)) : 0ull;
+        }
+        uint64_t h;
+        if constexpr (PACK) {
+          uint64_t p;
+          if (kp_pack_record(k0, k1, n, &p)) {
+            rec[j] = p;
+            h = hash_record_packed(p);
+          } else {  // not a digit key: a 16-B record on the overflow list
+            h = hash_raw(k0, k1, n);
+            sketch_update(regs, h);
+            FreqRec r;
+            r.k0 = k0;
+            r.k1 = k1 | ((unsigned long long)n << kRecLenShift);
+            const unsigned long long k = atomicAdd(ovf_n, 1ull);
+            if (k < ovf_cap) ovf[k] = r;
+            else atomicOr(flag, 1u);
+            ++n_side;
             continue;
           }
-          uint64_t h;
-          if constexpr (PACK) {
-            uint64_t p;
-            h = hash_raw(k0[i], k1[i], len[i]);
-            if (kp_pack_record(k0[i], k1[i], len[i], &p)) {
-              rec[g + i] = p;
-            } else {  // not a digit key: a 16-B record on the overflow list
-              sketch_update(regs, h);
-              FreqRec r;
-              r.k0 = k0[i];
-              r.k1 = k1[i] | ((unsigned long long)len[i] << kRecLenShift);
-              const unsigned long long k = atomicAdd(ovf_n, 1ull);
-              if (k < ovf_cap) ovf[k] = r;
-              else atomicOr(flag, 1u);
-              ++n_side;
-              continue;
-            }
-          } else {
-            h = hash_inline(k0[i], k1[i], len[i]);
-            rec[g + i].k0 = k0[i];
-            rec[g + i].k1 = k1[i] | ((unsigned long long)len[i] << kRecLenShift);
-          }
-          bin[g + i] = (uint32_t)(h >> (64 - b1)) & (nb - 1u);
-          sketch_update(regs, h);
+        } else {
+          h = hash_inline(k0, k1, n);
+          rec[j].k0 = k0;
+          rec[j].k1 = k1 | ((unsigned long long)n << kRecLenShift);
         }
+        bin[j] = (uint32_t)(h >> (64 - b1)) & (nb - 1u);
+        sketch_update(regs, h);
+        // one row at a time: interleaving the twelve rows' packing and hashing would need more
+        // registers than four waves per SIMD leave (the key words of the later rows are live)
+        __builtin_amdgcn_sched_barrier(0);
       }
     } else {
 #pragma unroll
@@ -1581,7 +1744,20 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(PA
       }
     }
     if (too_long) atomicMax(long_key, (unsigned long long)too_long);
-    part_tile(L, rec, bin, nb, 0, out, cap1, fill1, ovf, ovf_n, ovf_cap, flag, staged);
+#ifdef DQ_STAGE_PROF
+    constexpr bool kProf = true;
+#else
+    constexpr bool kProf = false;
+#endif
+    const int64_t next = tile + gridDim.x;  // its offsets load while this tile's records are written
+    auto prefetch = [&]() {
+      if constexpr (ONE_STRING)
+        if (next < n_tiles) stage_offsets(c0, n_rows, next, pob, poe, vword);
+      if constexpr (PACK)
+        if (t == 0) abort_v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    part_tile<kStagePer, (1 << kStageBinBits), R, (PACK ? kStageSubP : kPartSub), kProf, DQ_STAGE_WOUT_UNROLL>(
+        L, rec, bin, nb, 0, out, cap1, fill1, ovf, ovf_n, ovf_cap, flag, staged, nullptr, prof_t_, prefetch);
   }
   if (PACK && n_side) atomicAdd(staged, (unsigned long long)n_side);
   __syncthreads();
@@ -1672,10 +1848,10 @@ struct AggLdsP {
   uint32_t hist[kAggLdsHist];
 };
 
-__device__ inline bool lds_count_packed(unsigned long long* K, uint32_t* C, uint64_t p, uint64_t h) {
+// Count packed record p from LDS slot s on (probe `first` of its run); false if the image is full.
+__device__ inline bool lds_count_packed(unsigned long long* K, uint32_t* C, uint64_t p, uint32_t s, uint32_t first = 0) {
   constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
-  uint32_t s = (uint32_t)(h & (S - 1));
-  for (uint32_t probe = 0; probe < S; ++probe) {
+  for (uint32_t probe = first; probe < S; ++probe) {
     const unsigned long long c = atomicCAS(&K[s], kPackEmpty, (unsigned long long)p);
     if (c == kPackEmpty || c == p) {
       atomicAdd(&C[s], 1u);
@@ -1755,57 +1931,75 @@ __global__ __launch_bounds__(kAggPThreads) __attribute__((amdgpu_waves_per_eu(DQ
         const uint64_t i = base + (uint64_t)j * NT + threadIdx.x;
         if (i < r1) rb[j] = recs[i];
       }
+      // every record's first probe is issued before any result is looked at (independent LDS
+      // round trips); at the table's ~0.4 load most records are counted there
+      uint32_t sl[kAggPBatch];
+      unsigned long long cv[kAggPBatch];
+#pragma unroll
+      for (int j = 0; j < kAggPBatch; ++j) {
+        const uint64_t i = base + (uint64_t)j * NT + threadIdx.x;
+        sl[j] = (uint32_t)hash_record_packed(rb[j]) & (S - 1);
+        cv[j] = i < r1 ? atomicCAS(&L.K[sl[j]], kPackEmpty, (unsigned long long)rb[j]) : 0ull;
+      }
 #pragma unroll
       for (int j = 0; j < kAggPBatch; ++j) {
         const uint64_t i = base + (uint64_t)j * NT + threadIdx.x;
         if (i >= r1) continue;
-        if (!lds_count_packed(L.K, L.C, rb[j], hash_record_packed(rb[j]))) L.overflow = 1;
+        if (cv[j] == kPackEmpty || cv[j] == rb[j]) atomicAdd(&L.C[sl[j]], 1u);
+        else if (!lds_count_packed(L.K, L.C, rb[j], (sl[j] + 1) & (S - 1), 1)) L.overflow = 1;
       }
     }
     __syncthreads();
+    // The slice is written as 16-byte halves, one per lane, so each store instruction covers a
+    // contiguous 1 KiB (whole 128-byte lines): q = 2 * slot + half, half 0 = {ctrl, count},
+    // half 1 = {k0, k1}.
+    ulonglong2* halves = reinterpret_cast<ulonglong2*>(slice);
     if (L.overflow) {  // the slice is full: leave it untouched, hand the region's rows back
       if (threadIdx.x == 0) L.retry_base = atomicAdd(n_retry, (unsigned long long)(r1 - r0));
       __syncthreads();
       for (uint64_t i = r0 + threadIdx.x; i < r1; i += NT) retry[L.retry_base + (i - r0)] = rec_raw(recs[i]);
       if (tr.write_all)  // (the table was not cleared: the slice starts out empty)
-        for (uint32_t s = threadIdx.x; s < S; s += NT) slice[s] = FreqSlot{0ull, 0ull, 0ull, 0ull};
+        for (uint32_t q = threadIdx.x; q < 2 * S; q += NT) halves[q] = ulonglong2{0ull, 0ull};
       if (tr.smax && threadIdx.x == 0) tr.smax[b] = 0xFFFFFFFFu;  // unknown: never skipped
     } else {
-      for (uint32_t s = threadIdx.x; s < S; s += NT) {
+      for (uint32_t q = threadIdx.x; q < 2 * S; q += NT) {
+        const uint32_t s = q >> 1;
+        const bool hi = (q & 1u) != 0u;
         const uint32_t c = L.C[s];
-        if (!c) {
-          if (tr.write_all) slice[s] = FreqSlot{0ull, 0ull, 0ull, 0ull};
-          continue;
-        }
-        if (track || tr.smax) {
-          atomicMax(&L.cmax, c);
-          if (track) {
-            if (c < (uint32_t)kAggLdsHist) {
-              atomicAdd(&L.hist[c], 1u);
-            } else if (c < (uint32_t)kFreqHist) {
-              atomicAdd(&tr.hist[c], 1ull);
-            } else {
-              const unsigned long long i = atomicAdd(tr.n_big, 1ull);
-              if (i < tr.big_cap) tr.big[i] = c;
-            }
-          }
-        }
-        FreqSlot& e = slice[s];
         bool is_new = false;
-        if (!table_empty && (e.ctrl & kReady)) {
-          e.count += c;
+        if (!c) {
+          if (tr.write_all) halves[q] = ulonglong2{0ull, 0ull};
         } else {
+          const bool existing = !table_empty && (slice[s].ctrl & kReady);
           const uint64_t p = L.K[s];
-          uint64_t k0, k1;
-          uint32_t len;
-          kp_unpack(p, &k0, &k1, &len);
-          FreqSlot n;
-          n.ctrl = ((unsigned long long)tag_of(hash_record_packed(p)) << 32) | kReady | len;
-          n.count = c;
-          n.k0 = k0;
-          n.k1 = k1;
-          e = n;
-          is_new = true;
+          if (!hi) {
+            if (track || tr.smax) {
+              atomicMax(&L.cmax, c);
+              if (track) {
+                if (c < (uint32_t)kAggLdsHist) {
+                  atomicAdd(&L.hist[c], 1u);
+                } else if (c < (uint32_t)kFreqHist) {
+                  atomicAdd(&tr.hist[c], 1ull);
+                } else {
+                  const unsigned long long i = atomicAdd(tr.n_big, 1ull);
+                  if (i < tr.big_cap) tr.big[i] = c;
+                }
+              }
+            }
+            if (existing) {
+              slice[s].count += c;
+            } else {
+              const uint32_t len = p == kPackNull ? 9u : (uint32_t)(p >> 60);
+              halves[q] = ulonglong2{((unsigned long long)tag_of(hash_record_packed(p)) << 32) | kReady | len,
+                                     (unsigned long long)c};
+              is_new = true;
+            }
+          } else if (!existing) {
+            uint64_t k0, k1;
+            uint32_t len;
+            kp_unpack(p, &k0, &k1, &len);
+            halves[q] = ulonglong2{k0, k1};
+          }
         }
         const uint64_t nb = __ballot(is_new);  // one LDS add per wave, not one per new group
         if (nb && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(nb)) atomicAdd(&L.fresh, (uint32_t)__popcll(nb));
@@ -1853,19 +2047,6 @@ static unsigned slot_blocks(const FreqTable& T) {
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
   return (unsigned)blocks;
-}
-
-hipError_t launch_freq_part_count(const FreqTable& T, int n_parts, unsigned long long* d_cnt, hipStream_t stream) {
-  hipLaunchKernelGGL(dq_freq_part_count_kernel, dim3(slot_blocks(T)), dim3(kBlock), 0, stream, T, n_parts, d_cnt);
-  return hipGetLastError();
-}
-
-hipError_t launch_freq_part_scatter(const FreqTable& T, int n_parts, const unsigned long long* d_base,
-                                    unsigned long long* d_cursor, FreqSlot* out_groups, uint8_t* out_keys,
-                                    hipStream_t stream) {
-  hipLaunchKernelGGL(dq_freq_part_scatter_kernel, dim3(slot_blocks(T)), dim3(kBlock), 0, stream, T, n_parts,
-                     d_base, d_cursor, out_groups, out_keys);
-  return hipGetLastError();
 }
 
 hipError_t launch_freq_stage(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, FreqRec* d_out,
@@ -1975,6 +2156,12 @@ hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, bool p
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int64_t blocks = tiles < (int64_t)cus * 4 ? tiles : (int64_t)cus * 4;
+#ifdef DQ_STAGE_PROF
+  {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_stage_prof), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
+  }
+#endif
   if (packed)
     hipLaunchKernelGGL((dq_freq_stage_part_kernel<true, true>), dim3((unsigned)blocks), dim3(kPartThreads), 0, stream, ks,
                        d_cols, n_rows, b1, static_cast<uint64_t*>(d_out), cap1, d_fill1, d_ovf, d_ovf_n, ovf_cap, d_flag,
@@ -1987,6 +2174,18 @@ hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, bool p
     hipLaunchKernelGGL((dq_freq_stage_part_kernel<false, false>), dim3((unsigned)blocks), dim3(kPartThreads), 0, stream, ks,
                        d_cols, n_rows, b1, static_cast<FreqRec*>(d_out), cap1, d_fill1, d_ovf, d_ovf_n, ovf_cap, d_flag,
                        d_hll, d_long_key, d_staged);
+#ifdef DQ_STAGE_PROF
+  {
+    unsigned long long z[8];
+    (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_stage_prof), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
+    (void)hipStreamSynchronize(stream);
+    const double tiles_d = (double)tiles;
+    std::fprintf(stderr, "[stage_prof] rows %lld tiles %lld blocks %lld cycles/tile: own-loads+compute %.0f "
+                 "wait-others %.0f rank %.0f scan %.0f reserve %.0f lds-scatter %.0f write %.0f\n",
+                 (long long)n_rows, (long long)tiles, (long long)blocks, z[0] / tiles_d, z[1] / tiles_d, z[2] / tiles_d,
+                 z[3] / tiles_d, z[4] / tiles_d, z[5] / tiles_d, z[6] / tiles_d);
+  }
+#endif
   return hipGetLastError();
 }
 
@@ -2148,6 +2347,822 @@ hipError_t launch_freq_heap_need(const FreqKeySpec& ks, const DevColumn* d_cols,
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(dq_freq_heap_need_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, ks, d_cols,
                      n_rows, d_need, d_max_len);
+  return hipGetLastError();
+}
+
+
+// =============================================================================================
+// Key-hash exchange and table merges (round 4): FrequenciesAndNumRows.sum as an outer join of
+// two key sets (GroupingAnalyzers.scala:128-148) and the groupBy's hash exchange (:67-72).
+//
+// Sender: dq_freq_partition writes each owner's groups as a part = [packed records, 16 B:
+// {packed key word, count} for keys that pack (dq_keypack.h)] [general records, 32 B: FreqSlot
+// with READY clear, k0 of a long key = offset in the part's key bytes], each section in the
+// order of the sender's slice chunks (2^chunk_log slices per chunk, chunk_log = 0 unless parts x
+// chunks would be too many counters).  A slice is a range of the top hash bits, so a receiver
+// whose table has no more slice bits than the sender finds the records of each of its slices
+// contiguous in every part -- no sort, no per-group atomics.
+//
+// Receiver (dq_freq_import_parts / dq_freq_merge): every record stream ("run": a part's packed
+// section, its general section, or a whole source table's slot array) is
+//   1. sketched (HLL p = 9 of the record hashes) to size the table,
+//   2. cut at the receiver's slice boundaries (dq_import_bounds_kernel: start / end per (run,
+//      slice), one streaming pass; a run found out of order is flagged and imported group by
+//      group instead),
+//   3. merged by ONE workgroup per receiver slice (dq_import_merge_kernel): the slice is loaded
+//      into an LDS image (or starts empty), every run's records of that slice are counted in with
+//      their weights, and the slice is written back whole -- the slice-owner aggregation of the
+//      partition path, with weighted records.
+// Records whose keys do not fit the LDS image (longer than 15 bytes) and runs out of slice order
+// take dq_import_global_kernel (global_insert, per group); a slice whose keys overflow the image
+// is left untouched and listed, the table grows, and its records are inserted group by group.
+// =============================================================================================
+
+// A group's hash, packed word and class: 0 = its key packs (a packed wire record), 1 = general.
+__device__ inline uint64_t slot_key_hash(const FreqTable& T, const FreqSlot& e, uint32_t len, uint64_t* packed,
+                                         int* kind) {
+  *kind = 1;
+  if (e.ctrl & kHeapKey) return xxh64_any(T.heap + e.k0, len, 42);
+  uint64_t p;
+  if (kp_pack_record(e.k0, e.k1, len, &p)) {
+    *packed = p;
+    *kind = 0;
+    return hash_record_packed(p);
+  }
+  return hash_raw(e.k0, e.k1, len);
+}
+
+constexpr int kWireThreads = 256;
+constexpr int kWireMaxParts = 4096;
+
+// Counts per (part, kind, chunk) -- cnt[(2 p + kind) * n_chunks + chunk] -- and long-key bytes per
+// part.  One chunk per workgroup iteration (LDS counters, written out whole).
+__global__ __launch_bounds__(kWireThreads) void dq_wire_count_kernel(FreqTable T, int n_parts, int chunk_log,
+                                                                     uint64_t n_chunks, unsigned long long* cnt,
+                                                                     unsigned long long* kbytes) {
+  __shared__ uint32_t c_l[2 * kWireMaxParts];
+  const uint32_t np2 = 2u * (uint32_t)n_parts;
+  for (uint32_t i = threadIdx.x; i < np2; i += kWireThreads) c_l[i] = 0u;
+  __syncthreads();
+  const uint64_t per = (uint64_t)kFreqSliceSlots << chunk_log;
+  for (uint64_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+    for (uint64_t s = c * per + threadIdx.x; s < (c + 1) * per; s += kWireThreads) {
+      const FreqSlot e = T.slots[s];  // launch boundary: every insert is visible
+      if (!(e.ctrl & kReady)) continue;
+      const uint32_t len = (uint32_t)(e.ctrl & kLenMask);
+      uint64_t pk;
+      int kind;
+      const uint64_t h = slot_key_hash(T, e, len, &pk, &kind);
+      const uint32_t o = freq_owner(h, (uint32_t)n_parts);
+      atomicAdd(&c_l[2 * o + kind], 1u);
+      if (e.ctrl & kHeapKey) atomicAdd(&kbytes[o], ((unsigned long long)len + 7ull) & ~7ull);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < np2; i += kWireThreads) {
+      cnt[(uint64_t)i * n_chunks + c] = c_l[i];
+      c_l[i] = 0u;
+    }
+    __syncthreads();
+  }
+}
+
+// out[i] = scanned[i * stride] for i <= n (section starts of the scanned counts).
+__global__ void dq_gather_strided_kernel(const unsigned long long* __restrict__ scanned, uint64_t stride, uint64_t n,
+                                         unsigned long long* out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = scanned[i * stride];
+}
+
+// sec[4 p ..]: {byte offset of part p in out, first packed index, first general index, packed
+// records of p}; pos = the exclusive scan of dq_wire_count_kernel's counts.
+__global__ __launch_bounds__(kWireThreads) void dq_wire_scatter_kernel(FreqTable T, int n_parts, int chunk_log,
+                                                                       uint64_t n_chunks,
+                                                                       const unsigned long long* __restrict__ pos,
+                                                                       const unsigned long long* __restrict__ sec,
+                                                                       const unsigned long long* __restrict__ key_base,
+                                                                       unsigned long long* key_cursor, uint8_t* out,
+                                                                       uint8_t* keys) {
+  __shared__ uint32_t c_l[2 * kWireMaxParts];
+  const uint32_t np2 = 2u * (uint32_t)n_parts;
+  for (uint32_t i = threadIdx.x; i < np2; i += kWireThreads) c_l[i] = 0u;
+  __syncthreads();
+  const uint64_t per = (uint64_t)kFreqSliceSlots << chunk_log;
+  for (uint64_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+    for (uint64_t s = c * per + threadIdx.x; s < (c + 1) * per; s += kWireThreads) {
+      FreqSlot e = T.slots[s];
+      if (!(e.ctrl & kReady)) continue;
+      const uint32_t len = (uint32_t)(e.ctrl & kLenMask);
+      uint64_t pk = 0;
+      int kind;
+      const uint64_t h = slot_key_hash(T, e, len, &pk, &kind);
+      const uint32_t o = freq_owner(h, (uint32_t)n_parts);
+      const uint32_t k = 2u * o + (uint32_t)kind;
+      const unsigned long long idx = pos[(uint64_t)k * n_chunks + c] + atomicAdd(&c_l[k], 1u);
+      const unsigned long long* q = sec + 4 * o;
+      if (kind == 0) {
+        WirePacked w;
+        w.key = pk;
+        w.count = e.count;
+        *reinterpret_cast<WirePacked*>(out + q[0] + 16ull * (idx - q[1])) = w;
+      } else {
+        if (e.ctrl & kHeapKey) {
+          const unsigned long long bytes = ((unsigned long long)len + 7ull) & ~7ull;
+          const unsigned long long off = atomicAdd(&key_cursor[o], bytes);  // within part o's key bytes
+          const uint64_t* src = reinterpret_cast<const uint64_t*>(T.heap + e.k0);
+          uint64_t* dst = reinterpret_cast<uint64_t*>(keys + key_base[o] + off);
+          for (unsigned long long w = 0; w < bytes / 8; ++w) dst[w] = src[w];
+          e.k0 = off;
+        }
+        e.ctrl &= ~kReady;  // wire form: READY is a table-internal flag
+        *reinterpret_cast<FreqSlot*>(out + q[0] + 16ull * q[3] + 32ull * (idx - q[2])) = e;
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < np2; i += kWireThreads) c_l[i] = 0u;
+    __syncthreads();
+  }
+}
+
+// ---- receiver (ImportRun: dq_internal.h)
+// One record of a run, decoded: present (a group), its weight, hash, and -- when it fits the LDS
+// image (a key of <= 15 bytes) -- its key as k0 / k1 (length in k1's top byte) or packed word.
+struct ImpRec {
+  uint64_t k0, k1, p, hash;  // k1: the key's bytes 8..15 (the LDS image adds the length byte)
+  unsigned long long count;
+  uint32_t len;
+  bool present, lds_ok, heap;
+};
+
+template <bool PACKED>
+__device__ inline void imp_load(const ImportRun& R, uint64_t i, ImpRec& r) {
+  if (R.kind == 0) {
+    const WirePacked w = static_cast<const WirePacked*>(R.recs)[i];
+    r.p = w.key;
+    r.count = w.count;
+    r.present = true;
+    r.lds_ok = true;
+    r.heap = false;
+    r.hash = hash_record_packed(w.key);
+    if constexpr (!PACKED) {
+      uint64_t k0, k1;
+      uint32_t len;
+      kp_unpack(w.key, &k0, &k1, &len);
+      r.k0 = k0;
+      r.k1 = k1;
+      r.len = len;
+    }
+    return;
+  }
+  const FreqSlot e = static_cast<const FreqSlot*>(R.recs)[i];
+  r.present = R.kind == 1 || (e.ctrl & kReady);
+  r.count = e.count;
+  r.len = (uint32_t)(e.ctrl & kLenMask);
+  r.heap = (e.ctrl & kHeapKey) != 0;
+  r.lds_ok = !r.heap && r.len <= 15;
+  r.k0 = e.k0;
+  r.k1 = e.k1;
+  r.p = 0;
+  if (!r.present) return;
+  r.hash = r.heap ? xxh64_any(R.heap + e.k0, r.len, 42) : hash_inline(e.k0, e.k1, r.len);
+}
+
+__device__ inline uint64_t dst_slice(uint64_t h, int rb) { return rb ? (h >> (64 - rb)) : 0ull; }
+
+// The record range of run R for receiver slice r (rb slice bits): kind 2 from the source table's
+// geometry, wire runs from the bounds pass.
+__device__ inline void imp_range(const ImportRun& R, int run, uint64_t r, int rb, const uint32_t* start,
+                                 const uint32_t* end, uint64_t n_slices, uint64_t* b, uint64_t* e) {
+  if (R.kind == 2) {
+    if (rb <= R.src_bits) {
+      const int sh = R.src_bits - rb + kFreqSliceLog;
+      *b = r << sh;
+      *e = (r + 1) << sh;
+    } else {
+      const uint64_t sl = r >> (rb - R.src_bits);
+      *b = sl << kFreqSliceLog;
+      *e = (sl + 1) << kFreqSliceLog;
+    }
+    return;
+  }
+  *b = start[(uint64_t)run * n_slices + r];
+  *e = end[(uint64_t)run * n_slices + r];
+}
+
+// HLL p = 9 of every present record's hash (table sizing).
+__global__ __launch_bounds__(kBlock) void dq_import_sketch_kernel(const ImportRun* __restrict__ runs, uint32_t* hll) {
+  __shared__ uint32_t regs[kHllM];
+  for (int i = threadIdx.x; i < kHllM; i += kBlock) regs[i] = 0u;
+  __syncthreads();
+  const ImportRun R = runs[blockIdx.y];
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < R.n; i += (uint64_t)gridDim.x * kBlock) {
+    ImpRec r;
+    imp_load<false>(R, i, r);
+    if (r.present) sketch_update(regs, r.hash);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kHllM; i += kBlock)
+    if (regs[i]) atomicMax(&hll[i], regs[i]);
+}
+
+// Slice boundaries of each wire run (blockIdx.y): start[run][r] / end[run][r] for the receiver's
+// slices (both 0 for a slice the run does not hold); unsorted[run] = 1 if the run is not in slice
+// order (then its bounds are meaningless and it is imported group by group).
+__global__ __launch_bounds__(kBlock) void dq_import_bounds_kernel(const ImportRun* __restrict__ runs, int rb,
+                                                                  uint64_t n_slices, uint32_t* start, uint32_t* end,
+                                                                  unsigned int* unsorted) {
+  const int run = blockIdx.y;
+  const ImportRun R = runs[run];
+  if (R.kind == 2) return;
+  uint32_t* st = start + (uint64_t)run * n_slices;
+  uint32_t* en = end + (uint64_t)run * n_slices;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < R.n; i += (uint64_t)gridDim.x * kBlock) {
+    ImpRec r, q;
+    imp_load<true>(R, i, r);
+    const uint64_t si = dst_slice(r.hash, rb);
+    if (i == 0) {
+      st[si] = 0u;
+    } else {
+      imp_load<true>(R, i - 1, q);
+      const uint64_t sp = dst_slice(q.hash, rb);
+      if (sp != si) {
+        if (sp > si) unsorted[run] = 1u;
+        st[si] = (uint32_t)i;
+        en[sp] = (uint32_t)i;
+      }
+    }
+    if (i + 1 == R.n) en[si] = (uint32_t)R.n;
+  }
+}
+
+// The LDS image of a receiver slice: PACKED -- one word per slot (the packed key, kPackEmpty or
+// kPackForeign); general -- K0 / K1 as the partition path's 16-byte records (kLdsEmpty / kLdsBusy
+// / kLdsForeign in K1).  Counts are 64-bit (merged groups carry their weights).
+template <bool PACKED>
+struct MergeLds;
+template <>
+struct MergeLds<true> {
+  unsigned long long K[kFreqSliceSlots];
+  unsigned long long C[kFreqSliceSlots];
+  int overflow;
+  uint32_t fresh;
+  unsigned long long cmax;
+  uint32_t hist[kAggLdsHist];
+};
+template <>
+struct MergeLds<false> {
+  unsigned long long K0[kFreqSliceSlots], K1[kFreqSliceSlots];
+  unsigned long long C[kFreqSliceSlots];
+  int overflow;
+  uint32_t fresh;
+  unsigned long long cmax;
+  uint32_t hist[kAggLdsHist];
+};
+
+__device__ inline bool merge_count(MergeLds<true>& L, const ImpRec& r) {
+  constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
+  uint32_t s = (uint32_t)r.hash & (S - 1);
+  for (uint32_t probe = 0; probe < S; ++probe) {
+    const unsigned long long c = atomicCAS(&L.K[s], kPackEmpty, (unsigned long long)r.p);
+    if (c == kPackEmpty || c == r.p) {
+      atomicAdd(&L.C[s], r.count);
+      return true;
+    }
+    s = (s + 1) & (S - 1);
+  }
+  return false;
+}
+
+__device__ inline bool merge_count(MergeLds<false>& L, const ImpRec& r) {
+  constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
+  const unsigned long long k1 = r.k1 | ((unsigned long long)r.len << kRecLenShift);
+  uint32_t s = (uint32_t)r.hash & (S - 1);
+  bool done = false;
+  for (uint32_t probe = 0; probe < S && !done;) {  // (the publish stays inside the iteration: see lds_count)
+    const unsigned long long c = atomicCAS(&L.K1[s], kLdsEmpty, kLdsBusy);
+    if (c == kLdsEmpty) {
+      L.K0[s] = r.k0;
+      __threadfence_block();
+      atomicExch(&L.K1[s], k1);
+      atomicAdd(&L.C[s], r.count);
+      done = true;
+    } else if (c == kLdsBusy) {
+      // being published by another lane: look again
+    } else if (c == k1 && __hip_atomic_load(&L.K0[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == r.k0) {
+      atomicAdd(&L.C[s], r.count);
+      done = true;
+    } else {
+      s = (s + 1) & (S - 1);
+      ++probe;
+    }
+  }
+  return done;
+}
+
+constexpr int kMergeThreads = 256;
+
+// One workgroup per receiver slice (grid-stride): the slice's LDS image, every run's records of
+// the slice counted in with their weights, the slice written back whole.  ovf_list gets the
+// slices whose keys did not fit the image (left untouched; zero-filled when write_all).
+template <bool PACKED>
+__global__ __launch_bounds__(kMergeThreads) void dq_import_merge_kernel(
+    FreqTable T, const ImportRun* __restrict__ runs, int n_runs, const uint32_t* __restrict__ start,
+    const uint32_t* __restrict__ end, uint64_t n_slices, int table_empty, AggTrack tr, uint32_t* ovf_list,
+    unsigned long long* n_ovf, unsigned long long* new_groups) {
+  constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
+  constexpr int NT = kMergeThreads;
+  __shared__ MergeLds<PACKED> L;
+  const int rb = T.bucket_bits;
+  const bool track = tr.hist != nullptr;
+  if (track) {
+    for (int i = threadIdx.x; i < kAggLdsHist; i += NT) L.hist[i] = 0u;
+    __syncthreads();
+  }
+  for (uint64_t b = blockIdx.x; b < n_slices; b += gridDim.x) {
+    FreqSlot* slice = T.slots + (b << kFreqSliceLog);
+    for (uint32_t s = threadIdx.x; s < S; s += NT) {
+      bool have = false;
+      uint64_t k0 = 0, k1 = 0;
+      uint32_t len = 0;
+      bool fits = false;
+      if (!table_empty) {
+        const FreqSlot e = slice[s];
+        have = (e.ctrl & kReady) != 0;
+        len = (uint32_t)(e.ctrl & kLenMask);
+        fits = have && !(e.ctrl & kHeapKey) && len <= 15;
+        k0 = e.k0;
+        k1 = e.k1;
+      }
+      if constexpr (PACKED) {
+        uint64_t p;
+        L.K[s] = !have ? kPackEmpty : (fits && kp_pack_record(k0, k1, len, &p) ? p : kPackForeign);
+      } else {
+        L.K0[s] = k0;
+        L.K1[s] = !have ? kLdsEmpty : (fits ? (k1 | ((unsigned long long)len << kRecLenShift)) : kLdsForeign);
+      }
+      L.C[s] = 0ull;
+    }
+    if (threadIdx.x == 0) {
+      L.overflow = 0;
+      L.fresh = 0u;
+      L.cmax = 0ull;
+    }
+    __syncthreads();
+    for (int run = 0; run < n_runs; ++run) {
+      const ImportRun R = runs[run];
+      if (R.skip) continue;
+      uint64_t i0, i1;
+      imp_range(R, run, b, rb, start, end, n_slices, &i0, &i1);
+      for (uint64_t i = i0 + threadIdx.x; i < i1; i += NT) {
+        ImpRec r;
+        imp_load<PACKED>(R, i, r);
+        if (!r.present || !r.lds_ok || dst_slice(r.hash, rb) != b) continue;
+        if (!merge_count(L, r)) L.overflow = 1;
+      }
+    }
+    __syncthreads();
+    ulonglong2* halves = reinterpret_cast<ulonglong2*>(slice);
+    if (L.overflow) {
+      if (threadIdx.x == 0) ovf_list[atomicAdd(n_ovf, 1ull)] = (uint32_t)b;
+      if (tr.write_all)
+        for (uint32_t q = threadIdx.x; q < 2 * S; q += NT) halves[q] = ulonglong2{0ull, 0ull};
+      if (tr.smax && threadIdx.x == 0) tr.smax[b] = 0xFFFFFFFFu;
+    } else {
+      for (uint32_t q = threadIdx.x; q < 2 * S; q += NT) {
+        const uint32_t s = q >> 1;
+        const bool hi = (q & 1u) != 0u;
+        const unsigned long long c = L.C[s];
+        bool is_new = false;
+        if (!c) {
+          if (tr.write_all) halves[q] = ulonglong2{0ull, 0ull};
+        } else {
+          const bool existing = !table_empty && (slice[s].ctrl & kReady);
+          uint64_t k0, k1, h;
+          uint32_t len;
+          if constexpr (PACKED) {
+            kp_unpack(L.K[s], &k0, &k1, &len);
+            h = hash_record_packed(L.K[s]);
+          } else {
+            const unsigned long long kk1 = L.K1[s];
+            k0 = L.K0[s];
+            k1 = kk1 & kRecKeyMask;
+            len = (uint32_t)(kk1 >> kRecLenShift);
+            h = hash_inline(k0, k1, len);
+          }
+          if (!hi) {
+            if (track || tr.smax) {
+              atomicMax(&L.cmax, c);
+              if (track) {
+                if (c < (unsigned long long)kAggLdsHist) {
+                  atomicAdd(&L.hist[c], 1u);
+                } else if (c < (unsigned long long)kFreqHist) {
+                  atomicAdd(&tr.hist[c], 1ull);
+                } else {
+                  const unsigned long long i = atomicAdd(tr.n_big, 1ull);
+                  if (i < tr.big_cap) tr.big[i] = c;
+                }
+              }
+            }
+            if (existing) {
+              slice[s].count += c;
+            } else {
+              halves[q] = ulonglong2{((unsigned long long)tag_of(h) << 32) | kReady | len, c};
+              is_new = true;
+            }
+          } else if (!existing) {
+            halves[q] = ulonglong2{k0, k1};
+          }
+        }
+        const uint64_t nb = __ballot(is_new);
+        if (nb && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(nb)) atomicAdd(&L.fresh, (uint32_t)__popcll(nb));
+      }
+      __syncthreads();
+      if (threadIdx.x == 0 && L.fresh) atomicAdd(new_groups, (unsigned long long)L.fresh);
+      if (tr.smax && threadIdx.x == 0) tr.smax[b] = L.cmax > 0xFFFFFFFEull ? 0xFFFFFFFFu : (uint32_t)L.cmax;
+    }
+    __syncthreads();
+  }
+  if (track) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < kAggLdsHist; i += NT)
+      if (L.hist[i]) atomicAdd(&tr.hist[i], (unsigned long long)L.hist[i]);
+  }
+}
+
+// Group-by-group inserts (global_insert with the group's weight), blockIdx.y = run:
+//  mode 0: every present record of runs marked skip (out of slice order);
+//  mode 1: the records the LDS image cannot hold (keys longer than 15 bytes) of the other runs;
+//  mode 2: the records of the listed overflowed slices (ovf_list, rb_old = the slice bits they
+//          were cut with) that fit the image -- after the table has grown.
+__global__ __launch_bounds__(kBlock) void dq_import_global_kernel(FreqTable T, const ImportRun* __restrict__ runs,
+                                                                  int mode, int rb_old, const uint32_t* __restrict__ start,
+                                                                  const uint32_t* __restrict__ end, uint64_t n_slices_old,
+                                                                  const uint32_t* __restrict__ ovf_list, uint64_t n_ovf) {
+  const int run = blockIdx.y;
+  const ImportRun R = runs[run];
+  if (mode == 0 ? !R.skip : R.skip) return;
+  auto one = [&](uint64_t i, bool filter, uint64_t sl) -> bool {
+    ImpRec r;
+    imp_load<false>(R, i, r);
+    if (!r.present) return true;
+    if (mode == 1 && r.lds_ok) return true;
+    if (mode == 2 && (!r.lds_ok || dst_slice(r.hash, rb_old) != sl)) return true;
+    (void)filter;
+    Key k;
+    k.k0 = r.k0;
+    k.k1 = r.k1;
+    k.len = r.len;
+    k.ptr = r.heap ? R.heap + r.k0 : nullptr;
+    if (r.heap) k.k0 = k.k1 = 0;
+    k.hash = r.hash;
+    return global_insert(T, k, r.count);
+  };
+  if (mode != 2) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < R.n; i += (uint64_t)gridDim.x * kBlock)
+      if (!one(i, false, 0)) return;
+    return;
+  }
+  for (uint64_t o = blockIdx.x; o < n_ovf; o += gridDim.x) {
+    const uint64_t sl = ovf_list[o];
+    uint64_t i0, i1;
+    imp_range(R, run, sl, rb_old, start, end, n_slices_old, &i0, &i1);
+    for (uint64_t i = i0 + threadIdx.x; i < i1; i += kBlock)
+      if (!one(i, true, sl)) return;
+  }
+}
+
+static unsigned grid_for(uint64_t n, uint64_t per, unsigned cap) {
+  uint64_t b = (n + per - 1) / per;
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+hipError_t launch_wire_count(const FreqTable& T, int n_parts, int chunk_log, uint64_t n_chunks, unsigned long long* d_cnt,
+                             unsigned long long* d_kbytes, hipStream_t stream) {
+  if (n_parts < 1 || n_parts > kWireMaxParts) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dq_wire_count_kernel, dim3(grid_for(n_chunks, 1, 65536)), dim3(kWireThreads), 0, stream, T, n_parts,
+                     chunk_log, n_chunks, d_cnt, d_kbytes);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_strided(const unsigned long long* d_scanned, uint64_t stride, uint64_t n, unsigned long long* d_out,
+                                 hipStream_t stream) {
+  hipLaunchKernelGGL(dq_gather_strided_kernel, dim3(grid_for(n + 1, 256, 1024)), dim3(256), 0, stream, d_scanned, stride, n,
+                     d_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_wire_scatter(const FreqTable& T, int n_parts, int chunk_log, uint64_t n_chunks,
+                               const unsigned long long* d_pos, const unsigned long long* d_sec,
+                               const unsigned long long* d_key_base, unsigned long long* d_key_cursor, uint8_t* d_out,
+                               uint8_t* d_keys, hipStream_t stream) {
+  if (n_parts < 1 || n_parts > kWireMaxParts) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dq_wire_scatter_kernel, dim3(grid_for(n_chunks, 1, 65536)), dim3(kWireThreads), 0, stream, T, n_parts,
+                     chunk_log, n_chunks, d_pos, d_sec, d_key_base, d_key_cursor, d_out, d_keys);
+  return hipGetLastError();
+}
+
+hipError_t launch_import_sketch(const ImportRun* d_runs, int n_runs, uint64_t max_n, uint32_t* d_hll, hipStream_t stream) {
+  if (n_runs < 1 || n_runs > 65535 || max_n == 0) return hipSuccess;
+  hipLaunchKernelGGL(dq_import_sketch_kernel, dim3(grid_for(max_n, kBlock * 8, 2048), (unsigned)n_runs), dim3(kBlock), 0,
+                     stream, d_runs, d_hll);
+  return hipGetLastError();
+}
+
+hipError_t launch_import_bounds(const ImportRun* d_runs, int n_runs, uint64_t max_n, int rb, uint64_t n_slices,
+                                uint32_t* d_start, uint32_t* d_end, unsigned int* d_unsorted, hipStream_t stream) {
+  if (n_runs < 1 || n_runs > 65535 || max_n == 0) return hipSuccess;
+  hipLaunchKernelGGL(dq_import_bounds_kernel, dim3(grid_for(max_n, kBlock * 8, 2048), (unsigned)n_runs), dim3(kBlock), 0,
+                     stream, d_runs, rb, n_slices, d_start, d_end, d_unsorted);
+  return hipGetLastError();
+}
+
+hipError_t launch_import_merge(const FreqTable& T, bool packed, const ImportRun* d_runs, int n_runs, const uint32_t* d_start,
+                               const uint32_t* d_end, int table_empty, unsigned long long* d_hist, unsigned long long* d_big,
+                               unsigned long long* d_n_big, unsigned long long big_cap, uint32_t* d_smax, int write_all,
+                               uint32_t* d_ovf_list, unsigned long long* d_n_ovf, unsigned long long* d_new_groups,
+                               hipStream_t stream) {
+  const uint64_t n_slices = (T.mask + 1) >> kFreqSliceLog;
+  if (!table_empty && (d_hist || d_smax || write_all)) return hipErrorInvalidValue;
+  AggTrack tr{d_hist, d_big, d_n_big, big_cap, d_smax, write_all};
+  const unsigned blocks = grid_for(n_slices, 1, 65536);
+  if (packed)
+    hipLaunchKernelGGL(dq_import_merge_kernel<true>, dim3(blocks), dim3(kMergeThreads), 0, stream, T, d_runs, n_runs, d_start,
+                       d_end, n_slices, table_empty, tr, d_ovf_list, d_n_ovf, d_new_groups);
+  else
+    hipLaunchKernelGGL(dq_import_merge_kernel<false>, dim3(blocks), dim3(kMergeThreads), 0, stream, T, d_runs, n_runs, d_start,
+                       d_end, n_slices, table_empty, tr, d_ovf_list, d_n_ovf, d_new_groups);
+  return hipGetLastError();
+}
+
+hipError_t launch_import_global(const FreqTable& T, const ImportRun* d_runs, int n_runs, uint64_t max_n, int mode, int rb_old,
+                                const uint32_t* d_start, const uint32_t* d_end, uint64_t n_slices_old,
+                                const uint32_t* d_ovf_list, uint64_t n_ovf, hipStream_t stream) {
+  if (n_runs < 1 || n_runs > 65535) return hipSuccess;
+  const unsigned gx = mode == 2 ? grid_for(n_ovf, 1, 4096) : grid_for(max_n, kBlock * 4, 4096);
+  hipLaunchKernelGGL(dq_import_global_kernel, dim3(gx, (unsigned)n_runs), dim3(kBlock), 0, stream, T, d_runs, mode, rb_old,
+                     d_start, d_end, n_slices_old, d_ovf_list, n_ovf);
+  return hipGetLastError();
+}
+
+
+// =============================================================================================
+// Few groups (round 4): the profiler's low-cardinality histograms (ColumnProfiler.scala:564-606:
+// columns with at most 120 distinct values) and any grouping hinted to have at most
+// kFreqFewGroups groups (dq_freq_expect_groups).  One key column; every workgroup counts its
+// contiguous rows in an LDS table of kSmallSlots keys (each row: one probe, one LDS add), keys
+// loaded as the fused stage loads them (offset pairs one iteration ahead, one unaligned 16-byte
+// load per string), then writes its groups -- not into the global table (every workgroup would
+// hit the same few slots with device atomics) but to its own staging list; one small merge kernel
+// sums the lists and inserts each group once.  A key longer than 15 bytes, or more keys than the
+// LDS table holds, raises `bad` and the host takes the general insert path instead.
+// =============================================================================================
+constexpr int kSmallSlots = 1024;
+constexpr int kSmallThreads = 512;
+constexpr int kSmallPer = 8;  // rows per thread per iteration
+
+struct SmallLds {
+  unsigned long long K0[kSmallSlots], K1[kSmallSlots];  // K1 = key bytes 8..14 | length << 56
+  uint32_t C[kSmallSlots];
+  uint32_t n_used;
+};
+
+__device__ inline bool small_count(SmallLds& L, uint64_t k0, uint64_t k1l) {
+  uint32_t s = lds_hash(k0, k1l, 0) & (kSmallSlots - 1);
+  bool done = false;
+  for (uint32_t probe = 0; probe < (uint32_t)kSmallSlots && !done;) {  // (publish inside the iteration)
+    const unsigned long long c = __hip_atomic_load(&L.K1[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (c == k1l && __hip_atomic_load(&L.K0[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == k0) {
+      atomicAdd(&L.C[s], 1u);
+      done = true;
+    } else if (c == kLdsEmpty) {
+      if (atomicCAS(&L.K1[s], kLdsEmpty, kLdsBusy) == kLdsEmpty) {
+        L.K0[s] = k0;
+        __threadfence_block();
+        atomicExch(&L.K1[s], k1l);
+        atomicAdd(&L.C[s], 1u);
+        done = true;
+      }
+    } else if (c == kLdsBusy) {
+      // being published: look again
+    } else {
+      s = (s + 1) & (kSmallSlots - 1);
+      ++probe;
+    }
+  }
+  return done;
+}
+
+// out_k0 / out_k1 / out_c: kSmallSlots entries per workgroup, out_n[block] of them used.
+template <bool STRING>
+__global__ __launch_bounds__(kSmallThreads) void dq_freq_small_kernel(FreqKeySpec ks, const DevColumn* __restrict__ cols,
+                                                                      int64_t n_rows, unsigned long long* out_k0,
+                                                                      unsigned long long* out_k1, uint32_t* out_c,
+                                                                      uint32_t* out_n, unsigned int* bad) {
+  __shared__ SmallLds L;
+  const uint32_t t = threadIdx.x;
+  for (uint32_t i = t; i < (uint32_t)kSmallSlots; i += kSmallThreads) {
+    L.K1[i] = kLdsEmpty;
+    L.C[i] = 0u;
+  }
+  if (t == 0) L.n_used = 0u;
+  __syncthreads();
+  const DevColumn& c0 = cols[ks.key_cols[0]];
+  const bool null_key = ks.null_as_key != 0;
+  const uint8_t* validity = uniform_ptr(c0.validity);
+  const int64_t per = (((n_rows + gridDim.x - 1) / gridDim.x) + 63) & ~(int64_t)63;
+  const int64_t r0 = min((int64_t)blockIdx.x * per, n_rows);
+  const int64_t r1 = min(r0 + per, n_rows);
+  bool fail = false;
+  constexpr int64_t step = (int64_t)kSmallThreads * kSmallPer;
+  if constexpr (STRING) {
+    const int32_t* offs = uniform_ptr(c0.offsets);
+    const uint32_t heap_end = __builtin_amdgcn_readfirstlane((uint32_t)offs[n_rows]);
+    const uint8_t* vals = static_cast<const uint8_t*>(uniform_ptr(c0.values));
+    const __amdgpu_buffer_rsrc_t rs_vals =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vals), 0, (int)heap_end, 0x00020000);
+    uint32_t ob[kSmallPer], oe[kSmallPer];
+    auto load_offs = [&](int64_t base) {
+      const int64_t left = r1 - base;
+      const uint32_t m = (uint32_t)(left < step ? left : step);
+      const __amdgpu_buffer_rsrc_t rs_off = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<int32_t*>(offs + base), 0, (int)(4u * (m + 1u)), 0x00020000);
+#pragma unroll
+      for (int j = 0; j < kSmallPer; ++j) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs_off, (int)(4u * ((uint32_t)j * kSmallThreads + t)), 0, 0);
+        ob[j] = v[0];
+        oe[j] = v[1];
+      }
+    };
+    if (r0 < r1) load_offs(r0);
+    for (int64_t base = r0; base < r1 && !fail; base += step) {
+      uint32_t lens[(kSmallPer + 3) / 4] = {};
+      uint32_t kw[kSmallPer][4];
+      uint32_t sel = 0u, nul = 0u;
+#pragma unroll
+      for (int j = 0; j < kSmallPer; ++j) {
+        const int64_t row = base + (int64_t)j * kSmallThreads + t;
+        const uint32_t n = oe[j] - ob[j];
+        lens[j / 4] |= (n < 255u ? n : 255u) << (8 * (j % 4));
+        const bool valid = validity == nullptr || (row < r1 && ((validity[row >> 3] >> (row & 7)) & 1u));
+        if (row < r1 && (valid || null_key)) sel |= 1u << j;
+        if (row < r1 && !valid) nul |= 1u << j;
+        stage_key_load(rs_vals, vals, heap_end, ob[j], lens, j, kw[j]);
+      }
+      if (base + step < r1) load_offs(base + step);
+#pragma unroll
+      for (int j = 0; j < kSmallPer; ++j) {
+        if (!((sel >> j) & 1u)) continue;
+        uint64_t k0, k1;
+        uint32_t n;
+        if ((nul >> j) & 1u) {
+          n = 9;
+          k0 = kNullK0;
+          k1 = kNullK1;
+        } else {
+          n = (lens[j / 4] >> (8 * (j % 4))) & 0xFFu;
+          if (n > 15) {
+            fail = true;
+            continue;
+          }
+          const uint64_t lo = (uint64_t)kw[j][0] | ((uint64_t)kw[j][1] << 32);
+          const uint64_t hi = (uint64_t)kw[j][2] | ((uint64_t)kw[j][3] << 32);
+          k0 = n >= 8 ? lo : (lo & ((1ull << (8u * n)) - 1ull));
+          k1 = n > 8 ? (hi & ((1ull << (8u * (n - 8u))) - 1ull)) : 0ull;
+        }
+        if (!small_count(L, k0, k1 | ((unsigned long long)n << kRecLenShift))) fail = true;
+      }
+    }
+  } else {
+    const int w = width_of(c0.type);
+    for (int64_t base = r0; base < r1 && !fail; base += step) {
+      uint64_t v[kSmallPer];
+      uint32_t sel = 0u, nul = 0u;
+#pragma unroll
+      for (int j = 0; j < kSmallPer; ++j) {
+        const int64_t row = base + (int64_t)j * kSmallThreads + t;
+        v[j] = 0;
+        if (row >= r1) continue;
+        const bool valid = validity == nullptr || ((validity[row >> 3] >> (row & 7)) & 1u);
+        if (valid || null_key) sel |= 1u << j;
+        if (!valid) nul |= 1u << j;
+        else v[j] = fixed_bits(c0, row);
+      }
+#pragma unroll
+      for (int j = 0; j < kSmallPer; ++j) {
+        if (!((sel >> j) & 1u)) continue;
+        uint64_t k0 = v[j];
+        uint32_t n = (uint32_t)w;
+        if ((nul >> j) & 1u) {  // Histogram NULL of a non-string column: the empty key
+          k0 = 0;
+          n = 0;
+        } else if (null_key) {  // Histogram groups cast-to-string values: every NaN is "NaN"
+          if (c0.type == DQ_T_FLOAT64 && (k0 & 0x7fffffffffffffffull) > 0x7ff0000000000000ull) k0 = 0x7ff8000000000000ull;
+          if (c0.type == DQ_T_FLOAT32 && (k0 & 0x7fffffffull) > 0x7f800000ull) k0 = 0x7fc00000ull;
+        }
+        if (!small_count(L, k0, (unsigned long long)n << kRecLenShift)) fail = true;
+      }
+    }
+  }
+  if (fail) atomicOr(bad, 1u);
+  __syncthreads();
+  // this workgroup's groups, compacted into its staging list
+  for (uint32_t i = t; i < (uint32_t)kSmallSlots; i += kSmallThreads) {
+    const uint32_t c = L.C[i];
+    const bool used = c != 0u;
+    const uint64_t m = __ballot(used);
+    uint32_t at = 0;
+    if (m) {
+      const uint32_t lane = t & 63u;
+      uint32_t base_w = 0;
+      if (lane == (uint32_t)__builtin_ctzll(m)) base_w = atomicAdd(&L.n_used, (uint32_t)__popcll(m));
+      base_w = __shfl(base_w, __builtin_ctzll(m), 64);
+      at = base_w + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    }
+    if (used) {
+      const uint64_t o = (uint64_t)blockIdx.x * kSmallSlots + at;
+      out_k0[o] = L.K0[i];
+      out_k1[o] = L.K1[i];
+      out_c[o] = c;
+    }
+  }
+  __syncthreads();
+  if (t == 0) out_n[blockIdx.x] = L.n_used;
+}
+
+// Sums the workgroups' staging lists (one workgroup, an LDS table) and inserts each group into the
+// table once (global_insert: the table may already hold groups).
+__global__ __launch_bounds__(kSmallThreads) void dq_freq_small_merge_kernel(const unsigned long long* __restrict__ in_k0,
+                                                                            const unsigned long long* __restrict__ in_k1,
+                                                                            const uint32_t* __restrict__ in_c,
+                                                                            const uint32_t* __restrict__ in_n, int n_blocks,
+                                                                            FreqTable T, unsigned int* bad) {
+  __shared__ unsigned long long K0[kSmallSlots], K1[kSmallSlots];
+  __shared__ unsigned long long C[kSmallSlots];
+  const uint32_t t = threadIdx.x;
+  if (*bad) return;  // (the counting kernel failed: the host takes the general path)
+  for (uint32_t i = t; i < (uint32_t)kSmallSlots; i += kSmallThreads) {
+    K1[i] = kLdsEmpty;
+    C[i] = 0ull;
+  }
+  __syncthreads();
+  bool fail = false;
+  for (int b = 0; b < n_blocks; ++b) {
+    const uint32_t n = in_n[b];
+    for (uint32_t i = t; i < n; i += kSmallThreads) {
+      const uint64_t o = (uint64_t)b * kSmallSlots + i;
+      const uint64_t k0 = in_k0[o], k1l = in_k1[o];
+      uint32_t s = lds_hash(k0, k1l, 0) & (kSmallSlots - 1);
+      bool done = false;
+      for (uint32_t probe = 0; probe < (uint32_t)kSmallSlots && !done;) {
+        const unsigned long long c = atomicCAS(&K1[s], kLdsEmpty, kLdsBusy);
+        if (c == kLdsEmpty) {
+          K0[s] = k0;
+          __threadfence_block();
+          atomicExch(&K1[s], k1l);
+          atomicAdd(&C[s], (unsigned long long)in_c[o]);
+          done = true;
+        } else if (c == kLdsBusy) {
+        } else if (c == k1l && __hip_atomic_load(&K0[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == k0) {
+          atomicAdd(&C[s], (unsigned long long)in_c[o]);
+          done = true;
+        } else {
+          s = (s + 1) & (kSmallSlots - 1);
+          ++probe;
+        }
+      }
+      if (!done) fail = true;
+    }
+  }
+  __syncthreads();
+  if (fail) {
+    atomicOr(bad, 1u);
+    return;
+  }
+  for (uint32_t i = t; i < (uint32_t)kSmallSlots; i += kSmallThreads) {
+    if (!C[i]) continue;
+    Key k;
+    k.k0 = K0[i];
+    k.k1 = K1[i] & kRecKeyMask;
+    k.len = (uint32_t)(K1[i] >> kRecLenShift);
+    k.ptr = nullptr;
+    k.hash = hash_inline(k.k0, k.k1, k.len);
+    global_insert(T, k, C[i]);
+  }
+}
+
+hipError_t launch_freq_small(const FreqKeySpec& ks, bool string_key, const DevColumn* d_cols, int64_t n_rows, int blocks,
+                             unsigned long long* d_k0, unsigned long long* d_k1, uint32_t* d_c, uint32_t* d_n,
+                             unsigned int* d_bad, const FreqTable& T, hipStream_t stream) {
+  if (n_rows <= 0) return hipSuccess;
+  if (string_key)
+    hipLaunchKernelGGL(dq_freq_small_kernel<true>, dim3((unsigned)blocks), dim3(kSmallThreads), 0, stream, ks, d_cols, n_rows,
+                       d_k0, d_k1, d_c, d_n, d_bad);
+  else
+    hipLaunchKernelGGL(dq_freq_small_kernel<false>, dim3((unsigned)blocks), dim3(kSmallThreads), 0, stream, ks, d_cols,
+                       n_rows, d_k0, d_k1, d_c, d_n, d_bad);
+  hipLaunchKernelGGL(dq_freq_small_merge_kernel, dim3(1), dim3(kSmallThreads), 0, stream, d_k0, d_k1, d_c, d_n, blocks, T,
+                     d_bad);
   return hipGetLastError();
 }
 

@@ -180,13 +180,16 @@ struct FreqTable {
   FreqSlot* slots;
   uint64_t mask;                   // capacity - 1 (capacity: a power of two >= kFreqSliceSlots)
   int32_t bucket_bits;             // log2(capacity / kFreqSliceSlots)
-  int32_t pad_;
+  int32_t test_flags;              // kFreqTestNoPublish: a test-only broken publish (0 otherwise)
   unsigned long long* n_groups;    // device counter of claimed slots
   uint8_t* heap;                   // key bytes of keys longer than 16 B
   unsigned long long* heap_used;
   unsigned long long heap_cap;
-  unsigned int* overflow;          // bit 0 table full, bit 1 heap full, bit 2 key too long
+  unsigned int* overflow;          // bit 0 table full, bit 1 heap full, bit 2 key too long,
+                                   // bit 3 a wait for another lane's slot publish timed out
 };
+constexpr unsigned int kFreqWaitTimeout = 8u;
+constexpr int32_t kFreqTestNoPublish = 1;  // DQ_FREQ_TEST_NO_PUBLISH=1: claimed slots never turn READY
 
 struct FreqKeySpec {
   int32_t key_cols[kMaxKeyCols];
@@ -213,6 +216,49 @@ struct FreqIn {  // groups to merge in; heap offsets in k0 refer to `heap`
   uint64_t stride;  // elements between consecutive groups: 1 = separate arrays, 4 = FreqSlot records
 };
 
+// Key-hash exchange and table merges (dq_freq.hip, round 4).  A packed wire record: a key that
+// packs into one word (dq_keypack.h) and its count.
+struct WirePacked {
+  unsigned long long key, count;
+};
+// One record stream a merge takes in: a part's packed section (kind 0), its general section
+// (kind 1: FreqSlot, READY clear, k0 of a long key = offset in `heap`), or a source table's slot
+// array (kind 2, src_bits = its slice bits).  skip = 1: out of slice order, inserted group by group.
+struct ImportRun {
+  const void* recs;
+  uint64_t n;
+  const uint8_t* heap;
+  int32_t kind;
+  int32_t src_bits;
+  int32_t skip;
+  int32_t pad_;
+};
+hipError_t launch_wire_count(const FreqTable& T, int n_parts, int chunk_log, uint64_t n_chunks, unsigned long long* d_cnt,
+                             unsigned long long* d_kbytes, hipStream_t stream);
+hipError_t launch_gather_strided(const unsigned long long* d_scanned, uint64_t stride, uint64_t n, unsigned long long* d_out,
+                                 hipStream_t stream);
+hipError_t launch_wire_scatter(const FreqTable& T, int n_parts, int chunk_log, uint64_t n_chunks,
+                               const unsigned long long* d_pos, const unsigned long long* d_sec,
+                               const unsigned long long* d_key_base, unsigned long long* d_key_cursor, uint8_t* d_out,
+                               uint8_t* d_keys, hipStream_t stream);
+hipError_t launch_import_sketch(const ImportRun* d_runs, int n_runs, uint64_t max_n, uint32_t* d_hll, hipStream_t stream);
+hipError_t launch_import_bounds(const ImportRun* d_runs, int n_runs, uint64_t max_n, int rb, uint64_t n_slices,
+                                uint32_t* d_start, uint32_t* d_end, unsigned int* d_unsorted, hipStream_t stream);
+hipError_t launch_import_merge(const FreqTable& T, bool packed, const ImportRun* d_runs, int n_runs, const uint32_t* d_start,
+                               const uint32_t* d_end, int table_empty, unsigned long long* d_hist, unsigned long long* d_big,
+                               unsigned long long* d_n_big, unsigned long long big_cap, uint32_t* d_smax, int write_all,
+                               uint32_t* d_ovf_list, unsigned long long* d_n_ovf, unsigned long long* d_new_groups,
+                               hipStream_t stream);
+hipError_t launch_import_global(const FreqTable& T, const ImportRun* d_runs, int n_runs, uint64_t max_n, int mode, int rb_old,
+                                const uint32_t* d_start, const uint32_t* d_end, uint64_t n_slices_old,
+                                const uint32_t* d_ovf_list, uint64_t n_ovf, hipStream_t stream);
+// Few-groups group-by of one key column (dq_freq.hip): per-workgroup LDS tables, staging lists
+// (kFreqSmallSlots entries per workgroup in d_k0 / d_k1 / d_c, d_n[block] used), one merge into T;
+// *d_bad != 0: a key longer than 15 bytes or more keys than an LDS table holds (nothing merged).
+constexpr int kFreqSmallSlots = 1024;
+hipError_t launch_freq_small(const FreqKeySpec& ks, bool string_key, const DevColumn* d_cols, int64_t n_rows, int blocks,
+                             unsigned long long* d_k0, unsigned long long* d_k1, uint32_t* d_c, uint32_t* d_n,
+                             unsigned int* d_bad, const FreqTable& T, hipStream_t stream);
 hipError_t launch_freq_insert(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
                               const FreqTable& T, hipStream_t stream,
                               int max_blocks = 4096);
@@ -227,13 +273,6 @@ hipError_t launch_freq_lookup(const FreqTable& T, const uint8_t* d_key, uint32_t
                               hipStream_t stream);
 hipError_t launch_freq_heap_need(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
                                  unsigned long long* d_need, unsigned long long* d_max_len, hipStream_t stream);
-// Multi-GPU key-hash exchange: owner rank of a group = freq_owner(hash, n_parts).  `d_cnt` gets
-// per part {groups, long-key bytes}; the scatter writes part p's groups (FreqSlot records, k0 of
-// a long key = offset in the part's key region) from d_base[2p] / d_base[2p+1] on.
-hipError_t launch_freq_part_count(const FreqTable& T, int n_parts, unsigned long long* d_cnt, hipStream_t stream);
-hipError_t launch_freq_part_scatter(const FreqTable& T, int n_parts, const unsigned long long* d_base,
-                                    unsigned long long* d_cursor, FreqSlot* out_groups, uint8_t* out_keys,
-                                    hipStream_t stream);
 // Sorted-bucket path (dq_freq.hip): stage rows as FreqRec + an HLL sketch of their hashes (to size
 // the table), group them by slice (the bucket split below), then aggregate every slice's bucket
 // in LDS (split buckets merge atomically).
@@ -316,7 +355,7 @@ hipError_t launch_hll(const HllTask* d_tasks, int n_tasks, const DevColumn* d_co
                       uint32_t* d_registers, hipStream_t stream);
 hipError_t launch_predicates(const PredProgram* d_progs, int n_progs, const PredInsn* d_insns,
                              const uint8_t* d_pool, const DevColumn* d_cols, int64_t n_rows,
-                             uint64_t* d_mask_words, int64_t words_per_mask, hipStream_t stream);
+                             uint64_t* d_mask_words, int64_t words_per_mask, bool with_cast, hipStream_t stream);
 hipError_t launch_rebase_offsets(int32_t* d_offs, int64_t n, int32_t first, hipStream_t stream);
 hipError_t launch_realign_bitmap(const uint8_t* src, int64_t bit_offset, int64_t n_bits,
                                  uint8_t* dst, hipStream_t stream);

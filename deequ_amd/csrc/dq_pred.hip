@@ -89,6 +89,9 @@ __device__ inline bool cmp_result(int opcode, int ord) {
   }
 }
 
+// CAST: the program may cast a string to double (Double.parseDouble, whose exact slow path
+// carries ~1 KB of private scratch per lane); programs without one run a kernel without it.
+template <bool CAST>
 __device__ void eval_program(const PredInsn* code, int n, const uint8_t* pool, const DevColumn* cols, int64_t row,
                              bool& t, bool& nn) {
   Val st[kMaxStack];
@@ -103,9 +106,10 @@ __device__ void eval_program(const PredInsn* code, int n, const uint8_t* pool, c
       case DQ_P_LIT_STRING: st[sp++] = Val{(int64_t)ins.arg, 0.0, VT_STR, 0, pool + ins.i64}; break;
       case DQ_P_CAST_DOUBLE: {  // Spark 2.2 Cast(-> DoubleType): parseDouble of a string
         Val& a = st[sp - 1];
-        if (a.type == VT_STR) {
+        if (CAST && a.type == VT_STR) {
           double v = 0.0;
-          const int r = a.null ? 0 : parse_double(PtrSrc{a.s}, (int32_t)a.i, &v);
+          int r = 0;
+          if constexpr (CAST) r = a.null ? 0 : parse_double(PtrSrc{a.s}, (int32_t)a.i, &v);
           a.null = (r == 1) ? a.null : 1;
           a.f = v;
         } else {
@@ -181,6 +185,7 @@ __device__ void eval_program(const PredInsn* code, int n, const uint8_t* pool, c
 
 }  // namespace
 
+template <bool CAST>
 __global__ __launch_bounds__(kBlock) void dq_pred_kernel(const PredProgram* __restrict__ progs,
                                                          const PredInsn* __restrict__ insns,
                                                          const uint8_t* __restrict__ pool,
@@ -197,7 +202,7 @@ __global__ __launch_bounds__(kBlock) void dq_pred_kernel(const PredProgram* __re
        w += (int64_t)gridDim.x * (kBlock / 64)) {
     const int64_t row = (w << 6) + lane;
     bool t = false, nn = false;
-    if (row < n_rows) eval_program(code, prog.n, pool, cols, row, t, nn);
+    if (row < n_rows) eval_program<CAST>(code, prog.n, pool, cols, row, t, nn);
     const uint64_t bt = __ballot(t);
     const uint64_t bn = __ballot(nn);
     if (lane == 0) {
@@ -226,13 +231,17 @@ __global__ void dq_realign_kernel(const uint8_t* __restrict__ src, int64_t bit_o
 
 hipError_t launch_predicates(const PredProgram* d_progs, int n_progs, const PredInsn* d_insns,
                              const uint8_t* d_pool, const DevColumn* d_cols, int64_t n_rows,
-                             uint64_t* d_mask_words, int64_t words_per_mask, hipStream_t stream) {
+                             uint64_t* d_mask_words, int64_t words_per_mask, bool with_cast, hipStream_t stream) {
   if (n_progs <= 0 || n_rows <= 0) return hipSuccess;
   const int64_t n_words = (n_rows + 63) >> 6;
   int64_t blocks = (n_words + 3) / 4;
   if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(dq_pred_kernel, dim3((unsigned)blocks, n_progs), dim3(kBlock), 0, stream,
-                     d_progs, d_insns, d_pool, d_cols, n_rows, d_mask_words, words_per_mask);
+  if (with_cast)
+    hipLaunchKernelGGL(dq_pred_kernel<true>, dim3((unsigned)blocks, n_progs), dim3(kBlock), 0, stream,
+                       d_progs, d_insns, d_pool, d_cols, n_rows, d_mask_words, words_per_mask);
+  else
+    hipLaunchKernelGGL(dq_pred_kernel<false>, dim3((unsigned)blocks, n_progs), dim3(kBlock), 0, stream,
+                       d_progs, d_insns, d_pool, d_cols, n_rows, d_mask_words, words_per_mask);
   return hipGetLastError();
 }
 

@@ -229,6 +229,17 @@ __global__ __launch_bounds__(kBlock) void dq_datatype_kernel(const HllTask* __re
 #ifndef DQ_STR_U
 #define DQ_STR_U 4
 #endif
+// Little-endian p[0..n) (n <= 8), zero padded, from the aligned words that hold those bytes only.
+__device__ inline uint64_t ld_bytes(const uint8_t* p, uint32_t n) {
+  if (n == 0) return 0;
+  const uintptr_t a = (uintptr_t)p;
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(a & ~(uintptr_t)7);
+  const uint32_t sh = (uint32_t)(a & 7) * 8u;
+  uint64_t v = w[0] >> sh;
+  if (sh && (a & 7) + n > 8) v |= w[1] << (64u - sh);
+  return n >= 8 ? v : (v & ((1ull << (8u * n)) - 1ull));
+}
+
 // DT = false: the HLL alone (an ApproxCountDistinct without a DataType on the column), through
 // the same batched word loads.
 template <bool DT>
@@ -248,16 +259,17 @@ __global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* _
   const DevColumn& col = cols[task.column];
   const uint8_t* wt = task.where_mask >= 0 ? reinterpret_cast<const uint8_t*>(masks[task.where_mask].t) : nullptr;
   const uint8_t* vals = static_cast<const uint8_t*>(col.values);
-  const uintptr_t al = (uintptr_t)vals & ~(uintptr_t)7;
-  const uint32_t delta = (uint32_t)((uintptr_t)vals - al);
-  const uint32_t span = (delta + (uint32_t)col.offsets[n_rows] + 7u) & ~7u;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(al), 0, (int)span, 0x00020000);
+  // the first 24 bytes of each string as three words, read unaligned from its first byte (one
+  // 16-byte and one 8-byte buffer load); a string within 24 bytes of the heap's end reads the
+  // aligned words that hold its bytes instead (a buffer range check is per dword)
+  const uint32_t heap_end = (uint32_t)col.offsets[n_rows];
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vals), 0, (int)heap_end, 0x00020000);
   uint64_t c[5] = {0, 0, 0, 0, 0};
   constexpr int U = DQ_STR_U;
   for (int64_t base = r0 + threadIdx.x; base < r1; base += U * kBlock) {
     int32_t ob[U], oe[U];
     uint32_t sel[U];
-    uint64_t w[U][4];
+    uint64_t w[U][3];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t row = base + (int64_t)u * kBlock;
@@ -269,11 +281,17 @@ __global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* _
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t a = (delta + (uint32_t)ob[u]) & ~7u;
+      const uint32_t a = (uint32_t)ob[u];
+      if (a + 24u <= heap_end) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)a, 0, 0);
+        const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(a + 16u), 0, 0);
+        w[u][0] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+        w[u][1] = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
+        w[u][2] = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
+      } else {
+        const uint32_t m = heap_end - a < 24u ? heap_end - a : 24u;  // bytes of the heap from a
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(a + 8u * k), 0, 0);
-        w[u][k] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+        for (int k = 0; k < 3; ++k) w[u][k] = m > 8u * k ? ld_bytes(vals + a + 8u * k, min(8u, m - 8u * k)) : 0ull;
       }
     }
 #pragma unroll
@@ -284,8 +302,7 @@ __global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* _
       int k;
       W64 h;
       if (n <= 24) {
-        const uint32_t sh = ((delta + (uint32_t)ob[u]) & 7u) * 8u;
-        const uint64_t s[3] = {funnel(w[u][0], w[u][1], sh), funnel(w[u][1], w[u][2], sh), funnel(w[u][2], w[u][3], sh)};
+        const uint64_t s[3] = {w[u][0], w[u][1], w[u][2]};
         k = (DT && sel[u]) ? classify_shifted(s[0], s[1], s[2], n) : DT_NULL;
         h = xxh64_words_dev(s, (uint32_t)n);
       } else {

@@ -171,9 +171,11 @@ def allreduce_flag(flag: bool, group=None) -> bool:
 # key hash into `spark.sql.shuffle.partitions` and finishes the aggregate per partition
 # (GroupingAnalyzers.scala:67-72).  Here every rank groups its own row shard on its GPU, then:
 #   1. partitions its table by owner rank (dq_freq_partition, a device scatter),
-#   2. exchanges the partitions with ONE all-to-all of 32-B wire groups (+ one for long-key
-#      bytes) -- RCCL over xGMI with the nccl backend, gloo on host copies otherwise,
-#   3. merges what it received into the table of the keys it owns (dq_freq_import_wire).
+#   2. exchanges the partitions with ONE all-to-all of wire groups -- 16 B for keys that pack
+#      into one word (decimal ids), 32 B for others -- (+ one for long-key bytes): RCCL over xGMI
+#      with the nccl backend, gloo on host copies otherwise,
+#   3. merges what it received into the table of the keys it owns (dq_freq_import_parts: every
+#      part arrives in slice order, so each slice is merged once, in LDS, from all parts).
 # Owners then hold disjoint keys: the metrics need only an all-reduce of the count-of-counts
 # histograms (integers, exact), and Histogram's top-N an all-gather of per-owner top-N.
 
@@ -195,24 +197,25 @@ def exchange_frequencies(table, group=None):
     world = dist.get_world_size(group)
     dev = table.torch_device
     comm = dev if _comm_device(group) == "cuda" else torch.device("cpu")
-    W = table.WIRE_BYTES
-    part_g, part_k, err = [0] * world, [0] * world, None
+    part_p, part_g, part_k, err = [0] * world, [0] * world, [0] * world, None
     try:
-        part_g, part_k = table.partition_sizes(world)
-        send_g = torch.empty(max(1, sum(part_g)) * W, dtype=torch.uint8, device=dev)
+        part_p, part_g, part_k = table.partition_sizes(world)
+        nbytes = sum(table.part_bytes(p, g) for p, g in zip(part_p, part_g))
+        send_g = torch.empty(max(16, nbytes), dtype=torch.uint8, device=dev)
         send_k = torch.empty(max(8, sum(part_k)), dtype=torch.uint8, device=dev)
-        if sum(part_g):
+        if nbytes:
             table.partition_into(world, send_g, send_k)
     except Exception as e:  # noqa: BLE001 -- agreed on below, then re-raised
         err = e
     agree(err, "partitioning the frequency table by owner", group)
-    sizes = torch.tensor([[g, k] for g, k in zip(part_g, part_k)], dtype=torch.int64).reshape(-1).to(comm)
+    sizes = torch.tensor([[p, g, k] for p, g, k in zip(part_p, part_g, part_k)], dtype=torch.int64).reshape(-1).to(comm)
     recv_sizes = torch.empty_like(sizes)
     dist.all_to_all_single(recv_sizes, sizes, group=group)
-    recv = recv_sizes.cpu().reshape(world, 2).tolist()
-    in_g, out_g = [g * W for g in part_g], [r[0] * W for r in recv]
-    in_k, out_k = list(part_k), [r[1] for r in recv]
-    recv_g = torch.empty(max(W, sum(out_g)), dtype=torch.uint8, device=comm)
+    recv = recv_sizes.cpu().reshape(world, 3).tolist()
+    in_g = [table.part_bytes(p, g) for p, g in zip(part_p, part_g)]
+    out_g = [table.part_bytes(r[0], r[1]) for r in recv]
+    in_k, out_k = list(part_k), [r[2] for r in recv]
+    recv_g = torch.empty(max(16, sum(out_g)), dtype=torch.uint8, device=comm)
     recv_k = torch.empty(max(8, sum(out_k)), dtype=torch.uint8, device=comm)
     sg = _to(send_g, comm)
     sk = _to(send_k, comm)
@@ -224,16 +227,15 @@ def exchange_frequencies(table, group=None):
     owned, err = None, None
     try:
         owned = type(table).like(table)
-        og = ok = 0
-        for s in range(world):
-            n = recv[s][0]
-            if n:
-                owned.import_wire(recv_g[og:og + n * W], n, recv_k[ok:ok + max(1, recv[s][1])], recv[s][1], 0)
-            og += n * W
-            ok += recv[s][1]
+        owned.import_parts(recv_g, [r[0] for r in recv], [r[1] for r in recv], recv_k, [r[2] for r in recv], 0)
     except Exception as e:  # noqa: BLE001
         err = e
-    agree(err, "merging the received frequency parts", group)
+    try:
+        agree(err, "merging the received frequency parts", group)
+    except Exception:
+        if owned is not None:  # (a half-built table, or one another rank's failure orphans)
+            owned.close()
+        raise
     return owned
 
 
@@ -339,11 +341,12 @@ def compute_frequencies_distributed(data, grouping_columns, histogram: bool = Fa
         n_local = local.summary().num_rows
     except Exception as e:  # noqa: BLE001 -- every rank fails together (agree)
         err = e
-    if err is not None and local is not None:
-        local.close()
-    agree(err, "the frequency group-by", group)
-    owned = exchange_frequencies(local, group)
-    local.close()
+    try:  # the local table is closed on every exit (another rank's failure raises here too)
+        agree(err, "the frequency group-by", group)
+        owned = exchange_frequencies(local, group)
+    finally:
+        if local is not None:
+            local.close()
     n = torch.tensor([n_local], dtype=torch.int64)
     if _comm_device(group) == "cuda":
         n = n.to(owned.torch_device)

@@ -181,26 +181,40 @@ class FrequencyTable:
         L.check(L.lib().dq_freq_import(self.handle, groups, n, buf, int(num_rows)))
 
     # ---- multi-GPU key-hash exchange (deequ_amd/distributed.py)
-    WIRE_BYTES = 32  # sizeof(dq_freq_wire)
+    WIRE_PACKED_BYTES = 16  # sizeof(dq_freq_wire_packed): a key that packs into one word
+    WIRE_BYTES = 32         # sizeof(dq_freq_wire): any other key
 
-    def partition_sizes(self, n_parts: int) -> Tuple[List[int], List[int]]:
-        """Groups and long-key bytes per owner part (dq_freq_partition sizing call)."""
-        pg, pk = (ctypes.c_int64 * n_parts)(), (ctypes.c_int64 * n_parts)()
-        st = L.lib().dq_freq_partition(self.handle, n_parts, None, 0, None, 0, pg, pk)
+    @classmethod
+    def part_bytes(cls, packed: int, general: int) -> int:
+        return cls.WIRE_PACKED_BYTES * int(packed) + cls.WIRE_BYTES * int(general)
+
+    def partition_sizes(self, n_parts: int) -> Tuple[List[int], List[int], List[int]]:
+        """(packed groups, other groups, long-key bytes) per owner part (dq_freq_partition sizing)."""
+        pp, pg, pk = (ctypes.c_int64 * n_parts)(), (ctypes.c_int64 * n_parts)(), (ctypes.c_int64 * n_parts)()
+        st = L.lib().dq_freq_partition(self.handle, n_parts, None, 0, None, 0, pp, pg, pk)
         if st not in (L.DQ_OK, L.DQ_ERR_SPACE):
             L.check(st)
-        return list(pg), list(pk)
+        return list(pp), list(pg), list(pk)
 
-    def partition_into(self, n_parts: int, groups, keys) -> Tuple[List[int], List[int]]:
-        """Scatter the groups by owner into device byte tensors `groups` (32 B per group) and
-        `keys` (long-key bytes), both on this table's GPU."""
-        pg, pk = (ctypes.c_int64 * n_parts)(), (ctypes.c_int64 * n_parts)()
-        L.check(L.lib().dq_freq_partition(self.handle, n_parts, groups.data_ptr(), groups.numel() // self.WIRE_BYTES,
-                                          keys.data_ptr(), keys.numel(), pg, pk))
-        return list(pg), list(pk)
+    def partition_into(self, n_parts: int, parts, keys) -> Tuple[List[int], List[int], List[int]]:
+        """Scatter the groups by owner into device byte tensors `parts` (per part: its packed
+        records, then its other records, each in slice order) and `keys` (long-key bytes)."""
+        pp, pg, pk = (ctypes.c_int64 * n_parts)(), (ctypes.c_int64 * n_parts)(), (ctypes.c_int64 * n_parts)()
+        L.check(L.lib().dq_freq_partition(self.handle, n_parts, parts.data_ptr(), parts.numel(), keys.data_ptr(),
+                                          keys.numel(), pp, pg, pk))
+        return list(pp), list(pg), list(pk)
+
+    def import_parts(self, parts, packed: Sequence[int], general: Sequence[int], keys, key_bytes: Sequence[int],
+                     num_rows: int = 0) -> None:
+        """Merge the received parts (laid out one after the other in device tensors, as
+        partition_into writes each) into this table, every slice once."""
+        n = len(packed)
+        arr = lambda v: (ctypes.c_int64 * max(1, n))(*[int(x) for x in v])  # noqa: E731
+        L.check(L.lib().dq_freq_import_parts(self.handle, n, parts.data_ptr(), arr(packed), arr(general),
+                                             keys.data_ptr(), arr(key_bytes), int(num_rows)))
 
     def import_wire(self, groups, n: int, keys, key_bytes: int, num_rows: int = 0) -> None:
-        """Merge `n` wire groups held in device tensors (one sender's part) into this table."""
+        """Merge `n` general wire groups (dq_freq_wire, any order) held in device tensors."""
         L.check(L.lib().dq_freq_import_wire(self.handle, groups.data_ptr(), n, keys.data_ptr(), key_bytes,
                                             int(num_rows)))
 
@@ -227,10 +241,10 @@ class FrequencyTable:
 
     def paths(self) -> Dict[str, int]:
         """Which group-by paths this table's groupings took (dq_diag_freq_paths; tests)."""
-        out = (ctypes.c_int64 * 5)()
+        out = (ctypes.c_int64 * 7)()
         L.check(L.lib().dq_diag_freq_paths(self.handle, out))
         return {"slots": out[0], "partition_runs": out[1], "slice_bits": out[2], "sort_records": out[3],
-                "packed_runs": out[4]}
+                "packed_runs": out[4], "small_runs": out[5], "wait_timeouts": out[6]}
 
     def merge_from(self, other: "FrequencyTable") -> None:
         """self += other, device to device."""

@@ -188,6 +188,8 @@ class ColumnProfiler:
         from .distributed import is_sharded
         overlap = os.environ.get("DEEQU_AMD_PROFILE_SERIAL", "0") != "1"  # (A/B and debugging knob)
         side = ThreadPoolExecutor(max_workers=1) if overlap and targets and not is_sharded(data) else None
+        if side and printStatusUpdates:
+            print("### PROFILING: Computing histograms of low-cardinality columns in pass (3/3), beside pass 2...")
         pending = (side.submit(compute_histograms, data, targets, generic.approximateNumDistincts)
                    if side else None)
         try:
@@ -202,11 +204,12 @@ class ColumnProfiler:
                 for k, v in _extract_numeric_statistics(ctx2).items():
                     numeric[k].update(v)
         except BaseException:
-            if side:
-                side.shutdown(wait=True)
+            if side:  # raised now, as the sequential run would; the histogram pass is not awaited
+                pending.cancel()
+                side.shutdown(wait=False, cancel_futures=True)
             raise
 
-        if printStatusUpdates:
+        if printStatusUpdates and not side:
             print("### PROFILING: Computing histograms of low-cardinality columns in pass (3/3)...")
         if side:
             try:

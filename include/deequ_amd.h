@@ -412,7 +412,7 @@ dq_status dq_freq_import(dq_freq* f, const dq_freq_group* groups, int64_t n, con
  * group counts by key hash into spark.sql.shuffle.partitions before the final aggregate
  * (GroupingAnalyzers.scala:67-72).  Here every rank partitions its local table by owner rank
  * (a hash of the encoded key), the ranks exchange the partitions with one all-to-all (RCCL over
- * xGMI), and every owner merges what it receives with dq_freq_import_wire -- after which the
+ * xGMI), and every owner merges what it receives with dq_freq_import_parts -- after which the
  * owners hold disjoint keys, and their count-of-counts histograms add up to the global one. */
 typedef struct dq_freq_wire {  /* one group in device memory (32 B)                         */
   uint64_t ctrl;               /* key length (low 24 bits) | 1 << 30 if the key is in key bytes */
@@ -420,15 +420,31 @@ typedef struct dq_freq_wire {  /* one group in device memory (32 B)             
   uint64_t k0, k1;             /* key bytes (<= 16 B, little-endian), or k0 = key-byte offset  */
 } dq_freq_wire;
 
+typedef struct dq_freq_wire_packed {  /* a group whose key packs into one word (16 B):        */
+  uint64_t key;                       /* a decimal digit string of <= 15 bytes -- nibble i =   */
+  int64_t count;                      /* digit i, the length in the top nibble -- or 0xA for   */
+} dq_freq_wire_packed;                /* Histogram's "NullValue" group                         */
+
 /* Write every group of `f`, partitioned by owner (0 .. n_parts-1), into DEVICE buffers on f's
- * GPU: part p's groups follow parts 0..p-1 in d_groups, its long keys (8-byte padded) follow
- * theirs in d_key_bytes, with k0 relative to the start of part p's key region.  part_groups /
- * part_key_bytes (host, n_parts each) receive the sizes; if the buffers are too small nothing is
- * written and DQ_ERR_SPACE is returned (call once with max_groups = 0 to size them). */
-dq_status dq_freq_partition(dq_freq* f, int n_parts, dq_freq_wire* d_groups, int64_t max_groups,
-                            uint8_t* d_key_bytes, int64_t key_cap, int64_t* part_groups,
+ * GPU.  Part p follows parts 0..p-1 in d_out and is part_packed[p] dq_freq_wire_packed records
+ * (16 B: keys that pack) then part_groups[p] dq_freq_wire records (32 B: every other key), each
+ * section in the order of f's table slices -- so the receiver merges a part slice by slice with
+ * no sort.  Long keys (8-byte padded) of part p follow those of parts 0..p-1 in d_key_bytes, k0
+ * relative to the start of part p's key region.  The sizes go to the three host arrays (n_parts
+ * each); if a buffer is too small nothing is written and DQ_ERR_SPACE is returned (call once with
+ * out_bytes = 0 to size them: part p takes 16 part_packed[p] + 32 part_groups[p] bytes).
+ * Replaces the map side of the groupBy's hash exchange (GroupingAnalyzers.scala:67-72). */
+dq_status dq_freq_partition(dq_freq* f, int n_parts, void* d_out, int64_t out_bytes, uint8_t* d_key_bytes,
+                            int64_t key_cap, int64_t* part_packed, int64_t* part_groups,
                             int64_t* part_key_bytes);
-/* Merge groups held in DEVICE memory (one sender's part) into f; num_rows is added to numRows. */
+/* Merge the parts other ranks partitioned for this one (laid out as dq_freq_partition writes
+ * them, one after the other in d_parts / d_key_bytes) into f: each of f's slices is merged once,
+ * in LDS, from the matching records of every part (FrequenciesAndNumRows.sum's outer join,
+ * GroupingAnalyzers.scala:128-148); num_rows is added to numRows. */
+dq_status dq_freq_import_parts(dq_freq* f, int n_parts, const void* d_parts, const int64_t* part_packed,
+                               const int64_t* part_groups, const uint8_t* d_key_bytes,
+                               const int64_t* part_key_bytes, int64_t num_rows);
+/* Merge n general groups held in DEVICE memory (dq_freq_wire, any order) into f. */
 dq_status dq_freq_import_wire(dq_freq* f, const dq_freq_wire* d_groups, int64_t n,
                               const uint8_t* d_key_bytes, int64_t key_bytes, int64_t num_rows);
 /* Count-of-counts of f: hist[c] = number of groups with count c (1 <= c < n_bins, hist[0] = 0);

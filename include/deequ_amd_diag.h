@@ -24,7 +24,9 @@ dq_status dq_diag_hash_rate(int device, int with_hll, int reps, double* hashes_p
  * that a workload exercised the path it is meant to): out[0] = table slots (2048 per slice),
  * out[1] = partition-path aggregations, out[2] = hash bits (log2 slices) of the last one,
  * out[3] = records that went through the sort path (small stagings, retries, skew fallbacks),
- * out[4] = partition-path aggregations of packed digit-key records.  `out` holds 5 values. */
+ * out[4] = partition-path aggregations of packed digit-key records, out[5] = batches grouped by
+ * the few-groups kernel (dq_freq_small_kernel), out[6] = 1 if a wait for another lane's slot
+ * publish ever timed out (an error every API call also reports).  `out` holds 7 values. */
 dq_status dq_diag_freq_paths(dq_freq* f, int64_t* out);
 
 /* Host build of the library's java.lang.Double.parseDouble (the parser dq_cast_utf8 and the

@@ -23,6 +23,8 @@
  */
 #include <math.h>
 #include <pthread.h>
+
+#define DQO_MAX_THREADS 1024 /* threads of the timed baseline (the GPU box host has 256 CPUs) */
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -293,9 +295,9 @@ double dqo_time_c2_hll_for(int64_t rows, int threads, dqo_colstate* out8, uint8_
   }
   /* untimed generation, in byte-aligned slices so threads never share a bitmap byte */
   {
-    const int ng = threads < 1 ? 1 : (threads > 64 ? 64 : threads);
-    pthread_t th[64];
-    gen_job jobs[64];
+    const int ng = threads < 1 ? 1 : (threads > DQO_MAX_THREADS ? DQO_MAX_THREADS : threads);
+    pthread_t th[DQO_MAX_THREADS];
+    gen_job jobs[DQO_MAX_THREADS];
     for (int t = 0; t < ng; ++t) {
       const int64_t b = (rows * t / ng) & ~7ll;
       const int64_t e = t == ng - 1 ? rows : ((rows * (t + 1) / ng) & ~7ll);
@@ -312,8 +314,8 @@ double dqo_time_c2_hll_for(int64_t rows, int threads, dqo_colstate* out8, uint8_
   dqo_scan(rows, 8, types, (const void* const*)values, (const uint8_t* const*)validity, pred_op,
            as_f64, lit_i, lit_f, threads, out8);
   if (regs8x512) {
-    const int ng = threads < 1 ? 1 : (threads > 64 ? 64 : threads);
-    pthread_t th[64];
+    const int ng = threads < 1 ? 1 : (threads > DQO_MAX_THREADS ? DQO_MAX_THREADS : threads);
+    pthread_t th[DQO_MAX_THREADS];
     hll_job* jobs = (hll_job*)calloc((size_t)ng, sizeof(hll_job));
     if (!jobs) return -1.0;
     for (int t = 0; t < ng; ++t) {

@@ -1,6 +1,7 @@
 """Host stand-in for deequ_amd.frequencies.FrequencyTable, used ONLY by the CPU (gloo) tests of
-the multi-rank exchange orchestration (deequ_amd/distributed.py): same methods, same 32-B wire
-format, groups kept in a dict.  The GPU tests run the same orchestration on the real table."""
+the multi-rank exchange orchestration (deequ_amd/distributed.py): same methods, same wire layout
+(per part: 16-B packed records for keys that pack into one word, then 32-B general records),
+groups kept in a dict.  The GPU tests run the same orchestration on the real table."""
 import struct
 from typing import Dict, List, Tuple
 
@@ -12,8 +13,36 @@ from deequ_amd.frequencies import encode_key
 HEAP = 1 << 30
 
 
+PACK_NULL = 0xA
+
+
+def pack(key: bytes):
+    """dq_keypack.h: a digit string of <= 15 bytes (nibble i = digit i, length in the top nibble),
+    Histogram's "NullValue" as PACK_NULL; None for any other key."""
+    if key == b"NullValue":
+        return PACK_NULL
+    if len(key) > 15 or not all(0x30 <= c <= 0x39 for c in key):
+        return None
+    p = len(key) << 60
+    for i, c in enumerate(key):
+        p |= (c - 0x30) << (4 * i)
+    return p
+
+
+def unpack(p: int) -> bytes:
+    if p == PACK_NULL:
+        return b"NullValue"
+    n = p >> 60
+    return bytes(0x30 + ((p >> (4 * i)) & 0xF) for i in range(n))
+
+
 class FakeFrequencyTable:
+    WIRE_PACKED_BYTES = 16
     WIRE_BYTES = 32
+
+    @classmethod
+    def part_bytes(cls, packed, general):
+        return cls.WIRE_PACKED_BYTES * int(packed) + cls.WIRE_BYTES * int(general)
 
     def __init__(self, key_columns, schema, histogram=False, device=None):
         self.key_columns = list(key_columns)
@@ -57,17 +86,23 @@ class FakeFrequencyTable:
             parts[self._owner(k, n)].append(k)
         return parts
 
-    def partition_sizes(self, n) -> Tuple[List[int], List[int]]:
+    def partition_sizes(self, n) -> Tuple[List[int], List[int], List[int]]:
         parts = self._parts(n)
-        return [len(p) for p in parts], [sum((len(k) + 7) // 8 * 8 for k in p if len(k) > 16) for p in parts]
+        packed = [sum(1 for k in p if pack(k) is not None) for p in parts]
+        general = [len(p) - c for p, c in zip(parts, packed)]
+        kb = [sum((len(k) + 7) // 8 * 8 for k in p if len(k) > 16 and pack(k) is None) for p in parts]
+        return packed, general, kb
 
     def partition_into(self, n, groups, keys):
         g = groups.numpy()
         kb = keys.numpy()
-        gi, ko = 0, 0
+        go, ko = 0, 0
         for p in self._parts(n):
             base = ko
-            for k in p:
+            for k in [k for k in p if pack(k) is not None]:
+                g[go:go + 16] = np.frombuffer(struct.pack("<Qq", pack(k), self.groups[k]), dtype=np.uint8)
+                go += 16
+            for k in [k for k in p if pack(k) is None]:
                 if len(k) <= 16:
                     pad = k + b"\0" * (16 - len(k))
                     rec = struct.pack("<Qq", len(k), self.groups[k]) + pad
@@ -76,14 +111,30 @@ class FakeFrequencyTable:
                     kb[ko:ko + len(k)] = np.frombuffer(k, dtype=np.uint8)
                     ko += (len(k) + 7) // 8 * 8
                     rec = struct.pack("<QqQQ", HEAP | len(k), self.groups[k], off, 0)
-                g[gi * 32:(gi + 1) * 32] = np.frombuffer(rec, dtype=np.uint8)
-                gi += 1
+                g[go:go + 32] = np.frombuffer(rec, dtype=np.uint8)
+                go += 32
         return self.partition_sizes(n)
 
-    def import_wire(self, groups, n, keys, key_bytes, num_rows=0):
-        g = bytes(groups.numpy()[:n * 32])
-        kb = bytes(keys.numpy()[:key_bytes])
+    def import_parts(self, parts, packed, general, keys, key_bytes, num_rows=0):
+        g = bytes(parts.numpy())
+        kb = bytes(keys.numpy())
         self.num_rows += num_rows
+        go, ko = 0, 0
+        for np_, ng, nk in zip(packed, general, key_bytes):
+            for i in range(np_):
+                p, cnt = struct.unpack_from("<Qq", g, go + 16 * i)
+                k = unpack(p)
+                self.groups[k] = self.groups.get(k, 0) + cnt
+            go += 16 * np_
+            self._import_general(g[go:go + 32 * ng], ng, kb[ko:ko + nk])
+            go += 32 * ng
+            ko += nk
+
+    def import_wire(self, groups, n, keys, key_bytes, num_rows=0):
+        self.num_rows += num_rows
+        self._import_general(bytes(groups.numpy()[:n * 32]), n, bytes(keys.numpy()[:key_bytes]))
+
+    def _import_general(self, g, n, kb):
         for i in range(n):
             ctrl, cnt, k0, k1 = struct.unpack_from("<QqQQ", g, i * 32)
             ln = ctrl & ((1 << 24) - 1)

@@ -1,7 +1,7 @@
 """Multi-rank frequency family (deequ_amd/distributed.py) on CPU with gloo, world sizes 2 and 3.
 
 Each rank groups its own row shard, the ranks exchange their groups by owner with one
-all-to-all (32-B wire groups + long-key bytes), and the metrics come from the all-reduced
+all-to-all (16-B packed wire groups for digit keys, 32-B for others, + long-key bytes), and the metrics come from the all-reduced
 count-of-counts histogram.  The GPU table is replaced by tests/fake_freq.py (same methods and
 wire format) because these CPU tests run no GPU compute; tests/test_gpu_distributed.py runs the
 same orchestration on the real dq_freq tables.  Expected values: the oracle over the whole table.
@@ -31,6 +31,8 @@ def _keys(lo, hi):
             out.append(None)
         elif i % 5 == 0:
             out.append("a-rather-long-grouping-key-%03d" % (i % 17))  # > 16 B: key-byte path
+        elif i % 3 == 0:
+            out.append("%d" % ((i * 104729) % 997))  # digit keys: 16-B packed wire records
         else:
             out.append("k%d" % ((i * 7919) % 611))
     return out

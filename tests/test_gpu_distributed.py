@@ -1,7 +1,7 @@
 """The multi-rank frequency exchange on the real GPU tables: 2 ranks (gloo for the host-side
 collectives, both ranks on cuda:0 -- the one-GPU box cannot run RCCL between two ranks on one
 device), each grouping its own shard with dq_freq, partitioning it with dq_freq_partition and
-merging the received parts with dq_freq_import_wire.  Bit-exact against the oracle over the
+merging the received parts with dq_freq_import_parts (digit keys travel as 16-B packed records).  Bit-exact against the oracle over the
 whole table (frequencies, #groups, #unique, top-N); entropy within 1e-12 relative."""
 import os
 import socket
@@ -26,7 +26,8 @@ def _free_port():
 def _spec(lo, hi):
     rng = np.random.default_rng(5)
     a = rng.integers(0, 9000, N)
-    keys = [None if i % 17 == 0 else ("long-key-%020d" % a[i] if i % 3 == 0 else "k%d" % a[i])
+    keys = [None if i % 17 == 0 else ("long-key-%020d" % a[i] if i % 3 == 0 else
+                                      ("%d" % a[i] if i % 3 == 1 else "k%d" % a[i]))
             for i in range(N)]
     ints = [None if i % 11 == 0 else int(a[i] % 500) for i in range(N)]
     return keys[lo:hi], ints[lo:hi]

@@ -1,7 +1,8 @@
 """The group-by's table hash on the device (dq_diag_table_hash) against a host restatement.
 Every path (stage, splits, aggregations, inserts, imports, lookups, rehash, owner ranks) places
 a key with this one function, so it must be a pure function of the key bytes -- a packed digit
-record (deequ_amd/csrc/dq_keypack.h) hashes to the same value as the key it packs."""
+record (deequ_amd/csrc/dq_keypack.h) hashes to the same value as the key it packs: a key
+that packs (digits, or "NullValue") is hashed as its packed word, any other with hash_raw."""
 import ctypes
 import random
 
@@ -23,6 +24,15 @@ def hash_raw(k0, k1, n):
     return h ^ (h >> 32)
 
 
+def hash_packed(p):
+    x = (p + 0x9E3779B97F4A7C15) & M
+    x ^= x >> 32
+    x = (x * 0xD6E8FEB86659FD93) & M
+    x ^= x >> 32
+    x = (x * 0xD6E8FEB86659FD93) & M
+    return x ^ (x >> 32)
+
+
 def pack(key: bytes):
     if len(key) <= 15 and all(0x30 <= c <= 0x39 for c in key):
         p = len(key) << 60
@@ -36,8 +46,8 @@ def expect(key: bytes):
     k = key.ljust(16, b"\0")
     k0, k1 = int.from_bytes(k[:8], "little"), int.from_bytes(k[8:], "little")
     p = pack(key)
-    h = hash_raw(k0, k1, len(key))
     rec = p if p is not None else (0xA if key == b"NullValue" else M)
+    h = hash_packed(rec) if rec != M else hash_raw(k0, k1, len(key))
     return k0, k1, h, rec
 
 
