@@ -61,6 +61,9 @@ def parse_args():
     p.add_argument("--c4-rows", type=int, default=1_000_000_000, help="rows per GPU")
     p.add_argument("--c4-batch", type=int, default=125_000_000, help="rows per string batch")
     p.add_argument("--c4-distinct", type=int, default=201_500_000)
+    p.add_argument("--c4-keys", default="digits", choices=["digits", "alnum"],
+                   help="C4 key text: 12 decimal digits (packs into one word: 8-byte records) or 'k' + 11 "
+                        "digits (not a digit string: the 16-byte record path, after the packed staging gives up)")
     p.add_argument("--c4-verify", action="store_true",
                    help="after timing, check the C4 metrics against torch.unique over the integer ids on the "
                         "device (an independent sort-based group-by; 1 rank); adds `verify` to the line")
@@ -366,9 +369,10 @@ def c4_verify(args, metrics, dist_metric, analyzers):
     return out
 
 
-def make_c4_batches(rows: int, batch: int, distinct: int, rank: int, device: int):
+def make_c4_batches(rows: int, batch: int, distinct: int, rank: int, device: int, alnum: bool = False):
     """C4: a string key = 12-digit zero-padded decimal of a uniform int in [0, distinct), 1% NULL,
-    as Arrow utf8 batches of `batch` rows (int32 offsets cap one batch at 2 GiB of chars)."""
+    as Arrow utf8 batches of `batch` rows (int32 offsets cap one batch at 2 GiB of chars).
+    alnum: the first digit replaced by 'k' (same groups, keys that are not digit strings)."""
     import torch
     import deequ_amd as d
     dev = torch.device("cuda", device)
@@ -385,6 +389,8 @@ def make_c4_batches(rows: int, batch: int, distinct: int, rank: int, device: int
             e = min(m, s + sub)
             keys = torch.randint(0, distinct, (e - s,), generator=gen, device=dev, dtype=torch.int64)
             digits = (keys[:, None] // pow10[None, :]) % 10 + 48
+            if alnum:
+                digits[:, 0] = ord("k")
             chars[s * 12: e * 12] = digits.to(torch.uint8).reshape(-1)
             packed = _valid_bits(e - s, gen, dev, 0.01)
             valid[s // 8: s // 8 + packed.numel()] = packed
@@ -557,7 +563,7 @@ def run_c4(args, world, rank, local):
     GPUs every rank groups its own shard and the tables meet in the key-hash all-to-all."""
     import deequ_amd as d
     from deequ_amd.distributed import ShardedTable
-    shard = make_c4_batches(args.c4_rows, args.c4_batch, args.c4_distinct, rank, local)
+    shard = make_c4_batches(args.c4_rows, args.c4_batch, args.c4_distinct, rank, local, args.c4_keys == "alnum")
     data = ShardedTable(shard) if world > 1 else shard
     analyzers = [d.Uniqueness(["key"]), d.Distinctness(["key"]), d.Entropy("key"),
                  d.CountDistinct(["key"]), d.Histogram("key")]
@@ -568,7 +574,7 @@ def run_c4(args, world, rank, local):
     metrics = {str(a): ctx.metric(a).value.get() for a in analyzers[:4]}
     hist = ctx.metric(analyzers[4]).value.get()
     verify = None
-    if args.c4_verify and world == 1:
+    if args.c4_verify and world == 1 and args.c4_keys == "digits":
         del ctx
         verify = c4_verify(args, {a: metrics[str(a)] for a in analyzers[:4]}, hist, analyzers)
     in_bytes = sum(_column_bytes(b.columns["key"]) for b in shard.batches())
@@ -582,7 +588,8 @@ def run_c4(args, world, rank, local):
         "unit": "rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "utf8 keys, int64 counts",
-        "data": "synthetic 12-digit keys uniform in [0, %d), 1%% NULL, generated in HBM" % args.c4_distinct,
+        "data": "synthetic %s keys uniform in [0, %d), 1%% NULL, generated in HBM"
+                % ("12-digit" if args.c4_keys == "digits" else "'k' + 11-digit", args.c4_distinct),
         "config": {"workload": "C4: %d rows/GPU in %d-row utf8 batches; Uniqueness, Distinctness, Entropy, "
                                "CountDistinct + Histogram, all from one GPU group-by of the key (the "
                                "reference runs Histogram as a second job)%s"

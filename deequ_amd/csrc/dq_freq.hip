@@ -1185,7 +1185,8 @@ struct NoMid {
 };
 // mid(): called once the tile's room is reserved, before its records are written (the fused
 // stage issues the next tile's offset loads there, so they arrive during the writes).
-template <int PER, int MAXB, typename R, uint32_t SUBN, bool PROF = false, int WOUT_UNROLL = 16, typename Mid = NoMid>
+template <int PER, int MAXB, typename R, uint32_t SUBN, bool PROF = false, int WOUT_UNROLL = 0, typename Mid = NoMid,
+          bool REC_LDS = false>
 __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER], uint32_t (&bin)[PER],
                                  uint32_t nb, uint64_t base_id, R* __restrict__ out, uint64_t out_cap,
                                  unsigned long long* out_fill, FreqRec* ovf, unsigned long long* ovf_n,
@@ -1243,6 +1244,15 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
   __syncthreads();
   DQ_PROF_MARK(PROF, 5);
   mid();
+  // REC_LDS: the caller left the records in L.rec in row order (record i of thread t at
+  // i * kPartThreads + t; registers are short while the keys load): read back, then sorted
+  R rl[PER];
+  if constexpr (REC_LDS) {
+    static_assert(SUB >= (uint32_t)PER * (uint32_t)kPartThreads, "a tile's records in one image");
+#pragma unroll
+    for (int i = 0; i < PER; ++i) rl[i] = L.rec[i * kPartThreads + t];
+    __syncthreads();
+  }
   for (uint32_t r0 = 0; r0 < total; r0 += SUB) {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -1250,16 +1260,14 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
       const uint32_t b = bin[i] & 0xFFFFu;
       const uint32_t p = L.start[b] + (bin[i] >> 16) - r0;
       if (p < SUB) {
-        L.rec[p] = rec[i];
+        L.rec[p] = REC_LDS ? rl[i] : rec[i];
         L.bin[p] = (uint16_t)b;
       }
     }
     __syncthreads();
     DQ_PROF_MARK(PROF, 6);
     const uint32_t m = min(SUB, total - r0);
-    // (a bounded unroll: the fused stage holds the next tile's offsets across this loop)
-#pragma unroll WOUT_UNROLL
-    for (uint32_t j = t; j < m; j += kPartThreads) {
+    auto put = [&](uint32_t j) {
       const uint32_t b = L.bin[j];
       const uint64_t o = L.gbase[b] + (r0 + j - L.start[b]);
       const R r = L.rec[j];
@@ -1272,9 +1280,19 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
         if (k < ovf_cap) ovf[k] = rec_raw(r);
         else atomicOr(flag, 1u);
       }
+    };
+    if constexpr (WOUT_UNROLL > 0) {
+      // (a bounded unroll: the fused stage holds the next tile's offsets across this loop)
+#pragma unroll WOUT_UNROLL
+      for (uint32_t j = t; j < m; j += kPartThreads) put(j);
+    } else {  // the compiler's choice (the level-2 passes: no loop-carried state to keep)
+      for (uint32_t j = t; j < m; j += kPartThreads) put(j);
     }
     __syncthreads();
     DQ_PROF_MARK(PROF, 7);
+    // an image that holds a whole tile: one round, so rec[] is dead once it is in LDS (the
+    // registers go to the caller's loads issued in mid())
+    if constexpr (SUB >= (uint32_t)PER * (uint32_t)kPartThreads) break;
   }
 }
 
@@ -1522,6 +1540,29 @@ __device__ __forceinline__ void stage_offsets(const DevColumn& c0, int64_t n_row
   const int64_t left = n_rows - r0;
   const uint32_t m = (uint32_t)(left < (int64_t)kStageTile ? left : (int64_t)kStageTile);
   const uint32_t t = threadIdx.x;
+  // (the validity dword first: its address arithmetic waits on nothing then)
+  const uint8_t* validity = uniform_ptr(c0.validity);
+  if (validity != nullptr) {
+    const uint32_t l = t & 63u, w = t >> 6;
+    const uint8_t* vb = validity + (r0 >> 3);
+    const uint32_t nbytes = (m + 7u) >> 3;
+    // a 4-byte aligned bitmap (the usual case): the range covers the bitmap's last dword whole (it
+    // lies in the page of the bitmap's last byte; the bits past the batch are never used)
+    const bool al = ((uintptr_t)vb & 3u) == 0u;
+    const __amdgpu_buffer_rsrc_t rs_v = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(vb), 0, (int)(al ? (nbytes + 3u) & ~3u : nbytes), 0x00020000);
+    const uint32_t dw = 16u * (l >> 1) + 2u * w + (l & 1u);
+    vword = 0u;
+    if (l < 2u * kStagePer) {
+      if (al || 4u * dw + 4u <= nbytes) {
+        vword = __builtin_amdgcn_raw_buffer_load_b32(rs_v, (int)(4u * dw), 0, 0);
+      } else {  // an unaligned bitmap's last, partial dword: byte by byte (a range check is per dword)
+        for (uint32_t k = 0; k < 4u; ++k)
+          if (4u * dw + k < nbytes)
+            vword |= (uint32_t)(uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rs_v, (int)(4u * dw + k), 0, 0) << (8u * k);
+      }
+    }
+  }
   const __amdgpu_buffer_rsrc_t rs_off = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<int32_t*>(uniform_ptr(c0.offsets) + r0), 0, (int)(4u * (m + 1u)), 0x00020000);
 #pragma unroll
@@ -1530,48 +1571,28 @@ __device__ __forceinline__ void stage_offsets(const DevColumn& c0, int64_t n_row
     pob[j] = v[0];
     poe[j] = v[1];
   }
-  const uint8_t* validity = uniform_ptr(c0.validity);
-  if (validity != nullptr) {
-    const uint32_t l = t & 63u, w = t >> 6;
-    const __amdgpu_buffer_rsrc_t rs_v = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(validity + (r0 >> 3)), 0, (int)((m + 7u) >> 3), 0x00020000);
-    const uint32_t dw = 16u * (l >> 1) + 2u * w + (l & 1u);
-    const uint32_t nbytes = (m + 7u) >> 3;
-    vword = 0u;
-    if (l < 2u * kStagePer) {
-      if (4u * dw + 4u <= nbytes) {
-        vword = __builtin_amdgcn_raw_buffer_load_b32(rs_v, (int)(4u * dw), 0, 0);
-      } else {  // the bitmap's last, partial dword: byte by byte (a range check is per dword)
-        for (uint32_t k = 0; k < 4u; ++k)
-          if (4u * dw + k < nbytes)
-            vword |= (uint32_t)(uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rs_v, (int)(4u * dw + k), 0, 0) << (8u * k);
-      }
-    }
-  }
 }
 
-// The 16 bytes from a key's first byte (one unaligned buffer load), or -- for a key that ends
-// within 16 bytes of the heap's end -- its bytes from the aligned words that hold them.
-template <int N>
-__device__ __forceinline__ void stage_key_load(__amdgpu_buffer_rsrc_t rs_vals, const uint8_t* vals, uint32_t heap_end,
-                                               uint32_t ob, const uint32_t (&lens)[N], int j, uint32_t (&w)[4]) {
-  if (ob + 16u <= heap_end) {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_vals, (int)ob, 0, 0);
-    w[0] = v[0];
-    w[1] = v[1];
-    w[2] = v[2];
-    w[3] = v[3];
-  } else {
-    uint32_t n = (lens[j / 4] >> (8 * (j % 4))) & 0xFFu;
-    n = n > 16u ? 0u : n;  // (NULL / too long: no key bytes are used)
-    n = ob + n <= heap_end ? n : 0u;
-    const uint64_t lo = ld_partial(vals + ob, n < 8u ? n : 8u);
-    const uint64_t hi = n > 8u ? ld_partial(vals + ob + 8, n - 8u) : 0ull;
-    w[0] = (uint32_t)lo;
-    w[1] = (uint32_t)(lo >> 32);
-    w[2] = (uint32_t)hi;
-    w[3] = (uint32_t)(hi >> 32);
-  }
+// The 16 bytes from a key's first byte: one unaligned buffer load through a descriptor whose base
+// is the heap's 4-byte aligned start and whose range ends at the 4-byte boundary after the heap's
+// last byte (stage_heap_rsrc), so a key that ends within the heap's last dword is read whole (the
+// bytes past the key are masked off by its length; words wholly past the range read 0).
+__device__ __forceinline__ void stage_key_load(__amdgpu_buffer_rsrc_t rs_vals, uint32_t mis, uint32_t ob, uint32_t (&w)[4]) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_vals, (int)(ob + mis), 0, 0);
+  w[0] = v[0];
+  w[1] = v[1];
+  w[2] = v[2];
+  w[3] = v[3];
+}
+
+// The key heap's descriptor for stage_key_load: base rounded down to 4 bytes (mis = the bytes
+// skipped), range rounded up to 4 bytes (the dword holding the heap's last byte is in that byte's
+// page, so reading it whole cannot fault).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t stage_heap_rsrc(const void* values, uint32_t heap_end, uint32_t& mis) {
+  const uintptr_t a = (uintptr_t)values;
+  mis = (uint32_t)(a & 3u);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(a & ~(uintptr_t)3), 0,
+                                           (int)((heap_end + mis + 3u) & ~3u), 0x00020000);
 }
 
 // The validity of row j of every lane of this wave, as a lane mask (from stage_offsets' vword).
@@ -1586,7 +1607,7 @@ __device__ __forceinline__ uint64_t stage_valid_mask(uint32_t vword, int j) {
 #ifndef DQ_STAGE_LOAD_B
 #define DQ_STAGE_LOAD_B 0
 #endif
-constexpr int kStageLoadA = DQ_STAGE_LOAD_A;  // key loads issued before the first row is processed
+constexpr int kStageLoadA = DQ_STAGE_LOAD_A < DQ_STAGE_PER ? DQ_STAGE_LOAD_A : DQ_STAGE_PER;  // key loads issued before the first row is processed
 constexpr int kStageLoadB = DQ_STAGE_LOAD_B;  // the rest after this many rows
 #ifndef DQ_STAGE_WOUT_UNROLL
 #define DQ_STAGE_WOUT_UNROLL 2
@@ -1616,10 +1637,9 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(PA
   // its heap is < 2 GiB); each tile's offsets through a descriptor of that tile's offsets (bounded,
   // so rows past the batch read 0), as (begin, end) pairs: one 8-byte load per row.
   const uint32_t heap_end = ONE_STRING ? __builtin_amdgcn_readfirstlane((uint32_t)uniform_ptr(c0.offsets)[n_rows]) : 0u;
-  const __amdgpu_buffer_rsrc_t rs_vals =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(uniform_ptr(c0.values)), 0, (int)heap_end, 0x00020000);
+  uint32_t mis = 0u;
+  const __amdgpu_buffer_rsrc_t rs_vals = stage_heap_rsrc(uniform_ptr(c0.values), heap_end, mis);
   const bool has_validity = uniform_ptr(c0.validity) != nullptr;
-  const uint8_t* vals = static_cast<const uint8_t*>(uniform_ptr(c0.values));
   uint32_t pob[kStagePer], poe[kStagePer], vword = 0u;
   if (ONE_STRING && (int64_t)blockIdx.x < n_tiles) stage_offsets(c0, n_rows, blockIdx.x, pob, poe, vword);
   // PACK: once the overflow list has filled up (a column of keys that are not digit strings) the
@@ -1662,16 +1682,14 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(PA
       }
       // rows [0, kStageLoadA) are loaded first; the rest once row kStageLoadB - 1 is processed
       // (all twelve in flight at once would not leave registers for four waves per SIMD)
-      // (the keys that end within 16 bytes of the heap's end are read word by word instead: a
-      // buffer range check is per dword, and a wider read could leave the allocation)
       uint32_t kw[kStagePer][4];
 #pragma unroll
-      for (int j = 0; j < kStageLoadA; ++j) stage_key_load(rs_vals, vals, heap_end, pob[j], lens, j, kw[j]);
+      for (int j = 0; j < kStageLoadA; ++j) stage_key_load(rs_vals, mis, pob[j], kw[j]);
 #pragma unroll
       for (int j = 0; j < kStagePer; ++j) {
         if (j == kStageLoadB) {
 #pragma unroll
-          for (int q = kStageLoadA; q < kStagePer; ++q) stage_key_load(rs_vals, vals, heap_end, pob[q], lens, q, kw[q]);
+          for (int q = kStageLoadA; q < kStagePer; ++q) stage_key_load(rs_vals, mis, pob[q], kw[q]);
         }
         bin[j] = kPartNoBin;
         if (!((sel >> j) & 1u)) continue;
@@ -1694,7 +1712,7 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(PA
         if constexpr (PACK) {
           uint64_t p;
           if (kp_pack_record(k0, k1, n, &p)) {
-            rec[j] = p;
+            L.rec[j * kPartThreads + t] = p;  // (row order; part_tile sorts it)
             h = hash_record_packed(p);
           } else {  // not a digit key: a 16-B record on the overflow list
             h = hash_raw(k0, k1, n);
@@ -1750,13 +1768,15 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(PA
     constexpr bool kProf = false;
 #endif
     const int64_t next = tile + gridDim.x;  // its offsets load while this tile's records are written
-    auto prefetch = [&]() {
-      if constexpr (ONE_STRING)
-        if (next < n_tiles) stage_offsets(c0, n_rows, next, pob, poe, vword);
+    auto prefetch = [&]() {  // (the flag first: loads complete in order, so waiting for it is not
+                             // waiting for the offsets)
       if constexpr (PACK)
         if (t == 0) abort_v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if constexpr (ONE_STRING)
+        if (next < n_tiles) stage_offsets(c0, n_rows, next, pob, poe, vword);
     };
-    part_tile<kStagePer, (1 << kStageBinBits), R, (PACK ? kStageSubP : kPartSub), kProf, DQ_STAGE_WOUT_UNROLL>(
+    part_tile<kStagePer, (1 << kStageBinBits), R, (PACK ? kStageSubP : kPartSub), kProf, DQ_STAGE_WOUT_UNROLL,
+              decltype(prefetch), PACK>(
         L, rec, bin, nb, 0, out, cap1, fill1, ovf, ovf_n, ovf_cap, flag, staged, nullptr, prof_t_, prefetch);
   }
   if (PACK && n_side) atomicAdd(staged, (unsigned long long)n_side);
@@ -1861,6 +1881,11 @@ __device__ inline bool lds_count_packed(unsigned long long* K, uint32_t* C, uint
   }
   return false;
 }
+
+#ifndef DQ_AGG_SKIP_EMPTY_KEYS
+#define DQ_AGG_SKIP_EMPTY_KEYS 0
+#endif
+constexpr bool kAggSkipEmptyKeys = DQ_AGG_SKIP_EMPTY_KEYS != 0;  // A/B: empty slots written as {ctrl, count} only
 
 #ifndef DQ_AGGP_BATCH
 #define DQ_AGGP_BATCH 4
@@ -1968,7 +1993,8 @@ __global__ __launch_bounds__(kAggPThreads) __attribute__((amdgpu_waves_per_eu(DQ
         const uint32_t c = L.C[s];
         bool is_new = false;
         if (!c) {
-          if (tr.write_all) halves[q] = ulonglong2{0ull, 0ull};
+          // (an empty slot is ctrl = 0 and count = 0; its key half is never read)
+          if (tr.write_all && (!kAggSkipEmptyKeys || !hi)) halves[q] = ulonglong2{0ull, 0ull};
         } else {
           const bool existing = !table_empty && (slice[s].ctrl & kReady);
           const uint64_t p = L.K[s];
@@ -2667,7 +2693,7 @@ template <bool PACKED>
 __global__ __launch_bounds__(kMergeThreads) void dq_import_merge_kernel(
     FreqTable T, const ImportRun* __restrict__ runs, int n_runs, const uint32_t* __restrict__ start,
     const uint32_t* __restrict__ end, uint64_t n_slices, int table_empty, AggTrack tr, uint32_t* ovf_list,
-    unsigned long long* n_ovf, unsigned long long* new_groups) {
+    unsigned long long* n_ovf, unsigned long long* ovf_recs, unsigned long long* new_groups) {
   constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
   constexpr int NT = kMergeThreads;
   __shared__ MergeLds<PACKED> L;
@@ -2707,6 +2733,7 @@ __global__ __launch_bounds__(kMergeThreads) void dq_import_merge_kernel(
       L.cmax = 0ull;
     }
     __syncthreads();
+    uint32_t mine = 0;  // this thread's records of the slice (an overflowed slice's key bound)
     for (int run = 0; run < n_runs; ++run) {
       const ImportRun R = runs[run];
       if (R.skip) continue;
@@ -2716,6 +2743,7 @@ __global__ __launch_bounds__(kMergeThreads) void dq_import_merge_kernel(
         ImpRec r;
         imp_load<PACKED>(R, i, r);
         if (!r.present || !r.lds_ok || dst_slice(r.hash, rb) != b) continue;
+        ++mine;
         if (!merge_count(L, r)) L.overflow = 1;
       }
     }
@@ -2723,6 +2751,7 @@ __global__ __launch_bounds__(kMergeThreads) void dq_import_merge_kernel(
     ulonglong2* halves = reinterpret_cast<ulonglong2*>(slice);
     if (L.overflow) {
       if (threadIdx.x == 0) ovf_list[atomicAdd(n_ovf, 1ull)] = (uint32_t)b;
+      if (mine) atomicAdd(ovf_recs, (unsigned long long)mine);
       if (tr.write_all)
         for (uint32_t q = threadIdx.x; q < 2 * S; q += NT) halves[q] = ulonglong2{0ull, 0ull};
       if (tr.smax && threadIdx.x == 0) tr.smax[b] = 0xFFFFFFFFu;
@@ -2880,18 +2909,18 @@ hipError_t launch_import_bounds(const ImportRun* d_runs, int n_runs, uint64_t ma
 hipError_t launch_import_merge(const FreqTable& T, bool packed, const ImportRun* d_runs, int n_runs, const uint32_t* d_start,
                                const uint32_t* d_end, int table_empty, unsigned long long* d_hist, unsigned long long* d_big,
                                unsigned long long* d_n_big, unsigned long long big_cap, uint32_t* d_smax, int write_all,
-                               uint32_t* d_ovf_list, unsigned long long* d_n_ovf, unsigned long long* d_new_groups,
-                               hipStream_t stream) {
+                               uint32_t* d_ovf_list, unsigned long long* d_n_ovf, unsigned long long* d_ovf_recs,
+                               unsigned long long* d_new_groups, hipStream_t stream) {
   const uint64_t n_slices = (T.mask + 1) >> kFreqSliceLog;
   if (!table_empty && (d_hist || d_smax || write_all)) return hipErrorInvalidValue;
   AggTrack tr{d_hist, d_big, d_n_big, big_cap, d_smax, write_all};
   const unsigned blocks = grid_for(n_slices, 1, 65536);
   if (packed)
     hipLaunchKernelGGL(dq_import_merge_kernel<true>, dim3(blocks), dim3(kMergeThreads), 0, stream, T, d_runs, n_runs, d_start,
-                       d_end, n_slices, table_empty, tr, d_ovf_list, d_n_ovf, d_new_groups);
+                       d_end, n_slices, table_empty, tr, d_ovf_list, d_n_ovf, d_ovf_recs, d_new_groups);
   else
     hipLaunchKernelGGL(dq_import_merge_kernel<false>, dim3(blocks), dim3(kMergeThreads), 0, stream, T, d_runs, n_runs, d_start,
-                       d_end, n_slices, table_empty, tr, d_ovf_list, d_n_ovf, d_new_groups);
+                       d_end, n_slices, table_empty, tr, d_ovf_list, d_n_ovf, d_ovf_recs, d_new_groups);
   return hipGetLastError();
 }
 
@@ -2978,9 +3007,8 @@ __global__ __launch_bounds__(kSmallThreads) void dq_freq_small_kernel(FreqKeySpe
   if constexpr (STRING) {
     const int32_t* offs = uniform_ptr(c0.offsets);
     const uint32_t heap_end = __builtin_amdgcn_readfirstlane((uint32_t)offs[n_rows]);
-    const uint8_t* vals = static_cast<const uint8_t*>(uniform_ptr(c0.values));
-    const __amdgpu_buffer_rsrc_t rs_vals =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vals), 0, (int)heap_end, 0x00020000);
+    uint32_t mis = 0u;
+    const __amdgpu_buffer_rsrc_t rs_vals = stage_heap_rsrc(uniform_ptr(c0.values), heap_end, mis);
     uint32_t ob[kSmallPer], oe[kSmallPer];
     auto load_offs = [&](int64_t base) {
       const int64_t left = r1 - base;
@@ -3007,7 +3035,7 @@ __global__ __launch_bounds__(kSmallThreads) void dq_freq_small_kernel(FreqKeySpe
         const bool valid = validity == nullptr || (row < r1 && ((validity[row >> 3] >> (row & 7)) & 1u));
         if (row < r1 && (valid || null_key)) sel |= 1u << j;
         if (row < r1 && !valid) nul |= 1u << j;
-        stage_key_load(rs_vals, vals, heap_end, ob[j], lens, j, kw[j]);
+        stage_key_load(rs_vals, mis, ob[j], kw[j]);
       }
       if (base + step < r1) load_offs(base + step);
 #pragma unroll

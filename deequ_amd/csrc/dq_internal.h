@@ -247,8 +247,8 @@ hipError_t launch_import_bounds(const ImportRun* d_runs, int n_runs, uint64_t ma
 hipError_t launch_import_merge(const FreqTable& T, bool packed, const ImportRun* d_runs, int n_runs, const uint32_t* d_start,
                                const uint32_t* d_end, int table_empty, unsigned long long* d_hist, unsigned long long* d_big,
                                unsigned long long* d_n_big, unsigned long long big_cap, uint32_t* d_smax, int write_all,
-                               uint32_t* d_ovf_list, unsigned long long* d_n_ovf, unsigned long long* d_new_groups,
-                               hipStream_t stream);
+                               uint32_t* d_ovf_list, unsigned long long* d_n_ovf, unsigned long long* d_ovf_recs,
+                               unsigned long long* d_new_groups, hipStream_t stream);
 hipError_t launch_import_global(const FreqTable& T, const ImportRun* d_runs, int n_runs, uint64_t max_n, int mode, int rb_old,
                                 const uint32_t* d_start, const uint32_t* d_end, uint64_t n_slices_old,
                                 const uint32_t* d_ovf_list, uint64_t n_ovf, hipStream_t stream);

@@ -229,15 +229,24 @@ __global__ __launch_bounds__(kBlock) void dq_datatype_kernel(const HllTask* __re
 #ifndef DQ_STR_U
 #define DQ_STR_U 4
 #endif
-// Little-endian p[0..n) (n <= 8), zero padded, from the aligned words that hold those bytes only.
-__device__ inline uint64_t ld_bytes(const uint8_t* p, uint32_t n) {
-  if (n == 0) return 0;
-  const uintptr_t a = (uintptr_t)p;
-  const uint64_t* w = reinterpret_cast<const uint64_t*>(a & ~(uintptr_t)7);
-  const uint32_t sh = (uint32_t)(a & 7) * 8u;
-  uint64_t v = w[0] >> sh;
-  if (sh && (a & 7) + n > 8) v |= w[1] << (64u - sh);
-  return n >= 8 ? v : (v & ((1ull << (8u * n)) - 1ull));
+// A string heap's descriptor: base rounded down to 4 bytes (mis = the bytes skipped), range
+// rounded up to the 4-byte boundary after the heap's last byte (that dword lies in the last
+// byte's page, so reading it whole cannot fault; a buffer range check is per dword).
+__device__ inline __amdgpu_buffer_rsrc_t heap_rsrc(const uint8_t* vals, uint32_t heap_end, uint32_t& mis) {
+  const uintptr_t a = (uintptr_t)vals;
+  mis = (uint32_t)(a & 3u);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(a & ~(uintptr_t)3), 0, (int)((heap_end + mis + 3u) & ~3u),
+                                           0x00020000);
+}
+
+// 24 bytes from byte offset a of heap_rsrc's range (unaligned 16- and 8-byte loads; words past the
+// range read 0; the bytes past a string's end are not used by its consumers).
+__device__ __forceinline__ void load24(__amdgpu_buffer_rsrc_t rs, uint32_t a, uint64_t (&w)[3]) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)a, 0, 0);
+  const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(a + 16u), 0, 0);
+  w[0] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+  w[1] = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
+  w[2] = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
 }
 
 // DT = false: the HLL alone (an ApproxCountDistinct without a DataType on the column), through
@@ -260,10 +269,10 @@ __global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* _
   const uint8_t* wt = task.where_mask >= 0 ? reinterpret_cast<const uint8_t*>(masks[task.where_mask].t) : nullptr;
   const uint8_t* vals = static_cast<const uint8_t*>(col.values);
   // the first 24 bytes of each string as three words, read unaligned from its first byte (one
-  // 16-byte and one 8-byte buffer load); a string within 24 bytes of the heap's end reads the
-  // aligned words that hold its bytes instead (a buffer range check is per dword)
-  const uint32_t heap_end = (uint32_t)col.offsets[n_rows];
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vals), 0, (int)heap_end, 0x00020000);
+  // 16-byte and one 8-byte buffer load, unconditional) through heap_rsrc's descriptor: a string
+  // that ends in the heap's last dword reads it whole, words past the heap read 0
+  uint32_t mis;
+  const __amdgpu_buffer_rsrc_t rs = heap_rsrc(vals, (uint32_t)col.offsets[n_rows], mis);
   uint64_t c[5] = {0, 0, 0, 0, 0};
   constexpr int U = DQ_STR_U;
   for (int64_t base = r0 + threadIdx.x; base < r1; base += U * kBlock) {
@@ -280,20 +289,7 @@ __global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* _
       sel[u] = (in && (col.validity == nullptr || bit_at(col.validity, rr)) && (wt == nullptr || bit_at(wt, rr))) ? 1u : 0u;
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t a = (uint32_t)ob[u];
-      if (a + 24u <= heap_end) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)a, 0, 0);
-        const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(a + 16u), 0, 0);
-        w[u][0] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
-        w[u][1] = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
-        w[u][2] = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
-      } else {
-        const uint32_t m = heap_end - a < 24u ? heap_end - a : 24u;  // bytes of the heap from a
-#pragma unroll
-        for (int k = 0; k < 3; ++k) w[u][k] = m > 8u * k ? ld_bytes(vals + a + 8u * k, min(8u, m - 8u * k)) : 0ull;
-      }
-    }
+    for (int u = 0; u < U; ++u) load24(rs, (uint32_t)ob[u] + mis, w[u]);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t row = base + (int64_t)u * kBlock;
@@ -403,31 +399,55 @@ __device__ inline bool cast_one(const Src& p, int32_t n, int64_t* lv, double* dv
 template <int TO>
 __global__ __launch_bounds__(kBlock) void dq_cast_utf8_kernel(DevColumn src, int64_t n_rows, void* values,
                                                               uint8_t* validity) {
+  // U rows per lane per step, every load of the step issued before any parse: each row's offset
+  // pair (one 8-byte load), its validity byte, and the first 24 bytes of the string read unaligned
+  // from its first byte (a 16- and an 8-byte buffer load; within 24 bytes of the heap's end, the
+  // aligned words that hold its bytes).  Longer strings take the byte-pointer parser.
   constexpr int to_type = TO;
+  constexpr int U = 4;
   const uint32_t lane = threadIdx.x & 63u;
-  for (int64_t base = (int64_t)blockIdx.x * kBlock; base < n_rows; base += (int64_t)gridDim.x * kBlock) {
-    const int64_t row = base + threadIdx.x;
-    int64_t lv = 0;
-    double dv = 0.0;
-    bool ok = false;
-    if (row < n_rows && (src.validity == nullptr || bit_at(src.validity, row))) {
-      const int32_t b = src.offsets[row], e = src.offsets[row + 1];
-      const uint8_t* p = static_cast<const uint8_t*>(src.values) + b;
-      if (e - b <= 24) ok = cast_one<TO>(WordSrc(p, e - b), e - b, &lv, &dv);
-      else ok = cast_one<TO>(PtrSrc{p}, e - b, &lv, &dv);
+  const uint8_t* vals = static_cast<const uint8_t*>(src.values);
+  uint32_t mis;
+  const __amdgpu_buffer_rsrc_t rs = heap_rsrc(vals, (uint32_t)src.offsets[n_rows], mis);
+  const __amdgpu_buffer_rsrc_t ro =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(src.offsets), 0, (int)(4u * (uint32_t)(n_rows + 1)), 0x00020000);
+  for (int64_t base = (int64_t)blockIdx.x * kBlock * U; base < n_rows; base += (int64_t)gridDim.x * kBlock * U) {
+    uint32_t ob[U], oe[U], sel = 0u;
+    uint64_t w[U][3];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = base + (int64_t)u * kBlock + threadIdx.x;
+      const auto o = __builtin_amdgcn_raw_buffer_load_b64(ro, (int)(4u * (uint32_t)row), 0, 0);
+      ob[u] = o[0];
+      oe[u] = o[1];
+      if (row < n_rows && (src.validity == nullptr || bit_at(src.validity, row))) sel |= 1u << u;
     }
-    if (row < n_rows) {
-      if (to_type == DQ_T_INT64) static_cast<int64_t*>(values)[row] = ok ? lv : 0;
-      else static_cast<double*>(values)[row] = ok ? dv : 0.0;
-    }
-    const uint64_t m = __ballot(ok);
-    const int64_t row0 = row - (int64_t)lane;  // first row of the wave: a multiple of 64
-    if (lane == 0 && row0 < n_rows) {
-      if (row0 + 64 <= n_rows) {
-        *reinterpret_cast<uint64_t*>(validity + (row0 >> 3)) = m;
-      } else {
-        const int64_t nb = ((n_rows - row0) + 7) >> 3;
-        for (int64_t k = 0; k < nb; ++k) validity[(row0 >> 3) + k] = (uint8_t)(m >> (8 * k));
+#pragma unroll
+    for (int u = 0; u < U; ++u) load24(rs, ob[u] + mis, w[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = base + (int64_t)u * kBlock + threadIdx.x;
+      int64_t lv = 0;
+      double dv = 0.0;
+      bool ok = false;
+      if ((sel >> u) & 1u) {
+        const int32_t n = (int32_t)(oe[u] - ob[u]);
+        if (n <= 24) ok = cast_one<TO>(WordSrc(w[u][0], w[u][1], w[u][2], 0ull, 0u), n, &lv, &dv);
+        else ok = cast_one<TO>(PtrSrc{vals + ob[u]}, n, &lv, &dv);
+      }
+      if (row < n_rows) {
+        if (to_type == DQ_T_INT64) static_cast<int64_t*>(values)[row] = ok ? lv : 0;
+        else static_cast<double*>(values)[row] = ok ? dv : 0.0;
+      }
+      const uint64_t mk = __ballot(ok);
+      const int64_t row0 = row - (int64_t)lane;  // first row of the wave: a multiple of 64
+      if (lane == 0 && row0 < n_rows) {
+        if (row0 + 64 <= n_rows) {
+          *reinterpret_cast<uint64_t*>(validity + (row0 >> 3)) = mk;
+        } else {
+          const int64_t nb = ((n_rows - row0) + 7) >> 3;
+          for (int64_t k = 0; k < nb; ++k) validity[(row0 >> 3) + k] = (uint8_t)(mk >> (8 * k));
+        }
       }
     }
   }
@@ -456,15 +476,23 @@ hipError_t launch_datatype(const HllTask* d_tasks, int n_tasks, const DevColumn*
 
 hipError_t launch_cast_utf8(const DevColumn& src, int64_t n_rows, int to_type, void* d_values, uint8_t* d_validity,
                             hipStream_t stream) {
-  if (n_rows <= 0) return hipSuccess;
-  int64_t blocks = (n_rows + kBlock - 1) / kBlock;
-  if (blocks > 8192) blocks = 8192;
-  if (to_type == DQ_T_INT64)
-    hipLaunchKernelGGL(dq_cast_utf8_kernel<DQ_T_INT64>, dim3((unsigned)blocks), dim3(kBlock), 0, stream, src, n_rows,
-                       d_values, d_validity);
-  else
-    hipLaunchKernelGGL(dq_cast_utf8_kernel<DQ_T_FLOAT64>, dim3((unsigned)blocks), dim3(kBlock), 0, stream, src, n_rows,
-                       d_values, d_validity);
+  // chunks of at most 2^28 rows: the kernel's offsets descriptor spans 4 (rows + 1) bytes
+  constexpr int64_t kChunk = (int64_t)1 << 28;
+  for (int64_t start = 0; start < n_rows; start += kChunk) {
+    const int64_t m = n_rows - start < kChunk ? n_rows - start : kChunk;
+    DevColumn c = src;
+    c.offsets = src.offsets + start;  // (offsets stay absolute into the bytes)
+    if (c.validity) c.validity = src.validity + (start >> 3);
+    uint8_t* vout = d_validity + (start >> 3);
+    int64_t blocks = (m + 4 * kBlock - 1) / (4 * kBlock);  // (4 rows per lane per step)
+    if (blocks > 8192) blocks = 8192;
+    if (to_type == DQ_T_INT64)
+      hipLaunchKernelGGL(dq_cast_utf8_kernel<DQ_T_INT64>, dim3((unsigned)blocks), dim3(kBlock), 0, stream, c, m,
+                         static_cast<void*>(static_cast<int64_t*>(d_values) + start), vout);
+    else
+      hipLaunchKernelGGL(dq_cast_utf8_kernel<DQ_T_FLOAT64>, dim3((unsigned)blocks), dim3(kBlock), 0, stream, c, m,
+                         static_cast<void*>(static_cast<double*>(d_values) + start), vout);
+  }
   return hipGetLastError();
 }
 

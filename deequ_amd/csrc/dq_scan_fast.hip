@@ -382,6 +382,16 @@ __device__ inline void fast_acc_init(FastAcc& a) {
 
 }  // namespace
 
+// Diagnostic build only (-DDQ_SCAN_DIAG): how often a workgroup re-reads its chunk -- the exact
+// int64 statistics, the moments' cancellation guard, the HLL marker re-rank -- of all workgroups
+// (printed per launch by launch_scan_fast).  The re-reads are the only reads beyond one pass.
+#ifdef DQ_SCAN_DIAG
+__device__ unsigned long long g_scan_diag[4];
+#define DQ_SCAN_COUNT(i) do { if (threadIdx.x == 0) atomicAdd(&g_scan_diag[i], 1ull); } while (0)
+#else
+#define DQ_SCAN_COUNT(i) do { } while (0)
+#endif
+
 template <typename T, int PK, bool STATS, bool HLL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DQ_FAST_WAVES))) void dq_scan_fast_kernel(const ScanTask* __restrict__ tasks,
                                                               const int32_t* __restrict__ group,
@@ -497,6 +507,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DQ_FAST_
     const double dmax = (a.fmin <= a.fmax) ? fmax(fabs(a.fmin), fabs(a.fmax)) : 0.0;
     const bool bad = a.n_rows > 0 && (dmax >= 0x1p50 || dmax * (double)a.n_rows >= 0x1p62 || a.s2 != a.s2);
     if (__syncthreads_or(bad)) {
+      DQ_SCAN_COUNT(0);
       exact_stats = true;
       FastAcc e;
       fast_acc_init(e);
@@ -555,6 +566,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DQ_FAST_
           m_hi = (uint32_t)(b >> 32);
           m_shift = i64_to_f64(m_lo, m_hi);  // what the re-run converts a stand-in row to
         }
+        DQ_SCAN_COUNT(1);
         FastAcc e;
         fast_acc_init(e);
         fast_tail<T, PK_NONE, true, false, true, true>(e, rv, rvalid, no_valid, 0u, span, m_lo, m_hi, m_shift, cshift,
@@ -583,6 +595,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DQ_FAST_
       }
     }
     if (__syncthreads_or(mine)) {
+      DQ_SCAN_COUNT(2);
       for (uint32_t r = threadIdx.x; r < span; r += kBlock) {
         const auto v = __builtin_amdgcn_raw_buffer_load_b64(rv, (int)(r * 8u), 0, 0);
         const uint32_t bit = (((uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rvalid, (int)(r >> 3), 0, 0) |
@@ -608,6 +621,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DQ_FAST_
     }
   }
   __syncthreads();  // s_nan complete
+  DQ_SCAN_COUNT(3);
 
   // ---- lane accumulators -> the block's ScanAcc partial (same layout as dq_scan_values_kernel;
   // block_reduce_store sums / merges the lanes, so lane 0 carries the wave-level terms)
@@ -701,6 +715,18 @@ hipError_t launch_scan_fast(int ptype, int variant, const ScanTask* d_tasks, con
   const void* fn = fast_kernel_for(ptype, variant);
   if (!fn) return hipErrorInvalidValue;
   void* args[] = {&d_tasks, &d_group, &d_cols, &n_rows, &d_partials, &d_hll_regs};
+#ifdef DQ_SCAN_DIAG
+  {
+    unsigned long long z[4] = {0, 0, 0, 0};
+    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_scan_diag), z, sizeof(z), 0, hipMemcpyHostToDevice, stream);
+    const hipError_t e = hipLaunchKernel(fn, dim3(blocks_per_task, n_group), dim3(kBlock), args, 0, stream);
+    (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_scan_diag), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
+    (void)hipStreamSynchronize(stream);
+    std::fprintf(stderr, "[scan_diag] rows %lld blocks %llu (x%d tasks): exact-int64 redo %llu, moment-guard redo %llu, "
+                 "HLL marker re-rank %llu\n", (long long)n_rows, z[3], n_group, z[0], z[1], z[2]);
+    return e;
+  }
+#endif
   return hipLaunchKernel(fn, dim3(blocks_per_task, n_group), dim3(kBlock), args, 0, stream);
 }
 

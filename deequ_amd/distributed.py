@@ -274,17 +274,60 @@ class DistributedFrequencies:
             self._summary = summary_from_histogram(h.cpu().numpy(), all_big, self._num_rows)
         return self._summary
 
-    def frequencies(self, raw: bool = False):
-        """Every group (gathered on every rank; for small tables / tests)."""
+    def gather_arrays(self, dst: Optional[int] = None):
+        """Every owner's groups as flat arrays -- (counts int64, key lengths int32, key bytes uint8),
+        owners in rank order -- gathered with tensor collectives (no per-group Python objects):
+        on every rank (dst None) or only on rank `dst` (the others get None).  Collective."""
+        import torch
         import torch.distributed as dist
-        from .frequencies import decode_key
         counts, keys = self.owned.export()
-        parts = [None] * dist.get_world_size(self.group)
-        dist.all_gather_object(parts, (counts.tolist(), keys), group=self.group)
+        lens = np.array([len(k) for k in keys], dtype=np.int32)
+        blob = np.frombuffer(b"".join(keys), dtype=np.uint8)
+        world = dist.get_world_size(self.group)
+        dev = self.owned.torch_device if _comm_device(self.group) == "cuda" else torch.device("cpu")
+        size = torch.tensor([len(counts), len(blob)], dtype=torch.int64, device=dev)
+        sizes = [torch.empty_like(size) for _ in range(world)]
+        dist.all_gather(sizes, size, group=self.group)
+        sizes = [tuple(int(v) for v in t.cpu().tolist()) for t in sizes]
+        mg, mk = max(1, max(g for g, _ in sizes)), max(1, max(k for _, k in sizes))
+
+        def padded(a, n, dtype):
+            t = torch.zeros(n, dtype=dtype, device=dev)
+            if len(a):
+                t[:len(a)] = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+            return t
+        mine = [padded(counts, mg, torch.int64), padded(lens, mg, torch.int32), padded(blob, mk, torch.uint8)]
+        out = []
+        rank = dist.get_rank(self.group)
+        for t in mine:
+            if dst is None:
+                bufs = [torch.empty_like(t) for _ in range(world)]
+                dist.all_gather(bufs, t, group=self.group)
+            else:
+                bufs = [torch.empty_like(t) for _ in range(world)] if rank == dst else None
+                dist.gather(t, bufs, dst=dst, group=self.group)
+            out.append(bufs)
+        if dst is not None and rank != dst:
+            return None
+        cs = np.concatenate([out[0][r].cpu().numpy()[:sizes[r][0]] for r in range(world)])
+        ls = np.concatenate([out[1][r].cpu().numpy()[:sizes[r][0]] for r in range(world)])
+        kb = np.concatenate([out[2][r].cpu().numpy()[:sizes[r][1]] for r in range(world)])
+        return cs, ls, kb
+
+    def frequencies(self, raw: bool = False, dst: Optional[int] = None):
+        """Every group of the dataset ({key: count}), gathered as flat arrays (gather_arrays): on
+        every rank, or only on rank `dst` (the others get {}).  Collective."""
+        from .frequencies import decode_key
+        got = self.gather_arrays(dst)
+        if got is None:
+            return {}
+        cs, ls, kb = got
+        ends = np.cumsum(ls, dtype=np.int64)
+        raw_bytes = kb.tobytes()
         out = {}
-        for cs, ks in parts:
-            for c, k in zip(cs, ks):
-                out[k if raw else decode_key(k, self.owned.dtypes, self.owned.histogram)] = c
+        for c, e, n in zip(cs.tolist(), ends.tolist(), ls.tolist()):
+            k = raw_bytes[e - n:e]
+            out[k if raw else decode_key(k, self.owned.dtypes, self.owned.histogram)] = c
         return out
 
 
@@ -321,8 +364,11 @@ class _DistributedTableView:
         return int(t.item())
 
     def export(self):
-        fr = self._s.frequencies(raw=True)
-        return np.array(list(fr.values()), dtype=np.int64), list(fr.keys())
+        """(counts, keys) of every group of the dataset, on every rank (collective)."""
+        cs, ls, kb = self._s.gather_arrays()
+        ends = np.cumsum(ls, dtype=np.int64)
+        raw_bytes = kb.tobytes()
+        return cs, [raw_bytes[e - n:e] for e, n in zip(ends.tolist(), ls.tolist())]
 
 
 def compute_frequencies_distributed(data, grouping_columns, histogram: bool = False, group=None,

@@ -53,9 +53,14 @@ def _worker(rank, world, port, q):
         st = compute_frequencies_distributed(shard, ["key"], histogram=hist, table_factory=FakeFrequencyTable)
         s = st.summary()
         counts, keys = st.table.top(7)
+        freqs = st.frequencies(raw=True)
+        at0 = st.frequencies(raw=True, dst=0)  # gathered on rank 0 only
+        assert at0 == (freqs if rank == 0 else {})
+        ec, ek = st.table.export()
+        assert dict(zip(ek, ec.tolist())) == freqs
         out[hist] = dict(num_rows=st.numRows, groups=s.num_groups, unique=s.num_unique,
                          grouped=s.grouped_rows, entropy=s.entropy,
-                         top=list(zip(counts.tolist(), keys)), freqs=st.frequencies(raw=True))
+                         top=list(zip(counts.tolist(), keys)), freqs=freqs)
     q.put((rank, out))
     dist.barrier()
     dist.destroy_process_group()
