@@ -1595,6 +1595,40 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t stage_heap_rsrc(const void* va
                                            (int)((heap_end + mis + 3u) & ~3u), 0x00020000);
 }
 
+// The fused stage's sizing sketch in min form (as the value scan's HLL, dq_scan_fast.hip): per
+// register the minimum of s = bits 54..24 of the hash (in bits 30..0) with one unconditional
+// ds_min -- no LDS read and wait per row -- turned into the rank nlz(s) when folded (an untouched
+// register stays 0xFFFFFFFF; s = 0, rank >= 32, is taken as 32: the sketch only sizes the table).
+__device__ __forceinline__ void stage_sketch(uint32_t* regs, uint64_t h) {
+  const uint32_t s = __builtin_amdgcn_alignbit((uint32_t)(h >> 32), (uint32_t)h, 24) & 0x7FFFFFFFu;
+  __hip_atomic_fetch_min(&regs[(uint32_t)(h >> kHllIdxShift)], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t stage_sketch_rank(uint32_t s) { return s ? (uint32_t)__builtin_clz(s) : 32u; }
+
+// stage_pack's selectors for a key of n <= 15 bytes, word i: byte j of the word is the key's
+// byte (v_perm selector 4 + j, from the first operand) if 4 i + j < n, else '0' (selector 0:
+// byte 0 of the constant 0x30303030).
+__host__ __device__ inline uint32_t stage_pack_sel(uint32_t n, int i) {
+  uint32_t s = 0u;
+  for (uint32_t j = 0; j < 4u; ++j)
+    if (4u * (uint32_t)i + j < n) s |= (4u + j) << (8u * j);
+  return s;
+}
+
+// kp_pack of a key given as its first 16 loaded bytes w (bytes past its length n <= 15
+// arbitrary): the bytes past n become '0' with one v_perm per word (selectors by length from
+// an LDS table), then kp_pack's digit test and nibble packing -- the same word kp_pack makes of
+// the masked key, without the length masks' shifts and selects.
+__device__ __forceinline__ bool stage_pack(const uint32_t (&w)[4], uint32_t n, uint4 sel, uint64_t* p) {
+  const uint32_t y0 = __builtin_amdgcn_perm(w[0], 0x30303030u, sel.x), y1 = __builtin_amdgcn_perm(w[1], 0x30303030u, sel.y);
+  const uint32_t y2 = __builtin_amdgcn_perm(w[2], 0x30303030u, sel.z), y3 = __builtin_amdgcn_perm(w[3], 0x30303030u, sel.w);
+  if (kp_nondigit4(y0) | kp_nondigit4(y1) | kp_nondigit4(y2) | kp_nondigit4(y3)) return false;
+  const uint32_t lo = kp_nib4(y0) | (kp_nib4(y1) << 16);
+  const uint32_t hi = kp_nib4(y2) | (kp_nib4(y3) << 16) | (n << 28);
+  *p = (uint64_t)lo | ((uint64_t)hi << 32);
+  return true;
+}
+
 // The validity of row j of every lane of this wave, as a lane mask (from stage_offsets' vword).
 __device__ __forceinline__ uint64_t stage_valid_mask(uint32_t vword, int j) {
   const uint32_t lo = __builtin_amdgcn_readlane(vword, 2 * j), hi = __builtin_amdgcn_readlane(vword, 2 * j + 1);
@@ -1625,9 +1659,11 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(PA
   using R = typename std::conditional<PACK, uint64_t, FreqRec>::type;
   __shared__ PartLdsT<(1 << kStageBinBits), R, (PACK ? kStageSubP : kPartSub)> L;
   __shared__ uint32_t regs[kHllM];
+  __shared__ uint4 psel[16];  // stage_pack's byte selectors by key length
   const uint32_t t = threadIdx.x;
   const uint32_t nb = 1u << b1;
-  for (uint32_t i = t; i < (uint32_t)kHllM; i += kPartThreads) regs[i] = 0u;
+  for (uint32_t i = t; i < (uint32_t)kHllM; i += kPartThreads) regs[i] = 0xFFFFFFFFu;  // (stage_sketch)
+  if (PACK && t < 16u) psel[t] = make_uint4(stage_pack_sel(t, 0), stage_pack_sel(t, 1), stage_pack_sel(t, 2), stage_pack_sel(t, 3));
   __syncthreads();
   const DevColumn& c0 = cols[ks.key_cols[0]];
   alignas(8) uint8_t scratch[kMaxLocalKey];
@@ -1693,33 +1729,46 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(PA
         }
         bin[j] = kPartNoBin;
         if (!((sel >> j) & 1u)) continue;
-        uint64_t k0, k1;
         uint32_t n = (lens[j / 4] >> (8 * (j % 4))) & 0xFFu;
-        if (n == kLenNull) {
-          n = 9;
-          k0 = kNullK0;
-          k1 = kNullK1;
-        } else if (n > 15) {
+        if (n != kLenNull && n > 15) {
           too_long = max(too_long, n);
           continue;
-        } else {
-          const uint64_t lo = (uint64_t)kw[j][0] | ((uint64_t)kw[j][1] << 32);
-          const uint64_t hi = (uint64_t)kw[j][2] | ((uint64_t)kw[j][3] << 32);
-          k0 = n >= 8 ? lo : (lo & ((1ull << (8u * n)) - 1ull));
-          k1 = n > 8 ? (hi & ((1ull << (8u * (n - 8u))) - 1ull)) : 0ull;
         }
+        // the key bytes (NULL: Histogram's "NullValue"), masked to the length
+        auto key_words = [&](uint64_t& k0, uint64_t& k1, uint32_t& len) {
+          if (n == kLenNull) {
+            len = 9;
+            k0 = kNullK0;
+            k1 = kNullK1;
+          } else {
+            const uint64_t lo = (uint64_t)kw[j][0] | ((uint64_t)kw[j][1] << 32);
+            const uint64_t hi = (uint64_t)kw[j][2] | ((uint64_t)kw[j][3] << 32);
+            len = n;
+            k0 = n >= 8 ? lo : (lo & ((1ull << (8u * n)) - 1ull));
+            k1 = n > 8 ? (hi & ((1ull << (8u * (n - 8u))) - 1ull)) : 0ull;
+          }
+        };
         uint64_t h;
         if constexpr (PACK) {
-          uint64_t p;
-          if (kp_pack_record(k0, k1, n, &p)) {
+          // the digit test and packing straight from the loaded words (stage_pack); NULL packs
+          // as kPackNull; anything else is checked against the "NullValue" string, then listed
+          uint64_t p = kPackNull;
+          bool packed = n == kLenNull || stage_pack(kw[j], n, psel[n], &p);
+          uint64_t k0 = 0, k1 = 0;
+          uint32_t len = 0;
+          if (!packed) {
+            key_words(k0, k1, len);
+            packed = kp_pack_record(k0, k1, len, &p);
+          }
+          if (packed) {
             L.rec[j * kPartThreads + t] = p;  // (row order; part_tile sorts it)
             h = hash_record_packed(p);
           } else {  // not a digit key: a 16-B record on the overflow list
-            h = hash_raw(k0, k1, n);
-            sketch_update(regs, h);
+            h = hash_raw(k0, k1, len);
+            stage_sketch(regs, h);
             FreqRec r;
             r.k0 = k0;
-            r.k1 = k1 | ((unsigned long long)n << kRecLenShift);
+            r.k1 = k1 | ((unsigned long long)len << kRecLenShift);
             const unsigned long long k = atomicAdd(ovf_n, 1ull);
             if (k < ovf_cap) ovf[k] = r;
             else atomicOr(flag, 1u);
@@ -1727,12 +1776,15 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(PA
             continue;
           }
         } else {
-          h = hash_inline(k0, k1, n);
+          uint64_t k0, k1;
+          uint32_t len;
+          key_words(k0, k1, len);
+          h = hash_inline(k0, k1, len);
           rec[j].k0 = k0;
-          rec[j].k1 = k1 | ((unsigned long long)n << kRecLenShift);
+          rec[j].k1 = k1 | ((unsigned long long)len << kRecLenShift);
         }
         bin[j] = (uint32_t)(h >> (64 - b1)) & (nb - 1u);
-        sketch_update(regs, h);
+        stage_sketch(regs, h);
         // one row at a time: interleaving the twelve rows' packing and hashing would need more
         // registers than four waves per SIMD leave (the key words of the later rows are live)
         __builtin_amdgcn_sched_barrier(0);
@@ -1758,7 +1810,7 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(PA
           rec[i].k1 = k.k1 | ((unsigned long long)k.len << kRecLenShift);
         }
         bin[i] = (uint32_t)(k.hash >> (64 - b1)) & (nb - 1u);
-        sketch_update(regs, k.hash);
+        stage_sketch(regs, k.hash);
       }
     }
     if (too_long) atomicMax(long_key, (unsigned long long)too_long);
@@ -1782,7 +1834,7 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(PA
   if (PACK && n_side) atomicAdd(staged, (unsigned long long)n_side);
   __syncthreads();
   for (uint32_t i = t; i < (uint32_t)kHllM; i += kPartThreads)
-    if (regs[i]) atomicMax(&hll[i], regs[i]);
+    if (regs[i] != 0xFFFFFFFFu) atomicMax(&hll[i], stage_sketch_rank(regs[i]));
 }
 
 // Copy regions (min(fill, cap) records each) to out[prefix[r] ..]: the partitioned staging
