@@ -1116,9 +1116,17 @@ constexpr uint32_t kPartNoBin = 0xFFFFu;
 #define DQ_STAGE_PER 12
 #endif
 constexpr int kStagePer = DQ_STAGE_PER;   // rows per thread per fused-stage tile (register budget)
-constexpr uint32_t kStageTile = (uint32_t)kPartThreads * kStagePer;
+// The fused stage's workgroups: 384 threads (6 waves) at 3 waves per SIMD -- two workgroups per
+// CU, and 168 VGPRs per lane: a tile's 12 rows of key words in flight plus the next tile's offsets
+// fit without spills (at 4 waves per SIMD, 128 VGPRs, they do not).
+#ifndef DQ_STAGE_NT
+#define DQ_STAGE_NT 384
+#endif
+constexpr int kStageThreads = DQ_STAGE_NT;
+constexpr int kStageWaves = kStageThreads / 64;
+constexpr uint32_t kStageTile = (uint32_t)kStageThreads * kStagePer;
 #ifndef DQ_STAGEP_SUB
-#define DQ_STAGEP_SUB 6144
+#define DQ_STAGEP_SUB kStageTile
 #endif
 constexpr uint32_t kStageSubP = DQ_STAGEP_SUB;  // packed records per LDS round of the fused stage
 
@@ -1186,19 +1194,19 @@ struct NoMid {
 // mid(): called once the tile's room is reserved, before its records are written (the fused
 // stage issues the next tile's offset loads there, so they arrive during the writes).
 template <int PER, int MAXB, typename R, uint32_t SUBN, bool PROF = false, int WOUT_UNROLL = 0, typename Mid = NoMid,
-          bool REC_LDS = false>
+          bool REC_LDS = false, int NT = kPartThreads, typename PreRes = NoMid>
 __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER], uint32_t (&bin)[PER],
                                  uint32_t nb, uint64_t base_id, R* __restrict__ out, uint64_t out_cap,
                                  unsigned long long* out_fill, FreqRec* ovf, unsigned long long* ovf_n,
                                  uint64_t ovf_cap, unsigned int* flag, unsigned long long* staged,
                                  const unsigned long long* region_start = nullptr, unsigned long long prof_t_ = 0,
-                                 const Mid& mid = Mid()) {
+                                 const Mid& mid = Mid(), const PreRes& pre_res = PreRes()) {
   // region_start != nullptr: exact regions -- output region id starts at record region_start[id]
   // of `out` (sizes counted beforehand: nothing can overflow), out_fill is its cursor
   constexpr uint32_t SUB = SUBN;
   const uint32_t t = threadIdx.x;
   DQ_PROF_MARK(PROF, 1);
-  for (uint32_t i = t; i < nb; i += kPartThreads) L.hist[i] = 0u;
+  for (uint32_t i = t; i < nb; i += NT) L.hist[i] = 0u;
   __syncthreads();
   DQ_PROF_MARK(PROF, 2);
   // rank of each record within its bin (LDS atomics), packed with the bin: rank << 16 | bin
@@ -1235,7 +1243,8 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
   }
   __syncthreads();
   DQ_PROF_MARK(PROF, 4);
-  for (uint32_t b = t; b < nb; b += kPartThreads) {
+  pre_res();  // (the fused stage's flag read: its latency overlaps the reservation atomics')
+  for (uint32_t b = t; b < nb; b += NT) {
     const uint32_t c = L.hist[b];
     L.gbase[b] = c ? atomicAdd(&out_fill[base_id + b], (unsigned long long)c) : 0ull;
     if (region_start && c) L.gbase[b] += region_start[base_id + b];
@@ -1245,12 +1254,12 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
   DQ_PROF_MARK(PROF, 5);
   mid();
   // REC_LDS: the caller left the records in L.rec in row order (record i of thread t at
-  // i * kPartThreads + t; registers are short while the keys load): read back, then sorted
+  // i * NT + t; registers are short while the keys load): read back, then sorted
   R rl[PER];
   if constexpr (REC_LDS) {
-    static_assert(SUB >= (uint32_t)PER * (uint32_t)kPartThreads, "a tile's records in one image");
+    static_assert(SUB >= (uint32_t)PER * (uint32_t)NT, "a tile's records in one image");
 #pragma unroll
-    for (int i = 0; i < PER; ++i) rl[i] = L.rec[i * kPartThreads + t];
+    for (int i = 0; i < PER; ++i) rl[i] = L.rec[i * NT + t];
     __syncthreads();
   }
   for (uint32_t r0 = 0; r0 < total; r0 += SUB) {
@@ -1284,15 +1293,15 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
     if constexpr (WOUT_UNROLL > 0) {
       // (a bounded unroll: the fused stage holds the next tile's offsets across this loop)
 #pragma unroll WOUT_UNROLL
-      for (uint32_t j = t; j < m; j += kPartThreads) put(j);
+      for (uint32_t j = t; j < m; j += NT) put(j);
     } else {  // the compiler's choice (the level-2 passes: no loop-carried state to keep)
-      for (uint32_t j = t; j < m; j += kPartThreads) put(j);
+      for (uint32_t j = t; j < m; j += NT) put(j);
     }
     __syncthreads();
     DQ_PROF_MARK(PROF, 7);
     // an image that holds a whole tile: one round, so rec[] is dead once it is in LDS (the
     // registers go to the caller's loads issued in mid())
-    if constexpr (SUB >= (uint32_t)PER * (uint32_t)kPartThreads) break;
+    if constexpr (SUB >= (uint32_t)PER * (uint32_t)NT) break;
   }
 }
 
@@ -1529,7 +1538,7 @@ __device__ __forceinline__ T* uniform_ptr(T* p) {
 }
 
 // The (begin, end) offsets of tile `tl`'s kStagePer rows of one utf8 column (row j of this thread
-// = tl * kStageTile + j * kPartThreads + threadIdx.x): one 8-byte load of each row's offset pair
+// = tl * kStageTile + j * kStageThreads + threadIdx.x): one 8-byte load of each row's offset pair
 // through a descriptor of the tile's offsets (rows past the batch read 0).  The validity bits
 // come as ONE dword per lane: row j of lane l of wave w is bit l & 31 of tile dword
 // 16 j + 2 w + (l >> 5), which lane 2 j + (l >> 5) of the wave loads (stage_valid_mask).
@@ -1551,7 +1560,7 @@ __device__ __forceinline__ void stage_offsets(const DevColumn& c0, int64_t n_row
     const bool al = ((uintptr_t)vb & 3u) == 0u;
     const __amdgpu_buffer_rsrc_t rs_v = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t*>(vb), 0, (int)(al ? (nbytes + 3u) & ~3u : nbytes), 0x00020000);
-    const uint32_t dw = 16u * (l >> 1) + 2u * w + (l & 1u);
+    const uint32_t dw = 2u * kStageWaves * (l >> 1) + 2u * w + (l & 1u);
     vword = 0u;
     if (l < 2u * kStagePer) {
       if (al || 4u * dw + 4u <= nbytes) {
@@ -1567,34 +1576,43 @@ __device__ __forceinline__ void stage_offsets(const DevColumn& c0, int64_t n_row
       const_cast<int32_t*>(uniform_ptr(c0.offsets) + r0), 0, (int)(4u * (m + 1u)), 0x00020000);
 #pragma unroll
   for (int j = 0; j < kStagePer; ++j) {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs_off, (int)(4u * ((uint32_t)j * kPartThreads + t)), 0, 0);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs_off, (int)(4u * ((uint32_t)j * kStageThreads + t)), 0, 0);
     pob[j] = v[0];
     poe[j] = v[1];
   }
 }
 
-// The 16 bytes from a key's first byte: one unaligned buffer load through a descriptor whose base
-// is the heap's 4-byte aligned start and whose range ends at the 4-byte boundary after the heap's
-// last byte (stage_heap_rsrc), so a key that ends within the heap's last dword is read whole (the
-// bytes past the key are masked off by its length; words wholly past the range read 0).
-__device__ __forceinline__ void stage_key_load(__amdgpu_buffer_rsrc_t rs_vals, uint32_t mis, uint32_t ob, uint32_t (&w)[4]) {
-  const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_vals, (int)(ob + mis), 0, 0);
+// Key bytes through a buffer descriptor over the heap [0, heap_end).  A buffer load's range check
+// is per dword of the load, counted from the load's own offset, so a 16-byte load reaching past
+// heap_end would zero whole dwords -- key bytes included.  So every key is read as ONE unaligned
+// 16-byte load at min(ob, heap_end - 16), always wholly in range: a key that starts within the
+// heap's last 16 bytes lands s = ob - (heap_end - 16) bytes into the words (s + n <= 16), and is
+// shifted down when it is processed (key_shr_bytes; rare, no memory access in the branch).  The
+// kernels using it hand a batch whose whole heap is under 16 bytes back to the host's general
+// path (no per-load branch for it).
+__device__ __forceinline__ void key_load16(__amdgpu_buffer_rsrc_t rs_vals, uint32_t heap_end, uint32_t ob, uint32_t (&w)[4]) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_vals, (int)min(ob, heap_end - 16u), 0, 0);
   w[0] = v[0];
   w[1] = v[1];
   w[2] = v[2];
   w[3] = v[3];
 }
-
-// The key heap's descriptor for stage_key_load: base rounded down to 4 bytes (mis = the bytes
-// skipped), range rounded up to 4 bytes (the dword holding the heap's last byte is in that byte's
-// page, so reading it whole cannot fault).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t stage_heap_rsrc(const void* values, uint32_t heap_end, uint32_t& mis) {
-  const uintptr_t a = (uintptr_t)values;
-  mis = (uint32_t)(a & 3u);
-  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(a & ~(uintptr_t)3), 0,
-                                           (int)((heap_end + mis + 3u) & ~3u), 0x00020000);
+// The byte position of the key in key_load16's words (0 unless it starts in the last 16 bytes;
+// clamped to 15: only an empty key can start at heap_end itself).
+__device__ __forceinline__ uint32_t key_shift(uint32_t ob, uint32_t heap_end) {
+  const uint32_t s = ob > heap_end - 16u ? ob - (heap_end - 16u) : 0u;  // (heap_end >= 16)
+  return s < 15u ? s : 15u;
 }
-
+// w >>= 8 s bits (128-bit, s in 1..15).
+__device__ __forceinline__ void key_shr_bytes(uint32_t (&w)[4], uint32_t s) {
+  const uint32_t q = s >> 2, r = 8u * (s & 3u);
+  uint32_t d[5];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) d[i] = q == 0 ? w[i] : q == 1 ? (i < 3 ? w[i + 1] : 0u) : q == 2 ? (i < 2 ? w[i + 2] : 0u) : (i < 1 ? w[3] : 0u);
+  d[4] = 0u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = __builtin_amdgcn_alignbit(d[i + 1], d[i], r);
+}
 // The fused stage's sizing sketch in min form (as the value scan's HLL, dq_scan_fast.hip): per
 // register the minimum of s = bits 54..24 of the hash (in bits 30..0) with one unconditional
 // ds_min -- no LDS read and wait per row -- turned into the rank nlz(s) when folded (an untouched
@@ -1647,10 +1665,10 @@ constexpr int kStageLoadB = DQ_STAGE_LOAD_B;  // the rest after this many rows
 #define DQ_STAGE_WOUT_UNROLL 2
 #endif
 #ifndef DQ_STAGEP_WAVES
-#define DQ_STAGEP_WAVES 4
+#define DQ_STAGEP_WAVES 3
 #endif
 template <bool ONE_STRING, bool PACK>
-__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(PACK ? DQ_STAGEP_WAVES : 4))) void dq_freq_stage_part_kernel(
+__global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(DQ_STAGEP_WAVES))) void dq_freq_stage_part_kernel(
     FreqKeySpec ks, const DevColumn* __restrict__ cols, int64_t n_rows, int b1,
     typename std::conditional<PACK, uint64_t, FreqRec>::type* __restrict__ out, uint64_t cap1,
     unsigned long long* fill1, FreqRec* ovf, unsigned long long* ovf_n, uint64_t ovf_cap, unsigned int* flag,
@@ -1662,7 +1680,7 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(PA
   __shared__ uint4 psel[16];  // stage_pack's byte selectors by key length
   const uint32_t t = threadIdx.x;
   const uint32_t nb = 1u << b1;
-  for (uint32_t i = t; i < (uint32_t)kHllM; i += kPartThreads) regs[i] = 0xFFFFFFFFu;  // (stage_sketch)
+  for (uint32_t i = t; i < (uint32_t)kHllM; i += kStageThreads) regs[i] = 0xFFFFFFFFu;  // (stage_sketch)
   if (PACK && t < 16u) psel[t] = make_uint4(stage_pack_sel(t, 0), stage_pack_sel(t, 1), stage_pack_sel(t, 2), stage_pack_sel(t, 3));
   __syncthreads();
   const DevColumn& c0 = cols[ks.key_cols[0]];
@@ -1673,14 +1691,19 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(PA
   // its heap is < 2 GiB); each tile's offsets through a descriptor of that tile's offsets (bounded,
   // so rows past the batch read 0), as (begin, end) pairs: one 8-byte load per row.
   const uint32_t heap_end = ONE_STRING ? __builtin_amdgcn_readfirstlane((uint32_t)uniform_ptr(c0.offsets)[n_rows]) : 0u;
-  uint32_t mis = 0u;
-  const __amdgpu_buffer_rsrc_t rs_vals = stage_heap_rsrc(uniform_ptr(c0.values), heap_end, mis);
+  const uint8_t* vals = static_cast<const uint8_t*>(uniform_ptr(c0.values));
+  const __amdgpu_buffer_rsrc_t rs_vals =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vals), 0, (int)heap_end, 0x00020000);
+  if (ONE_STRING && heap_end < 16u) {  // (a heap under 16 bytes: key_load16's general path, as a long key)
+    if (blockIdx.x == 0 && t == 0) atomicMax(long_key, 16ull);
+    return;
+  }
   const bool has_validity = uniform_ptr(c0.validity) != nullptr;
   uint32_t pob[kStagePer], poe[kStagePer], vword = 0u;
   if (ONE_STRING && (int64_t)blockIdx.x < n_tiles) stage_offsets(c0, n_rows, blockIdx.x, pob, poe, vword);
   // PACK: once the overflow list has filled up (a column of keys that are not digit strings) the
   // batch will be rolled back, so the workgroups stop: thread 0 reads `flag` while each tile's
-  // records are written (abort_v) and the workgroup leaves at the next tile's top.
+  // room is reserved (abort_v) and the workgroup leaves at the next tile's top.
   __shared__ unsigned int abort_s;
   unsigned int abort_v = 0u;
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
@@ -1705,34 +1728,40 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(PA
       // all in flight together, and the NEXT tile's offsets are issued before this tile's split.
       // key lengths as bytes, 4 to a register (kLenNull = Histogram's NULL, "NullValue"; lengths
       // above 15 are clamped to 255: such a batch is rolled back, only "too long" matters)
-      constexpr uint32_t kLenNull = 254u;
+      // lens byte: n | s << 4 for a key of n <= 15 bytes at byte s of its loaded words
+      // (key_shift; s + n <= 16, so the codes below are never taken by a key)
+      constexpr uint32_t kLenNull = 254u, kLenLong = 255u;
       uint32_t lens[(kStagePer + 3) / 4] = {}, sel = 0u;
 #pragma unroll
       for (int j = 0; j < kStagePer; ++j) {
-        const int64_t row = row0 + j * kPartThreads + t;
+        const int64_t row = row0 + j * kStageThreads + t;
         const uint32_t n = poe[j] - pob[j];
         const bool valid = !has_validity || ((stage_valid_mask(vword, j) >> (t & 63u)) & 1u);
         if (row < n_rows && (valid || ks.null_as_key)) sel |= 1u << j;
-        const uint32_t nb8 = (row < n_rows && !valid) ? kLenNull : (n < 254u ? n : 255u);
+        const uint32_t nb8 = (row < n_rows && !valid) ? kLenNull : (n > 15u ? kLenLong : n | (key_shift(pob[j], heap_end) << 4));
         lens[j / 4] |= nb8 << (8 * (j % 4));
       }
       // rows [0, kStageLoadA) are loaded first; the rest once row kStageLoadB - 1 is processed
       // (all twelve in flight at once would not leave registers for four waves per SIMD)
       uint32_t kw[kStagePer][4];
 #pragma unroll
-      for (int j = 0; j < kStageLoadA; ++j) stage_key_load(rs_vals, mis, pob[j], kw[j]);
+      for (int j = 0; j < kStageLoadA; ++j) key_load16(rs_vals, heap_end, pob[j], kw[j]);
 #pragma unroll
       for (int j = 0; j < kStagePer; ++j) {
         if (j == kStageLoadB) {
 #pragma unroll
-          for (int q = kStageLoadA; q < kStagePer; ++q) stage_key_load(rs_vals, mis, pob[q], kw[q]);
+          for (int q = kStageLoadA; q < kStagePer; ++q) key_load16(rs_vals, heap_end, pob[q], kw[q]);
         }
         bin[j] = kPartNoBin;
         if (!((sel >> j) & 1u)) continue;
         uint32_t n = (lens[j / 4] >> (8 * (j % 4))) & 0xFFu;
-        if (n != kLenNull && n > 15) {
-          too_long = max(too_long, n);
+        if (n == kLenLong) {  // (a key longer than 15 bytes: the host only tests > 15)
+          too_long = 16u;
           continue;
+        }
+        if (n != kLenNull) {
+          if (n > 15u) key_shr_bytes(kw[j], n >> 4);  // a key in the heap's last 16 bytes (rare)
+          n &= 15u;
         }
         // the key bytes (NULL: Histogram's "NullValue"), masked to the length
         auto key_words = [&](uint64_t& k0, uint64_t& k1, uint32_t& len) {
@@ -1761,7 +1790,7 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(PA
             packed = kp_pack_record(k0, k1, len, &p);
           }
           if (packed) {
-            L.rec[j * kPartThreads + t] = p;  // (row order; part_tile sorts it)
+            L.rec[j * kStageThreads + t] = p;  // (row order; part_tile sorts it)
             h = hash_record_packed(p);
           } else {  // not a digit key: a 16-B record on the overflow list
             h = hash_raw(k0, k1, len);
@@ -1792,7 +1821,7 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(PA
     } else {
 #pragma unroll
       for (int i = 0; i < kStagePer; ++i) {
-        const int64_t row = row0 + i * kPartThreads + t;
+        const int64_t row = row0 + i * kStageThreads + t;
         bin[i] = kPartNoBin;
         if (row >= n_rows) continue;
         Key k;
@@ -1820,20 +1849,23 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(PA
     constexpr bool kProf = false;
 #endif
     const int64_t next = tile + gridDim.x;  // its offsets load while this tile's records are written
-    auto prefetch = [&]() {  // (the flag first: loads complete in order, so waiting for it is not
-                             // waiting for the offsets)
+    // PACK: thread 0 reads `flag` as the tile's room is reserved (its wait is the atomics' wait);
+    // the workgroup leaves at the next tile's top
+    auto flag_read = [&]() {
       if constexpr (PACK)
         if (t == 0) abort_v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    auto prefetch = [&]() {
       if constexpr (ONE_STRING)
         if (next < n_tiles) stage_offsets(c0, n_rows, next, pob, poe, vword);
     };
     part_tile<kStagePer, (1 << kStageBinBits), R, (PACK ? kStageSubP : kPartSub), kProf, DQ_STAGE_WOUT_UNROLL,
-              decltype(prefetch), PACK>(
-        L, rec, bin, nb, 0, out, cap1, fill1, ovf, ovf_n, ovf_cap, flag, staged, nullptr, prof_t_, prefetch);
+              decltype(prefetch), PACK, kStageThreads, decltype(flag_read)>(
+        L, rec, bin, nb, 0, out, cap1, fill1, ovf, ovf_n, ovf_cap, flag, staged, nullptr, prof_t_, prefetch, flag_read);
   }
   if (PACK && n_side) atomicAdd(staged, (unsigned long long)n_side);
   __syncthreads();
-  for (uint32_t i = t; i < (uint32_t)kHllM; i += kPartThreads)
+  for (uint32_t i = t; i < (uint32_t)kHllM; i += kStageThreads)
     if (regs[i] != 0xFFFFFFFFu) atomicMax(&hll[i], stage_sketch_rank(regs[i]));
 }
 
@@ -2231,9 +2263,17 @@ hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, bool p
   if (n_rows <= 0) return hipSuccess;
   if (b1 < 1 || b1 > kStageBinBits || (packed && !one_string)) return hipErrorInvalidValue;
   const int64_t tiles = (n_rows + kStageTile - 1) / kStageTile;
-  int dev = 0, cus = 256;
+  int dev = 0, cus = 256, per_cu = 2;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const int64_t blocks = tiles < (int64_t)cus * 4 ? tiles : (int64_t)cus * 4;
+  // one resident round of workgroups (grid-stride over the tiles)
+  if (packed)
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dq_freq_stage_part_kernel<true, true>, kStageThreads, 0);
+  else if (one_string)
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dq_freq_stage_part_kernel<true, false>, kStageThreads, 0);
+  else
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dq_freq_stage_part_kernel<false, false>, kStageThreads, 0);
+  const int64_t resident = (int64_t)cus * (per_cu > 0 ? per_cu : 1);
+  const int64_t blocks = tiles < resident ? tiles : resident;
 #ifdef DQ_STAGE_PROF
   {
     unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -2241,15 +2281,15 @@ hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, bool p
   }
 #endif
   if (packed)
-    hipLaunchKernelGGL((dq_freq_stage_part_kernel<true, true>), dim3((unsigned)blocks), dim3(kPartThreads), 0, stream, ks,
+    hipLaunchKernelGGL((dq_freq_stage_part_kernel<true, true>), dim3((unsigned)blocks), dim3(kStageThreads), 0, stream, ks,
                        d_cols, n_rows, b1, static_cast<uint64_t*>(d_out), cap1, d_fill1, d_ovf, d_ovf_n, ovf_cap, d_flag,
                        d_hll, d_long_key, d_staged);
   else if (one_string)
-    hipLaunchKernelGGL((dq_freq_stage_part_kernel<true, false>), dim3((unsigned)blocks), dim3(kPartThreads), 0, stream, ks,
+    hipLaunchKernelGGL((dq_freq_stage_part_kernel<true, false>), dim3((unsigned)blocks), dim3(kStageThreads), 0, stream, ks,
                        d_cols, n_rows, b1, static_cast<FreqRec*>(d_out), cap1, d_fill1, d_ovf, d_ovf_n, ovf_cap, d_flag,
                        d_hll, d_long_key, d_staged);
   else
-    hipLaunchKernelGGL((dq_freq_stage_part_kernel<false, false>), dim3((unsigned)blocks), dim3(kPartThreads), 0, stream, ks,
+    hipLaunchKernelGGL((dq_freq_stage_part_kernel<false, false>), dim3((unsigned)blocks), dim3(kStageThreads), 0, stream, ks,
                        d_cols, n_rows, b1, static_cast<FreqRec*>(d_out), cap1, d_fill1, d_ovf, d_ovf_n, ovf_cap, d_flag,
                        d_hll, d_long_key, d_staged);
 #ifdef DQ_STAGE_PROF
@@ -3059,8 +3099,13 @@ __global__ __launch_bounds__(kSmallThreads) void dq_freq_small_kernel(FreqKeySpe
   if constexpr (STRING) {
     const int32_t* offs = uniform_ptr(c0.offsets);
     const uint32_t heap_end = __builtin_amdgcn_readfirstlane((uint32_t)offs[n_rows]);
-    uint32_t mis = 0u;
-    const __amdgpu_buffer_rsrc_t rs_vals = stage_heap_rsrc(uniform_ptr(c0.values), heap_end, mis);
+    const uint8_t* vals = static_cast<const uint8_t*>(uniform_ptr(c0.values));
+    const __amdgpu_buffer_rsrc_t rs_vals =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vals), 0, (int)heap_end, 0x00020000);
+    if (heap_end < 16u) {  // (key_load16: the general path groups a heap under 16 bytes)
+      if (t == 0) atomicOr(bad, 1u);
+      return;
+    }
     uint32_t ob[kSmallPer], oe[kSmallPer];
     auto load_offs = [&](int64_t base) {
       const int64_t left = r1 - base;
@@ -3080,14 +3125,14 @@ __global__ __launch_bounds__(kSmallThreads) void dq_freq_small_kernel(FreqKeySpe
       uint32_t kw[kSmallPer][4];
       uint32_t sel = 0u, nul = 0u;
 #pragma unroll
-      for (int j = 0; j < kSmallPer; ++j) {
+      for (int j = 0; j < kSmallPer; ++j) {  // (lens byte: as the fused stage's, 255 = too long)
         const int64_t row = base + (int64_t)j * kSmallThreads + t;
         const uint32_t n = oe[j] - ob[j];
-        lens[j / 4] |= (n < 255u ? n : 255u) << (8 * (j % 4));
+        lens[j / 4] |= (n > 15u ? 255u : n | (key_shift(ob[j], heap_end) << 4)) << (8 * (j % 4));
         const bool valid = validity == nullptr || (row < r1 && ((validity[row >> 3] >> (row & 7)) & 1u));
         if (row < r1 && (valid || null_key)) sel |= 1u << j;
         if (row < r1 && !valid) nul |= 1u << j;
-        stage_key_load(rs_vals, mis, ob[j], kw[j]);
+        key_load16(rs_vals, heap_end, ob[j], kw[j]);
       }
       if (base + step < r1) load_offs(base + step);
 #pragma unroll
@@ -3101,10 +3146,12 @@ __global__ __launch_bounds__(kSmallThreads) void dq_freq_small_kernel(FreqKeySpe
           k1 = kNullK1;
         } else {
           n = (lens[j / 4] >> (8 * (j % 4))) & 0xFFu;
-          if (n > 15) {
+          if (n == 255u) {
             fail = true;
             continue;
           }
+          if (n > 15u) key_shr_bytes(kw[j], n >> 4);
+          n &= 15u;
           const uint64_t lo = (uint64_t)kw[j][0] | ((uint64_t)kw[j][1] << 32);
           const uint64_t hi = (uint64_t)kw[j][2] | ((uint64_t)kw[j][3] << 32);
           k0 = n >= 8 ? lo : (lo & ((1ull << (8u * n)) - 1ull));

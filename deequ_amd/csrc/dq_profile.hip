@@ -229,24 +229,49 @@ __global__ __launch_bounds__(kBlock) void dq_datatype_kernel(const HllTask* __re
 #ifndef DQ_STR_U
 #define DQ_STR_U 4
 #endif
-// A string heap's descriptor: base rounded down to 4 bytes (mis = the bytes skipped), range
-// rounded up to the 4-byte boundary after the heap's last byte (that dword lies in the last
-// byte's page, so reading it whole cannot fault; a buffer range check is per dword).
-__device__ inline __amdgpu_buffer_rsrc_t heap_rsrc(const uint8_t* vals, uint32_t heap_end, uint32_t& mis) {
-  const uintptr_t a = (uintptr_t)vals;
-  mis = (uint32_t)(a & 3u);
-  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(a & ~(uintptr_t)3), 0, (int)((heap_end + mis + 3u) & ~3u),
-                                           0x00020000);
+// Little-endian p[0..n) (n <= 8), zero padded, from the aligned words that hold those bytes only.
+__device__ inline uint64_t ld_bytes(const uint8_t* p, uint32_t n) {
+  if (n == 0) return 0;
+  const uintptr_t a = (uintptr_t)p;
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(a & ~(uintptr_t)7);
+  const uint32_t sh = (uint32_t)(a & 7) * 8u;
+  uint64_t v = w[0] >> sh;
+  if (sh && (a & 7) + n > 8) v |= w[1] << (64u - sh);
+  return n >= 8 ? v : (v & ((1ull << (8u * n)) - 1ull));
 }
 
-// 24 bytes from byte offset a of heap_rsrc's range (unaligned 16- and 8-byte loads; words past the
-// range read 0; the bytes past a string's end are not used by its consumers).
-__device__ __forceinline__ void load24(__amdgpu_buffer_rsrc_t rs, uint32_t a, uint64_t (&w)[3]) {
-  const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)a, 0, 0);
-  const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(a + 16u), 0, 0);
-  w[0] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
-  w[1] = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
-  w[2] = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
+// 24 bytes of a string heap (a descriptor over [0, heap_end)) from byte a: one unaligned 16-byte
+// and one 8-byte buffer load at lo = min(a, heap_end - 24), always wholly in range -- a buffer
+// load's range check is per dword counted from the load's own offset, so a load reaching past
+// heap_end would zero whole dwords, string bytes included.  A string starting in the heap's last
+// 24 bytes lands s = a - lo bytes into the words (s + n <= 24; returned): load24_fix shifts it
+// down once the words have arrived (no memory access in that rare branch).  A heap of fewer than
+// 24 bytes (uniform) is read byte-exactly.  The bytes past a string's end are not used.
+__device__ __forceinline__ uint32_t load24(__amdgpu_buffer_rsrc_t rs, const uint8_t* vals, uint32_t heap_end, uint32_t a,
+                                           uint64_t (&w)[3]) {
+  if (heap_end >= 24u) {
+    const uint32_t lo = min(a, heap_end - 24u);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)lo, 0, 0);
+    const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(lo + 16u), 0, 0);
+    w[0] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+    w[1] = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
+    w[2] = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
+    return a - lo;
+  }
+  const uint32_t m = a < heap_end ? heap_end - a : 0u;  // bytes of the heap from a (< 24)
+#pragma unroll
+  for (int k = 0; k < 3; ++k) w[k] = m > 8u * k ? ld_bytes(vals + a + 8u * k, min(8u, m - 8u * k)) : 0ull;
+  return 0u;
+}
+// w >>= 8 s bits (192-bit; s = load24's result, 1..24).
+__device__ __forceinline__ void load24_fix(uint64_t (&w)[3], uint32_t s) {
+  const uint32_t q = s >> 3, r = 8u * (s & 7u);
+  const uint64_t d0 = q == 0 ? w[0] : q == 1 ? w[1] : q == 2 ? w[2] : 0ull;
+  const uint64_t d1 = q == 0 ? w[1] : q == 1 ? w[2] : 0ull;
+  const uint64_t d2 = q == 0 ? w[2] : 0ull;
+  w[0] = r ? (d0 >> r) | (d1 << (64u - r)) : d0;
+  w[1] = r ? (d1 >> r) | (d2 << (64u - r)) : d1;
+  w[2] = r ? (d2 >> r) : d2;
 }
 
 // DT = false: the HLL alone (an ApproxCountDistinct without a DataType on the column), through
@@ -268,16 +293,14 @@ __global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* _
   const DevColumn& col = cols[task.column];
   const uint8_t* wt = task.where_mask >= 0 ? reinterpret_cast<const uint8_t*>(masks[task.where_mask].t) : nullptr;
   const uint8_t* vals = static_cast<const uint8_t*>(col.values);
-  // the first 24 bytes of each string as three words, read unaligned from its first byte (one
-  // 16-byte and one 8-byte buffer load, unconditional) through heap_rsrc's descriptor: a string
-  // that ends in the heap's last dword reads it whole, words past the heap read 0
-  uint32_t mis;
-  const __amdgpu_buffer_rsrc_t rs = heap_rsrc(vals, (uint32_t)col.offsets[n_rows], mis);
+  // the first 24 bytes of each string as three words (load24: unaligned, from its first byte)
+  const uint32_t heap_end = (uint32_t)col.offsets[n_rows];
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vals), 0, (int)heap_end, 0x00020000);
   uint64_t c[5] = {0, 0, 0, 0, 0};
   constexpr int U = DQ_STR_U;
   for (int64_t base = r0 + threadIdx.x; base < r1; base += U * kBlock) {
     int32_t ob[U], oe[U];
-    uint32_t sel[U];
+    uint32_t sel[U], sh[U];
     uint64_t w[U][3];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -289,7 +312,7 @@ __global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* _
       sel[u] = (in && (col.validity == nullptr || bit_at(col.validity, rr)) && (wt == nullptr || bit_at(wt, rr))) ? 1u : 0u;
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) load24(rs, (uint32_t)ob[u] + mis, w[u]);
+    for (int u = 0; u < U; ++u) sh[u] = load24(rs, vals, heap_end, (uint32_t)ob[u], w[u]);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t row = base + (int64_t)u * kBlock;
@@ -298,6 +321,7 @@ __global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* _
       int k;
       W64 h;
       if (n <= 24) {
+        if (sh[u]) load24_fix(w[u], sh[u]);  // (a string in the heap's last 24 bytes)
         const uint64_t s[3] = {w[u][0], w[u][1], w[u][2]};
         k = (DT && sel[u]) ? classify_shifted(s[0], s[1], s[2], n) : DT_NULL;
         h = xxh64_words_dev(s, (uint32_t)n);
@@ -400,19 +424,18 @@ template <int TO>
 __global__ __launch_bounds__(kBlock) void dq_cast_utf8_kernel(DevColumn src, int64_t n_rows, void* values,
                                                               uint8_t* validity) {
   // U rows per lane per step, every load of the step issued before any parse: each row's offset
-  // pair (one 8-byte load), its validity byte, and the first 24 bytes of the string read unaligned
-  // from its first byte (a 16- and an 8-byte buffer load; within 24 bytes of the heap's end, the
-  // aligned words that hold its bytes).  Longer strings take the byte-pointer parser.
+  // pair (one 8-byte load), its validity byte, and the first 24 bytes of the string (load24: a 16-
+  // and an 8-byte unaligned buffer load).  Longer strings take the byte-pointer parser.
   constexpr int to_type = TO;
   constexpr int U = 4;
   const uint32_t lane = threadIdx.x & 63u;
   const uint8_t* vals = static_cast<const uint8_t*>(src.values);
-  uint32_t mis;
-  const __amdgpu_buffer_rsrc_t rs = heap_rsrc(vals, (uint32_t)src.offsets[n_rows], mis);
+  const uint32_t heap_end = (uint32_t)src.offsets[n_rows];
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vals), 0, (int)heap_end, 0x00020000);
   const __amdgpu_buffer_rsrc_t ro =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(src.offsets), 0, (int)(4u * (uint32_t)(n_rows + 1)), 0x00020000);
   for (int64_t base = (int64_t)blockIdx.x * kBlock * U; base < n_rows; base += (int64_t)gridDim.x * kBlock * U) {
-    uint32_t ob[U], oe[U], sel = 0u;
+    uint32_t ob[U], oe[U], sh[U], sel = 0u;
     uint64_t w[U][3];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -423,7 +446,7 @@ __global__ __launch_bounds__(kBlock) void dq_cast_utf8_kernel(DevColumn src, int
       if (row < n_rows && (src.validity == nullptr || bit_at(src.validity, row))) sel |= 1u << u;
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) load24(rs, ob[u] + mis, w[u]);
+    for (int u = 0; u < U; ++u) sh[u] = load24(rs, vals, heap_end, ob[u], w[u]);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t row = base + (int64_t)u * kBlock + threadIdx.x;
@@ -432,7 +455,10 @@ __global__ __launch_bounds__(kBlock) void dq_cast_utf8_kernel(DevColumn src, int
       bool ok = false;
       if ((sel >> u) & 1u) {
         const int32_t n = (int32_t)(oe[u] - ob[u]);
-        if (n <= 24) ok = cast_one<TO>(WordSrc(w[u][0], w[u][1], w[u][2], 0ull, 0u), n, &lv, &dv);
+        if (n <= 24) {
+          if (sh[u]) load24_fix(w[u], sh[u]);  // (a string in the heap's last 24 bytes)
+          ok = cast_one<TO>(WordSrc(w[u][0], w[u][1], w[u][2], 0ull, 0u), n, &lv, &dv);
+        }
         else ok = cast_one<TO>(PtrSrc{vals + ob[u]}, n, &lv, &dv);
       }
       if (row < n_rows) {
