@@ -1120,7 +1120,7 @@ constexpr int kStagePer = DQ_STAGE_PER;   // rows per thread per fused-stage til
 // CU, and 168 VGPRs per lane: a tile's 12 rows of key words in flight plus the next tile's offsets
 // fit without spills (at 4 waves per SIMD, 128 VGPRs, they do not).
 #ifndef DQ_STAGE_NT
-#define DQ_STAGE_NT 384
+#define DQ_STAGE_NT 512
 #endif
 constexpr int kStageThreads = DQ_STAGE_NT;
 constexpr int kStageWaves = kStageThreads / 64;
@@ -1137,9 +1137,10 @@ struct PartLdsT {
   static constexpr uint32_t SUB = SUBN;
   R rec[SUB];
   uint16_t bin[SUB];
-  uint32_t hist[MAXB];
-  uint32_t start[MAXB];
-  unsigned long long gbase[MAXB];
+  alignas(16) uint32_t hist[MAXB];
+  alignas(16) uint32_t start[MAXB];
+  unsigned long long gbase[MAXB];  // per bin: output index of the tile's position 0 (see part_tile)
+  uint32_t lim[MAXB];              // per bin: tile positions below lim fit the bin's region
   uint32_t total;
 };
 
@@ -1172,10 +1173,11 @@ __device__ inline FreqRec rec_raw(uint64_t p) {
 // printed per launch by launch_freq_stage_part).
 #ifdef DQ_STAGE_PROF
 __device__ unsigned long long g_stage_prof[8];
+__device__ unsigned long long g_stage_blk[4096][2];  // per workgroup: wall-clock start, end
 #define DQ_PROF_MARK(PROF, i)                                                        \
   do {                                                                               \
     if (PROF && threadIdx.x == 0) {                                                  \
-      const unsigned long long now_ = clock64();                                     \
+      const unsigned long long now_ = wall_clock64();                                \
       if (i > 0) atomicAdd(&g_stage_prof[i - 1], now_ - prof_t_);                    \
       prof_t_ = now_;                                                                \
     }                                                                                \
@@ -1188,6 +1190,20 @@ __device__ unsigned long long g_stage_prof[8];
 // 2^bin_bits, or kPartNoBin for none); output region of a bin = base_id + bin.  Ranks come from
 // LDS atomics, the room in each region from ONE device atomic per (tile, non-empty bin), and the
 // records are written from an LDS image sorted by bin, kPartSub at a time (coalesced runs).
+// A workgroup barrier for LDS only: the LDS writes before it complete (lgkmcnt) but global loads
+// and stores stay in flight across it -- __syncthreads() would wait for every outstanding vector
+// memory operation (the next tile's prefetched offsets, the write-out's stores, a no-return
+// atomic) at each of a tile's barriers.  Used where the barrier orders LDS data only.
+__device__ __forceinline__ void lds_barrier() {
+#ifdef DQ_FULL_BARRIERS  // (A/B: the full barrier)
+  __syncthreads();
+#else
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#endif
+}
+
 struct NoMid {
   __device__ void operator()() const {}
 };
@@ -1207,50 +1223,103 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
   const uint32_t t = threadIdx.x;
   DQ_PROF_MARK(PROF, 1);
   for (uint32_t i = t; i < nb; i += NT) L.hist[i] = 0u;
-  __syncthreads();
+  lds_barrier();
   DQ_PROF_MARK(PROF, 2);
   // rank of each record within its bin (LDS atomics), packed with the bin: rank << 16 | bin
 #pragma unroll
   for (int i = 0; i < PER; ++i)
     if (bin[i] != kPartNoBin) bin[i] |= atomicAdd(&L.hist[bin[i]], 1u) << 16;
-  __syncthreads();
+  lds_barrier();
   DQ_PROF_MARK(PROF, 3);
-  // exclusive scan of the bins by wave 0 (nb / 64 consecutive bins per lane)
+  // exclusive scan of the bins by wave 0 (nb / 64 consecutive bins per lane; 512 bins -- the
+  // fused stage's level-1 split -- as two 16-byte LDS reads and writes per lane)
   if (t < 64) {
-    const uint32_t per = (nb + 63u) / 64u;
-    uint32_t s = 0;
-    for (uint32_t k = 0; k < per; ++k) {
-      const uint32_t b = t * per + k;
-      if (b < nb) s += L.hist[b];
-    }
-    uint32_t incl = s;
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t o = __shfl_up(incl, d, 64);
-      if ((int)t >= d) incl += o;
-    }
-    uint32_t run = incl - s;
-    for (uint32_t k = 0; k < per; ++k) {
-      const uint32_t b = t * per + k;
-      if (b < nb) {
-        L.start[b] = run;
-        run += L.hist[b];
+    if (nb == 512u && MAXB >= 512) {
+      const uint4 h0 = reinterpret_cast<const uint4*>(L.hist)[2 * t], h1 = reinterpret_cast<const uint4*>(L.hist)[2 * t + 1];
+      const uint32_t s = h0.x + h0.y + h0.z + h0.w + h1.x + h1.y + h1.z + h1.w;
+      uint32_t incl = s;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d, 64);
+        if ((int)t >= d) incl += o;
+      }
+      uint4 s0, s1;
+      s0.x = incl - s;
+      s0.y = s0.x + h0.x;
+      s0.z = s0.y + h0.y;
+      s0.w = s0.z + h0.z;
+      s1.x = s0.w + h0.w;
+      s1.y = s1.x + h1.x;
+      s1.z = s1.y + h1.y;
+      s1.w = s1.z + h1.z;
+      reinterpret_cast<uint4*>(L.start)[2 * t] = s0;
+      reinterpret_cast<uint4*>(L.start)[2 * t + 1] = s1;
+      if (t == 63) {
+        L.total = incl;
+        if (staged && incl) atomicAdd(staged, (unsigned long long)incl);
+      }
+    } else {
+      const uint32_t per = (nb + 63u) / 64u;
+      uint32_t s = 0;
+      for (uint32_t k = 0; k < per; ++k) {
+        const uint32_t b = t * per + k;
+        if (b < nb) s += L.hist[b];
+      }
+      uint32_t incl = s;
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d, 64);
+        if ((int)t >= d) incl += o;
+      }
+      uint32_t run = incl - s;
+      for (uint32_t k = 0; k < per; ++k) {
+        const uint32_t b = t * per + k;
+        if (b < nb) {
+          L.start[b] = run;
+          run += L.hist[b];
+        }
+      }
+      if (t == 63) {
+        L.total = incl;
+        if (staged && incl) atomicAdd(staged, (unsigned long long)incl);
       }
     }
-    if (t == 63) {
-      L.total = incl;
-      if (staged && incl) atomicAdd(staged, (unsigned long long)incl);
-    }
   }
-  __syncthreads();
+  lds_barrier();
   DQ_PROF_MARK(PROF, 4);
   pre_res();  // (the fused stage's flag read: its latency overlaps the reservation atomics')
-  for (uint32_t b = t; b < nb; b += NT) {
-    const uint32_t c = L.hist[b];
-    L.gbase[b] = c ? atomicAdd(&out_fill[base_id + b], (unsigned long long)c) : 0ull;
-    if (region_start && c) L.gbase[b] += region_start[base_id + b];
+  // The tile's room in each bin's region: ONE device atomic per non-empty bin, issued here and
+  // published to LDS only after the records are placed in the image, so the atomics' latency
+  // overlaps that work.  Published per bin: gbase = the output index of tile position 0 (the
+  // bin's first record sits at position start[b]) and lim = the positions that fit the region.
+  constexpr int GB = (MAXB + NT - 1) / NT;
+  unsigned long long room[GB];
+#pragma unroll
+  for (int k = 0; k < GB; ++k) {
+    const uint32_t b = t + (uint32_t)k * NT;
+    room[k] = 0ull;
+    if (b < nb) {
+      const uint32_t c = L.hist[b];
+      if (c) room[k] = atomicAdd(&out_fill[base_id + b], (unsigned long long)c);
+    }
   }
+  auto publish = [&]() {
+#pragma unroll
+    for (int k = 0; k < GB; ++k) {
+      const uint32_t b = t + (uint32_t)k * NT;
+      if (b < nb) {
+        const uint64_t st = L.start[b], fill = room[k];
+        if (region_start) {
+          L.gbase[b] = region_start[base_id + b] + fill - st;
+          L.lim[b] = 0xFFFFFFFFu;
+        } else {
+          L.gbase[b] = (base_id + b) * out_cap + fill - st;
+          const uint64_t lim = out_cap + st > fill ? out_cap + st - fill : 0ull;
+          L.lim[b] = lim < 0xFFFFFFFFull ? (uint32_t)lim : 0xFFFFFFFFu;
+        }
+      }
+    }
+  };
   const uint32_t total = L.total;
-  __syncthreads();
   DQ_PROF_MARK(PROF, 5);
   mid();
   // REC_LDS: the caller left the records in L.rec in row order (record i of thread t at
@@ -1260,7 +1329,7 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
     static_assert(SUB >= (uint32_t)PER * (uint32_t)NT, "a tile's records in one image");
 #pragma unroll
     for (int i = 0; i < PER; ++i) rl[i] = L.rec[i * NT + t];
-    __syncthreads();
+    lds_barrier();
   }
   for (uint32_t r0 = 0; r0 < total; r0 += SUB) {
 #pragma unroll
@@ -1273,17 +1342,16 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
         L.bin[p] = (uint16_t)b;
       }
     }
-    __syncthreads();
+    if (r0 == 0) publish();
+    lds_barrier();
     DQ_PROF_MARK(PROF, 6);
     const uint32_t m = min(SUB, total - r0);
     auto put = [&](uint32_t j) {
       const uint32_t b = L.bin[j];
-      const uint64_t o = L.gbase[b] + (r0 + j - L.start[b]);
+      const uint32_t pos = r0 + j;  // the record's tile position
       const R r = L.rec[j];
-      if (region_start) {
-        out[o] = r;
-      } else if (o < out_cap) {
-        out[(base_id + b) * out_cap + o] = r;
+      if (pos < L.lim[b]) {
+        out[L.gbase[b] + pos] = r;
       } else {  // the region is full: the overflow list (16-B records, aggregated by the sort path)
         const unsigned long long k = atomicAdd(ovf_n, 1ull);
         if (k < ovf_cap) ovf[k] = rec_raw(r);
@@ -1297,7 +1365,7 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
     } else {  // the compiler's choice (the level-2 passes: no loop-carried state to keep)
       for (uint32_t j = t; j < m; j += NT) put(j);
     }
-    __syncthreads();
+    lds_barrier();
     DQ_PROF_MARK(PROF, 7);
     // an image that holds a whole tile: one round, so rec[] is dead once it is in LDS (the
     // registers go to the caller's loads issued in mid())
@@ -1653,19 +1721,24 @@ __device__ __forceinline__ uint64_t stage_valid_mask(uint32_t vword, int j) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-#ifndef DQ_STAGE_LOAD_A
-#define DQ_STAGE_LOAD_A 12
+#ifndef DQ_STAGE_WIN
+#define DQ_STAGE_WIN 4
 #endif
-#ifndef DQ_STAGE_LOAD_B
-#define DQ_STAGE_LOAD_B 0
+constexpr int kStageWin = DQ_STAGE_WIN < DQ_STAGE_PER ? DQ_STAGE_WIN : DQ_STAGE_PER;  // rows' key loads in flight
+#ifndef DQ_STAGE_PIPE
+#define DQ_STAGE_PIPE 0
 #endif
-constexpr int kStageLoadA = DQ_STAGE_LOAD_A < DQ_STAGE_PER ? DQ_STAGE_LOAD_A : DQ_STAGE_PER;  // key loads issued before the first row is processed
-constexpr int kStageLoadB = DQ_STAGE_LOAD_B;  // the rest after this many rows
+constexpr bool kStagePipe = DQ_STAGE_PIPE != 0;
+#ifndef DQ_STAGE_PREFETCH
+#define DQ_STAGE_PREFETCH 0
+#endif
+// the next tile's offsets loaded during this tile's split (else at the tile's top)
+constexpr bool kStagePrefetch = DQ_STAGE_PREFETCH != 0 || DQ_STAGE_PIPE != 0;
 #ifndef DQ_STAGE_WOUT_UNROLL
 #define DQ_STAGE_WOUT_UNROLL 2
 #endif
 #ifndef DQ_STAGEP_WAVES
-#define DQ_STAGEP_WAVES 3
+#define DQ_STAGEP_WAVES 4
 #endif
 template <bool ONE_STRING, bool PACK>
 __global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(DQ_STAGEP_WAVES))) void dq_freq_stage_part_kernel(
@@ -1682,7 +1755,10 @@ __global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(D
   const uint32_t nb = 1u << b1;
   for (uint32_t i = t; i < (uint32_t)kHllM; i += kStageThreads) regs[i] = 0xFFFFFFFFu;  // (stage_sketch)
   if (PACK && t < 16u) psel[t] = make_uint4(stage_pack_sel(t, 0), stage_pack_sel(t, 1), stage_pack_sel(t, 2), stage_pack_sel(t, 3));
-  __syncthreads();
+#ifdef DQ_STAGE_PROF
+  if (t == 0 && blockIdx.x < 4096u) g_stage_blk[blockIdx.x][0] = wall_clock64();
+#endif
+  lds_barrier();
   const DevColumn& c0 = cols[ks.key_cols[0]];
   alignas(8) uint8_t scratch[kMaxLocalKey];
   const int64_t n_tiles = (n_rows + kStageTile - 1) / kStageTile;
@@ -1700,7 +1776,39 @@ __global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(D
   }
   const bool has_validity = uniform_ptr(c0.validity) != nullptr;
   uint32_t pob[kStagePer], poe[kStagePer], vword = 0u;
-  if (ONE_STRING && (int64_t)blockIdx.x < n_tiles) stage_offsets(c0, n_rows, blockIdx.x, pob, poe, vword);
+  // ONE_STRING: a tile's key words (kw), key lengths as bytes, 4 to a register (lens: n | s << 4
+  // for a key of n <= 15 bytes at byte s of its loaded words -- key_shift; s + n <= 16, so the
+  // codes below are never taken by a key; kLenNull = Histogram's NULL, "NullValue"; kLenLong = a
+  // key over 15 bytes: the batch is rolled back) and its selected rows (sel)
+  constexpr uint32_t kLenNull = 254u, kLenLong = 255u;
+  uint32_t kw[kStagePer][4], lens[(kStagePer + 3) / 4], sel = 0u;
+  auto tile_lens = [&](int64_t tl) {  // lens / sel of tile tl, from its offsets (pob / poe / vword)
+    const int64_t r0 = tl * (int64_t)kStageTile;
+    sel = 0u;
+#pragma unroll
+    for (int j = 0; j < (kStagePer + 3) / 4; ++j) lens[j] = 0u;
+#pragma unroll
+    for (int j = 0; j < kStagePer; ++j) {
+      const int64_t row = r0 + j * kStageThreads + t;
+      const uint32_t n = poe[j] - pob[j];
+      const bool valid = !has_validity || ((stage_valid_mask(vword, j) >> (t & 63u)) & 1u);
+      if (row < n_rows && (valid || ks.null_as_key)) sel |= 1u << j;
+      const uint32_t nb8 = (row < n_rows && !valid) ? kLenNull : (n > 15u ? kLenLong : n | (key_shift(pob[j], heap_end) << 4));
+      lens[j / 4] |= nb8 << (8 * (j % 4));
+    }
+  };
+  // kStagePipe: tile k+1's key words are loaded while tile k is split and written (issued when
+  // tile k's keys have been consumed; registers: three waves per SIMD leave room for them)
+  constexpr bool kPipe = ONE_STRING && kStagePipe;
+  if (ONE_STRING && kStagePrefetch && (int64_t)blockIdx.x < n_tiles) {
+    stage_offsets(c0, n_rows, blockIdx.x, pob, poe, vword);
+    if constexpr (kPipe) {
+      tile_lens(blockIdx.x);
+#pragma unroll
+      for (int j = 0; j < kStagePer; ++j) key_load16(rs_vals, heap_end, pob[j], kw[j]);
+      if ((int64_t)blockIdx.x + gridDim.x < n_tiles) stage_offsets(c0, n_rows, blockIdx.x + gridDim.x, pob, poe, vword);
+    }
+  }
   // PACK: once the overflow list has filled up (a column of keys that are not digit strings) the
   // batch will be rolled back, so the workgroups stop: thread 0 reads `flag` while each tile's
   // room is reserved (abort_v) and the workgroup leaves at the next tile's top.
@@ -1710,7 +1818,7 @@ __global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(D
     if constexpr (PACK) {
       if (tile != (int64_t)blockIdx.x) {
         if (t == 0) abort_s = abort_v;
-        __syncthreads();
+        lds_barrier();
         if (abort_s) break;
       }
     }
@@ -1723,35 +1831,22 @@ __global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(D
     uint32_t too_long = 0u;
     if constexpr (ONE_STRING) {
       // This tile's offsets (and validity bits) were loaded during the previous tile's
-      // multi-split (pob / poe / vword); the keys of all kStagePer rows are loaded now, 16 bytes
-      // each from the key's first byte (one unaligned buffer load; bytes past the heap read 0),
-      // all in flight together, and the NEXT tile's offsets are issued before this tile's split.
-      // key lengths as bytes, 4 to a register (kLenNull = Histogram's NULL, "NullValue"; lengths
-      // above 15 are clamped to 255: such a batch is rolled back, only "too long" matters)
-      // lens byte: n | s << 4 for a key of n <= 15 bytes at byte s of its loaded words
-      // (key_shift; s + n <= 16, so the codes below are never taken by a key)
-      constexpr uint32_t kLenNull = 254u, kLenLong = 255u;
-      uint32_t lens[(kStagePer + 3) / 4] = {}, sel = 0u;
+      // multi-split (pob / poe / vword); the keys of its kStagePer rows are loaded 16 bytes each
+      // from the key's first byte (key_load16), all in flight together -- now, or (kPipe) during
+      // the previous tile's split -- and the NEXT tile's offsets are issued before this tile's
+      // split.
+      if constexpr (!kPipe) {
+        if constexpr (!kStagePrefetch) stage_offsets(c0, n_rows, tile, pob, poe, vword);
+        tile_lens(tile);
+        // a window of kStageWin rows' key words in flight: rows [0, kStageWin) now, row
+        // j + kStageWin as row j is processed (the whole tile at once would not leave registers
+        // for four waves per SIMD)
 #pragma unroll
-      for (int j = 0; j < kStagePer; ++j) {
-        const int64_t row = row0 + j * kStageThreads + t;
-        const uint32_t n = poe[j] - pob[j];
-        const bool valid = !has_validity || ((stage_valid_mask(vword, j) >> (t & 63u)) & 1u);
-        if (row < n_rows && (valid || ks.null_as_key)) sel |= 1u << j;
-        const uint32_t nb8 = (row < n_rows && !valid) ? kLenNull : (n > 15u ? kLenLong : n | (key_shift(pob[j], heap_end) << 4));
-        lens[j / 4] |= nb8 << (8 * (j % 4));
+        for (int j = 0; j < kStageWin; ++j) key_load16(rs_vals, heap_end, pob[j], kw[j]);
       }
-      // rows [0, kStageLoadA) are loaded first; the rest once row kStageLoadB - 1 is processed
-      // (all twelve in flight at once would not leave registers for four waves per SIMD)
-      uint32_t kw[kStagePer][4];
-#pragma unroll
-      for (int j = 0; j < kStageLoadA; ++j) key_load16(rs_vals, heap_end, pob[j], kw[j]);
 #pragma unroll
       for (int j = 0; j < kStagePer; ++j) {
-        if (j == kStageLoadB) {
-#pragma unroll
-          for (int q = kStageLoadA; q < kStagePer; ++q) key_load16(rs_vals, heap_end, pob[q], kw[q]);
-        }
+        if (!kPipe && j + kStageWin < kStagePer) key_load16(rs_vals, heap_end, pob[j + kStageWin], kw[j + kStageWin]);
         bin[j] = kPartNoBin;
         if (!((sel >> j) & 1u)) continue;
         uint32_t n = (lens[j / 4] >> (8 * (j % 4))) & 0xFFu;
@@ -1842,6 +1937,14 @@ __global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(D
         stage_sketch(regs, k.hash);
       }
     }
+    if constexpr (kPipe) {  // the next tile's keys, loaded during this tile's split
+      const int64_t next = tile + gridDim.x;
+      if (next < n_tiles) {
+        tile_lens(next);
+#pragma unroll
+        for (int j = 0; j < kStagePer; ++j) key_load16(rs_vals, heap_end, pob[j], kw[j]);
+      }
+    }
     if (too_long) atomicMax(long_key, (unsigned long long)too_long);
 #ifdef DQ_STAGE_PROF
     constexpr bool kProf = true;
@@ -1856,15 +1959,20 @@ __global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(D
         if (t == 0) abort_v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     auto prefetch = [&]() {
-      if constexpr (ONE_STRING)
-        if (next < n_tiles) stage_offsets(c0, n_rows, next, pob, poe, vword);
+      if constexpr (ONE_STRING && kStagePrefetch) {
+        const int64_t ahead = kPipe ? next + gridDim.x : next;  // (kPipe: the next tile's are in use)
+        if (ahead < n_tiles) stage_offsets(c0, n_rows, ahead, pob, poe, vword);
+      }
     };
     part_tile<kStagePer, (1 << kStageBinBits), R, (PACK ? kStageSubP : kPartSub), kProf, DQ_STAGE_WOUT_UNROLL,
               decltype(prefetch), PACK, kStageThreads, decltype(flag_read)>(
         L, rec, bin, nb, 0, out, cap1, fill1, ovf, ovf_n, ovf_cap, flag, staged, nullptr, prof_t_, prefetch, flag_read);
   }
   if (PACK && n_side) atomicAdd(staged, (unsigned long long)n_side);
-  __syncthreads();
+#ifdef DQ_STAGE_PROF
+  if (t == 0 && blockIdx.x < 4096u) g_stage_blk[blockIdx.x][1] = wall_clock64();
+#endif
+  lds_barrier();
   for (uint32_t i = t; i < (uint32_t)kHllM; i += kStageThreads)
     if (regs[i] != 0xFFFFFFFFu) atomicMax(&hll[i], stage_sketch_rank(regs[i]));
 }
@@ -1993,7 +2101,7 @@ __global__ __launch_bounds__(kAggPThreads) __attribute__((amdgpu_waves_per_eu(DQ
   const bool track = tr.hist != nullptr;
   if (track) {
     for (int i = threadIdx.x; i < kAggLdsHist; i += NT) L.hist[i] = 0u;
-    __syncthreads();
+    lds_barrier();
   }
   for (uint64_t b = blockIdx.x; b < n_slices; b += gridDim.x) {
     const uint64_t r0 = b * cap;
@@ -2032,7 +2140,7 @@ __global__ __launch_bounds__(kAggPThreads) __attribute__((amdgpu_waves_per_eu(DQ
       L.fresh = 0u;
       L.cmax = 0u;
     }
-    __syncthreads();
+    lds_barrier();
     uint64_t rb[kAggPBatch];
     for (uint64_t base = r0; base < r1; base += (uint64_t)NT * kAggPBatch) {
 #pragma unroll
@@ -2058,14 +2166,14 @@ __global__ __launch_bounds__(kAggPThreads) __attribute__((amdgpu_waves_per_eu(DQ
         else if (!lds_count_packed(L.K, L.C, rb[j], (sl[j] + 1) & (S - 1), 1)) L.overflow = 1;
       }
     }
-    __syncthreads();
+    lds_barrier();
     // The slice is written as 16-byte halves, one per lane, so each store instruction covers a
     // contiguous 1 KiB (whole 128-byte lines): q = 2 * slot + half, half 0 = {ctrl, count},
     // half 1 = {k0, k1}.
     ulonglong2* halves = reinterpret_cast<ulonglong2*>(slice);
     if (L.overflow) {  // the slice is full: leave it untouched, hand the region's rows back
       if (threadIdx.x == 0) L.retry_base = atomicAdd(n_retry, (unsigned long long)(r1 - r0));
-      __syncthreads();
+      lds_barrier();
       for (uint64_t i = r0 + threadIdx.x; i < r1; i += NT) retry[L.retry_base + (i - r0)] = rec_raw(recs[i]);
       if (tr.write_all)  // (the table was not cleared: the slice starts out empty)
         for (uint32_t q = threadIdx.x; q < 2 * S; q += NT) halves[q] = ulonglong2{0ull, 0ull};
@@ -2114,15 +2222,15 @@ __global__ __launch_bounds__(kAggPThreads) __attribute__((amdgpu_waves_per_eu(DQ
         const uint64_t nb = __ballot(is_new);  // one LDS add per wave, not one per new group
         if (nb && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(nb)) atomicAdd(&L.fresh, (uint32_t)__popcll(nb));
       }
-      __syncthreads();
+      lds_barrier();
       if (threadIdx.x == 0 && L.fresh) atomicAdd(new_groups, (unsigned long long)L.fresh);
       if (tr.smax && threadIdx.x == 0) tr.smax[b] = L.cmax;
     }
-    __syncthreads();  // LDS is reused by the next slice
+    lds_barrier();  // LDS is reused by the next slice
     asm volatile("" ::"v"(touch));
   }
   if (track) {
-    __syncthreads();
+    lds_barrier();
     for (int i = threadIdx.x; i < kAggLdsHist; i += NT)
       if (L.hist[i]) atomicAdd(&tr.hist[i], (unsigned long long)L.hist[i]);
   }
@@ -2298,10 +2406,23 @@ hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, bool p
     (void)hipMemcpyFromSymbolAsync(z, HIP_SYMBOL(g_stage_prof), sizeof(z), 0, hipMemcpyDeviceToHost, stream);
     (void)hipStreamSynchronize(stream);
     const double tiles_d = (double)tiles;
-    std::fprintf(stderr, "[stage_prof] rows %lld tiles %lld blocks %lld cycles/tile: own-loads+compute %.0f "
+    {
+      std::vector<unsigned long long> bt((size_t)std::min<int64_t>(blocks, 4096) * 2);
+      (void)hipMemcpyFromSymbol(bt.data(), HIP_SYMBOL(g_stage_blk), bt.size() * sizeof(unsigned long long), 0,
+                                hipMemcpyDeviceToHost);
+      unsigned long long lo = ~0ull, hi = 0, sum = 0;
+      for (size_t b = 0; b < bt.size() / 2; ++b) {
+        lo = std::min(lo, bt[2 * b]);
+        hi = std::max(hi, bt[2 * b + 1]);
+        sum += bt[2 * b + 1] - bt[2 * b];
+      }
+      std::fprintf(stderr, "[stage_prof] workgroups: span %.1f us, mean life %.1f us, mean concurrency %.1f\n",
+                   (hi - lo) / 100.0, sum / 100.0 / (double)(bt.size() / 2), (double)sum / (double)(hi - lo));
+    }
+    std::fprintf(stderr, "[stage_prof] rows %lld tiles %lld blocks %lld ns/tile (100 MHz wall clock): own-loads+compute %.0f "
                  "wait-others %.0f rank %.0f scan %.0f reserve %.0f lds-scatter %.0f write %.0f\n",
-                 (long long)n_rows, (long long)tiles, (long long)blocks, z[0] / tiles_d, z[1] / tiles_d, z[2] / tiles_d,
-                 z[3] / tiles_d, z[4] / tiles_d, z[5] / tiles_d, z[6] / tiles_d);
+                 (long long)n_rows, (long long)tiles, (long long)blocks, 10 * z[0] / tiles_d, 10 * z[1] / tiles_d,
+                 10 * z[2] / tiles_d, 10 * z[3] / tiles_d, 10 * z[4] / tiles_d, 10 * z[5] / tiles_d, 10 * z[6] / tiles_d);
   }
 #endif
   return hipGetLastError();

@@ -21,6 +21,26 @@ def _have_gpu() -> bool:
         return False
 
 
+@pytest.fixture(autouse=True)
+def _release_device_memory(request):
+    """After each GPU test: collect unreachable tables and hand the cached device blocks (the
+    library's pool, torch's allocator) back, so one test's memory does not crowd the next."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import gc
+    gc.collect()
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+        from deequ_amd import _lib as L
+        L.lib().dq_release_cached_memory(0)
+    except Exception:  # noqa: BLE001 -- best effort
+        pass
+
+
 @pytest.fixture(scope="session")
 def gpu():
     """Skips nothing: a test marked `gpu` that runs without a GPU must fail loudly."""
