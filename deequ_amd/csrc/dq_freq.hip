@@ -1605,6 +1605,36 @@ __device__ __forceinline__ T* uniform_ptr(T* p) {
   return reinterpret_cast<T*>(((uint64_t)hi << 32) | lo);
 }
 
+// The validity bits of a tile of NT * PER rows starting at row r0 (a multiple of 32; m rows in
+// the batch) as ONE dword per lane: row j of lane l of wave w is bit l & 31 of tile dword
+// 2 NW j + 2 w + (l >> 5) (NW = NT / 64), which lane 2 j + (l >> 5) of the wave loads
+// (stage_valid_mask).  0 for a column without a bitmap (never read then).
+template <int NT, int PER>
+__device__ __forceinline__ uint32_t tile_valid_word(const uint8_t* validity, int64_t r0, uint32_t m) {
+  static_assert(2 * PER <= 64, "two lanes per row of the tile");
+  if (validity == nullptr) return 0u;
+  const uint32_t l = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint8_t* vb = validity + (r0 >> 3);
+  const uint32_t nbytes = (m + 7u) >> 3;
+  // a 4-byte aligned bitmap (the usual case): the range covers the bitmap's last dword whole (it
+  // lies in the page of the bitmap's last byte; the bits past the batch are never used)
+  const bool al = ((uintptr_t)vb & 3u) == 0u;
+  const __amdgpu_buffer_rsrc_t rs_v =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vb), 0, (int)(al ? (nbytes + 3u) & ~3u : nbytes), 0x00020000);
+  const uint32_t dw = 2u * (NT / 64) * (l >> 1) + 2u * w + (l & 1u);
+  uint32_t vword = 0u;
+  if (l < 2u * PER) {
+    if (al || 4u * dw + 4u <= nbytes) {
+      vword = __builtin_amdgcn_raw_buffer_load_b32(rs_v, (int)(4u * dw), 0, 0);
+    } else {  // an unaligned bitmap's last, partial dword: byte by byte (a range check is per dword)
+      for (uint32_t k = 0; k < 4u; ++k)
+        if (4u * dw + k < nbytes)
+          vword |= (uint32_t)(uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rs_v, (int)(4u * dw + k), 0, 0) << (8u * k);
+    }
+  }
+  return vword;
+}
+
 // The (begin, end) offsets of tile `tl`'s kStagePer rows of one utf8 column (row j of this thread
 // = tl * kStageTile + j * kStageThreads + threadIdx.x): one 8-byte load of each row's offset pair
 // through a descriptor of the tile's offsets (rows past the batch read 0).  The validity bits
@@ -1618,28 +1648,7 @@ __device__ __forceinline__ void stage_offsets(const DevColumn& c0, int64_t n_row
   const uint32_t m = (uint32_t)(left < (int64_t)kStageTile ? left : (int64_t)kStageTile);
   const uint32_t t = threadIdx.x;
   // (the validity dword first: its address arithmetic waits on nothing then)
-  const uint8_t* validity = uniform_ptr(c0.validity);
-  if (validity != nullptr) {
-    const uint32_t l = t & 63u, w = t >> 6;
-    const uint8_t* vb = validity + (r0 >> 3);
-    const uint32_t nbytes = (m + 7u) >> 3;
-    // a 4-byte aligned bitmap (the usual case): the range covers the bitmap's last dword whole (it
-    // lies in the page of the bitmap's last byte; the bits past the batch are never used)
-    const bool al = ((uintptr_t)vb & 3u) == 0u;
-    const __amdgpu_buffer_rsrc_t rs_v = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(vb), 0, (int)(al ? (nbytes + 3u) & ~3u : nbytes), 0x00020000);
-    const uint32_t dw = 2u * kStageWaves * (l >> 1) + 2u * w + (l & 1u);
-    vword = 0u;
-    if (l < 2u * kStagePer) {
-      if (al || 4u * dw + 4u <= nbytes) {
-        vword = __builtin_amdgcn_raw_buffer_load_b32(rs_v, (int)(4u * dw), 0, 0);
-      } else {  // an unaligned bitmap's last, partial dword: byte by byte (a range check is per dword)
-        for (uint32_t k = 0; k < 4u; ++k)
-          if (4u * dw + k < nbytes)
-            vword |= (uint32_t)(uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rs_v, (int)(4u * dw + k), 0, 0) << (8u * k);
-      }
-    }
-  }
+  vword = tile_valid_word<kStageThreads, kStagePer>(uniform_ptr(c0.validity), r0, m);
   const __amdgpu_buffer_rsrc_t rs_off = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<int32_t*>(uniform_ptr(c0.offsets) + r0), 0, (int)(4u * (m + 1u)), 0x00020000);
 #pragma unroll
@@ -3171,6 +3180,18 @@ struct SmallLds {
 
 __device__ inline bool small_count(SmallLds& L, uint64_t k0, uint64_t k1l) {
   uint32_t s = lds_hash(k0, k1l, 0) & (kSmallSlots - 1);
+  // the common case once the few keys are in: the key in its first slot (both words read in
+  // one LDS round trip; volatile keeps K1's read before K0's -- a wave's LDS reads execute in
+  // order and a slot's K0 is written before its K1 is published -- so a matching K1 comes with
+  // its own K0, never an older word)
+  {
+    const unsigned long long c1 = *reinterpret_cast<volatile unsigned long long*>(&L.K1[s]);
+    const unsigned long long c0 = *reinterpret_cast<volatile unsigned long long*>(&L.K0[s]);
+    if (c1 == k1l && c0 == k0) {
+      atomicAdd(&L.C[s], 1u);
+      return true;
+    }
+  }
   bool done = false;
   for (uint32_t probe = 0; probe < (uint32_t)kSmallSlots && !done;) {  // (publish inside the iteration)
     const unsigned long long c = __hip_atomic_load(&L.K1[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -3227,10 +3248,11 @@ __global__ __launch_bounds__(kSmallThreads) void dq_freq_small_kernel(FreqKeySpe
       if (t == 0) atomicOr(bad, 1u);
       return;
     }
-    uint32_t ob[kSmallPer], oe[kSmallPer];
-    auto load_offs = [&](int64_t base) {
+    uint32_t ob[kSmallPer], oe[kSmallPer], vword = 0u;
+    auto load_offs = [&](int64_t base) {  // the offsets (and validity bits) of the step at base
       const int64_t left = r1 - base;
       const uint32_t m = (uint32_t)(left < step ? left : step);
+      vword = tile_valid_word<kSmallThreads, kSmallPer>(validity, base, m);
       const __amdgpu_buffer_rsrc_t rs_off = __builtin_amdgcn_make_buffer_rsrc(
           const_cast<int32_t*>(offs + base), 0, (int)(4u * (m + 1u)), 0x00020000);
 #pragma unroll
@@ -3250,7 +3272,7 @@ __global__ __launch_bounds__(kSmallThreads) void dq_freq_small_kernel(FreqKeySpe
         const int64_t row = base + (int64_t)j * kSmallThreads + t;
         const uint32_t n = oe[j] - ob[j];
         lens[j / 4] |= (n > 15u ? 255u : n | (key_shift(ob[j], heap_end) << 4)) << (8 * (j % 4));
-        const bool valid = validity == nullptr || (row < r1 && ((validity[row >> 3] >> (row & 7)) & 1u));
+        const bool valid = validity == nullptr || ((stage_valid_mask(vword, j) >> (t & 63u)) & 1u);
         if (row < r1 && (valid || null_key)) sel |= 1u << j;
         if (row < r1 && !valid) nul |= 1u << j;
         key_load16(rs_vals, heap_end, ob[j], kw[j]);
@@ -3354,37 +3376,64 @@ __global__ __launch_bounds__(kSmallThreads) void dq_freq_small_merge_kernel(cons
     C[i] = 0ull;
   }
   __syncthreads();
+  __shared__ unsigned int any_fail;
+  if (t == 0) any_fail = 0u;
+  __syncthreads();
+  // thread t merges the lists of blocks t, t + kSmallThreads, ..., 8 entries at a time with
+  // their loads issued together (one list per thread: the lists' loads all in flight at once)
   bool fail = false;
-  for (int b = 0; b < n_blocks; ++b) {
+  constexpr int U = 8;
+  for (int b = (int)t; b < n_blocks; b += kSmallThreads) {
     const uint32_t n = in_n[b];
-    for (uint32_t i = t; i < n; i += kSmallThreads) {
-      const uint64_t o = (uint64_t)b * kSmallSlots + i;
-      const uint64_t k0 = in_k0[o], k1l = in_k1[o];
-      uint32_t s = lds_hash(k0, k1l, 0) & (kSmallSlots - 1);
-      bool done = false;
-      for (uint32_t probe = 0; probe < (uint32_t)kSmallSlots && !done;) {
-        const unsigned long long c = atomicCAS(&K1[s], kLdsEmpty, kLdsBusy);
-        if (c == kLdsEmpty) {
-          K0[s] = k0;
-          __threadfence_block();
-          atomicExch(&K1[s], k1l);
-          atomicAdd(&C[s], (unsigned long long)in_c[o]);
-          done = true;
-        } else if (c == kLdsBusy) {
-        } else if (c == k1l && __hip_atomic_load(&K0[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == k0) {
-          atomicAdd(&C[s], (unsigned long long)in_c[o]);
-          done = true;
-        } else {
-          s = (s + 1) & (kSmallSlots - 1);
-          ++probe;
-        }
+    for (uint32_t i0 = 0; i0 < n; i0 += U) {
+      unsigned long long k0[U], k1[U];
+      uint32_t cnt[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const uint64_t o = (uint64_t)b * kSmallSlots + i0 + j;
+        const bool in = i0 + j < n;
+        k0[j] = in ? in_k0[o] : 0ull;
+        k1[j] = in ? in_k1[o] : 0ull;
+        cnt[j] = in ? in_c[o] : 0u;
       }
-      if (!done) fail = true;
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        if (i0 + j >= n) continue;
+        uint32_t s = lds_hash(k0[j], k1[j], 0) & (kSmallSlots - 1);
+        bool done = false;
+        {  // the key already in its first slot (as small_count: K1's read ordered before K0's)
+          const unsigned long long c1 = *reinterpret_cast<volatile unsigned long long*>(&K1[s]);
+          const unsigned long long c0 = *reinterpret_cast<volatile unsigned long long*>(&K0[s]);
+          if (c1 == k1[j] && c0 == k0[j]) {
+            atomicAdd(&C[s], (unsigned long long)cnt[j]);
+            done = true;
+          }
+        }
+        for (uint32_t probe = 0; probe < (uint32_t)kSmallSlots && !done;) {
+          const unsigned long long c = atomicCAS(&K1[s], kLdsEmpty, kLdsBusy);
+          if (c == kLdsEmpty) {
+            K0[s] = k0[j];
+            __threadfence_block();
+            atomicExch(&K1[s], k1[j]);
+            atomicAdd(&C[s], (unsigned long long)cnt[j]);
+            done = true;
+          } else if (c == kLdsBusy) {
+          } else if (c == k1[j] && __hip_atomic_load(&K0[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == k0[j]) {
+            atomicAdd(&C[s], (unsigned long long)cnt[j]);
+            done = true;
+          } else {
+            s = (s + 1) & (kSmallSlots - 1);
+            ++probe;
+          }
+        }
+        if (!done) fail = true;
+      }
     }
   }
+  if (fail) any_fail = 1u;
   __syncthreads();
-  if (fail) {
-    atomicOr(bad, 1u);
+  if (any_fail) {  // more keys than the image holds: nothing is inserted, the host regroups
+    if (t == 0) atomicOr(bad, 1u);
     return;
   }
   for (uint32_t i = t; i < (uint32_t)kSmallSlots; i += kSmallThreads) {
