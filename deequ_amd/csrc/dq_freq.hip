@@ -1192,31 +1192,26 @@ __device__ unsigned long long g_stage_blk[4096][2];  // per workgroup: wall-cloc
 // records are written from an LDS image sorted by bin, kPartSub at a time (coalesced runs).
 // A workgroup barrier for LDS only: the LDS writes before it complete (lgkmcnt) but global loads
 // and stores stay in flight across it -- __syncthreads() would wait for every outstanding vector
-// memory operation (the next tile's prefetched offsets, the write-out's stores, a no-return
-// atomic) at each of a tile's barriers.  Used where the barrier orders LDS data only.
+// memory operation (the write-out's stores, the reservation's no-return atomics, loads already
+// issued) at each of a tile's barriers.  Used where the barrier orders LDS data only.
 __device__ __forceinline__ void lds_barrier() {
-#ifdef DQ_FULL_BARRIERS  // (A/B: the full barrier)
-  __syncthreads();
-#else
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-#endif
 }
 
 struct NoMid {
   __device__ void operator()() const {}
 };
-// mid(): called once the tile's room is reserved, before its records are written (the fused
-// stage issues the next tile's offset loads there, so they arrive during the writes).
-template <int PER, int MAXB, typename R, uint32_t SUBN, bool PROF = false, int WOUT_UNROLL = 0, typename Mid = NoMid,
+// pre_res(): called as the tile's room is reserved (the fused stage reads its abort flag there).
+template <int PER, int MAXB, typename R, uint32_t SUBN, bool PROF = false, int WOUT_UNROLL = 0,
           bool REC_LDS = false, int NT = kPartThreads, typename PreRes = NoMid>
 __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER], uint32_t (&bin)[PER],
                                  uint32_t nb, uint64_t base_id, R* __restrict__ out, uint64_t out_cap,
                                  unsigned long long* out_fill, FreqRec* ovf, unsigned long long* ovf_n,
                                  uint64_t ovf_cap, unsigned int* flag, unsigned long long* staged,
                                  const unsigned long long* region_start = nullptr, unsigned long long prof_t_ = 0,
-                                 const Mid& mid = Mid(), const PreRes& pre_res = PreRes()) {
+                                 const PreRes& pre_res = PreRes()) {
   // region_start != nullptr: exact regions -- output region id starts at record region_start[id]
   // of `out` (sizes counted beforehand: nothing can overflow), out_fill is its cursor
   constexpr uint32_t SUB = SUBN;
@@ -1321,7 +1316,6 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
   };
   const uint32_t total = L.total;
   DQ_PROF_MARK(PROF, 5);
-  mid();
   // REC_LDS: the caller left the records in L.rec in row order (record i of thread t at
   // i * NT + t; registers are short while the keys load): read back, then sorted
   R rl[PER];
@@ -1359,7 +1353,7 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
       }
     };
     if constexpr (WOUT_UNROLL > 0) {
-      // (a bounded unroll: the fused stage holds the next tile's offsets across this loop)
+      // (a bounded unroll: the fused stage's registers)
 #pragma unroll WOUT_UNROLL
       for (uint32_t j = t; j < m; j += NT) put(j);
     } else {  // the compiler's choice (the level-2 passes: no loop-carried state to keep)
@@ -1367,8 +1361,7 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
     }
     lds_barrier();
     DQ_PROF_MARK(PROF, 7);
-    // an image that holds a whole tile: one round, so rec[] is dead once it is in LDS (the
-    // registers go to the caller's loads issued in mid())
+    // an image that holds a whole tile: one round, so rec[] is dead once it is in LDS
     if constexpr (SUB >= (uint32_t)PER * (uint32_t)NT) break;
   }
 }
@@ -1734,15 +1727,7 @@ __device__ __forceinline__ uint64_t stage_valid_mask(uint32_t vword, int j) {
 #define DQ_STAGE_WIN 4
 #endif
 constexpr int kStageWin = DQ_STAGE_WIN < DQ_STAGE_PER ? DQ_STAGE_WIN : DQ_STAGE_PER;  // rows' key loads in flight
-#ifndef DQ_STAGE_PIPE
-#define DQ_STAGE_PIPE 0
-#endif
-constexpr bool kStagePipe = DQ_STAGE_PIPE != 0;
-#ifndef DQ_STAGE_PREFETCH
-#define DQ_STAGE_PREFETCH 0
-#endif
-// the next tile's offsets loaded during this tile's split (else at the tile's top)
-constexpr bool kStagePrefetch = DQ_STAGE_PREFETCH != 0 || DQ_STAGE_PIPE != 0;
+
 #ifndef DQ_STAGE_WOUT_UNROLL
 #define DQ_STAGE_WOUT_UNROLL 2
 #endif
@@ -1806,18 +1791,6 @@ __global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(D
       lens[j / 4] |= nb8 << (8 * (j % 4));
     }
   };
-  // kStagePipe: tile k+1's key words are loaded while tile k is split and written (issued when
-  // tile k's keys have been consumed; registers: three waves per SIMD leave room for them)
-  constexpr bool kPipe = ONE_STRING && kStagePipe;
-  if (ONE_STRING && kStagePrefetch && (int64_t)blockIdx.x < n_tiles) {
-    stage_offsets(c0, n_rows, blockIdx.x, pob, poe, vword);
-    if constexpr (kPipe) {
-      tile_lens(blockIdx.x);
-#pragma unroll
-      for (int j = 0; j < kStagePer; ++j) key_load16(rs_vals, heap_end, pob[j], kw[j]);
-      if ((int64_t)blockIdx.x + gridDim.x < n_tiles) stage_offsets(c0, n_rows, blockIdx.x + gridDim.x, pob, poe, vword);
-    }
-  }
   // PACK: once the overflow list has filled up (a column of keys that are not digit strings) the
   // batch will be rolled back, so the workgroups stop: thread 0 reads `flag` while each tile's
   // room is reserved (abort_v) and the workgroup leaves at the next tile's top.
@@ -1839,23 +1812,18 @@ __global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(D
     uint32_t bin[kStagePer];
     uint32_t too_long = 0u;
     if constexpr (ONE_STRING) {
-      // This tile's offsets (and validity bits) were loaded during the previous tile's
-      // multi-split (pob / poe / vword); the keys of its kStagePer rows are loaded 16 bytes each
-      // from the key's first byte (key_load16), all in flight together -- now, or (kPipe) during
-      // the previous tile's split -- and the NEXT tile's offsets are issued before this tile's
-      // split.
-      if constexpr (!kPipe) {
-        if constexpr (!kStagePrefetch) stage_offsets(c0, n_rows, tile, pob, poe, vword);
-        tile_lens(tile);
-        // a window of kStageWin rows' key words in flight: rows [0, kStageWin) now, row
-        // j + kStageWin as row j is processed (the whole tile at once would not leave registers
-        // for four waves per SIMD)
+      // The tile's offsets (and validity bits: one word per lane), then its keys 16 bytes each
+      // from the key's first byte (key_load16) through a window of kStageWin rows in flight:
+      // rows [0, kStageWin) now, row j + kStageWin as row j is processed.  (Deeper pipelines --
+      // the next tile's offsets or keys loaded during this tile's split -- need more registers
+      // than four waves per SIMD leave; at three waves a 6-wave workgroup runs alone on its CU.)
+      stage_offsets(c0, n_rows, tile, pob, poe, vword);
+      tile_lens(tile);
 #pragma unroll
-        for (int j = 0; j < kStageWin; ++j) key_load16(rs_vals, heap_end, pob[j], kw[j]);
-      }
+      for (int j = 0; j < kStageWin; ++j) key_load16(rs_vals, heap_end, pob[j], kw[j]);
 #pragma unroll
       for (int j = 0; j < kStagePer; ++j) {
-        if (!kPipe && j + kStageWin < kStagePer) key_load16(rs_vals, heap_end, pob[j + kStageWin], kw[j + kStageWin]);
+        if (j + kStageWin < kStagePer) key_load16(rs_vals, heap_end, pob[j + kStageWin], kw[j + kStageWin]);
         bin[j] = kPartNoBin;
         if (!((sel >> j) & 1u)) continue;
         uint32_t n = (lens[j / 4] >> (8 * (j % 4))) & 0xFFu;
@@ -1946,36 +1914,21 @@ __global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(D
         stage_sketch(regs, k.hash);
       }
     }
-    if constexpr (kPipe) {  // the next tile's keys, loaded during this tile's split
-      const int64_t next = tile + gridDim.x;
-      if (next < n_tiles) {
-        tile_lens(next);
-#pragma unroll
-        for (int j = 0; j < kStagePer; ++j) key_load16(rs_vals, heap_end, pob[j], kw[j]);
-      }
-    }
     if (too_long) atomicMax(long_key, (unsigned long long)too_long);
 #ifdef DQ_STAGE_PROF
     constexpr bool kProf = true;
 #else
     constexpr bool kProf = false;
 #endif
-    const int64_t next = tile + gridDim.x;  // its offsets load while this tile's records are written
     // PACK: thread 0 reads `flag` as the tile's room is reserved (its wait is the atomics' wait);
     // the workgroup leaves at the next tile's top
     auto flag_read = [&]() {
       if constexpr (PACK)
         if (t == 0) abort_v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
-    auto prefetch = [&]() {
-      if constexpr (ONE_STRING && kStagePrefetch) {
-        const int64_t ahead = kPipe ? next + gridDim.x : next;  // (kPipe: the next tile's are in use)
-        if (ahead < n_tiles) stage_offsets(c0, n_rows, ahead, pob, poe, vword);
-      }
-    };
     part_tile<kStagePer, (1 << kStageBinBits), R, (PACK ? kStageSubP : kPartSub), kProf, DQ_STAGE_WOUT_UNROLL,
-              decltype(prefetch), PACK, kStageThreads, decltype(flag_read)>(
-        L, rec, bin, nb, 0, out, cap1, fill1, ovf, ovf_n, ovf_cap, flag, staged, nullptr, prof_t_, prefetch, flag_read);
+              PACK, kStageThreads, decltype(flag_read)>(
+        L, rec, bin, nb, 0, out, cap1, fill1, ovf, ovf_n, ovf_cap, flag, staged, nullptr, prof_t_, flag_read);
   }
   if (PACK && n_side) atomicAdd(staged, (unsigned long long)n_side);
 #ifdef DQ_STAGE_PROF
@@ -2083,10 +2036,6 @@ __device__ inline bool lds_count_packed(unsigned long long* K, uint32_t* C, uint
   return false;
 }
 
-#ifndef DQ_AGG_SKIP_EMPTY_KEYS
-#define DQ_AGG_SKIP_EMPTY_KEYS 0
-#endif
-constexpr bool kAggSkipEmptyKeys = DQ_AGG_SKIP_EMPTY_KEYS != 0;  // A/B: empty slots written as {ctrl, count} only
 
 #ifndef DQ_AGGP_BATCH
 #define DQ_AGGP_BATCH 4
@@ -2195,7 +2144,7 @@ __global__ __launch_bounds__(kAggPThreads) __attribute__((amdgpu_waves_per_eu(DQ
         bool is_new = false;
         if (!c) {
           // (an empty slot is ctrl = 0 and count = 0; its key half is never read)
-          if (tr.write_all && (!kAggSkipEmptyKeys || !hi)) halves[q] = ulonglong2{0ull, 0ull};
+          if (tr.write_all) halves[q] = ulonglong2{0ull, 0ull};
         } else {
           const bool existing = !table_empty && (slice[s].ctrl & kReady);
           const uint64_t p = L.K[s];
