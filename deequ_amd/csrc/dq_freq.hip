@@ -2856,6 +2856,7 @@ __device__ inline bool merge_count(MergeLds<false>& L, const ImpRec& r) {
 }
 
 constexpr int kMergeThreads = 256;
+constexpr int kImpBatch = 4;  // records per thread in flight in the import merge
 
 // One workgroup per receiver slice (grid-stride): the slice's LDS image, every run's records of
 // the slice counted in with their weights, the slice written back whole.  ovf_list gets the
@@ -2872,7 +2873,7 @@ __global__ __launch_bounds__(kMergeThreads) void dq_import_merge_kernel(
   const bool track = tr.hist != nullptr;
   if (track) {
     for (int i = threadIdx.x; i < kAggLdsHist; i += NT) L.hist[i] = 0u;
-    __syncthreads();
+    lds_barrier();
   }
   for (uint64_t b = blockIdx.x; b < n_slices; b += gridDim.x) {
     FreqSlot* slice = T.slots + (b << kFreqSliceLog);
@@ -2903,22 +2904,30 @@ __global__ __launch_bounds__(kMergeThreads) void dq_import_merge_kernel(
       L.fresh = 0u;
       L.cmax = 0ull;
     }
-    __syncthreads();
+    lds_barrier();
     uint32_t mine = 0;  // this thread's records of the slice (an overflowed slice's key bound)
     for (int run = 0; run < n_runs; ++run) {
       const ImportRun R = runs[run];
       if (R.skip) continue;
       uint64_t i0, i1;
       imp_range(R, run, b, rb, start, end, n_slices, &i0, &i1);
-      for (uint64_t i = i0 + threadIdx.x; i < i1; i += NT) {
-        ImpRec r;
-        imp_load<PACKED>(R, i, r);
-        if (!r.present || !r.lds_ok || dst_slice(r.hash, rb) != b) continue;
-        ++mine;
-        if (!merge_count(L, r)) L.overflow = 1;
+      // kImpBatch records per thread loaded together, then counted (one load latency per batch)
+      for (uint64_t i = i0 + threadIdx.x; i < i1; i += (uint64_t)kImpBatch * NT) {
+        ImpRec r[kImpBatch];
+#pragma unroll
+        for (int j = 0; j < kImpBatch; ++j) {
+          r[j].present = false;
+          if (i + (uint64_t)j * NT < i1) imp_load<PACKED>(R, i + (uint64_t)j * NT, r[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < kImpBatch; ++j) {
+          if (!r[j].present || !r[j].lds_ok || dst_slice(r[j].hash, rb) != b) continue;
+          ++mine;
+          if (!merge_count(L, r[j])) L.overflow = 1;
+        }
       }
     }
-    __syncthreads();
+    lds_barrier();
     ulonglong2* halves = reinterpret_cast<ulonglong2*>(slice);
     if (L.overflow) {
       if (threadIdx.x == 0) ovf_list[atomicAdd(n_ovf, 1ull)] = (uint32_t)b;
@@ -2975,14 +2984,14 @@ __global__ __launch_bounds__(kMergeThreads) void dq_import_merge_kernel(
         const uint64_t nb = __ballot(is_new);
         if (nb && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(nb)) atomicAdd(&L.fresh, (uint32_t)__popcll(nb));
       }
-      __syncthreads();
+      lds_barrier();
       if (threadIdx.x == 0 && L.fresh) atomicAdd(new_groups, (unsigned long long)L.fresh);
       if (tr.smax && threadIdx.x == 0) tr.smax[b] = L.cmax > 0xFFFFFFFEull ? 0xFFFFFFFFu : (uint32_t)L.cmax;
     }
-    __syncthreads();
+    lds_barrier();
   }
   if (track) {
-    __syncthreads();
+    lds_barrier();
     for (int i = threadIdx.x; i < kAggLdsHist; i += NT)
       if (L.hist[i]) atomicAdd(&tr.hist[i], (unsigned long long)L.hist[i]);
   }
