@@ -2794,6 +2794,7 @@ __global__ __launch_bounds__(kBlock) void dq_import_bounds_kernel(const ImportRu
 // The LDS image of a receiver slice: PACKED -- one word per slot (the packed key, kPackEmpty or
 // kPackForeign); general -- K0 / K1 as the partition path's 16-byte records (kLdsEmpty / kLdsBusy
 // / kLdsForeign in K1).  Counts are 64-bit (merged groups carry their weights).
+constexpr int kMergeLdsRuns = 64;  // runs whose slice bounds are staged in LDS (more: read per run)
 template <bool PACKED>
 struct MergeLds;
 template <>
@@ -2804,6 +2805,8 @@ struct MergeLds<true> {
   uint32_t fresh;
   unsigned long long cmax;
   uint32_t hist[kAggLdsHist];
+  unsigned long long rb[kMergeLdsRuns], re[kMergeLdsRuns];  // the slice's record range per run
+  uint32_t pre[kMergeLdsRuns + 1];  // (flat path) records of the slice in runs before each run
 };
 template <>
 struct MergeLds<false> {
@@ -2813,12 +2816,24 @@ struct MergeLds<false> {
   uint32_t fresh;
   unsigned long long cmax;
   uint32_t hist[kAggLdsHist];
+  unsigned long long rb[kMergeLdsRuns], re[kMergeLdsRuns];  // the slice's record range per run
+  uint32_t pre[kMergeLdsRuns + 1];  // (flat path) records of the slice in runs before each run
 };
 
 __device__ inline bool merge_count(MergeLds<true>& L, const ImpRec& r) {
   constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
   uint32_t s = (uint32_t)r.hash & (S - 1);
   for (uint32_t probe = 0; probe < S; ++probe) {
+    // (a slot's key word is written once, by CAS: a plain read that finds the key is final)
+    const unsigned long long k = *reinterpret_cast<volatile unsigned long long*>(&L.K[s]);
+    if (k == r.p) {
+      atomicAdd(&L.C[s], r.count);
+      return true;
+    }
+    if (k != kPackEmpty) {
+      s = (s + 1) & (S - 1);
+      continue;
+    }
     const unsigned long long c = atomicCAS(&L.K[s], kPackEmpty, (unsigned long long)r.p);
     if (c == kPackEmpty || c == r.p) {
       atomicAdd(&L.C[s], r.count);
@@ -2875,6 +2890,10 @@ __global__ __launch_bounds__(kMergeThreads) void dq_import_merge_kernel(
     for (int i = threadIdx.x; i < kAggLdsHist; i += NT) L.hist[i] = 0u;
     lds_barrier();
   }
+  bool flat = PACKED && n_runs <= kMergeLdsRuns;  // (uniform: every run packed and not skipped)
+  for (int r = 0; r < n_runs && flat; ++r) flat = runs[r].kind == 0 && !runs[r].skip;
+  __shared__ const WirePacked* run_recs[kMergeLdsRuns];  // (flat path) each run's records
+  if (flat && (int)threadIdx.x < n_runs) run_recs[threadIdx.x] = static_cast<const WirePacked*>(runs[threadIdx.x].recs);
   for (uint64_t b = blockIdx.x; b < n_slices; b += gridDim.x) {
     FreqSlot* slice = T.slots + (b << kFreqSliceLog);
     for (uint32_t s = threadIdx.x; s < S; s += NT) {
@@ -2904,13 +2923,66 @@ __global__ __launch_bounds__(kMergeThreads) void dq_import_merge_kernel(
       L.fresh = 0u;
       L.cmax = 0ull;
     }
+    // every run's range for this slice at once (one load latency, not one per run)
+    if ((int)threadIdx.x < n_runs && threadIdx.x < (uint32_t)kMergeLdsRuns) {
+      uint64_t i0, i1;
+      imp_range(runs[threadIdx.x], (int)threadIdx.x, b, rb, start, end, n_slices, &i0, &i1);
+      L.rb[threadIdx.x] = i0;
+      L.re[threadIdx.x] = i1;
+    }
     lds_barrier();
     uint32_t mine = 0;  // this thread's records of the slice (an overflowed slice's key bound)
-    for (int run = 0; run < n_runs; ++run) {
+    if (flat) {
+      // every run is a packed wire run with its bounds in LDS: the slice's records of all runs
+      // as ONE index space, kImpBatch per thread loaded together (a run holds only ~1/n_runs of a
+      // slice's records, so per-run batches would leave most threads idle per load latency)
+      if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int r = 0; r < n_runs; ++r) {
+          L.pre[r] = acc;
+          acc += (uint32_t)(L.re[r] - L.rb[r]);
+        }
+        L.pre[n_runs] = acc;
+      }
+      lds_barrier();
+      const uint32_t total = L.pre[n_runs];
+      for (uint32_t f0 = threadIdx.x; f0 < total; f0 += (uint32_t)kImpBatch * NT) {
+        WirePacked w[kImpBatch];
+#pragma unroll
+        for (int j = 0; j < kImpBatch; ++j) {
+          const uint32_t f = f0 + (uint32_t)j * NT;
+          w[j].key = kPackEmpty;
+          if (f < total) {
+            int r = 0;
+            while (r + 1 < n_runs && L.pre[r + 1] <= f) ++r;
+            w[j] = run_recs[r][L.rb[r] + (f - L.pre[r])];
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < kImpBatch; ++j) {
+          if (w[j].key == kPackEmpty) continue;
+          ImpRec rr;
+          rr.p = w[j].key;
+          rr.count = w[j].count;
+          rr.hash = hash_record_packed(w[j].key);
+          if (dst_slice(rr.hash, rb) != b) continue;
+          ++mine;
+          if constexpr (PACKED) {
+            if (!merge_count(L, rr)) L.overflow = 1;
+          }
+        }
+      }
+    }
+    for (int run = 0; run < (flat ? 0 : n_runs); ++run) {
       const ImportRun R = runs[run];
       if (R.skip) continue;
       uint64_t i0, i1;
-      imp_range(R, run, b, rb, start, end, n_slices, &i0, &i1);
+      if (run < kMergeLdsRuns) {
+        i0 = L.rb[run];
+        i1 = L.re[run];
+      } else {
+        imp_range(R, run, b, rb, start, end, n_slices, &i0, &i1);
+      }
       // kImpBatch records per thread loaded together, then counted (one load latency per batch)
       for (uint64_t i = i0 + threadIdx.x; i < i1; i += (uint64_t)kImpBatch * NT) {
         ImpRec r[kImpBatch];
