@@ -2795,18 +2795,20 @@ __global__ __launch_bounds__(kBlock) void dq_import_bounds_kernel(const ImportRu
 // kPackForeign); general -- K0 / K1 as the partition path's 16-byte records (kLdsEmpty / kLdsBusy
 // / kLdsForeign in K1).  Counts are 64-bit (merged groups carry their weights).
 constexpr int kMergeLdsRuns = 64;  // runs whose slice bounds are staged in LDS (more: read per run)
+constexpr int kFlatRuns = kImportFlatRuns;  // packed runs merged as one index space (more: run by run)
 template <bool PACKED>
 struct MergeLds;
 template <>
 struct MergeLds<true> {
   unsigned long long K[kFreqSliceSlots];
-  unsigned long long C[kFreqSliceSlots];
+  uint32_t C[kFreqSliceSlots];  // (32-bit: a weight or sum that does not fit fails the slice, see merge_add)
   int overflow;
   uint32_t fresh;
   unsigned long long cmax;
   uint32_t hist[kAggLdsHist];
   unsigned long long rb[kMergeLdsRuns], re[kMergeLdsRuns];  // the slice's record range per run
-  uint32_t pre[kMergeLdsRuns + 1];  // (flat path) records of the slice in runs before each run
+  uint32_t pe[kFlatRuns];             // (flat path) records of the slice in runs 0..k, inclusive
+  unsigned long long fb[kFlatRuns];   // (flat path) address of flat index 0 in run k's records
 };
 template <>
 struct MergeLds<false> {
@@ -2817,31 +2819,28 @@ struct MergeLds<false> {
   unsigned long long cmax;
   uint32_t hist[kAggLdsHist];
   unsigned long long rb[kMergeLdsRuns], re[kMergeLdsRuns];  // the slice's record range per run
-  uint32_t pre[kMergeLdsRuns + 1];  // (flat path) records of the slice in runs before each run
 };
 
-__device__ inline bool merge_count(MergeLds<true>& L, const ImpRec& r) {
+// Adds weight w to a 32-bit LDS count; false if w or the sum does not fit 32 bits (the slice then
+// takes the overflow path: left untouched and its records inserted group by group, 64-bit).
+__device__ inline bool merge_add(uint32_t* C, uint32_t s, unsigned long long w) {
+  const uint32_t old = atomicAdd(&C[s], (uint32_t)w);
+  return (w >> 32) == 0ull && (uint32_t)(old + (uint32_t)w) >= old;
+}
+
+// Counts packed key p with weight w into the image, probing from slot s.
+__device__ inline bool merge_count_at(MergeLds<true>& L, uint64_t p, unsigned long long w, uint32_t s) {
   constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
-  uint32_t s = (uint32_t)r.hash & (S - 1);
   for (uint32_t probe = 0; probe < S; ++probe) {
-    // (a slot's key word is written once, by CAS: a plain read that finds the key is final)
-    const unsigned long long k = *reinterpret_cast<volatile unsigned long long*>(&L.K[s]);
-    if (k == r.p) {
-      atomicAdd(&L.C[s], r.count);
-      return true;
-    }
-    if (k != kPackEmpty) {
-      s = (s + 1) & (S - 1);
-      continue;
-    }
-    const unsigned long long c = atomicCAS(&L.K[s], kPackEmpty, (unsigned long long)r.p);
-    if (c == kPackEmpty || c == r.p) {
-      atomicAdd(&L.C[s], r.count);
-      return true;
-    }
+    const unsigned long long c = atomicCAS(&L.K[s], kPackEmpty, (unsigned long long)p);
+    if (c == kPackEmpty || c == p) return merge_add(L.C, s, w);
     s = (s + 1) & (S - 1);
   }
   return false;
+}
+
+__device__ inline bool merge_count(MergeLds<true>& L, const ImpRec& r) {
+  return merge_count_at(L, r.p, r.count, (uint32_t)r.hash & (uint32_t)(kFreqSliceSlots - 1));
 }
 
 __device__ inline bool merge_count(MergeLds<false>& L, const ImpRec& r) {
@@ -2871,13 +2870,20 @@ __device__ inline bool merge_count(MergeLds<false>& L, const ImpRec& r) {
 }
 
 constexpr int kMergeThreads = 256;
-constexpr int kImpBatch = 4;  // records per thread in flight in the import merge
+#ifndef DQ_IMP_BATCH
+#define DQ_IMP_BATCH 4
+#endif
+constexpr int kImpBatch = DQ_IMP_BATCH;  // records per thread in flight in the import merge
 
 // One workgroup per receiver slice (grid-stride): the slice's LDS image, every run's records of
 // the slice counted in with their weights, the slice written back whole.  ovf_list gets the
 // slices whose keys did not fit the image (left untouched; zero-filled when write_all).
-template <bool PACKED>
-__global__ __launch_bounds__(kMergeThreads) void dq_import_merge_kernel(
+#ifndef DQ_IMP_WAVES
+#define DQ_IMP_WAVES 5
+#endif
+// FLAT (PACKED only): every run is a packed wire run, at most kFlatRuns of them, none skipped.
+template <bool PACKED, bool FLAT>
+__global__ __launch_bounds__(kMergeThreads) __attribute__((amdgpu_waves_per_eu(FLAT ? DQ_IMP_WAVES : 1))) void dq_import_merge_kernel(
     FreqTable T, const ImportRun* __restrict__ runs, int n_runs, const uint32_t* __restrict__ start,
     const uint32_t* __restrict__ end, uint64_t n_slices, int table_empty, AggTrack tr, uint32_t* ovf_list,
     unsigned long long* n_ovf, unsigned long long* ovf_recs, unsigned long long* new_groups) {
@@ -2890,10 +2896,14 @@ __global__ __launch_bounds__(kMergeThreads) void dq_import_merge_kernel(
     for (int i = threadIdx.x; i < kAggLdsHist; i += NT) L.hist[i] = 0u;
     lds_barrier();
   }
-  bool flat = PACKED && n_runs <= kMergeLdsRuns;  // (uniform: every run packed and not skipped)
-  for (int r = 0; r < n_runs && flat; ++r) flat = runs[r].kind == 0 && !runs[r].skip;
-  __shared__ const WirePacked* run_recs[kMergeLdsRuns];  // (flat path) each run's records
-  if (flat && (int)threadIdx.x < n_runs) run_recs[threadIdx.x] = static_cast<const WirePacked*>(runs[threadIdx.x].recs);
+  static_assert(PACKED || !FLAT, "the flat merge takes packed runs");
+  // thread t < n_runs keeps run t's descriptor and fetches its range of the NEXT slice while this
+  // one is merged (the bounds' load latency is off the slice's critical path)
+  const int my_run = (int)threadIdx.x < n_runs && threadIdx.x < (uint32_t)kMergeLdsRuns ? (int)threadIdx.x : -1;
+  ImportRun myR{};
+  if (my_run >= 0) myR = runs[my_run];
+  uint64_t nx0 = 0, nx1 = 0;
+  if (my_run >= 0 && blockIdx.x < n_slices) imp_range(myR, my_run, blockIdx.x, rb, start, end, n_slices, &nx0, &nx1);
   for (uint64_t b = blockIdx.x; b < n_slices; b += gridDim.x) {
     FreqSlot* slice = T.slots + (b << kFreqSliceLog);
     for (uint32_t s = threadIdx.x; s < S; s += NT) {
@@ -2923,57 +2933,78 @@ __global__ __launch_bounds__(kMergeThreads) void dq_import_merge_kernel(
       L.fresh = 0u;
       L.cmax = 0ull;
     }
-    // every run's range for this slice at once (one load latency, not one per run)
-    if ((int)threadIdx.x < n_runs && threadIdx.x < (uint32_t)kMergeLdsRuns) {
-      uint64_t i0, i1;
-      imp_range(runs[threadIdx.x], (int)threadIdx.x, b, rb, start, end, n_slices, &i0, &i1);
-      L.rb[threadIdx.x] = i0;
-      L.re[threadIdx.x] = i1;
+    if (my_run >= 0) {
+      L.rb[my_run] = nx0;
+      L.re[my_run] = nx1;
+      if (b + gridDim.x < n_slices) imp_range(myR, my_run, b + gridDim.x, rb, start, end, n_slices, &nx0, &nx1);
     }
     lds_barrier();
     uint32_t mine = 0;  // this thread's records of the slice (an overflowed slice's key bound)
-    if (flat) {
-      // every run is a packed wire run with its bounds in LDS: the slice's records of all runs
-      // as ONE index space, kImpBatch per thread loaded together (a run holds only ~1/n_runs of a
-      // slice's records, so per-run batches would leave most threads idle per load latency)
-      if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (int r = 0; r < n_runs; ++r) {
-          L.pre[r] = acc;
-          acc += (uint32_t)(L.re[r] - L.rb[r]);
-        }
-        L.pre[n_runs] = acc;
-      }
-      lds_barrier();
-      const uint32_t total = L.pre[n_runs];
-      for (uint32_t f0 = threadIdx.x; f0 < total; f0 += (uint32_t)kImpBatch * NT) {
-        WirePacked w[kImpBatch];
+    if constexpr (FLAT) {
+      {
+        // every run is a packed wire run: the slice's records of all runs as ONE index space f,
+        // kImpBatch per thread loaded together (a run holds only ~1/n_runs of a slice's records,
+        // so per-run batches would leave most threads idle per load latency).  Run k holds
+        // f in [pe[k-1], pe[k]); its record f sits at fb[k] + 16 f.
+        if (threadIdx.x < 64u) {  // wave 0: inclusive scan of the per-run counts
+          const int lane = (int)threadIdx.x;
+          const uint32_t v = lane < n_runs ? (uint32_t)(L.re[lane] - L.rb[lane]) : 0u;
+          uint32_t incl = v;
 #pragma unroll
-        for (int j = 0; j < kImpBatch; ++j) {
-          const uint32_t f = f0 + (uint32_t)j * NT;
-          w[j].key = kPackEmpty;
-          if (f < total) {
-            int r = 0;
-            while (r + 1 < n_runs && L.pre[r + 1] <= f) ++r;
-            w[j] = run_recs[r][L.rb[r] + (f - L.pre[r])];
+          for (int d = 1; d < kFlatRuns; d <<= 1) {
+            const uint32_t u = __shfl_up(incl, (unsigned)d, 64);
+            if (lane >= d) incl += u;
+          }
+          if (lane < kFlatRuns) {
+            L.pe[lane] = lane < n_runs ? incl : 0xFFFFFFFFu;
+            if (lane < n_runs)
+              L.fb[lane] = reinterpret_cast<unsigned long long>(myR.recs) +
+                           16ull * (L.rb[lane] - (unsigned long long)(incl - v));
           }
         }
+        lds_barrier();
+        uint32_t pe[kFlatRuns - 1];
 #pragma unroll
-        for (int j = 0; j < kImpBatch; ++j) {
-          if (w[j].key == kPackEmpty) continue;
-          ImpRec rr;
-          rr.p = w[j].key;
-          rr.count = w[j].count;
-          rr.hash = hash_record_packed(w[j].key);
-          if (dst_slice(rr.hash, rb) != b) continue;
-          ++mine;
-          if constexpr (PACKED) {
-            if (!merge_count(L, rr)) L.overflow = 1;
+        for (int k = 0; k < kFlatRuns - 1; ++k) pe[k] = L.pe[k];
+        const uint32_t total = L.pe[n_runs - 1];
+        for (uint32_t f0 = threadIdx.x; f0 < total; f0 += (uint32_t)kImpBatch * NT) {
+          unsigned long long key[kImpBatch], cnt[kImpBatch];
+#pragma unroll
+          for (int j = 0; j < kImpBatch; ++j) {
+            const uint32_t f = f0 + (uint32_t)j * NT;
+            key[j] = kPackEmpty;
+            cnt[j] = 0ull;
+            if (f < total) {
+              uint32_t r = 0;
+#pragma unroll
+              for (int k = 0; k < kFlatRuns - 1; ++k) r += pe[k] <= f ? 1u : 0u;
+              const WirePacked w = *reinterpret_cast<const WirePacked*>(L.fb[r] + 16ull * f);
+              key[j] = w.key;
+              cnt[j] = w.count;
+            }
+          }
+          // every record's first probe is issued before any result is looked at
+          uint32_t sl[kImpBatch];
+          unsigned long long cv[kImpBatch];
+#pragma unroll
+          for (int j = 0; j < kImpBatch; ++j) {
+            const uint64_t h = hash_record_packed(key[j]);
+            if (key[j] != kPackEmpty && dst_slice(h, rb) != b) key[j] = kPackEmpty;
+            sl[j] = (uint32_t)h & (S - 1);
+            cv[j] = key[j] != kPackEmpty ? atomicCAS(&L.K[sl[j]], kPackEmpty, key[j]) : 0ull;
+          }
+#pragma unroll
+          for (int j = 0; j < kImpBatch; ++j) {
+            if (key[j] == kPackEmpty) continue;
+            ++mine;
+            if (cv[j] == kPackEmpty || cv[j] == key[j]) {
+              if (!merge_add(L.C, sl[j], cnt[j])) L.overflow = 1;
+            } else if (!merge_count_at(L, key[j], cnt[j], (sl[j] + 1) & (S - 1))) L.overflow = 1;
           }
         }
       }
     }
-    for (int run = 0; run < (flat ? 0 : n_runs); ++run) {
+    for (int run = 0; run < (FLAT ? 0 : n_runs); ++run) {
       const ImportRun R = runs[run];
       if (R.skip) continue;
       uint64_t i0, i1;
@@ -3158,7 +3189,7 @@ hipError_t launch_import_bounds(const ImportRun* d_runs, int n_runs, uint64_t ma
   return hipGetLastError();
 }
 
-hipError_t launch_import_merge(const FreqTable& T, bool packed, const ImportRun* d_runs, int n_runs, const uint32_t* d_start,
+hipError_t launch_import_merge(const FreqTable& T, bool packed, bool flat, const ImportRun* d_runs, int n_runs, const uint32_t* d_start,
                                const uint32_t* d_end, int table_empty, unsigned long long* d_hist, unsigned long long* d_big,
                                unsigned long long* d_n_big, unsigned long long big_cap, uint32_t* d_smax, int write_all,
                                uint32_t* d_ovf_list, unsigned long long* d_n_ovf, unsigned long long* d_ovf_recs,
@@ -3167,11 +3198,14 @@ hipError_t launch_import_merge(const FreqTable& T, bool packed, const ImportRun*
   if (!table_empty && (d_hist || d_smax || write_all)) return hipErrorInvalidValue;
   AggTrack tr{d_hist, d_big, d_n_big, big_cap, d_smax, write_all};
   const unsigned blocks = grid_for(n_slices, 1, 65536);
-  if (packed)
-    hipLaunchKernelGGL(dq_import_merge_kernel<true>, dim3(blocks), dim3(kMergeThreads), 0, stream, T, d_runs, n_runs, d_start,
-                       d_end, n_slices, table_empty, tr, d_ovf_list, d_n_ovf, d_ovf_recs, d_new_groups);
+  if (packed && flat)
+    hipLaunchKernelGGL((dq_import_merge_kernel<true, true>), dim3(blocks), dim3(kMergeThreads), 0, stream, T, d_runs, n_runs,
+                       d_start, d_end, n_slices, table_empty, tr, d_ovf_list, d_n_ovf, d_ovf_recs, d_new_groups);
+  else if (packed)
+    hipLaunchKernelGGL((dq_import_merge_kernel<true, false>), dim3(blocks), dim3(kMergeThreads), 0, stream, T, d_runs, n_runs,
+                       d_start, d_end, n_slices, table_empty, tr, d_ovf_list, d_n_ovf, d_ovf_recs, d_new_groups);
   else
-    hipLaunchKernelGGL(dq_import_merge_kernel<false>, dim3(blocks), dim3(kMergeThreads), 0, stream, T, d_runs, n_runs, d_start,
+    hipLaunchKernelGGL((dq_import_merge_kernel<false, false>), dim3(blocks), dim3(kMergeThreads), 0, stream, T, d_runs, n_runs, d_start,
                        d_end, n_slices, table_empty, tr, d_ovf_list, d_n_ovf, d_ovf_recs, d_new_groups);
   return hipGetLastError();
 }

@@ -224,6 +224,7 @@ struct WirePacked {
 // One record stream a merge takes in: a part's packed section (kind 0), its general section
 // (kind 1: FreqSlot, READY clear, k0 of a long key = offset in `heap`), or a source table's slot
 // array (kind 2, src_bits = its slice bits).  skip = 1: out of slice order, inserted group by group.
+constexpr int kImportFlatRuns = 16;  // packed runs the import merge takes as one index space
 struct ImportRun {
   const void* recs;
   uint64_t n;
@@ -244,7 +245,7 @@ hipError_t launch_wire_scatter(const FreqTable& T, int n_parts, int chunk_log, u
 hipError_t launch_import_sketch(const ImportRun* d_runs, int n_runs, uint64_t max_n, uint32_t* d_hll, hipStream_t stream);
 hipError_t launch_import_bounds(const ImportRun* d_runs, int n_runs, uint64_t max_n, int rb, uint64_t n_slices,
                                 uint32_t* d_start, uint32_t* d_end, unsigned int* d_unsorted, hipStream_t stream);
-hipError_t launch_import_merge(const FreqTable& T, bool packed, const ImportRun* d_runs, int n_runs, const uint32_t* d_start,
+hipError_t launch_import_merge(const FreqTable& T, bool packed, bool flat, const ImportRun* d_runs, int n_runs, const uint32_t* d_start,
                                const uint32_t* d_end, int table_empty, unsigned long long* d_hist, unsigned long long* d_big,
                                unsigned long long* d_n_big, unsigned long long big_cap, uint32_t* d_smax, int write_all,
                                uint32_t* d_ovf_list, unsigned long long* d_n_ovf, unsigned long long* d_ovf_recs,

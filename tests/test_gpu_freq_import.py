@@ -146,6 +146,36 @@ def test_merge_tables(gpu, sizes):
         t.close()
 
 
+@pytest.mark.parametrize("n_parts", [2, 20])
+def test_import_wide_weights(gpu, n_parts):
+    """Packed runs (digit keys only) imported twice over in one call -- 2 parts take the flat
+    merge (one index space over <= 16 runs), 20 parts the run-by-run merge -- with weights that do
+    not fit the LDS image's 32-bit counts: one record of 2^33 + 3 and one of 2^32 - 16 whose double
+    wraps 32 bits.  Their slices take the overflow path (64-bit, group by group): exact counts."""
+    import torch
+    keys_in = ["%d" % (v % 50000) for v in range(120000)]
+    t = _table({"key": ["string", keys_in]}, batches=1)
+    want = _want({"key": ["string", keys_in]})
+    buf, keys, pp, pg, pk = _parts(t, n_parts)
+    assert sum(pg) == 0 and sum(pk) == 0 and pp[0] >= 2
+    recs = buf[:16 * sum(pp)].view(torch.int64).view(-1, 2)
+    wide = {0: (1 << 33) + 3, 1: (1 << 32) - 16}
+    for i, w in wide.items():
+        recs[i, 1] = w
+    o = FrequencyTable.like(t)
+    o.import_parts(torch.cat([buf[:16 * sum(pp)]] * 2), pp * 2, pg * 2, keys, pk * 2)
+    got = _groups(o)
+    assert len(got) == len(want)
+    changed = 0
+    for k, c in want.items():
+        if got[k] != 2 * c:
+            changed += 1
+            assert got[k] in (2 * wide[0], 2 * wide[1]), (k, got[k])
+    assert changed == 2 and sorted(v for v in got.values() if v > 1 << 31) == sorted(2 * w for w in wide.values())
+    o.close()
+    t.close()
+
+
 def test_import_slices_overflow_lds(gpu, monkeypatch):
     """A destination forced far too small (DQ_FREQ_PART_SLOTS: 2^20 slots for 2M keys, ~4000 per
     2048-slot slice): every slice overflows its LDS image, is listed, the table grows, and the
