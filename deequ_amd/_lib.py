@@ -157,6 +157,8 @@ SIGNATURES = {
     "dq_freq_merge": (c_int, [c_void_p, c_void_p]),
     "dq_freq_import": (c_int, [c_void_p, POINTER(DqFreqGroup), c_int64, c_void_p, c_int64]),
     "dq_cast_utf8": (c_int, [c_void_p, POINTER(DqColumn), c_int64, c_int32, c_void_p, c_void_p, POINTER(c_int64)]),
+    "dq_cast_utf8_batch": (c_int, [c_void_p, c_int32, POINTER(DqColumn), c_int64, POINTER(c_int32),
+                                   POINTER(c_void_p), POINTER(c_void_p)]),
     "dq_freq_partition": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_void_p, c_int64, POINTER(c_int64),
                                   POINTER(c_int64), POINTER(c_int64)]),
     "dq_freq_import_parts": (c_int, [c_void_p, c_int, c_void_p, POINTER(c_int64), POINTER(c_int64), c_void_p,

@@ -22,7 +22,8 @@ from .metrics import (DoubleMetric, Entity, Failure, IllegalAnalyzerParameterExc
                       NoSuchColumnException, NumberOfSpecifiedColumnsException,
                       WrongColumnTypeException, empty_state_exception, metric_from_failure,
                       metric_from_value, wrap_if_necessary)
-from .states import State, merge
+from . import engine as _engine
+from .states import State, merge, state_from_dq
 
 NUMERIC_TYPES = ("int8", "int16", "int32", "int64", "float32", "float64")
 
@@ -138,13 +139,10 @@ class ScanShareableAnalyzer(Analyzer):
     where: Optional[str] = None
 
     def aggregationFunctions(self, schema):
-        from .engine import op_spec_for
-        return op_spec_for(self, schema)
+        return _engine.op_spec_for(self, schema)
 
     def fromAggregationResult(self, raw) -> Optional[State]:
-        from .engine import OpUnsupported
-        from .states import state_from_dq
-        if isinstance(raw, OpUnsupported):
+        if isinstance(raw, _engine.OpUnsupported):
             raise raw.error
         return state_from_dq(raw)
 
@@ -743,3 +741,34 @@ def _udf_result_to_string(b) -> str:
     if isinstance(b, float):
         return spark_cast_to_string(b, "float64")
     return str(b)
+
+
+def _memoise_hashes() -> None:
+    """Analyzers are frozen dataclasses: their hash never changes, but the generated __hash__
+    rebuilds and hashes the field tuple on every call, and a profiler run keys several dicts by
+    hundreds of analyzers.  Each class's hash is computed once per instance and kept, with the
+    class mixed in: Completeness(c), Mean(c), Sum(c) ... have equal field tuples, so without it
+    they collide in every dict and each insert pays two __eq__ calls."""
+    def caching(h):
+        def __hash__(self):
+            try:
+                return self.__dict__["_dq_hash"]
+            except KeyError:
+                v = hash((type(self).__qualname__, h(self)))
+                object.__setattr__(self, "_dq_hash", v)
+                return v
+        __hash__._dq_cached = True
+        return __hash__
+    stack, seen = [Analyzer], set()
+    while stack:
+        for sub in stack.pop().__subclasses__():
+            if sub in seen:
+                continue
+            seen.add(sub)
+            stack.append(sub)
+            h = sub.__dict__.get("__hash__")
+            if h is not None and not getattr(h, "_dq_cached", False):
+                sub.__hash__ = caching(h)
+
+
+_memoise_hashes()

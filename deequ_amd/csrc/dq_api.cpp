@@ -767,11 +767,20 @@ struct dq_plan : Stager {
   // host batches: staging slot k % 2, filled on copy_stream while the previous batch scans
   uint64_t batch_seq = 0;
   hipEvent_t copy_done[2] = {nullptr, nullptr}, scan_done[2] = {nullptr, nullptr};
+  // the fused string pass runs on side_stream beside the value scans of the same batch (both are
+  // issue- / latency-bound, so the CUs interleave them); `stream` waits for it before the batch's
+  // scan_done, so every later use of the batch's descriptors stays ordered after it
+  hipStream_t side_stream = nullptr;
+  hipEvent_t side_ready = nullptr, side_done = nullptr;
 
   ~dq_plan() {
     if (stream) {
       (void)hipStreamSynchronize(stream);
     }
+    if (side_stream) (void)hipStreamSynchronize(side_stream);
+    if (side_ready) (void)hipEventDestroy(side_ready);
+    if (side_done) (void)hipEventDestroy(side_done);
+    if (side_stream) StreamPool::get().release(device, side_stream);
     if (copy_stream) (void)hipStreamSynchronize(copy_stream);
     for (int k = 0; k < 2; ++k) {
       if (copy_done[k]) (void)hipEventDestroy(copy_done[k]);
@@ -1119,6 +1128,12 @@ extern "C" dq_status dq_plan_create(dq_ctx* ctx, const dq_op* ops, int n_ops,
     if (e == hipSuccess) e = hipEventCreateWithFlags(&plan->scan_done[k], hipEventDisableTiming);
   }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&plan->desc_done, hipEventDisableTiming);
+  const char* side_env = std::getenv("DQ_PLAN_SIDE");  // 0: the string pass on the plan's stream (A/B)
+  if (e == hipSuccess && !plan->str_tasks.empty() && !(side_env && side_env[0] == '0')) {
+    e = StreamPool::get().acquire(ctx->device, &plan->side_stream);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&plan->side_ready, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&plan->side_done, hipEventDisableTiming);
+  }
   plan->h_desc_size = std::max(1, n_columns) * sizeof(DevColumn) +
                       std::max<size_t>(1, plan->programs.size()) * sizeof(DevMask) +
                       std::max<size_t>(1, plan->scan_tasks.size()) * sizeof(PartRange);
@@ -1398,6 +1413,22 @@ extern "C" dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, in
                              static_cast<uint64_t*>(plan->d_mask_words.ptr), plan->mask_words, plan->pred_cast,
                              plan->stream));
 
+  const int n_str = (int)plan->str_tasks.size();
+  // the string pass first, on the side stream when there is other work to run beside it
+  const bool side = n_str > 0 && plan->side_stream && (n_scan > 0 || !plan->hll_launch.empty());
+  if (n_str > 0) {
+    hipStream_t ss = side ? plan->side_stream : plan->stream;
+    if (side) {
+      DQ_HIP(hipEventRecord(plan->side_ready, plan->stream));
+      DQ_HIP(hipStreamWaitEvent(ss, plan->side_ready, 0));
+    }
+    int64_t bpt = std::max<int64_t>(1, plan->target_blocks / n_str);
+    bpt = std::min<int64_t>(bpt, chunks);
+    DQ_HIP(launch_string_pass(static_cast<const StrTask*>(plan->d_str.ptr), n_str, d_cols, d_masks, n_rows, (int)bpt,
+                              static_cast<uint32_t*>(plan->d_regs.ptr),
+                              static_cast<unsigned long long*>(plan->d_dtype_counts.ptr), ss));
+    if (side) DQ_HIP(hipEventRecord(plan->side_done, ss));
+  }
   if (n_scan > 0) {
     ScanAcc* parts = static_cast<ScanAcc*>(plan->d_partials.ptr);
     const ScanTask* d_tasks = static_cast<const ScanTask*>(plan->d_tasks.ptr);
@@ -1415,14 +1446,6 @@ extern "C" dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, in
     }
     DQ_HIP(launch_scan_reduce(parts, static_cast<const PartRange*>(plan->d_ranges.ptr), n_scan,
                               static_cast<ScanAcc*>(plan->d_acc.ptr), plan->stream));
-  }
-  const int n_str = (int)plan->str_tasks.size();
-  if (n_str > 0) {
-    int64_t bpt = std::max<int64_t>(1, plan->target_blocks / n_str);
-    bpt = std::min<int64_t>(bpt, chunks);
-    DQ_HIP(launch_string_pass(static_cast<const StrTask*>(plan->d_str.ptr), n_str, d_cols, d_masks, n_rows, (int)bpt,
-                              static_cast<uint32_t*>(plan->d_regs.ptr),
-                              static_cast<unsigned long long*>(plan->d_dtype_counts.ptr), plan->stream));
   }
   const int n_hll = (int)plan->hll_launch.size();
   if (n_hll > 0) {
@@ -1454,6 +1477,7 @@ extern "C" dq_status dq_plan_consume(dq_plan* plan, const dq_column* columns, in
                        static_cast<CorrAcc*>(plan->d_corr_part.ptr), static_cast<CorrAcc*>(plan->d_corr_acc.ptr),
                        plan->stream));
   }
+  if (side) DQ_HIP(hipStreamWaitEvent(plan->stream, plan->side_done, 0));
   plan->total_rows += n_rows;
   DQ_HIP(hipEventRecord(plan->scan_done[slot], plan->stream));
   ++plan->batch_seq;
@@ -1909,6 +1933,53 @@ extern "C" dq_status dq_cast_utf8(dq_ctx* ctx, const dq_column* src, int64_t n_r
   st.stream = nullptr;
   if (s != DQ_OK) return s;
   if (e != hipSuccess) return fail(DQ_ERR_DEVICE, std::string("dq_cast_utf8: ") + hipGetErrorString(e));
+  return DQ_OK;
+}
+
+// Several columns cast in one call (the profiler's pass 2 casts every string column pass 1 typed
+// numeric): the casts alternate over two pooled streams and the call waits once, instead of one
+// launch + one synchronisation per column.
+extern "C" dq_status dq_cast_utf8_batch(dq_ctx* ctx, int32_t n, const dq_column* srcs, int64_t n_rows,
+                                        const int32_t* to_types, void* const* d_values,
+                                        uint8_t* const* d_validity) {
+  if (!ctx || n < 0 || (n > 0 && (!srcs || !to_types || !d_values || !d_validity)))
+    return fail(DQ_ERR_INVALID, "NULL argument");
+  for (int32_t i = 0; i < n; ++i) {
+    if (srcs[i].type != DQ_T_UTF8) return fail(DQ_ERR_INVALID, "dq_cast_utf8_batch needs utf8 columns");
+    if (to_types[i] != DQ_T_INT64 && to_types[i] != DQ_T_FLOAT64)
+      return fail(DQ_ERR_UNSUPPORTED, "cast target must be int64 or float64");
+    if (n_rows > 0 && (!d_values[i] || !d_validity[i])) return fail(DQ_ERR_INVALID, "NULL output buffer");
+  }
+  if (n_rows < 0) return fail(DQ_ERR_INVALID, "bad n_rows");
+  for (int32_t i = 0; i < n; ++i)
+    if (srcs[i].length < n_rows) return fail(DQ_ERR_INVALID, "bad n_rows");
+  if (n == 0 || n_rows == 0) return DQ_OK;
+  DQ_HIP(hipSetDevice(ctx->device));
+  constexpr int kLanes = 2;
+  Stager st[kLanes];
+  dq_status s = DQ_OK;
+  hipError_t e = hipSuccess;
+  int acquired = 0;
+  for (; acquired < kLanes && e == hipSuccess; ++acquired) {
+    e = StreamPool::get().acquire(ctx->device, &st[acquired].stream);
+    if (e != hipSuccess) break;
+    st[acquired].col_types.assign((size_t)n, DQ_T_UTF8);
+    st[acquired].resize_stage(n);
+  }
+  for (int32_t i = 0; i < n && e == hipSuccess && s == DQ_OK; ++i) {
+    Stager& L = st[i % kLanes];
+    DevColumn dc;
+    s = prepare_column(&L, i, srcs[i], n_rows, &dc);
+    if (s == DQ_OK) e = launch_cast_utf8(dc, n_rows, to_types[i], d_values[i], d_validity[i], L.stream);
+  }
+  for (int k = 0; k < acquired; ++k) {
+    const hipError_t w = hipStreamSynchronize(st[k].stream);
+    if (e == hipSuccess) e = w;
+    StreamPool::get().release(ctx->device, st[k].stream);
+    st[k].stream = nullptr;
+  }
+  if (s != DQ_OK) return s;
+  if (e != hipSuccess) return fail(DQ_ERR_DEVICE, std::string("dq_cast_utf8_batch: ") + hipGetErrorString(e));
   return DQ_OK;
 }
 

@@ -95,11 +95,17 @@ def pack_ops(specs: Sequence[OpSpec]) -> bytes:
 
 
 _SCHEMA_CACHE: Dict[tuple, tuple] = {}
+_SCHEMA_BY_ID: Dict[int, tuple] = {}
 
 
 def _schema_info(schema: Dict[str, str]):
     """(name -> (index, dtype), dq type codes) of a schema, memoised on its contents: a profiler
-    run builds hundreds of ops over the same 100-column schema."""
+    run builds hundreds of ops over the same 100-column schema.  A table's schema dict is fixed,
+    so the same dict object is answered by identity (it is kept referenced, so its id stays its
+    own) without rebuilding the content key."""
+    e = _SCHEMA_BY_ID.get(id(schema))
+    if e is not None and e[0] is schema and e[1] == len(schema):
+        return e[2]
     key = tuple(schema.items())
     hit = _SCHEMA_CACHE.get(key)
     if hit is None:
@@ -109,6 +115,9 @@ def _schema_info(schema: Dict[str, str]):
         if len(_SCHEMA_CACHE) > 256:
             _SCHEMA_CACHE.clear()
         _SCHEMA_CACHE[key] = hit
+    if len(_SCHEMA_BY_ID) > 256:
+        _SCHEMA_BY_ID.clear()
+    _SCHEMA_BY_ID[id(schema)] = (schema, len(schema), hit)
     return hit
 
 
@@ -129,12 +138,29 @@ def op_spec_for(analyzer, schema: Dict[str, str]) -> OpSpec:
     return OpSpec(kind, idx[analyzer.column][0], None, where)
 
 
+_SUPPORTED: Dict[tuple, bool] = {}
+
+
 def op_supported(spec: OpSpec, schema: Dict[str, str]) -> None:
-    """Raises UnsupportedOnGpu / DeequAmdError if the op is not GPU-eligible."""
+    """Raises UnsupportedOnGpu / DeequAmdError if the op is not GPU-eligible.  The answer for an
+    op without predicate programs depends only on (kind, column types), so accepted ones are
+    remembered: a profiler run checks hundreds of such ops, again on every run."""
     types = _schema_info(schema)[1]
+    key = None
+    if spec.predicate is None and spec.where is None:
+        n = len(schema)
+        t1 = types[spec.column] if 0 <= spec.column < n else None
+        t2 = types[spec.column2] if 0 <= spec.column2 < n else None
+        key = (spec.kind, spec.column, spec.column2, n, t1, t2)
+        if key in _SUPPORTED:
+            return
     op = L.DqOp()
     spec.fill(op)
     L.check(L.lib().dq_op_supported(ctypes.byref(op), types, len(schema)))
+    if key is not None:
+        if len(_SUPPORTED) > 65536:
+            _SUPPORTED.clear()
+        _SUPPORTED[key] = True
 
 
 class Plan:

@@ -261,6 +261,33 @@ def cast_string_column(col, to_dtype: str, device: Optional[int] = None):
     return Column(to_dtype, n, vals, valid, device=True)
 
 
+def cast_string_columns(cols, to_dtypes, device: Optional[int] = None):
+    """cast_string_column over several columns of one batch in ONE library call
+    (dq_cast_utf8_batch: the casts overlap on the device, one wait for all)."""
+    import torch
+    from .engine import current_device
+    from .table import Column
+    dev_idx = current_device() if device is None else device
+    dev = torch.device("cuda", dev_idx)
+    n = len(cols)
+    if n == 0:
+        return []
+    rows = cols[0].length
+    if any(c.length != rows for c in cols):
+        raise ValueError("cast_string_columns: columns of one batch have one length")
+    outs = []
+    for t in to_dtypes:
+        vals = torch.empty(max(1, rows), dtype=torch.int64 if t == "int64" else torch.float64, device=dev)
+        valid = torch.empty((rows + 7) // 8 + 8, dtype=torch.uint8, device=dev)
+        outs.append((vals, valid))
+    srcs = (L.DqColumn * n)(*[c.to_dq() for c in cols])
+    types = (ctypes.c_int32 * n)(*[L.TYPE_CODES[t] for t in to_dtypes])
+    vptr = (ctypes.c_void_p * n)(*[v.data_ptr() for v, _ in outs])
+    bptr = (ctypes.c_void_p * n)(*[b.data_ptr() for _, b in outs])
+    L.check(L.lib().dq_cast_utf8_batch(L.Context.get(dev_idx).handle, n, srcs, rows, types, vptr, bptr))
+    return [Column(t, rows, v, b, device=True) for t, (v, b) in zip(to_dtypes, outs)]
+
+
 def _cast_numeric_string_columns(columns, data, generic):
     """castNumericStringColumns (:427-445): string columns typed Integral -> LongType, Fractional
     -> DoubleType.  (Numeric columns keep their type: the reference's cast of them is value
@@ -296,9 +323,11 @@ def _cast_batches(data, targets):
     for batch in data.batches():
         if isinstance(batch, ArrowBatch):  # zero-copy host view of the record batch
             batch = Table.from_arrow(batch.batch)
+        names = [name for name in batch.columns if name in targets]
+        casted = dict(zip(names, cast_string_columns([batch.columns[n] for n in names], [targets[n] for n in names])))
         cols = OrderedDict()
         for name, col in batch.columns.items():
-            cols[name] = cast_string_column(col, targets[name]) if name in targets else col
+            cols[name] = casted.get(name, col)
         parts.append(Table(cols))
     return parts[0] if len(parts) == 1 else PartitionedTable(parts)
 

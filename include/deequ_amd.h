@@ -337,6 +337,12 @@ uint64_t dq_xxh64(const void* data, size_t len, uint64_t seed);
 dq_status dq_cast_utf8(dq_ctx* ctx, const dq_column* src, int64_t n_rows, int32_t to_type,
                        void* d_values, uint8_t* d_validity, int64_t* n_unsupported);
 
+/* dq_cast_utf8 of n columns of n_rows rows each in one call (castNumericStringColumns casts every
+ * string column pass 1 typed numeric): column i (utf8) -> to_types[i] into d_values[i] /
+ * d_validity[i].  The casts overlap on the device; the call returns when all are done. */
+dq_status dq_cast_utf8_batch(dq_ctx* ctx, int32_t n, const dq_column* srcs, int64_t n_rows,
+                             const int32_t* to_types, void* const* d_values, uint8_t* const* d_validity);
+
 /* ---------------------------------------------------------------- frequency group-by
  * Replaces FrequencyBasedAnalyzer.computeFrequencies (GroupingAnalyzers.scala:53-80) and the
  * group-by of Histogram (Histogram.scala:54-69).  A dq_freq is the device-resident state
