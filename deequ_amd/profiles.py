@@ -386,11 +386,13 @@ def compute_histograms(data, target_columns: Sequence[str],
     schema = data.schema
     out = {}
     bool_cols = [c for c in target_columns if schema[c] == "bool" and _IDENT.match(c)]
-    if bool_cols:
-        out.update(_bool_histograms(data, bool_cols))
+    order = list(bool_cols)  # (the boolean columns' histograms first, as computed sequentially)
     from .distributed import is_sharded
     from .engine import current_device
-    rest = [c for c in target_columns if c not in out]
+    rest = [c for c in target_columns if c not in bool_cols]
+    if bool_cols and (is_sharded(data) or len(rest) <= 1):
+        out.update(_bool_histograms(data, bool_cols))
+        bool_cols = []
     if is_sharded(data):  # the key-hash exchanged table of the whole dataset (collective, in order)
         from .frequencies import compute_frequencies
         for c in rest:
@@ -417,12 +419,16 @@ def compute_histograms(data, target_columns: Sequence[str],
         return out
     # Each table has its own HIP stream and the library releases the GIL in every call, so the
     # group-bys of several columns run concurrently on the device (each alone is latency-bound:
-    # few groups, LDS pre-aggregation).  Results are per column, so the order does not matter.
+    # few groups, LDS pre-aggregation), and beside them the boolean columns' fused scan (its own
+    # plan and stream).  Results are per column, so the order does not matter.
     from concurrent.futures import ThreadPoolExecutor
-    with ThreadPoolExecutor(max_workers=min(len(rest), 8)) as ex:
+    with ThreadPoolExecutor(max_workers=min(len(rest) + (1 if bool_cols else 0), 8)) as ex:
+        bools = ex.submit(_bool_histograms, data, bool_cols) if bool_cols else None
         for c, dist in zip(rest, ex.map(one, rest)):
             out[c] = dist
-    return out
+        if bools is not None:
+            out.update(bools.result())
+    return {c: out[c] for c in order + rest}
 
 
 def _histogram_distribution(counts, keys, dtype) -> Distribution:

@@ -178,6 +178,34 @@ def test_cast_to_long_random_digit_strings(gpu):
     assert got == [_spark_to_long(v) for v in vals]
 
 
+def test_cast_batch_equals_single_casts(gpu):
+    """dq_cast_utf8_batch (pass 2's casts in one call, alternating over two streams) writes exactly
+    what one dq_cast_utf8 per column writes: long and double targets mixed, NULLs, junk, the
+    heap's last bytes, an odd column count."""
+    from deequ_amd.profiles import cast_string_columns
+    rng = np.random.default_rng(77)
+    alpha = "0123456789" * 6 + "-+.eE a"
+    cols, targets = [], []
+    for k in range(5):
+        vals = []
+        for _ in range(3001):
+            s = "".join(alpha[int(rng.integers(0, len(alpha)))] for _ in range(int(rng.integers(0, 19))))
+            vals.append(None if rng.random() < 0.05 else s)
+        vals[-1] = "12345"  # a string ending exactly at the heap end
+        cols.append(d.Column.from_pylist(vals, "string"))
+        targets.append("int64" if k % 2 == 0 else "float64")
+    got = cast_string_columns(cols, targets)
+    for c, t, g in zip(cols, targets, got):
+        want = cast_string_column(c, t)
+        assert g.dtype == t
+        a, b = g.to_pylist(), want.to_pylist()
+        if t == "int64":
+            assert a == b
+        else:
+            assert [None if x is None else struct.pack("<d", x) for x in a] == \
+                   [None if x is None else struct.pack("<d", x) for x in b]
+
+
 def test_cast_to_double_matches_java(gpu):
     rng = np.random.default_rng(9)
     vals = ["1.5", "-0.25", ".5", "5.", ".", "-.", "", "  2.0  ", "- 1.5", "+3", "1e3", "1E-3", "2.5f", "7d",

@@ -16,6 +16,11 @@ for r in 1 2; do
     echo "side=$side $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/r04_c5ab_$side.log)"
   done
 done
+for side in 1 0; do
+  DQ_PLAN_SIDE=$side timeout -k 10 200 python -u bench.py --workload c1 --steps 20 --warmup 3 --no-cpu-baseline \
+    > gpurun_out/r04_c1ab_$side.log 2>&1 || exit $?
+  echo "c1 side=$side $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/r04_c1ab_$side.log)"
+done
 if [ "${SPANS:-1}" = 1 ]; then
   SPANS=1 timeout -k 10 300 python -u tools/prof_host.py c5 > gpurun_out/r04_spans_c5b.txt 2>&1 || exit $?
   grep -v amdgpu.ids gpurun_out/r04_spans_c5b.txt | tail -20
