@@ -420,6 +420,9 @@ __device__ inline bool cast_one(const Src& p, int32_t n, int64_t* lv, double* dv
 // are stored by its first lane -- one 8-byte word when the wave's rows are all in range.  One
 // instantiation per target type: the string -> long cast does not carry the double parser's
 // registers (its exact big-number path) into its occupancy.
+#ifndef DQ_CAST_PIPE
+#define DQ_CAST_PIPE 1
+#endif
 template <int TO>
 __global__ __launch_bounds__(kBlock) void dq_cast_utf8_kernel(DevColumn src, int64_t n_rows, void* values,
                                                               uint8_t* validity) {
@@ -434,19 +437,35 @@ __global__ __launch_bounds__(kBlock) void dq_cast_utf8_kernel(DevColumn src, int
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vals), 0, (int)heap_end, 0x00020000);
   const __amdgpu_buffer_rsrc_t ro =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(src.offsets), 0, (int)(4u * (uint32_t)(n_rows + 1)), 0x00020000);
-  for (int64_t base = (int64_t)blockIdx.x * kBlock * U; base < n_rows; base += (int64_t)gridDim.x * kBlock * U) {
-    uint32_t ob[U], oe[U], sh[U], sel = 0u;
-    uint64_t w[U][3];
+  // the offsets and validity bits of the NEXT step are loaded while this step's strings load and
+  // parse (DQ_CAST_PIPE): the offsets -> string bytes round trip is paid once per step, not twice
+  const int64_t stride = (int64_t)gridDim.x * kBlock * U;
+  uint32_t ob[U], oe[U], sel = 0u;
+  auto load_offs = [&](int64_t base, uint32_t (&b)[U], uint32_t (&e)[U], uint32_t& sl) {
+    sl = 0u;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t row = base + (int64_t)u * kBlock + threadIdx.x;
       const auto o = __builtin_amdgcn_raw_buffer_load_b64(ro, (int)(4u * (uint32_t)row), 0, 0);
-      ob[u] = o[0];
-      oe[u] = o[1];
-      if (row < n_rows && (src.validity == nullptr || bit_at(src.validity, row))) sel |= 1u << u;
+      b[u] = o[0];
+      e[u] = o[1];
+      if (row < n_rows && (src.validity == nullptr || bit_at(src.validity, row))) sl |= 1u << u;
     }
+  };
+  if ((int64_t)blockIdx.x * kBlock * U < n_rows) load_offs((int64_t)blockIdx.x * kBlock * U, ob, oe, sel);
+  for (int64_t base = (int64_t)blockIdx.x * kBlock * U; base < n_rows; base += stride) {
+    uint32_t sh[U];
+    uint64_t w[U][3];
+#if DQ_CAST_PIPE
 #pragma unroll
     for (int u = 0; u < U; ++u) sh[u] = load24(rs, vals, heap_end, ob[u], w[u]);
+    uint32_t nob[U], noe[U], nsel = 0u;
+    if (base + stride < n_rows) load_offs(base + stride, nob, noe, nsel);
+#else
+    if (base != (int64_t)blockIdx.x * kBlock * U) load_offs(base, ob, oe, sel);
+#pragma unroll
+    for (int u = 0; u < U; ++u) sh[u] = load24(rs, vals, heap_end, ob[u], w[u]);
+#endif
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t row = base + (int64_t)u * kBlock + threadIdx.x;
@@ -476,6 +495,14 @@ __global__ __launch_bounds__(kBlock) void dq_cast_utf8_kernel(DevColumn src, int
         }
       }
     }
+#if DQ_CAST_PIPE
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      ob[u] = nob[u];
+      oe[u] = noe[u];
+    }
+    sel = nsel;
+#endif
   }
 }
 
