@@ -297,8 +297,21 @@ __global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* _
   const uint32_t heap_end = (uint32_t)col.offsets[n_rows];
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vals), 0, (int)heap_end, 0x00020000);
   uint64_t c[5] = {0, 0, 0, 0, 0};
+  // the five type counts of this lane as 12-bit fields of one word (count k at bit 12 k: one
+  // shift and one 64-bit add per row), folded into c[] before a field can reach 4096
+  uint64_t packed = 0ull;
+  uint32_t since_fold = 0u;
   constexpr int U = DQ_STR_U;
   for (int64_t base = r0 + threadIdx.x; base < r1; base += U * kBlock) {
+    if constexpr (DT) {
+      if (since_fold >= 4096u - U) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) c[i] += (packed >> (12 * i)) & 0xFFFull;
+        packed = 0ull;
+        since_fold = 0u;
+      }
+      since_fold += U;
+    }
     int32_t ob[U], oe[U];
     uint32_t sel[U], sh[U];
     uint64_t w[U][3];
@@ -329,10 +342,7 @@ __global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* _
         k = (DT && sel[u]) ? classify_utf8(PtrSrc{vals + ob[u]}, n) : DT_NULL;
         h = xxh64_utf8_dev(vals + ob[u], (uint32_t)n);
       }
-      if constexpr (DT) {
-#pragma unroll
-        for (int i = 0; i < 5; ++i) c[i] += (k == i) ? 1u : 0u;
-      }
+      if constexpr (DT) packed += 1ull << (12u * (uint32_t)k);
       uint32_t idx, nlz, r;
       hll_slot(h, idx, nlz);
       asm("v_mad_u32_u24 %0, %1, %2, %2" : "=v"(r) : "v"(nlz), "v"(sel[u]));  // rank * sel
@@ -342,7 +352,7 @@ __global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* _
   if constexpr (DT) {
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
-      const uint64_t s = wave_sum(c[i]);
+      const uint64_t s = wave_sum(c[i] + ((packed >> (12 * i)) & 0xFFFull));
       if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6][i] = s;
     }
   }
