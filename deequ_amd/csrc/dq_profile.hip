@@ -247,9 +247,19 @@ __device__ inline uint64_t ld_bytes(const uint8_t* p, uint32_t n) {
 // 24 bytes lands s = a - lo bytes into the words (s + n <= 24; returned): load24_fix shifts it
 // down once the words have arrived (no memory access in that rare branch).  A heap of fewer than
 // 24 bytes (uniform) is read byte-exactly.  The bytes past a string's end are not used.
+// n = the string's length: a string of at most 16 bytes takes ONE 16-byte load at
+// min(a, heap_end - 16) (w[2] = 0), so the common short string costs one memory instruction.
 __device__ __forceinline__ uint32_t load24(__amdgpu_buffer_rsrc_t rs, const uint8_t* vals, uint32_t heap_end, uint32_t a,
-                                           uint64_t (&w)[3]) {
+                                           uint32_t n, uint64_t (&w)[3]) {
   if (heap_end >= 24u) {
+    if (n <= 16u) {
+      const uint32_t lo = min(a, heap_end - 16u);
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)lo, 0, 0);
+      w[0] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+      w[1] = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
+      w[2] = 0ull;
+      return a - lo;
+    }
     const uint32_t lo = min(a, heap_end - 24u);
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)lo, 0, 0);
     const auto x = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(lo + 16u), 0, 0);
@@ -293,6 +303,9 @@ __global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* _
   const DevColumn& col = cols[task.column];
   const uint8_t* wt = task.where_mask >= 0 ? reinterpret_cast<const uint8_t*>(masks[task.where_mask].t) : nullptr;
   const uint8_t* vals = static_cast<const uint8_t*>(col.values);
+  // each row's offset pair as one 8-byte buffer load, relative to the block's first row
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int32_t*>(col.offsets + r0), 0, (int)(4u * (uint32_t)(r1 - r0 + 1)), 0x00020000);
   // the first 24 bytes of each string as three words (load24: unaligned, from its first byte)
   const uint32_t heap_end = (uint32_t)col.offsets[n_rows];
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vals), 0, (int)heap_end, 0x00020000);
@@ -320,12 +333,13 @@ __global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* _
       const int64_t row = base + (int64_t)u * kBlock;
       const bool in = row < r1;
       const int64_t rr = in ? row : r0;
-      ob[u] = col.offsets[rr];
-      oe[u] = col.offsets[rr + 1];
+      const auto o = __builtin_amdgcn_raw_buffer_load_b64(ro, (int)(4u * (uint32_t)(rr - r0)), 0, 0);
+      ob[u] = (int32_t)o[0];
+      oe[u] = (int32_t)o[1];
       sel[u] = (in && (col.validity == nullptr || bit_at(col.validity, rr)) && (wt == nullptr || bit_at(wt, rr))) ? 1u : 0u;
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) sh[u] = load24(rs, vals, heap_end, (uint32_t)ob[u], w[u]);
+    for (int u = 0; u < U; ++u) sh[u] = load24(rs, vals, heap_end, (uint32_t)ob[u], (uint32_t)(oe[u] - ob[u]), w[u]);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t row = base + (int64_t)u * kBlock;
@@ -468,13 +482,13 @@ __global__ __launch_bounds__(kBlock) void dq_cast_utf8_kernel(DevColumn src, int
     uint64_t w[U][3];
 #if DQ_CAST_PIPE
 #pragma unroll
-    for (int u = 0; u < U; ++u) sh[u] = load24(rs, vals, heap_end, ob[u], w[u]);
+    for (int u = 0; u < U; ++u) sh[u] = load24(rs, vals, heap_end, ob[u], oe[u] - ob[u], w[u]);
     uint32_t nob[U], noe[U], nsel = 0u;
     if (base + stride < n_rows) load_offs(base + stride, nob, noe, nsel);
 #else
     if (base != (int64_t)blockIdx.x * kBlock * U) load_offs(base, ob, oe, sel);
 #pragma unroll
-    for (int u = 0; u < U; ++u) sh[u] = load24(rs, vals, heap_end, ob[u], w[u]);
+    for (int u = 0; u < U; ++u) sh[u] = load24(rs, vals, heap_end, ob[u], oe[u] - ob[u], w[u]);
 #endif
 #pragma unroll
     for (int u = 0; u < U; ++u) {
