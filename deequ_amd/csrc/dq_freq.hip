@@ -2330,10 +2330,11 @@ __global__ __launch_bounds__(kBlock) void dq_freq_pack_probe_kernel(FreqKeySpec 
                                                                     int64_t n_rows, unsigned long long* out) {
   const DevColumn& c = cols[ks.key_cols[0]];
   const int64_t samples = n_rows < kPackProbe ? n_rows : kPackProbe;
-  const int64_t stride = n_rows / samples;
   uint32_t bad = 0u;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < samples; i += (int64_t)gridDim.x * kBlock) {
-    const int64_t row = i * stride;
+    // scattered rows (a multiplicative hash of i), not a fixed stride: a periodic key pattern
+    // would alias with a stride
+    const int64_t row = samples == n_rows ? i : (int64_t)(((uint64_t)i * 11400714819323198485ull) % (uint64_t)n_rows);
     if (c.validity != nullptr && !((c.validity[row >> 3] >> (row & 7)) & 1u)) continue;
     const uint8_t* v = static_cast<const uint8_t*>(c.values) + c.offsets[row];
     const uint32_t n = (uint32_t)(c.offsets[row + 1] - c.offsets[row]);
