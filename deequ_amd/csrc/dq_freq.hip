@@ -2321,6 +2321,46 @@ hipError_t launch_freq_part(const void* d_in, uint64_t in_n, const unsigned long
   return hipGetLastError();
 }
 
+// Whether a single-utf8-key staging should pack its keys (dq_keypack.h): a strided sample of
+// the batch's rows (kPackProbe of them) is checked, and out[0] counts the sampled non-NULL keys
+// that do not pack (longer than 15 bytes or not a digit string).  A batch whose keys mostly do
+// not pack would fill the packed stage's overflow list and be staged twice.
+constexpr int kPackProbe = 16384;
+__global__ __launch_bounds__(kBlock) void dq_freq_pack_probe_kernel(FreqKeySpec ks, const DevColumn* __restrict__ cols,
+                                                                    int64_t n_rows, unsigned long long* out) {
+  const DevColumn& c = cols[ks.key_cols[0]];
+  const int64_t samples = n_rows < kPackProbe ? n_rows : kPackProbe;
+  uint32_t bad = 0u;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < samples; i += (int64_t)gridDim.x * kBlock) {
+    // scattered rows (a multiplicative hash of i), not a fixed stride: a periodic key pattern
+    // would alias with a stride
+    const int64_t row = samples == n_rows ? i : (int64_t)(((uint64_t)i * 11400714819323198485ull) % (uint64_t)n_rows);
+    if (c.validity != nullptr && !((c.validity[row >> 3] >> (row & 7)) & 1u)) continue;
+    const uint8_t* v = static_cast<const uint8_t*>(c.values) + c.offsets[row];
+    const uint32_t n = (uint32_t)(c.offsets[row + 1] - c.offsets[row]);
+    if (n > 15u) {
+      ++bad;
+      continue;
+    }
+    uint64_t k0 = 0ull, k1 = 0ull, p;
+    for (uint32_t b = 0; b < n; ++b) {
+      const uint64_t x = (uint64_t)v[b];
+      if (b < 8u) k0 |= x << (8u * b);
+      else k1 |= x << (8u * (b - 8u));
+    }
+    if (!kp_pack_record(k0, k1, n, &p)) ++bad;
+  }
+  if (bad) atomicAdd(out, (unsigned long long)bad);
+}
+
+hipError_t launch_freq_pack_probe(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, unsigned long long* d_out,
+                                  hipStream_t stream) {
+  if (n_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(dq_freq_pack_probe_kernel, dim3((kPackProbe + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, ks,
+                     d_cols, n_rows, d_out);
+  return hipGetLastError();
+}
+
 hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, bool packed, const DevColumn* d_cols,
                                   int64_t n_rows, int b1, void* d_out,
                                   uint64_t cap1, unsigned long long* d_fill1, FreqRec* d_ovf, unsigned long long* d_ovf_n,

@@ -312,6 +312,8 @@ hipError_t launch_freq_part(const void* d_in, uint64_t in_n, const unsigned long
 // regions -> contiguous (prefix = exclusive sum of the clamped fills) for the sort path.
 // one_string: the only key column is utf8 (the kernel's batched-load fast path); packed (needs
 // one_string): digit keys staged as packed words, other keys onto the overflow list.
+hipError_t launch_freq_pack_probe(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, unsigned long long* d_out,
+                                  hipStream_t stream);
 hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, bool packed, const DevColumn* d_cols,
                                   int64_t n_rows, int b1, void* d_out,
                                   uint64_t cap1, unsigned long long* d_fill1, FreqRec* d_ovf, unsigned long long* d_ovf_n,

@@ -210,6 +210,21 @@ def test_packed_then_other_keys(gpu, part):
     t.close()
 
 
+@pytest.mark.parametrize("frac", [0.0, 0.03, 0.2, 1.0])
+def test_pack_probe_mixed_first_batch(gpu, part, frac):
+    """The table's first batch holds a fraction `frac` of hex keys: the pack probe samples it and
+    stages packed records (few keys that do not pack: the overflow list takes them) or 16-B
+    records from the start (many: no packed staging to roll back).  Exact either way."""
+    rng = np.random.default_rng(24)
+    n = 300_000
+    keys = [("%012x" % v) if rng.random() < frac else ("%012d" % (v % 10**12))
+            for v in rng.integers(0, 2**40, n)]
+    t = _consume_batches(keys, False, 2)
+    assert _export(t) == _count(keys, False)
+    assert t.paths()["wait_timeouts"] == 0
+    t.close()
+
+
 @pytest.mark.parametrize("mode", ["budget", "load", "few"])
 def test_packed_paths_equal_unpacked(gpu, part, monkeypatch, mode):
     """The same digit keys with DQ_FREQ_PACK=0 (16-B records) and packed: identical tables.
