@@ -104,6 +104,7 @@ ArrowArray._fields_ = [("length", c_int64), ("null_count", c_int64), ("offset", 
 DIAG_SIGNATURES = {
     "dq_diag_hash_rate": (c_int, [c_int, c_int, c_int, POINTER(c_double)]),
     "dq_diag_freq_paths": (c_int, [c_void_p, POINTER(c_int64)]),
+    "dq_diag_freq_test_flags": (c_int, [c_void_p, c_int32]),
     "dq_diag_parse_double": (c_int, [c_char_p, c_int64, POINTER(c_double), POINTER(c_int32)]),
     "dq_diag_table_hash": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "dq_diag_key_pack": (c_int, [c_char_p, c_int32, POINTER(c_uint64), c_char_p, POINTER(c_int32), POINTER(c_int32)]),

@@ -91,6 +91,13 @@ class Analyzer:
     name = "Analyzer"
     entity = Entity.Column
 
+    def __getstate__(self):
+        # the memoised hash (_memoise_hashes) is per process: str hashes are salted per
+        # interpreter, so a pickled copy must recompute it where it is unpickled
+        state = dict(self.__dict__)
+        state.pop("_dq_hash", None)
+        return state
+
     def instance(self) -> str:
         raise NotImplementedError
 

@@ -189,7 +189,7 @@ struct FreqTable {
                                    // bit 3 a wait for another lane's slot publish timed out
 };
 constexpr unsigned int kFreqWaitTimeout = 8u;
-constexpr int32_t kFreqTestNoPublish = 1;  // DQ_FREQ_TEST_NO_PUBLISH=1: claimed slots never turn READY
+constexpr int32_t kFreqTestNoPublish = 1;  // dq_diag_freq_test_flags (tests only): claimed slots never turn READY
 
 struct FreqKeySpec {
   int32_t key_cols[kMaxKeyCols];

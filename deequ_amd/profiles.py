@@ -204,9 +204,11 @@ class ColumnProfiler:
                 for k, v in _extract_numeric_statistics(ctx2).items():
                     numeric[k].update(v)
         except BaseException:
-            if side:  # raised now, as the sequential run would; the histogram pass is not awaited
+            if side:  # raised as the sequential run would, once the histogram pass has stopped:
+                # a running pass still launches GPU work, so it is awaited (its own error, if
+                # any, is dropped in favour of pass 2's, which the sequential run raises first)
                 pending.cancel()
-                side.shutdown(wait=False, cancel_futures=True)
+                side.shutdown(wait=True, cancel_futures=True)
             raise
 
         if printStatusUpdates and not side:

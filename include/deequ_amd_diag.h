@@ -29,6 +29,12 @@ dq_status dq_diag_hash_rate(int device, int with_hll, int reps, double* hashes_p
  * publish ever timed out (an error every API call also reports).  `out` holds 7 values. */
 dq_status dq_diag_freq_paths(dq_freq* f, int64_t* out);
 
+/* Test hooks of one table (tests only; never set by the product): flags = 1 makes claimed
+ * global slots never turn READY, so a wait for another lane's publish times out (the timeout is
+ * a hard error, DQ_ERR_DEVICE).  0 restores normal publishing.  Replaces an environment variable
+ * the production library used to read on every dq_freq_create. */
+dq_status dq_diag_freq_test_flags(dq_freq* f, int32_t flags);
+
 /* Host build of the library's java.lang.Double.parseDouble (the parser dq_cast_utf8 and the
  * predicate IR's string -> double cast run on the device, compiled from the same source):
  * *ok = 1 and *out = the correctly rounded value, or *ok = 0 (NumberFormatException, NULL in

@@ -4,7 +4,7 @@ hinted with dq_freq_expect_groups.  Per-workgroup LDS counts, staging lists, one
 against the oracle for string keys (NULL as "NullValue" for Histogram) and fixed-width keys (NaN
 canonical, NULL as the empty key), into empty and non-empty tables; a wrong hint (too many keys)
 and keys longer than 15 bytes fall back to the general path with the same result.  Also: a slot
-publish that never comes (a test-only broken publish, DQ_FREQ_TEST_NO_PUBLISH) is a hard error,
+publish that never comes (a test-only broken publish, dq_diag_freq_test_flags) is a hard error,
 never a miscount."""
 import math
 
@@ -118,14 +118,14 @@ def test_small_long_keys_fall_back(gpu):
 
 
 def test_publish_wait_timeout_is_an_error(gpu, monkeypatch):
-    """A claimed global slot that never turns READY (DQ_FREQ_TEST_NO_PUBLISH=1, per-row inserts):
+    """A claimed global slot that never turns READY (dq_diag_freq_test_flags, per-row inserts):
     the lanes waiting on it time out and the batch fails with that error -- it is not reported as
     a full slice and the rows are not regrouped."""
-    monkeypatch.setenv("DQ_FREQ_TEST_NO_PUBLISH", "1")
     monkeypatch.setenv("DQ_FREQ_PATH", "atomic")
     n = 60_000
     spec = {"c": ["string", ["k%d" % (i % 6000) for i in range(n)]]}  # > 1024 keys: LDS overflows
     t = FrequencyTable(["c"], {"c": "string"})
+    L.check(L.lib().dq_diag_freq_test_flags(t.handle, 1))
     with pytest.raises(L.DeequAmdError, match="timed out"):
         _consume(t, spec, "c", batches=1)
     assert t.paths()["wait_timeouts"] == 1
