@@ -398,7 +398,9 @@ def c4_verify(args, metrics, dist_metric, analyzers):
     uh, ch = u.cpu().numpy(), c.cpu().numpy()
     vals = {k: v.absolute for k, v in dist_metric.values.items()}
     nonnull = {k: a for k, a in vals.items() if k != "NullValue"}
-    idx = np.array([int(k) for k in nonnull], dtype=np.int64)
+    # (alnum keys: 'k' + the id's last 11 digits -- the first digit of a 12-digit id below 1e11 is
+    # always 0, so the map is one to one)
+    idx = np.array([int(k[1:]) if args.c4_keys == "alnum" else int(k) for k in nonnull], dtype=np.int64)
     cnt = np.array(list(nonnull.values()), dtype=np.int64)
     pos = np.clip(np.searchsorted(uh, idx), 0, len(uh) - 1)
     out["detail_bins"] = len(nonnull)
@@ -615,7 +617,7 @@ def run_c4(args, world, rank, local):
     metrics = {str(a): ctx.metric(a).value.get() for a in analyzers[:4]}
     hist = ctx.metric(analyzers[4]).value.get()
     verify = None
-    if args.c4_verify and world == 1 and args.c4_keys == "digits":
+    if args.c4_verify and world == 1:
         del ctx
         verify = c4_verify(args, {a: metrics[str(a)] for a in analyzers[:4]}, hist, analyzers)
     in_bytes = sum(_column_bytes(b.columns["key"]) for b in shard.batches())
@@ -650,7 +652,27 @@ def run_c4(args, world, rank, local):
                          "table_slots_written_per_row": _c4_table_slots(groups) / float(args.c4_rows)},
         "check": dict(metrics, histogram_bins=hist.numberOfBins),
         **({"verify": verify} if verify is not None else {}),
+        **({"exchange": _exchange_stats(world, local)} if world > 1 else {}),
     }
+
+
+def _exchange_stats(world: int, local: int):
+    """The key-hash exchange of the last timed C4 step (deequ_amd.distributed.last_exchange_stats):
+    rank 0's bytes and milliseconds, plus the maximum over ranks of each time (collective)."""
+    import torch
+    import torch.distributed as dist
+    from deequ_amd.distributed import last_exchange_stats
+    st = last_exchange_stats()
+    keys = ["partition_ms", "alltoall_ms", "import_ms", "exchange_ms"]
+    t = torch.tensor([float(st.get(k, 0.0)) for k in keys], dtype=torch.float64)
+    if dist.get_backend() == "nccl":
+        t = t.to(torch.device("cuda", local))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    out = {k: st.get(k) for k in ("bytes_sent", "bytes_sent_remote", "bytes_received")}
+    out.update({k: st.get(k) for k in keys})
+    out.update({"max_" + k: v for k, v in zip(keys, t.cpu().tolist())})
+    out["exchange_bytes"] = st.get("bytes_sent")
+    return out
 
 
 def _c4_table_slots(groups: float) -> float:

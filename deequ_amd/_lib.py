@@ -34,6 +34,7 @@ DQ_CMP_AS_INT64, DQ_CMP_AS_FLOAT64 = 0, 1
 
 DQ_HLL_NUM_WORDS = 52
 DQ_FREQ_NULL_AS_KEY = 0x1
+DQ_FLAT_DEVICE = 0x1
 
 TYPE_CODES = {
     "bool": DQ_T_BOOL, "int8": DQ_T_INT8, "int16": DQ_T_INT16, "int32": DQ_T_INT32,
@@ -157,6 +158,9 @@ SIGNATURES = {
                             POINTER(c_int64), POINTER(c_int64)]),
     "dq_freq_merge": (c_int, [c_void_p, c_void_p]),
     "dq_freq_import": (c_int, [c_void_p, POINTER(DqFreqGroup), c_int64, c_void_p, c_int64]),
+    "dq_freq_export_flat": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int,
+                                    POINTER(c_int64), POINTER(c_int64)]),
+    "dq_freq_import_flat": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int]),
     "dq_cast_utf8": (c_int, [c_void_p, POINTER(DqColumn), c_int64, c_int32, c_void_p, c_void_p, POINTER(c_int64)]),
     "dq_cast_utf8_batch": (c_int, [c_void_p, c_int32, POINTER(DqColumn), c_int64, POINTER(c_int32),
                                    POINTER(c_void_p), POINTER(c_void_p)]),

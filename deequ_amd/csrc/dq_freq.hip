@@ -673,6 +673,124 @@ __global__ __launch_bounds__(kBlock) void dq_freq_import_kernel(FreqTable T, Fre
   }
 }
 
+// ---- Flat (columnar) export and import: dq_freq_export_flat / dq_freq_import_flat.
+// The export lists every group in SLOT order (deterministic: the same table exports the same
+// columns), as the Arrow layout of the state's DataFrame wants it: counts[i], and key i's bytes
+// at [offs[i], offs[i + 1]) of one byte array.  No per-group record on the host.
+constexpr uint32_t kFlatRounds = 16;
+constexpr uint32_t kFlatChunk = (uint32_t)kBlock * kFlatRounds;  // slots per workgroup
+
+// chunk_n[b] = the groups among slots [b kFlatChunk, (b + 1) kFlatChunk); chunk_n[n_chunks] = 0
+// (the exclusive scan's total lands there).
+__global__ __launch_bounds__(kBlock) void dq_flat_count_kernel(FreqTable T, unsigned long long* chunk_n,
+                                                               uint64_t n_chunks) {
+  __shared__ uint32_t ws[kBlock / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kFlatChunk;
+  uint32_t c = 0;
+#pragma unroll 4
+  for (uint32_t r = 0; r < kFlatRounds; ++r) {
+    const uint64_t s = base + (uint64_t)r * kBlock + threadIdx.x;
+    if (s <= T.mask && (T.slots[s].ctrl & kReady)) ++c;
+  }
+  for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+  if ((threadIdx.x & 63u) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (int w = 0; w < kBlock / 64; ++w) s += ws[w];
+    chunk_n[blockIdx.x] = s;
+    if (blockIdx.x == 0) chunk_n[n_chunks] = 0ull;
+  }
+}
+
+// Each workgroup writes its chunk's groups from position chunk_base[b], in slot order: per round
+// of kBlock slots a ballot gives each ready slot its rank within the wave, LDS the waves' offsets.
+// lens[i] = key length (the exclusive scan turns it into the byte offsets); lens[n] = 0.
+__global__ __launch_bounds__(kBlock) void dq_flat_fill_kernel(FreqTable T, const unsigned long long* __restrict__ chunk_base,
+                                                              uint64_t n, unsigned long long* __restrict__ ctrl,
+                                                              unsigned long long* __restrict__ count,
+                                                              unsigned long long* __restrict__ k0,
+                                                              unsigned long long* __restrict__ k1,
+                                                              unsigned long long* __restrict__ lens) {
+  __shared__ uint32_t ws[kBlock / 64];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint64_t base = (uint64_t)blockIdx.x * kFlatChunk;
+  uint64_t pos = chunk_base[blockIdx.x];
+  if (blockIdx.x == 0 && threadIdx.x == 0) lens[n] = 0ull;
+  for (uint32_t r = 0; r < kFlatRounds; ++r) {
+    const uint64_t s = base + (uint64_t)r * kBlock + threadIdx.x;
+    FreqSlot e;
+    bool ready = false;
+    if (s <= T.mask) {
+      e = T.slots[s];
+      ready = (e.ctrl & kReady) != 0;
+    }
+    const uint64_t b = __ballot(ready);
+    const uint32_t below = (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
+    if (lane == 0) ws[wave] = (uint32_t)__popcll(b);
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (uint32_t w = 0; w < (uint32_t)(kBlock / 64); ++w) {
+      off += w < wave ? ws[w] : 0u;
+      tot += ws[w];
+    }
+    if (ready) {
+      const uint64_t i = pos + off + below;
+      if (i < n) {
+        ctrl[i] = e.ctrl;
+        count[i] = e.count;
+        k0[i] = e.k0;
+        k1[i] = e.k1;
+        lens[i] = e.ctrl & kLenMask;
+      }
+    }
+    pos += tot;
+    __syncthreads();  // (ws is rewritten by the next round)
+  }
+}
+
+// Key bytes of group i at out[offs[i] ..]: inline keys from k0 / k1, long keys from the heap.
+__global__ __launch_bounds__(kBlock) void dq_flat_keys_kernel(FreqTable T, const unsigned long long* __restrict__ ctrl,
+                                                              const unsigned long long* __restrict__ k0,
+                                                              const unsigned long long* __restrict__ k1,
+                                                              const unsigned long long* __restrict__ offs, uint64_t n,
+                                                              uint8_t* __restrict__ out) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    const unsigned long long c = ctrl[i];
+    const uint32_t len = (uint32_t)(c & kLenMask);
+    uint8_t* dst = out + offs[i];
+    if (c & kHeapKey) {
+      const uint8_t* src = T.heap + k0[i];
+      for (uint32_t j = 0; j < len; ++j) dst[j] = src[j];
+    } else {
+      const uint64_t a = k0[i], b = k1[i];
+      for (uint32_t j = 0; j < len; ++j) dst[j] = (uint8_t)((j < 8 ? a >> (8 * j) : b >> (8 * (j - 8))) & 0xFFu);
+    }
+  }
+}
+
+// Insert flat groups (a loaded state): group i = (counts[i], bytes[offs[i] .. offs[i + 1])).
+__global__ __launch_bounds__(kBlock) void dq_freq_import_flat_kernel(FreqTable T, const long long* __restrict__ counts,
+                                                                     const long long* __restrict__ offs,
+                                                                     const uint8_t* __restrict__ bytes, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t o = (uint64_t)offs[i];
+    Key k;
+    k.len = (uint32_t)((uint64_t)offs[i + 1] - o);
+    if (k.len > 16u) {
+      k.ptr = bytes + o;
+      k.k0 = k.k1 = 0;
+      k.hash = xxh64_any(k.ptr, k.len, 42);
+    } else {
+      k.ptr = nullptr;
+      k.k0 = ld_partial(bytes + o, k.len < 8u ? k.len : 8u);
+      k.k1 = k.len > 8u ? ld_partial(bytes + o + 8, k.len - 8u) : 0ull;
+      k.hash = hash_inline(k.k0, k.k1, k.len);
+    }
+    if (!global_insert(T, k, (unsigned long long)counts[i])) return;
+  }
+}
+
 // Count of one encoded key (0 if absent): a single-thread probe of the key's slice.
 __global__ void dq_freq_lookup_kernel(FreqTable T, const uint8_t* key, uint32_t len, unsigned long long* out) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
@@ -2566,6 +2684,45 @@ hipError_t launch_freq_hash(const uint64_t* d_k0, const uint64_t* d_k1, const ui
 hipError_t launch_freq_lookup(const FreqTable& T, const uint8_t* d_key, uint32_t len, unsigned long long* d_out,
                               hipStream_t stream) {
   hipLaunchKernelGGL(dq_freq_lookup_kernel, dim3(1), dim3(64), 0, stream, T, d_key, len, d_out);
+  return hipGetLastError();
+}
+
+uint64_t freq_flat_chunks(uint64_t slots) { return (slots + kFlatChunk - 1) / kFlatChunk; }
+
+hipError_t launch_freq_flat_count(const FreqTable& T, unsigned long long* d_chunk_n, uint64_t n_chunks,
+                                  unsigned long long* d_sums, hipStream_t stream) {
+  if (n_chunks == 0 || n_chunks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dq_flat_count_kernel, dim3((unsigned)n_chunks), dim3(kBlock), 0, stream, T, d_chunk_n, n_chunks);
+  return exclusive_scan<unsigned long long>(d_chunk_n, n_chunks + 1, d_sums, stream);
+}
+
+hipError_t launch_freq_flat_fill(const FreqTable& T, const unsigned long long* d_chunk_base, uint64_t n_chunks, uint64_t n,
+                                 unsigned long long* d_ctrl, unsigned long long* d_count, unsigned long long* d_k0,
+                                 unsigned long long* d_k1, unsigned long long* d_offs, unsigned long long* d_sums,
+                                 hipStream_t stream) {
+  hipLaunchKernelGGL(dq_flat_fill_kernel, dim3((unsigned)n_chunks), dim3(kBlock), 0, stream, T, d_chunk_base, n, d_ctrl,
+                     d_count, d_k0, d_k1, d_offs);
+  return exclusive_scan<unsigned long long>(d_offs, n + 1, d_sums, stream);
+}
+
+hipError_t launch_freq_flat_keys(const FreqTable& T, const unsigned long long* d_ctrl, const unsigned long long* d_k0,
+                                 const unsigned long long* d_k1, const unsigned long long* d_offs, uint64_t n,
+                                 uint8_t* d_out, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  uint64_t blocks = (n + kBlock - 1) / kBlock;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(dq_flat_keys_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, d_ctrl, d_k0, d_k1, d_offs,
+                     n, d_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_import_flat(const FreqTable& T, const long long* d_counts, const long long* d_offs,
+                                   const uint8_t* d_bytes, uint64_t n, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  uint64_t blocks = (n + kBlock * 4 - 1) / (kBlock * 4);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(dq_freq_import_flat_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, d_counts, d_offs,
+                     d_bytes, n);
   return hipGetLastError();
 }
 

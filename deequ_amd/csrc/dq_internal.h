@@ -268,6 +268,22 @@ hipError_t launch_freq_hist(const FreqTable& T, unsigned long long* d_hist, unsi
 hipError_t launch_freq_export(const FreqTable& T, unsigned long long min_count, const FreqOut& out,
                               hipStream_t stream, const uint32_t* d_smax = nullptr);
 hipError_t launch_freq_import(const FreqTable& T, const FreqIn& in, hipStream_t stream);
+// Flat (columnar) export in slot order (dq_freq.hip): chunk counts -> scanned chunk bases (the
+// total at d_chunk_n[n_chunks]); then the groups' ctrl/count/k0/k1 arrays and the scanned key
+// byte offsets (n + 1, the total at d_offs[n]); then the key bytes.  d_sums: scan scratch of
+// ceil((max(n, n_chunks) + 1) / 4096) words.
+uint64_t freq_flat_chunks(uint64_t slots);
+hipError_t launch_freq_flat_count(const FreqTable& T, unsigned long long* d_chunk_n, uint64_t n_chunks,
+                                  unsigned long long* d_sums, hipStream_t stream);
+hipError_t launch_freq_flat_fill(const FreqTable& T, const unsigned long long* d_chunk_base, uint64_t n_chunks, uint64_t n,
+                                 unsigned long long* d_ctrl, unsigned long long* d_count, unsigned long long* d_k0,
+                                 unsigned long long* d_k1, unsigned long long* d_offs, unsigned long long* d_sums,
+                                 hipStream_t stream);
+hipError_t launch_freq_flat_keys(const FreqTable& T, const unsigned long long* d_ctrl, const unsigned long long* d_k0,
+                                 const unsigned long long* d_k1, const unsigned long long* d_offs, uint64_t n,
+                                 uint8_t* d_out, hipStream_t stream);
+hipError_t launch_freq_import_flat(const FreqTable& T, const long long* d_counts, const long long* d_offs,
+                                   const uint8_t* d_bytes, uint64_t n, hipStream_t stream);
 hipError_t launch_freq_hash(const uint64_t* d_k0, const uint64_t* d_k1, const uint32_t* d_len, int64_t n, uint64_t* d_out,
                             hipStream_t stream);
 hipError_t launch_freq_lookup(const FreqTable& T, const uint8_t* d_key, uint32_t len, unsigned long long* d_out,

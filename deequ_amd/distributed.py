@@ -185,19 +185,54 @@ def _comm_device(group):
     return "cuda" if dist.get_backend(group) == "nccl" else "cpu"
 
 
+def _comm_tensor_device(group, table):
+    """Where a collective's tensors live: the table's GPU for an nccl (RCCL) group, else host."""
+    import torch
+    return table.torch_device if _comm_device(group) == "cuda" else torch.device("cpu")
+
+
 def _to(t, device):
     return t if t.device.type == device.type else t.to(device)
 
 
-def exchange_frequencies(table, group=None):
+def _allgather_var(t, group=None):
+    """All-gather a 1-D tensor whose length differs per rank (tensor collectives only: the
+    lengths, then the tensors padded to the longest); returns every rank's tensor, trimmed."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
+    ns = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    ns = [int(x.item()) for x in ns]
+    m = max(1, max(ns))
+    pad = torch.zeros(m, dtype=t.dtype, device=t.device)
+    if t.numel():
+        pad[:t.numel()] = t
+    bufs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(bufs, pad, group=group)
+    return [b[:k] for b, k in zip(bufs, ns)]
+
+
+def _sync(dev):
+    import torch
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def exchange_frequencies(table, group=None, stats: Optional[dict] = None):
     """Key-hash all-to-all of a local FrequencyTable; returns the table of the keys this rank
-    owns (numRows 0: the global numRows is the all-reduce of the local ones)."""
+    owns (numRows 0: the global numRows is the all-reduce of the local ones).  `stats` (a dict)
+    receives this rank's exchange cost: bytes sent / received over the all-to-all and the
+    milliseconds of the partition, the all-to-all and the owner-side import."""
+    import time
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     dev = table.torch_device
     comm = dev if _comm_device(group) == "cuda" else torch.device("cpu")
     part_p, part_g, part_k, err = [0] * world, [0] * world, [0] * world, None
+    t0 = time.perf_counter()
     try:
         part_p, part_g, part_k = table.partition_sizes(world)
         nbytes = sum(table.part_bytes(p, g) for p, g in zip(part_p, part_g))
@@ -208,6 +243,8 @@ def exchange_frequencies(table, group=None):
     except Exception as e:  # noqa: BLE001 -- agreed on below, then re-raised
         err = e
     agree(err, "partitioning the frequency table by owner", group)
+    _sync(dev)
+    t1 = time.perf_counter()
     sizes = torch.tensor([[p, g, k] for p, g, k in zip(part_p, part_g, part_k)], dtype=torch.int64).reshape(-1).to(comm)
     recv_sizes = torch.empty_like(sizes)
     dist.all_to_all_single(recv_sizes, sizes, group=group)
@@ -224,6 +261,7 @@ def exchange_frequencies(table, group=None):
     if comm.type == "cuda":
         torch.cuda.current_stream(dev).synchronize()  # the library reads them on its own stream
     recv_g, recv_k = _to(recv_g, dev), _to(recv_k, dev)
+    t2 = time.perf_counter()
     owned, err = None, None
     try:
         owned = type(table).like(table)
@@ -236,7 +274,27 @@ def exchange_frequencies(table, group=None):
         if owned is not None:  # (a half-built table, or one another rank's failure orphans)
             owned.close()
         raise
+    _sync(dev)
+    t3 = time.perf_counter()
+    rank = dist.get_rank(group)
+    _LAST_EXCHANGE.clear()
+    _LAST_EXCHANGE.update({"bytes_sent": int(sum(in_g) + sum(in_k)),
+                      "bytes_sent_remote": int(sum(in_g) + sum(in_k) - in_g[rank] - in_k[rank]),
+                      "bytes_received": int(sum(out_g) + sum(out_k)),
+                      "partition_ms": (t1 - t0) * 1e3, "alltoall_ms": (t2 - t1) * 1e3, "import_ms": (t3 - t2) * 1e3,
+                      "exchange_ms": (t3 - t0) * 1e3})
+    if stats is not None:
+        stats.update(_LAST_EXCHANGE)
     return owned
+
+
+_LAST_EXCHANGE: dict = {}
+
+
+def last_exchange_stats() -> dict:
+    """This rank's cost of the last key-hash exchange (exchange_frequencies' stats): bench.py
+    reports it beside the C4 step time at N > 1."""
+    return dict(_LAST_EXCHANGE)
 
 
 class DistributedFrequencies:
@@ -244,12 +302,13 @@ class DistributedFrequencies:
     held as the keys each rank owns after the exchange.  Collective: every rank calls the same
     methods in the same order."""
 
-    def __init__(self, owned, num_rows: int, group=None):
+    def __init__(self, owned, num_rows: int, group=None, exchange: Optional[dict] = None):
         self.owned = owned
         self.group = group
         self._num_rows = int(num_rows)
         self._summary = None
         self.table = _DistributedTableView(self)
+        self.exchange = exchange or {}  # this rank's exchange cost (exchange_frequencies' stats)
 
     @property
     def columns(self):
@@ -265,38 +324,41 @@ class DistributedFrequencies:
             import torch.distributed as dist
             from .frequencies import summary_from_histogram
             hist, big = self.owned.count_histogram()
-            comm = _comm_device(self.group)
-            h = torch.from_numpy(hist).to(self.owned.torch_device if comm == "cuda" else "cpu")
+            dev = _comm_tensor_device(self.group, self.owned)
+            h = torch.from_numpy(hist).to(dev)
             dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
-            bigs = [None] * dist.get_world_size(self.group)
-            dist.all_gather_object(bigs, big.tolist(), group=self.group)
-            all_big = np.array(sorted(c for b in bigs for c in b), dtype=np.int64)
+            # the counts above the histogram's range: a variable-length tensor gather
+            bigs = _allgather_var(torch.from_numpy(np.ascontiguousarray(big, dtype=np.int64)).to(dev), self.group)
+            all_big = np.sort(np.concatenate([b.cpu().numpy() for b in bigs])) if bigs else np.zeros(0, np.int64)
             self._summary = summary_from_histogram(h.cpu().numpy(), all_big, self._num_rows)
         return self._summary
 
     def gather_arrays(self, dst: Optional[int] = None):
         """Every owner's groups as flat arrays -- (counts int64, key lengths int32, key bytes uint8),
-        owners in rank order -- gathered with tensor collectives (no per-group Python objects):
-        on every rank (dst None) or only on rank `dst` (the others get None).  Collective."""
+        owners in rank order -- from each owner's flat export (dq_freq_export_flat; straight
+        into device tensors for an nccl group) gathered with tensor collectives: no per-group
+        Python object anywhere.  On every rank (dst None) or only on rank `dst` (the others get
+        None).  Collective."""
         import torch
         import torch.distributed as dist
-        counts, keys = self.owned.export()
-        lens = np.array([len(k) for k in keys], dtype=np.int32)
-        blob = np.frombuffer(b"".join(keys), dtype=np.uint8)
         world = dist.get_world_size(self.group)
-        dev = self.owned.torch_device if _comm_device(self.group) == "cuda" else torch.device("cpu")
-        size = torch.tensor([len(counts), len(blob)], dtype=torch.int64, device=dev)
+        dev = _comm_tensor_device(self.group, self.owned)
+        counts, offs, blob = self.owned.export_flat(device=dev.type == "cuda")
+        if dev.type != "cuda":
+            counts, offs, blob = (torch.from_numpy(np.ascontiguousarray(a)) for a in (counts, offs, blob))
+        lens = (offs[1:] - offs[:-1]).to(torch.int32)
+        size = torch.tensor([counts.numel(), blob.numel()], dtype=torch.int64, device=dev)
         sizes = [torch.empty_like(size) for _ in range(world)]
         dist.all_gather(sizes, size, group=self.group)
         sizes = [tuple(int(v) for v in t.cpu().tolist()) for t in sizes]
         mg, mk = max(1, max(g for g, _ in sizes)), max(1, max(k for _, k in sizes))
 
-        def padded(a, n, dtype):
-            t = torch.zeros(n, dtype=dtype, device=dev)
-            if len(a):
-                t[:len(a)] = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-            return t
-        mine = [padded(counts, mg, torch.int64), padded(lens, mg, torch.int32), padded(blob, mk, torch.uint8)]
+        def padded(t, n):
+            out = torch.zeros(n, dtype=t.dtype, device=dev)
+            if t.numel():
+                out[:t.numel()] = t
+            return out
+        mine = [padded(counts, mg), padded(lens, mg), padded(blob, mk)]
         out = []
         rank = dist.get_rank(self.group)
         for t in mine:
@@ -309,10 +371,27 @@ class DistributedFrequencies:
             out.append(bufs)
         if dst is not None and rank != dst:
             return None
-        cs = np.concatenate([out[0][r].cpu().numpy()[:sizes[r][0]] for r in range(world)])
-        ls = np.concatenate([out[1][r].cpu().numpy()[:sizes[r][0]] for r in range(world)])
-        kb = np.concatenate([out[2][r].cpu().numpy()[:sizes[r][1]] for r in range(world)])
+        cs = np.concatenate([out[0][r][:sizes[r][0]].cpu().numpy() for r in range(world)])
+        ls = np.concatenate([out[1][r][:sizes[r][0]].cpu().numpy() for r in range(world)])
+        kb = np.concatenate([out[2][r][:sizes[r][1]].cpu().numpy() for r in range(world)])
         return cs, ls, kb
+
+    def to_arrow(self, strings: Optional[bool] = None, dst: Optional[int] = None):
+        """The whole dataset's frequencies DataFrame as an Arrow table (gather_arrays, then the
+        columnar key codec); on every rank or only on `dst`.  Collective."""
+        import pyarrow as pa
+        from .keycols import decode_columns
+        got = self.gather_arrays(dst)
+        if got is None:
+            return None
+        cs, ls, kb = got
+        offs = np.zeros(len(ls) + 1, dtype=np.int64)
+        np.cumsum(ls, out=offs[1:])
+        o = self.owned
+        strings = o.histogram if strings is None else strings
+        cols = decode_columns(offs, kb, o.dtypes, o.histogram, strings=strings)
+        name = "count" if o.histogram else "com_amazon_deequ_dq_metrics_count"
+        return pa.Table.from_arrays(cols + [pa.array(cs, type=pa.int64())], names=list(o.key_columns) + [name])
 
     def frequencies(self, raw: bool = False, dst: Optional[int] = None):
         """Every group of the dataset ({key: count}), gathered as flat arrays (gather_arrays): on
@@ -343,11 +422,21 @@ class _DistributedTableView:
     def top(self, n: int):
         """Union of every owner's top-n (owners hold disjoint keys), cut at the n-th largest
         count with the ties kept -- the contract of FrequencyTable.top."""
-        import torch.distributed as dist
+        import torch
         counts, keys = self._s.owned.top(n)
-        parts = [None] * dist.get_world_size(self._s.group)
-        dist.all_gather_object(parts, (counts.tolist(), keys), group=self._s.group)
-        items = sorted(((c, k) for cs, ks in parts for c, k in zip(cs, ks)), key=lambda ck: (-ck[0], ck[1]))
+        dev = _comm_tensor_device(self._s.group, self._s.owned)
+        lens = np.array([len(k) for k in keys], dtype=np.int64)
+        blob = np.frombuffer(b"".join(keys), dtype=np.uint8)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        g_counts = _allgather_var(t(np.asarray(counts, dtype=np.int64)), self._s.group)
+        g_lens = _allgather_var(t(lens), self._s.group)
+        g_blob = _allgather_var(t(blob), self._s.group)
+        items = []
+        for c, ln, b in zip(g_counts, g_lens, g_blob):
+            raw = b.cpu().numpy().tobytes()
+            ends = np.cumsum(ln.cpu().numpy())
+            items += [(int(ci), raw[e - m:e]) for ci, e, m in zip(c.cpu().tolist(), ends.tolist(), ln.cpu().tolist())]
+        items.sort(key=lambda ck: (-ck[0], ck[1]))
         if len(items) > n:
             cut = items[n - 1][0]
             items = [ck for ck in items if ck[0] >= cut]
@@ -387,9 +476,10 @@ def compute_frequencies_distributed(data, grouping_columns, histogram: bool = Fa
         n_local = local.summary().num_rows
     except Exception as e:  # noqa: BLE001 -- every rank fails together (agree)
         err = e
+    stats: dict = {}
     try:  # the local table is closed on every exit (another rank's failure raises here too)
         agree(err, "the frequency group-by", group)
-        owned = exchange_frequencies(local, group)
+        owned = exchange_frequencies(local, group, stats)
     finally:
         if local is not None:
             local.close()
@@ -397,4 +487,4 @@ def compute_frequencies_distributed(data, grouping_columns, histogram: bool = Fa
     if _comm_device(group) == "cuda":
         n = n.to(owned.torch_device)
     dist.all_reduce(n, op=dist.ReduceOp.SUM, group=group)
-    return DistributedFrequencies(owned, int(n.item()), group)
+    return DistributedFrequencies(owned, int(n.item()), group, stats)

@@ -133,15 +133,66 @@ class FrequencyTable:
     def num_rows(self) -> int:
         return self.summary().num_rows
 
-    def export(self) -> Tuple[np.ndarray, List[bytes]]:
-        """Every group: (counts int64[n], encoded keys), in an unspecified order."""
+    def export_flat(self, device: bool = False):
+        """Every group as flat columns, in slot order (dq_freq_export_flat): (counts int64[n],
+        key offsets int64[n + 1], encoded key bytes uint8) -- numpy arrays, or with `device` torch
+        tensors on this table's GPU.  No per-group object is made."""
         n, kb = ctypes.c_int64(), ctypes.c_int64()
-        L.check(L.lib().dq_freq_size(self.handle, ctypes.byref(n), ctypes.byref(kb)))
-        groups = (L.DqFreqGroup * max(1, n.value))()
-        keys = ctypes.create_string_buffer(max(1, kb.value))
-        got = ctypes.c_int64()
-        L.check(L.lib().dq_freq_export(self.handle, groups, n.value, keys, kb.value, ctypes.byref(got)))
-        return _unpack_groups(groups, got.value, keys.raw)
+        st = L.lib().dq_freq_export_flat(self.handle, None, None, None, 0, 0, 0, ctypes.byref(n), ctypes.byref(kb))
+        if st != L.DQ_ERR_SPACE:
+            L.check(st)
+        if device:
+            import torch
+            counts = torch.empty(max(1, n.value), dtype=torch.int64, device=self.torch_device)
+            offs = torch.empty(n.value + 1, dtype=torch.int64, device=self.torch_device)
+            blob = torch.empty(max(1, kb.value), dtype=torch.uint8, device=self.torch_device)
+            ptrs = (counts.data_ptr(), offs.data_ptr(), blob.data_ptr())
+        else:
+            counts = np.empty(max(1, n.value), dtype=np.int64)
+            offs = np.empty(n.value + 1, dtype=np.int64)
+            blob = np.empty(max(1, kb.value), dtype=np.uint8)
+            ptrs = (counts.ctypes.data, offs.ctypes.data, blob.ctypes.data)
+        got_n, got_k = ctypes.c_int64(), ctypes.c_int64()
+        L.check(L.lib().dq_freq_export_flat(self.handle, ptrs[0], ptrs[1], ptrs[2], n.value, kb.value,
+                                            L.DQ_FLAT_DEVICE if device else 0, ctypes.byref(got_n), ctypes.byref(got_k)))
+        return counts[:got_n.value], offs[:got_n.value + 1], blob[:got_k.value]
+
+    def import_flat(self, counts, offsets, blob, num_rows: int = 0) -> None:
+        """FrequenciesAndNumRows.sum of flat groups (dq_freq_import_flat): numpy arrays or device
+        tensors on this table's GPU; duplicate keys add up."""
+        n = len(counts)
+        if len(offsets) != n + 1:
+            raise ValueError("offsets must hold one more value than counts")
+        if hasattr(counts, "data_ptr"):
+            c, o, b = counts.contiguous(), offsets.contiguous(), blob.contiguous()
+            L.check(L.lib().dq_freq_import_flat(self.handle, c.data_ptr(), o.data_ptr(), b.data_ptr() if b.numel() else None,
+                                                n, int(num_rows), L.DQ_FLAT_DEVICE))
+            return
+        c = np.ascontiguousarray(counts, dtype=np.int64)
+        o = np.ascontiguousarray(offsets, dtype=np.int64)
+        b = np.ascontiguousarray(blob, dtype=np.uint8)
+        L.check(L.lib().dq_freq_import_flat(self.handle, c.ctypes.data, o.ctypes.data, b.ctypes.data if len(b) else None,
+                                            n, int(num_rows), 0))
+
+    def to_arrow(self, strings: Optional[bool] = None, count_column: Optional[str] = None):
+        """The state's DataFrame as an Arrow table: the grouping columns + the count column, built
+        from the flat export with array operations only.  `strings` (default: a Histogram table)
+        casts the key to string as the reference's Histogram state holds it (Histogram.scala:63-66)."""
+        import pyarrow as pa
+        from .keycols import decode_columns
+        strings = self.histogram if strings is None else strings
+        counts, offs, blob = self.export_flat()
+        cols = decode_columns(offs, blob, self.dtypes, self.histogram, strings=strings)
+        name = count_column or ("count" if self.histogram else COUNT_COL)
+        return pa.Table.from_arrays(cols + [pa.array(counts, type=pa.int64())], names=list(self.key_columns) + [name])
+
+    def export(self) -> Tuple[np.ndarray, List[bytes]]:
+        """Every group: (counts int64[n], encoded keys), in slot order (a list of byte strings:
+        the small-state convenience; export_flat / to_arrow carry large states)."""
+        counts, offs, blob = self.export_flat()
+        raw = blob.tobytes()
+        o = offs.tolist()
+        return counts, [raw[o[i]:o[i + 1]] for i in range(len(counts))]
 
     def top(self, n: int) -> Tuple[np.ndarray, List[bytes]]:
         """Groups whose count is at least the n-th largest count (ties at the cut included),
@@ -168,17 +219,11 @@ class FrequencyTable:
 
     def import_groups(self, counts: Sequence[int], keys: Sequence[bytes], num_rows: int) -> None:
         """FrequenciesAndNumRows.sum for the given groups (GroupingAnalyzers.scala:128-148)."""
-        n = len(keys)
-        groups = (L.DqFreqGroup * max(1, n))()
-        off = 0
-        for i, (c, k) in enumerate(zip(counts, keys)):
-            groups[i].count = int(c)
-            groups[i].key_offset = off
-            groups[i].key_len = len(k)
-            off += len(k)
-        blob = b"".join(keys)
-        buf = ctypes.create_string_buffer(blob, max(1, len(blob)))
-        L.check(L.lib().dq_freq_import(self.handle, groups, n, buf, int(num_rows)))
+        lens = np.fromiter((len(k) for k in keys), dtype=np.int64, count=len(keys))
+        offs = np.zeros(len(keys) + 1, dtype=np.int64)
+        np.cumsum(lens, out=offs[1:])
+        blob = np.frombuffer(b"".join(keys), dtype=np.uint8)
+        self.import_flat(np.asarray(counts, dtype=np.int64).reshape(len(keys)), offs, blob, num_rows)
 
     # ---- multi-GPU key-hash exchange (deequ_amd/distributed.py)
     WIRE_PACKED_BYTES = 16  # sizeof(dq_freq_wire_packed): a key that packs into one word
@@ -263,6 +308,7 @@ class FrequencyTable:
 
 
 _GROUP_DTYPE = np.dtype([("count", "<i8"), ("key_offset", "<i8"), ("key_len", "<i4"), ("reserved", "<i4")])
+COUNT_COL = "com_amazon_deequ_dq_metrics_count"  # Analyzer.scala:363-364
 
 
 def _unpack_groups(groups, n: int, raw: bytes) -> Tuple[np.ndarray, List[bytes]]:
@@ -345,22 +391,39 @@ class FrequenciesAndNumRows(State):
         -> "NullValue", Histogram.scala:63-66, 108): the form the reference persists."""
         if not self.table.histogram or self.table.dtypes == ["string"]:
             return self
-        from .javafmt import spark_cast_to_string
-        dtype = self.table.dtypes[0]
-        out: Dict[tuple, int] = {}
-        for (v,), c in self.frequencies().items():
-            k = ("NullValue" if v is None else spark_cast_to_string(v, dtype),)
-            out[k] = out.get(k, 0) + c
-        return FrequenciesAndNumRows.from_frequencies(self.columns, ["string"], out, self.numRows, histogram=True)
+        arrow = self.table.to_arrow(strings=True)
+        return FrequenciesAndNumRows.from_arrow(arrow, self.columns, ["string"], self.numRows, histogram=True)
 
     def frequencies(self, raw: bool = False) -> Dict:
         """{key tuple: count} on the host (decoded Python values), or with `raw` the encoded
-        key bytes -- the exact group identity (decoded floats conflate 0.0 and -0.0)."""
+        key bytes -- the exact group identity (decoded floats conflate 0.0 and -0.0).  A dict
+        of every group: for large states use to_arrow() / table.export_flat()."""
         counts, keys = self.table.export()
         if raw:
             return {k: int(c) for k, c in zip(keys, counts.tolist())}
         return {decode_key(k, self.table.dtypes, self.table.histogram): int(c)
                 for k, c in zip(keys, counts.tolist())}
+
+    def to_arrow(self, strings: Optional[bool] = None):
+        """The state's frequencies DataFrame as an Arrow table (see FrequencyTable.to_arrow)."""
+        return self.table.to_arrow(strings)
+
+    @staticmethod
+    def from_arrow(table, columns: Sequence[str], dtypes: Sequence[str], numRows: int,
+                   histogram: bool = False, count_column: Optional[str] = None) -> "FrequenciesAndNumRows":
+        """A device state from an Arrow table of the grouping columns + a count column (the
+        last column unless named), e.g. a state persisted by Spark deequ: encoded with array
+        operations and merged on the device (dq_freq_import_flat; duplicate keys add up)."""
+        from .keycols import encode_columns
+        names = list(table.column_names)
+        ci = names.index(count_column) if count_column else len(names) - 1
+        keys = [table.column(i) for i in range(len(names)) if i != ci]
+        counts = table.column(ci)
+        counts = counts.combine_chunks() if hasattr(counts, "combine_chunks") else counts
+        t = FrequencyTable(columns, dict(zip(columns, dtypes)), histogram)
+        offs, blob = encode_columns(keys, dtypes, histogram)
+        t.import_flat(np.asarray(counts.to_numpy(zero_copy_only=False), dtype=np.int64), offs, blob, numRows)
+        return FrequenciesAndNumRows(t)
 
     @staticmethod
     def from_frequencies(columns: Sequence[str], dtypes: Sequence[str], frequencies: Dict[tuple, int],

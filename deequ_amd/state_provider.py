@@ -27,7 +27,9 @@ from __future__ import annotations
 import os
 import shutil
 import struct
-from typing import Dict, List
+from typing import List
+
+import numpy as np
 
 from .analyzers import (ApproxCountDistinct, Completeness, Compliance, Correlation, DataType,
                         FrequencyBasedAnalyzer, Histogram, MaxLength, Maximum, Mean, MinLength, Minimum,
@@ -162,7 +164,7 @@ class HdfsStateProvider:
                 raise FileExistsError("path %s already exists." % directory)
             shutil.rmtree(directory)
         os.makedirs(directory)
-        _write_frequency_part(os.path.join(directory, "part-00000.snappy.parquet"), state.table, state.frequencies())
+        _write_frequency_part(os.path.join(directory, "part-00000.snappy.parquet"), state.table)
         self._write(self._path(ident, "-num_rows.bin"), struct.pack(">q", state.numRows))
 
     def _persist_frequencies_sharded(self, ident: str, directory: str, state) -> None:
@@ -173,7 +175,6 @@ class HdfsStateProvider:
         partition).  Collective; the ranks share the filesystem (one node)."""
         import torch.distributed as dist
         from .distributed import agree, allreduce_flag
-        from .frequencies import decode_key
         group = state.group
         rank = dist.get_rank(group)
         exists = rank == 0 and os.path.exists(directory)
@@ -189,10 +190,7 @@ class HdfsStateProvider:
                 err = e
         agree(err, "creating %s" % directory, group)
         try:
-            owned = state.owned
-            counts, keys = owned.export()
-            freqs = {decode_key(k, owned.dtypes, owned.histogram): int(c) for k, c in zip(keys, counts.tolist())}
-            _write_frequency_part(os.path.join(directory, "part-%05d.snappy.parquet" % rank), state.table, freqs)
+            _write_frequency_part(os.path.join(directory, "part-%05d.snappy.parquet" % rank), state.owned)
             if rank == 0:
                 self._write(self._path(ident, "-num_rows.bin"), struct.pack(">q", state.numRows))
         except Exception as e:  # noqa: BLE001
@@ -233,54 +231,51 @@ class HdfsStateProvider:
         return raw[4:4 + n]
 
     def _load_frequencies(self, ident: str, analyzer):
+        """The parquet parts -> one device table, part by part through the flat import (array
+        operations only; a key in several parts adds up, as the reference's union of partitions
+        does), then numRows (StateProvider.scala:280-311)."""
         import pyarrow.parquet as pq
-        from .frequencies import FrequenciesAndNumRows
+        from .frequencies import FrequenciesAndNumRows, FrequencyTable
+        from .keycols import encode_columns
         # file by file: Histogram("count")'s state has two columns named "count", which
         # pyarrow's dataset reader (read_table of a directory) refuses to unify
         directory = self._path(ident, "-frequencies.pqt")
         parts = sorted(f for f in os.listdir(directory) if f.endswith(".parquet")) if os.path.isdir(directory) else []
-        tables = [pq.ParquetFile(os.path.join(directory, f)).read() for f in parts] or \
-            [pq.ParquetFile(directory).read()]
-        table = tables[0] if len(tables) == 1 else _concat(tables)
+        paths = [os.path.join(directory, f) for f in parts] or [directory]
         num_rows = struct.unpack(">q", self._read(self._path(ident, "-num_rows.bin")))[0]
-        # the count column: deequ's name for grouping states, Spark's "count" for Histogram;
-        # anything else (a state written by another tool) -- the last column
-        # (by position: Histogram("count") gives two columns named "count")
-        names_all = list(table.column_names)
-        ci = names_all.index(COUNT_COL) if COUNT_COL in names_all else len(names_all) - 1
-        keys = [i for i in range(len(names_all)) if i != ci]
-        names = [names_all[i] for i in keys]
-        dtypes = [_dtype_of(table.schema.field(i).type) for i in keys]
-        counts = table.column(ci).to_pylist()
-        cols = [table.column(i).to_pylist() for i in keys]
-        freqs: Dict[tuple, int] = {}
-        for i, c in enumerate(counts):
-            key = tuple(col[i] for col in cols)
-            freqs[key] = freqs.get(key, 0) + int(c)
-        return FrequenciesAndNumRows.from_frequencies(names, dtypes, freqs, num_rows,
-                                                      histogram=isinstance(analyzer, Histogram))
+        histogram = isinstance(analyzer, Histogram)
+        table = None
+        try:
+            for path in paths:
+                part = pq.ParquetFile(path).read()
+                # the count column: deequ's name for grouping states, Spark's "count" for Histogram;
+                # anything else (a state written by another tool) -- the last column
+                # (by position: Histogram("count") gives two columns named "count")
+                names_all = list(part.column_names)
+                ci = names_all.index(COUNT_COL) if COUNT_COL in names_all else len(names_all) - 1
+                keys = [i for i in range(len(names_all)) if i != ci]
+                if table is None:
+                    names = [names_all[i] for i in keys]
+                    dtypes = [_dtype_of(part.schema.field(i).type) for i in keys]
+                    table = FrequencyTable(names, dict(zip(names, dtypes)), histogram)
+                offs, blob = encode_columns([part.column(i) for i in keys], table.dtypes, histogram)
+                counts = part.column(ci).combine_chunks().to_numpy(zero_copy_only=False)
+                table.import_flat(counts.astype(np.int64, copy=False), offs, blob, 0)
+            table.import_flat(np.zeros(0, np.int64), np.zeros(1, np.int64), np.zeros(0, np.uint8), num_rows)
+        except BaseException:
+            if table is not None:
+                table.close()
+            raise
+        return FrequenciesAndNumRows(table)
 
 
-def _write_frequency_part(path: str, table, freqs: Dict[tuple, int]) -> None:
+def _write_frequency_part(path: str, table) -> None:
     """One parquet part of a frequency state: the grouping columns + the count column (Histogram:
-    the column cast to string, Histogram.scala:63-66, NULL -> "NullValue")."""
-    import pyarrow as pa
+    the column cast to string, Histogram.scala:63-66, NULL -> "NullValue"), built from the flat
+    export with array operations (FrequencyTable.to_arrow)."""
     import pyarrow.parquet as pq
-    from .javafmt import spark_cast_to_string
-    columns = list(table.key_columns)
-    if table.histogram:
-        dtype = table.dtypes[0]
-        names, types = columns, ["string"]
-        rows = [((("NullValue" if k[0] is None else (k[0] if dtype == "string" else
-                                                     spark_cast_to_string(k[0], dtype))),), c)
-                for k, c in freqs.items()]
-    else:
-        names, types = columns, list(table.dtypes)
-        rows = list(freqs.items())
-    arrays = [pa.array([r[0][i] for r in rows], type=getattr(pa, _PA_TYPES[t])()) for i, t in enumerate(types)]
-    arrays.append(pa.array([r[1] for r in rows], type=pa.int64()))
     count_col = HISTOGRAM_COUNT_COL if table.histogram else COUNT_COL
-    pq.write_table(pa.Table.from_arrays(arrays, names=names + [count_col]), path)
+    pq.write_table(table.to_arrow(count_column=count_col), path)
 
 
 def _concat(tables):

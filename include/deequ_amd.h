@@ -413,6 +413,24 @@ dq_status dq_freq_lookup(dq_freq* f, const uint8_t* key, int64_t key_len, int64_
 dq_status dq_freq_import(dq_freq* f, const dq_freq_group* groups, int64_t n, const uint8_t* key_bytes,
                          int64_t num_rows);
 
+/* ---- Columnar (Arrow-layout) state interchange: FrequenciesAndNumRows.frequencies as the
+ * DataFrame columns HdfsStateProvider persists (StateProvider.scala:222-240) and loads
+ * (:280-311), with no per-group record anywhere.  Group i = (counts[i], the encoded key
+ * key_bytes[key_offsets[i] .. key_offsets[i + 1])); key_offsets holds n + 1 values (Arrow's
+ * large-offset layout).  DQ_FLAT_DEVICE: the three buffers are device memory on the table's
+ * device, else host memory. */
+#define DQ_FLAT_DEVICE 0x1
+/* Every group in slot order (the same table exports the same columns).  *n_out / *key_bytes_out
+ * receive the sizes; when they exceed max_groups / key_cap (or a buffer is NULL) nothing is
+ * written and DQ_ERR_SPACE is returned -- the export stays on the device for the filling call,
+ * which hands it over. */
+dq_status dq_freq_export_flat(dq_freq* f, int64_t* counts, int64_t* key_offsets, uint8_t* key_bytes,
+                              int64_t max_groups, int64_t key_cap, int flags, int64_t* n_out, int64_t* key_bytes_out);
+/* FrequenciesAndNumRows.sum of n flat groups (+ num_rows): duplicate keys add up, as the
+ * reference's outer join does (GroupingAnalyzers.scala:128-148).  Offsets are validated first. */
+dq_status dq_freq_import_flat(dq_freq* f, const int64_t* counts, const int64_t* key_offsets, const uint8_t* key_bytes,
+                              int64_t n, int64_t num_rows, int flags);
+
 /* ---------------------------------------------------------------- multi-GPU key-hash exchange
  * The frequency family's one real exchange step: Spark shuffles the partial
  * group counts by key hash into spark.sql.shuffle.partitions before the final aggregate

@@ -8,7 +8,7 @@ from typing import Dict, List, Tuple
 import numpy as np
 import torch
 
-from deequ_amd.frequencies import encode_key
+from deequ_amd.frequencies import FrequencyTable, encode_key
 
 HEAP = 1 << 30
 
@@ -163,6 +163,14 @@ class FakeFrequencyTable:
 
     def export(self):
         return np.array(list(self.groups.values()), dtype=np.int64), list(self.groups.keys())
+
+    to_arrow = FrequencyTable.to_arrow  # (built on export_flat only)
+
+    def export_flat(self, device=False):
+        counts, keys = self.export()
+        offs = np.zeros(len(keys) + 1, dtype=np.int64)
+        np.cumsum([len(k) for k in keys], out=offs[1:])
+        return counts, offs, np.frombuffer(b"".join(keys), dtype=np.uint8).copy()
 
     def close(self):
         pass

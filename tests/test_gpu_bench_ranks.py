@@ -34,3 +34,8 @@ def test_bench_two_ranks_gloo(gpu, workload):
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["value"] > 0 and out["steps"] == 2, out
     assert out["scaling"] == "weak"
+    if workload == "c4":  # the key-hash exchange's cost is reported beside the step time
+        ex = out["exchange"]
+        assert ex["exchange_bytes"] > 0 and ex["bytes_received"] > 0, ex
+        assert ex["max_exchange_ms"] >= ex["exchange_ms"] > 0, ex
+        assert ex["exchange_ms"] >= ex["alltoall_ms"] >= 0 and ex["import_ms"] > 0, ex

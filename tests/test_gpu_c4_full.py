@@ -15,14 +15,17 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_c4_full_size_against_torch_unique(gpu):
+@pytest.mark.parametrize("keys", ["digits", "alnum"])
+def test_c4_full_size_against_torch_unique(gpu, keys):
+    """digits: 12-digit keys (packed 8-byte records); alnum: 'k' + 11 digits -- keys that are not
+    digit strings, staged as 16-byte records from the first batch (the pack probe)."""
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "c4", "--c4-verify", "--steps", "1",
-           "--warmup", "0"]
+           "--warmup", "0", "--c4-keys", keys]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600,
                        env=dict(os.environ, PYTHONUNBUFFERED="1"))
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     v = line["verify"]
-    print("\n[c4 full] %s" % json.dumps(v))
+    print("\n[c4 full %s] %s" % (keys, json.dumps(v)))
     assert v["ok"], v
     assert v["groups"] > 180_000_000 and v["detail_bins"] >= 999
