@@ -2938,8 +2938,9 @@ __device__ inline void imp_range(const ImportRun& R, int run, uint64_t r, int rb
     }
     return;
   }
-  *b = start[(uint64_t)run * n_slices + r];
-  *e = end[(uint64_t)run * n_slices + r];
+  const uint64_t q = R.bits < rb ? r >> (rb - R.bits) : r;  // (coarser bounds: the enclosing range)
+  *b = start[(uint64_t)run * n_slices + q];
+  *e = end[(uint64_t)run * n_slices + q];
 }
 
 // HLL p = 9 of every present record's hash (table sizing).
@@ -2958,33 +2959,44 @@ __global__ __launch_bounds__(kBlock) void dq_import_sketch_kernel(const ImportRu
     if (regs[i]) atomicMax(&hll[i], regs[i]);
 }
 
-// Slice boundaries of each wire run (blockIdx.y): start[run][r] / end[run][r] for the receiver's
-// slices (both 0 for a slice the run does not hold); unsorted[run] = 1 if the run is not in slice
-// order (then its bounds are meaningless and it is imported group by group).
+// Slice boundaries of each wire run (blockIdx.y) at its R.bits slice bits: start[run][r] /
+// end[run][r] (both 0 for a slice the run does not hold); unsorted[run] = 1 if the run is not in
+// order at those bits -- then drop[run] = the fewest top bits to drop for it to be in order (the
+// largest depth, below R.bits, at which two adjacent records' slices first differ the wrong way).
+// rerun: only the runs whose bits were lowered (R.bits < rb) are cut again.
 __global__ __launch_bounds__(kBlock) void dq_import_bounds_kernel(const ImportRun* __restrict__ runs, int rb,
                                                                   uint64_t n_slices, uint32_t* start, uint32_t* end,
-                                                                  unsigned int* unsorted) {
+                                                                  unsigned int* unsorted, unsigned int* drop, int rerun) {
   const int run = blockIdx.y;
   const ImportRun R = runs[run];
-  if (R.kind == 2) return;
+  if (R.kind == 2 || (rerun && R.bits >= rb)) return;
+  const int g = R.bits;
   uint32_t* st = start + (uint64_t)run * n_slices;
   uint32_t* en = end + (uint64_t)run * n_slices;
+  unsigned int worst = 0u;
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < R.n; i += (uint64_t)gridDim.x * kBlock) {
     ImpRec r, q;
     imp_load<true>(R, i, r);
-    const uint64_t si = dst_slice(r.hash, rb);
+    const uint64_t si = dst_slice(r.hash, g);
     if (i == 0) {
       st[si] = 0u;
     } else {
       imp_load<true>(R, i - 1, q);
-      const uint64_t sp = dst_slice(q.hash, rb);
+      const uint64_t sp = dst_slice(q.hash, g);
       if (sp != si) {
-        if (sp > si) unsorted[run] = 1u;
+        if (sp > si) {  // equal top bits: clz of the difference within the g-bit slice number
+          const unsigned int same = (unsigned int)(__clzll((long long)(sp ^ si)) - (64 - g));
+          worst = max(worst, (unsigned int)g - same);
+        }
         st[si] = (uint32_t)i;
         en[sp] = (uint32_t)i;
       }
     }
     if (i + 1 == R.n) en[si] = (uint32_t)R.n;
+  }
+  if (worst) {
+    unsorted[run] = 1u;
+    atomicMax(&drop[run], worst);
   }
 }
 
@@ -3379,10 +3391,11 @@ hipError_t launch_import_sketch(const ImportRun* d_runs, int n_runs, uint64_t ma
 }
 
 hipError_t launch_import_bounds(const ImportRun* d_runs, int n_runs, uint64_t max_n, int rb, uint64_t n_slices,
-                                uint32_t* d_start, uint32_t* d_end, unsigned int* d_unsorted, hipStream_t stream) {
+                                uint32_t* d_start, uint32_t* d_end, unsigned int* d_unsorted, unsigned int* d_drop,
+                                int rerun, hipStream_t stream) {
   if (n_runs < 1 || n_runs > 65535 || max_n == 0) return hipSuccess;
   hipLaunchKernelGGL(dq_import_bounds_kernel, dim3(grid_for(max_n, kBlock * 8, 2048), (unsigned)n_runs), dim3(kBlock), 0,
-                     stream, d_runs, rb, n_slices, d_start, d_end, d_unsorted);
+                     stream, d_runs, rb, n_slices, d_start, d_end, d_unsorted, d_drop, rerun);
   return hipGetLastError();
 }
 

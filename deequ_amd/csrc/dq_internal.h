@@ -224,6 +224,9 @@ struct WirePacked {
 // One record stream a merge takes in: a part's packed section (kind 0), its general section
 // (kind 1: FreqSlot, READY clear, k0 of a long key = offset in `heap`), or a source table's slot
 // array (kind 2, src_bits = its slice bits).  skip = 1: out of slice order, inserted group by group.
+// bits (wire runs): the slice bits its bounds are cut at -- the receiver's, or fewer when the run
+// is in order only by its top `bits` hash bits (a sender that sorted by coarser slices or chunks
+// than the receiver's slices); the merge then reads the coarser range and filters by slice.
 constexpr int kImportFlatRuns = 16;  // packed runs the import merge takes as one index space
 struct ImportRun {
   const void* recs;
@@ -232,7 +235,7 @@ struct ImportRun {
   int32_t kind;
   int32_t src_bits;
   int32_t skip;
-  int32_t pad_;
+  int32_t bits;
 };
 hipError_t launch_wire_count(const FreqTable& T, int n_parts, int chunk_log, uint64_t n_chunks, unsigned long long* d_cnt,
                              unsigned long long* d_kbytes, hipStream_t stream);
@@ -244,7 +247,8 @@ hipError_t launch_wire_scatter(const FreqTable& T, int n_parts, int chunk_log, u
                                uint8_t* d_keys, hipStream_t stream);
 hipError_t launch_import_sketch(const ImportRun* d_runs, int n_runs, uint64_t max_n, uint32_t* d_hll, hipStream_t stream);
 hipError_t launch_import_bounds(const ImportRun* d_runs, int n_runs, uint64_t max_n, int rb, uint64_t n_slices,
-                                uint32_t* d_start, uint32_t* d_end, unsigned int* d_unsorted, hipStream_t stream);
+                                uint32_t* d_start, uint32_t* d_end, unsigned int* d_unsorted, unsigned int* d_drop,
+                                int rerun, hipStream_t stream);
 hipError_t launch_import_merge(const FreqTable& T, bool packed, bool flat, const ImportRun* d_runs, int n_runs, const uint32_t* d_start,
                                const uint32_t* d_end, int table_empty, unsigned long long* d_hist, unsigned long long* d_big,
                                unsigned long long* d_n_big, unsigned long long big_cap, uint32_t* d_smax, int write_all,

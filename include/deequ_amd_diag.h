@@ -26,7 +26,9 @@ dq_status dq_diag_hash_rate(int device, int with_hll, int reps, double* hashes_p
  * out[3] = records that went through the sort path (small stagings, retries, skew fallbacks),
  * out[4] = partition-path aggregations of packed digit-key records, out[5] = batches grouped by
  * the few-groups kernel (dq_freq_small_kernel), out[6] = 1 if a wait for another lane's slot
- * publish ever timed out (an error every API call also reports).  `out` holds 7 values. */
+ * publish ever timed out (an error every API call also reports), out[7] = imported wire runs
+ * that were in order only by coarser slices than the table's (merged from the enclosing ranges),
+ * out[8] = imported wire runs out of order (inserted group by group).  `out` holds 9 values. */
 dq_status dq_diag_freq_paths(dq_freq* f, int64_t* out);
 
 /* Test hooks of one table (tests only; never set by the product): flags = 1 makes claimed

@@ -254,3 +254,33 @@ def test_c4_scale_partition_import(gpu):
     assert o.lookup(b"not-a-key") == 0
     o.close()
     t.close()
+
+
+@pytest.mark.parametrize("grow", [1, 2, 3, 5])
+def test_import_into_finer_receiver(gpu, monkeypatch, grow):
+    """a receiver table with more slice bits than the sender's (2^grow times the
+    slots; e.g. owners of disjoint key sets sized independently).  The sender's runs are in order
+    only by its own coarser slices: they are cut at those (each receiver slice reads the
+    enclosing range and filters) when the difference is at most 3 bits -- no group-by-group
+    fallback -- and inserted group by group beyond that.  Exact either way."""
+    spec = _spec(60000, 12)
+    t = _table(spec)
+    want = _want(spec)
+    buf, keys, pp, pg, pk = _parts(t, 2)
+    send_slots = t.paths()["slots"]
+    monkeypatch.setenv("DQ_FREQ_PART_SLOTS", str(send_slots << grow))
+    o = FrequencyTable.like(t)
+    o.import_parts(buf, pp, pg, keys, pk)
+    assert _groups(o) == want
+    paths = o.paths()
+    assert paths["slots"] == send_slots << grow
+    n_wire = sum(1 for v in pp + pg if v)
+    if grow <= 3:
+        assert paths["import_coarse_runs"] == n_wire and paths["import_skipped_runs"] == 0, paths
+    else:
+        assert paths["import_skipped_runs"] == n_wire, paths
+    # a second import into the now non-empty table: the same cut, doubled counts
+    o.import_parts(buf, pp, pg, keys, pk)
+    assert _groups(o) == {k: 2 * c for k, c in want.items()}
+    o.close()
+    t.close()
