@@ -58,6 +58,8 @@ def parse_args():
     p.add_argument("--c3-rows", type=int, default=125_000_000, help="rows per GPU (one batch)")
     p.add_argument("--c3-batches", type=int, default=1,
                    help="> 1: also run the whole C3 job, one plan over this many batches (8 = 1e9 rows)")
+    p.add_argument("--c3-verify", action="store_true",
+                   help="with --c3-batches: column 0's registers of the whole job against the oracle (untimed)")
     p.add_argument("--c4-rows", type=int, default=1_000_000_000, help="rows per GPU")
     p.add_argument("--c4-batch", type=int, default=125_000_000, help="rows per string batch")
     p.add_argument("--c4-distinct", type=int, default=201_500_000)
@@ -467,6 +469,7 @@ def valu_roofline(device: int, hashes: float, kernel_ms: float):
 
 def run_c3(args, world, rank, local):
     """HLL++ ApproxCountDistinct on C3 columns: one fused dq_plan, HIP events on its stream."""
+    import numpy as np
     import torch
     import deequ_amd as d
     from deequ_amd.distributed import allgather_merge
@@ -498,6 +501,7 @@ def run_c3(args, world, rank, local):
         # consumes -- untimed); the scans of all batches are timed with HIP events on the plan's stream
         plan.reset()
         scan_ms = 0.0
+        oracle_regs = None
         for b in range(args.c3_batches):
             if b > 0:
                 make_c3_table(args.c3_rows, args.c3_columns, rank, local, batch=b, into=table)
@@ -507,6 +511,11 @@ def run_c3(args, world, rank, local):
             e1.record(stream)
             e1.synchronize()
             scan_ms += e0.elapsed_time(e1)
+            if args.c3_verify and world == 1:  # column 0 of this batch through the oracle (untimed)
+                c0 = table.columns["h0"]
+                regs = _oracle_hll_int64(c0.values[:args.c3_rows].cpu().numpy(),
+                                         c0.validity[:(args.c3_rows + 7) // 8].cpu().numpy())
+                oracle_regs = regs if oracle_regs is None else np.maximum(oracle_regs, regs)
         fraw = plan.finish_raw()
         if world > 1:
             fraw = allgather_merge(fraw, len(analyzers), device=_comm_dev(args, local))
@@ -518,6 +527,8 @@ def run_c3(args, world, rank, local):
                     "note": "one plan, %d consumes of %d-row batches regenerated in HBM between them "
                             "(untimed); scan time = sum of the consumes' HIP-event times"
                             % (args.c3_batches, args.c3_rows)}
+        if oracle_regs is not None:
+            full_job["verify"] = _c3_verify(oracle_regs, list(fraw[0].words))
     rows_total = args.c3_rows * world * args.steps
     achieved = bpr * args.c3_rows / (kernel_ms * 1e-3) / 1e9
     return {
@@ -538,6 +549,33 @@ def run_c3(args, world, rank, local):
         "check": {"column0_estimate": est, "rows_column0": args.c3_rows},
         "full_job": full_job,
     }
+
+
+def _oracle_hll_int64(values, validity):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cdq_oracle
+    return cdq_oracle.hll_registers_int64(values, validity, host_cpu_share())
+
+
+def _c3_verify(oracle_regs, gpu_words):
+    """Column 0 of the whole C3 job: the GPU plan's 52 words against the oracle's registers of
+    every batch (max-merged), and the estimate explained register by register: Deequ's count
+    adds 1.0 / (1 << m) with Java's Int shift (StatefulHyperloglogPlus.scala:222), whose count is
+    taken mod 32 -- a register of rank m >= 32 adds 2^-(m - 32) instead of 2^-m."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+    want = O.hll_pack([int(r) for r in oracle_regs])
+    regs = O.hll_unpack(gpu_words)
+    high = {i: r for i, r in enumerate(regs) if r >= 32}
+    z_low = sum(2.0 ** -r for r in regs if r < 32)
+    return {"words_equal": [int(w) for w in gpu_words] == want,
+            "registers_ge_32": high,
+            "register_max": max(regs),
+            "estimate_oracle": O.hll_count(want),
+            "estimate_without_int_shift": O.HLL_ALPHA_M2 / (z_low + sum(2.0 ** -r for r in high.values()))
+            if high else None,
+            "z_inverse_terms": {"ranks_below_32": z_low,
+                                "ranks_ge_32_java": sum(1.0 / float(O._java_int_shift_one(r)) for r in high.values())}}
 
 
 def _column_bytes(col) -> float:

@@ -1270,7 +1270,7 @@ __device__ inline uint64_t rec_hash(const FreqRec& r, bool* hole) {
   return hash_inline(r.k0, k1, len);
 }
 __device__ inline uint64_t rec_hash(uint64_t p, bool* hole) {
-  *hole = false;
+  *hole = p == kPackEmpty;  // (a row the row-order staging left empty)
   return hash_record_packed(p);
 }
 
@@ -1412,6 +1412,10 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
     room[k] = 0ull;
     if (b < nb) {
       const uint32_t c = L.hist[b];
+#ifdef DQ_X_NORES  // (timing experiment, results wrong: no reservation round trip)
+      if (REC_LDS) room[k] = (unsigned long long)(blockIdx.x & 63u) * 64ull;
+      else
+#endif
       if (c) room[k] = atomicAdd(&out_fill[base_id + b], (unsigned long long)c);
     }
   }
@@ -1463,6 +1467,9 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
       const uint32_t pos = r0 + j;  // the record's tile position
       const R r = L.rec[j];
       if (pos < L.lim[b]) {
+#ifdef DQ_X_NOWRITE  // (timing experiment, results wrong: no record stores)
+        if (!REC_LDS)
+#endif
         out[L.gbase[b] + pos] = r;
       } else {  // the region is full: the overflow list (16-B records, aggregated by the sort path)
         const unsigned long long k = atomicAdd(ovf_n, 1ull);
@@ -1496,7 +1503,7 @@ template <typename R, int MAXB>
 __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(sizeof(R) == 8 && MAXB <= 512 ? DQ_PARTP_WAVES : 1))) void dq_freq_part_kernel(
     const R* __restrict__ in, uint64_t in_n, const unsigned long long* __restrict__ in_fill, uint64_t in_cap,
     int id_bits, int bin_bits, R* __restrict__ out, uint64_t out_cap, unsigned long long* out_fill,
-    FreqRec* ovf, unsigned long long* ovf_n, uint64_t ovf_cap, unsigned int* flag) {
+    FreqRec* ovf, unsigned long long* ovf_n, uint64_t ovf_cap, unsigned int* flag, unsigned long long* staged) {
   // (2048 bins: the smaller LDS rounds keep two workgroups per CU)
   __shared__ PartLdsT<MAXB, R, (sizeof(R) == 8 && MAXB <= 512 ? kPartSubP : kPartSub)> L;
   constexpr uint32_t TILE = sizeof(R) == 8 ? kPartTileP : kPartTile;
@@ -1535,7 +1542,7 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(si
       if (!hole) bin[i] = (uint32_t)(h >> (64 - id_bits)) & (nb - 1u);
     }
   }
-  part_tile(L, rec, bin, nb, base_id, out, out_cap, out_fill, ovf, ovf_n, ovf_cap, flag, nullptr);
+  part_tile(L, rec, bin, nb, base_id, out, out_cap, out_fill, ovf, ovf_n, ovf_cap, flag, staged);
 }
 
 // ---- bucket split: the sort path's grouping of staged records by slice (small stagings, and the
@@ -1980,7 +1987,11 @@ __global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(D
             packed = kp_pack_record(k0, k1, len, &p);
           }
           if (packed) {
+#ifdef DQ_X_NOPARK  // (experiment: records stay in registers)
+            rec[j] = p;
+#else
             L.rec[j * kStageThreads + t] = p;  // (row order; part_tile sorts it)
+#endif
             h = hash_record_packed(p);
           } else {  // not a digit key: a 16-B record on the overflow list
             h = hash_raw(k0, k1, len);
@@ -2044,14 +2055,204 @@ __global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(D
       if constexpr (PACK)
         if (t == 0) abort_v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
+#ifdef DQ_X_NOSPLIT  // (timing experiment, results wrong: no multi-split, nothing written)
+#ifdef DQ_X_ROWWRITE  // (... but the records written in row order, coalesced)
+    if constexpr (PACK) {
+#pragma unroll
+      for (int j = 0; j < kStagePer; ++j) out[(uint64_t)tile * kStageTile + (uint64_t)j * kStageThreads + t] = L.rec[j * kStageThreads + t];
+    }
+#else
+    if (t == 0 && bin[0] == 0xFFFFFFFEu) out[0] = L.rec[0];
+#endif
+#else
     part_tile<kStagePer, (1 << kStageBinBits), R, (PACK ? kStageSubP : kPartSub), kProf, DQ_STAGE_WOUT_UNROLL,
-              PACK, kStageThreads, decltype(flag_read)>(
+#ifdef DQ_X_NOPARK
+              false,
+#else
+              PACK,
+#endif
+              kStageThreads, decltype(flag_read)>(
         L, rec, bin, nb, 0, out, cap1, fill1, ovf, ovf_n, ovf_cap, flag, staged, nullptr, prof_t_, flag_read);
+#endif
   }
   if (PACK && n_side) atomicAdd(staged, (unsigned long long)n_side);
 #ifdef DQ_STAGE_PROF
   if (t == 0 && blockIdx.x < 4096u) g_stage_blk[blockIdx.x][1] = wall_clock64();
 #endif
+  lds_barrier();
+  for (uint32_t i = t; i < (uint32_t)kHllM; i += kStageThreads)
+    if (regs[i] != 0xFFFFFFFFu) atomicMax(&hll[i], stage_sketch_rank(regs[i]));
+}
+
+// The stage's first half on its own (round 5): every row of the batch becomes its record in ROW
+// order -- out[row] -- with no split, so the kernel is a pure stream (the input read once, the
+// records written with coalesced stores) that keeps the key loads of many workgroups in flight;
+// the level-1 split runs next as dq_freq_part_kernel over the row array (level 1: records of
+// 24 per thread in 6144-record LDS rounds).  Measured on one box (125M-row batches, C4): the
+// fused stage + level-1 kernel 1.36-1.40 ms, its loads + packing + sketch alone 0.47 ms, with the
+// row-order record stores 0.58 ms.  A row that stages nothing (NULL outside a Histogram, a key
+// put on the overflow list, a key over 15 bytes) holds a hole: kPackEmpty / length kRecHole,
+// which the split drops.  Sketch, long-key flag, overflow list and `staged` (the overflow list's
+// share; the split counts the rest) are kept as the fused kernel keeps them.
+template <bool ONE_STRING, bool PACK>
+__global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(DQ_STAGEP_WAVES))) void dq_freq_stage_rows_kernel(
+    FreqKeySpec ks, const DevColumn* __restrict__ cols, int64_t n_rows,
+    typename std::conditional<PACK, uint64_t, FreqRec>::type* __restrict__ out, FreqRec* ovf,
+    unsigned long long* ovf_n, uint64_t ovf_cap, unsigned int* flag, uint32_t* hll, unsigned long long* long_key,
+    unsigned long long* staged) {
+  static_assert(ONE_STRING || !PACK, "packed records are staged from one string key column");
+  __shared__ uint32_t regs[kHllM];
+  __shared__ uint4 psel[16];  // stage_pack's byte selectors by key length
+  const uint32_t t = threadIdx.x;
+  for (uint32_t i = t; i < (uint32_t)kHllM; i += kStageThreads) regs[i] = 0xFFFFFFFFu;  // (stage_sketch)
+  if (PACK && t < 16u) psel[t] = make_uint4(stage_pack_sel(t, 0), stage_pack_sel(t, 1), stage_pack_sel(t, 2), stage_pack_sel(t, 3));
+  lds_barrier();
+  const DevColumn& c0 = cols[ks.key_cols[0]];
+  alignas(8) uint8_t scratch[kMaxLocalKey];
+  const int64_t n_tiles = (n_rows + kStageTile - 1) / kStageTile;
+  uint32_t n_side = 0;  // PACK: this thread's keys put on the overflow list (not digit strings)
+  const uint32_t heap_end = ONE_STRING ? __builtin_amdgcn_readfirstlane((uint32_t)uniform_ptr(c0.offsets)[n_rows]) : 0u;
+  const uint8_t* vals = static_cast<const uint8_t*>(uniform_ptr(c0.values));
+  const __amdgpu_buffer_rsrc_t rs_vals =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vals), 0, (int)heap_end, 0x00020000);
+  if (ONE_STRING && heap_end < 16u) {  // (a heap under 16 bytes: key_load16's general path, as a long key)
+    if (blockIdx.x == 0 && t == 0) atomicMax(long_key, 16ull);
+    return;
+  }
+  const bool has_validity = uniform_ptr(c0.validity) != nullptr;
+  uint32_t pob[kStagePer], poe[kStagePer], vword = 0u;
+  constexpr uint32_t kLenNull = 254u, kLenLong = 255u;
+  uint32_t kw[kStagePer][4], lens[(kStagePer + 3) / 4], sel = 0u;
+  using R = typename std::conditional<PACK, uint64_t, FreqRec>::type;
+  auto hole = [&]() -> R {
+    if constexpr (PACK) {
+      return kPackEmpty;
+    } else {
+      FreqRec r;
+      r.k0 = 0ull;
+      r.k1 = (unsigned long long)kRecHole << kRecLenShift;
+      return r;
+    }
+  };
+  // PACK: once the overflow list has filled up (a column of keys that are not digit strings) the
+  // batch will be rolled back, so a wave stops at its next tile once one of its lanes found the
+  // list full (no flag read per tile: the atomic's own return says it)
+  bool full = false;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    if constexpr (PACK)
+      if (__ballot(full)) break;
+    const int64_t row0 = tile * (int64_t)kStageTile;
+    uint32_t too_long = 0u;
+    if constexpr (ONE_STRING) {
+      stage_offsets(c0, n_rows, tile, pob, poe, vword);
+      sel = 0u;
+#pragma unroll
+      for (int j = 0; j < (kStagePer + 3) / 4; ++j) lens[j] = 0u;
+#pragma unroll
+      for (int j = 0; j < kStagePer; ++j) {
+        const int64_t row = row0 + j * kStageThreads + t;
+        const uint32_t n = poe[j] - pob[j];
+        const bool valid = !has_validity || ((stage_valid_mask(vword, j) >> (t & 63u)) & 1u);
+        if (row < n_rows && (valid || ks.null_as_key)) sel |= 1u << j;
+        const uint32_t nb8 = (row < n_rows && !valid) ? kLenNull : (n > 15u ? kLenLong : n | (key_shift(pob[j], heap_end) << 4));
+        lens[j / 4] |= nb8 << (8 * (j % 4));
+      }
+#pragma unroll
+      for (int j = 0; j < kStageWin; ++j) key_load16(rs_vals, heap_end, pob[j], kw[j]);
+#pragma unroll
+      for (int j = 0; j < kStagePer; ++j) {
+        if (j + kStageWin < kStagePer) key_load16(rs_vals, heap_end, pob[j + kStageWin], kw[j + kStageWin]);
+        const int64_t row = row0 + j * kStageThreads + t;
+        if (row >= n_rows) continue;
+        R r = hole();
+        if ((sel >> j) & 1u) {
+          uint32_t n = (lens[j / 4] >> (8 * (j % 4))) & 0xFFu;
+          if (n == kLenLong) {
+            too_long = 16u;
+          } else {
+            if (n != kLenNull) {
+              if (n > 15u) key_shr_bytes(kw[j], n >> 4);  // a key in the heap's last 16 bytes (rare)
+              n &= 15u;
+            }
+            auto key_words = [&](uint64_t& k0, uint64_t& k1, uint32_t& len) {
+              if (n == kLenNull) {
+                len = 9;
+                k0 = kNullK0;
+                k1 = kNullK1;
+              } else {
+                const uint64_t lo = (uint64_t)kw[j][0] | ((uint64_t)kw[j][1] << 32);
+                const uint64_t hi = (uint64_t)kw[j][2] | ((uint64_t)kw[j][3] << 32);
+                len = n;
+                k0 = n >= 8 ? lo : (lo & ((1ull << (8u * n)) - 1ull));
+                k1 = n > 8 ? (hi & ((1ull << (8u * (n - 8u))) - 1ull)) : 0ull;
+              }
+            };
+            if constexpr (PACK) {
+              uint64_t p = kPackNull;
+              bool packed = n == kLenNull || stage_pack(kw[j], n, psel[n], &p);
+              uint64_t k0 = 0, k1 = 0;
+              uint32_t len = 0;
+              if (!packed) {
+                key_words(k0, k1, len);
+                packed = kp_pack_record(k0, k1, len, &p);
+              }
+              if (packed) {
+                r = p;
+                stage_sketch(regs, hash_record_packed(p));
+              } else {  // not a digit key: a 16-B record on the overflow list, a hole in the rows
+                stage_sketch(regs, hash_raw(k0, k1, len));
+                FreqRec o;
+                o.k0 = k0;
+                o.k1 = k1 | ((unsigned long long)len << kRecLenShift);
+                const unsigned long long k = atomicAdd(ovf_n, 1ull);
+                if (k < ovf_cap) {
+                  ovf[k] = o;
+                } else {
+                  atomicOr(flag, 1u);
+                  full = true;
+                }
+                ++n_side;
+              }
+            } else {
+              uint64_t k0, k1;
+              uint32_t len;
+              key_words(k0, k1, len);
+              stage_sketch(regs, hash_inline(k0, k1, len));
+              r.k0 = k0;
+              r.k1 = k1 | ((unsigned long long)len << kRecLenShift);
+            }
+          }
+        }
+        out[row] = r;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < kStagePer; ++i) {
+        const int64_t row = row0 + i * kStageThreads + t;
+        if (row >= n_rows) continue;
+        R r = hole();
+        Key k;
+        bool tl;
+        if (make_key(ks, cols, row, k, scratch, tl)) {
+          if (k.len > 15 || k.ptr != nullptr) {
+            too_long = max(too_long, k.len > 15 ? k.len : 16u);
+          } else {
+            if constexpr (!PACK) {
+              r.k0 = k.k0;
+              r.k1 = k.k1 | ((unsigned long long)k.len << kRecLenShift);
+            }
+            stage_sketch(regs, k.hash);
+          }
+        } else if (tl) {
+          too_long = max(too_long, (uint32_t)kMaxLocalKey + 1u);
+        }
+        out[row] = r;
+      }
+    }
+    if (too_long) atomicMax(long_key, (unsigned long long)too_long);
+  }
+  if (PACK && n_side) atomicAdd(staged, (unsigned long long)n_side);
   lds_barrier();
   for (uint32_t i = t; i < (uint32_t)kHllM; i += kStageThreads)
     if (regs[i] != 0xFFFFFFFFu) atomicMax(&hll[i], stage_sketch_rank(regs[i]));
@@ -2413,7 +2614,8 @@ hipError_t launch_freq_agg(const FreqTable& T, const FreqRec* d_recs, const uint
 hipError_t launch_freq_part(const void* d_in, uint64_t in_n, const unsigned long long* d_in_fill, uint64_t in_cap,
                             uint64_t n_in_regions, int id_bits, int bin_bits, void* d_out, uint64_t out_cap,
                             unsigned long long* d_out_fill, FreqRec* d_ovf, unsigned long long* d_ovf_n,
-                            uint64_t ovf_cap, unsigned int* d_flag, bool packed, hipStream_t stream) {
+                            uint64_t ovf_cap, unsigned int* d_flag, bool packed, hipStream_t stream,
+                            unsigned long long* d_staged) {
   if (bin_bits < 0 || bin_bits > kPartMaxBinBits || id_bits < bin_bits || id_bits > 32) return hipErrorInvalidValue;
   const uint64_t tile = packed ? kPartTileP : kPartTile;  // (the kernel's records per workgroup)
   dim3 grid;
@@ -2427,15 +2629,15 @@ hipError_t launch_freq_part(const void* d_in, uint64_t in_n, const unsigned long
   if (packed && bin_bits <= kStageBinBits)
     hipLaunchKernelGGL((dq_freq_part_kernel<uint64_t, (1 << kStageBinBits)>), grid, dim3(kPartThreads), 0, stream,
                        static_cast<const uint64_t*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
-                       static_cast<uint64_t*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag);
+                       static_cast<uint64_t*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag, d_staged);
   else if (packed)
     hipLaunchKernelGGL((dq_freq_part_kernel<uint64_t, (1 << kPartMaxBinBits)>), grid, dim3(kPartThreads), 0, stream,
                        static_cast<const uint64_t*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
-                       static_cast<uint64_t*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag);
+                       static_cast<uint64_t*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag, d_staged);
   else
     hipLaunchKernelGGL((dq_freq_part_kernel<FreqRec, (1 << kPartMaxBinBits)>), grid, dim3(kPartThreads), 0, stream,
                        static_cast<const FreqRec*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
-                       static_cast<FreqRec*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag);
+                       static_cast<FreqRec*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag, d_staged);
   return hipGetLastError();
 }
 
@@ -2483,12 +2685,38 @@ hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, bool p
                                   int64_t n_rows, int b1, void* d_out,
                                   uint64_t cap1, unsigned long long* d_fill1, FreqRec* d_ovf, unsigned long long* d_ovf_n,
                                   uint64_t ovf_cap, unsigned int* d_flag, uint32_t* d_hll, unsigned long long* d_long_key,
-                                  unsigned long long* d_staged, hipStream_t stream) {
+                                  unsigned long long* d_staged, hipStream_t stream, void* d_rows) {
   if (n_rows <= 0) return hipSuccess;
   if (b1 < 1 || b1 > kStageBinBits || (packed && !one_string)) return hipErrorInvalidValue;
   const int64_t tiles = (n_rows + kStageTile - 1) / kStageTile;
   int dev = 0, cus = 256, per_cu = 2;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (d_rows) {  // row-order staging, then the level-1 split over the rows (dq_freq_stage_rows_kernel)
+    if (packed)
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dq_freq_stage_rows_kernel<true, true>, kStageThreads, 0);
+    else if (one_string)
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dq_freq_stage_rows_kernel<true, false>, kStageThreads, 0);
+    else
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dq_freq_stage_rows_kernel<false, false>, kStageThreads, 0);
+    const int64_t resident = (int64_t)cus * (per_cu > 0 ? per_cu : 1);
+    const int64_t blocks = tiles < resident ? tiles : resident;
+    if (packed)
+      hipLaunchKernelGGL((dq_freq_stage_rows_kernel<true, true>), dim3((unsigned)blocks), dim3(kStageThreads), 0, stream, ks,
+                         d_cols, n_rows, static_cast<uint64_t*>(d_rows), d_ovf, d_ovf_n, ovf_cap, d_flag, d_hll,
+                         d_long_key, d_staged);
+    else if (one_string)
+      hipLaunchKernelGGL((dq_freq_stage_rows_kernel<true, false>), dim3((unsigned)blocks), dim3(kStageThreads), 0, stream, ks,
+                         d_cols, n_rows, static_cast<FreqRec*>(d_rows), d_ovf, d_ovf_n, ovf_cap, d_flag, d_hll,
+                         d_long_key, d_staged);
+    else
+      hipLaunchKernelGGL((dq_freq_stage_rows_kernel<false, false>), dim3((unsigned)blocks), dim3(kStageThreads), 0, stream, ks,
+                         d_cols, n_rows, static_cast<FreqRec*>(d_rows), d_ovf, d_ovf_n, ovf_cap, d_flag, d_hll,
+                         d_long_key, d_staged);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_freq_part(d_rows, (uint64_t)n_rows, nullptr, 0, 0, b1, b1, d_out, cap1, d_fill1, d_ovf, d_ovf_n, ovf_cap,
+                            d_flag, packed, stream, d_staged);
+  }
   // one resident round of workgroups (grid-stride over the tiles)
   if (packed)
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dq_freq_stage_part_kernel<true, true>, kStageThreads, 0);

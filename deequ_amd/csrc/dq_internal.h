@@ -324,7 +324,8 @@ hipError_t launch_freq_agg(const FreqTable& T, const FreqRec* d_recs, const uint
 hipError_t launch_freq_part(const void* d_in, uint64_t in_n, const unsigned long long* d_in_fill, uint64_t in_cap,
                             uint64_t n_in_regions, int id_bits, int bin_bits, void* d_out, uint64_t out_cap,
                             unsigned long long* d_out_fill, FreqRec* d_ovf, unsigned long long* d_ovf_n,
-                            uint64_t ovf_cap, unsigned int* d_flag, bool packed, hipStream_t stream);
+                            uint64_t ovf_cap, unsigned int* d_flag, bool packed, hipStream_t stream,
+                            unsigned long long* d_staged = nullptr);
 // With an empty table it can also produce the count-of-counts histogram (d_hist, counts >=
 // kFreqHist into d_big), each slice's largest count (d_smax) and write every slot (write_all:
 // the table needs no clearing).
@@ -338,7 +339,8 @@ hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, bool p
                                   int64_t n_rows, int b1, void* d_out,
                                   uint64_t cap1, unsigned long long* d_fill1, FreqRec* d_ovf, unsigned long long* d_ovf_n,
                                   uint64_t ovf_cap, unsigned int* d_flag, uint32_t* d_hll, unsigned long long* d_long_key,
-                                  unsigned long long* d_staged, hipStream_t stream);
+                                  unsigned long long* d_staged, hipStream_t stream,
+                                  void* d_rows = nullptr);
 hipError_t launch_freq_compact(const void* d_in, bool packed, const unsigned long long* d_fill, uint64_t cap,
                                uint64_t n_regions, const unsigned long long* d_prefix, FreqRec* d_out, hipStream_t stream);
 hipError_t launch_freq_agg_region(const FreqTable& T, const void* d_recs, bool packed, const unsigned long long* d_fill,

@@ -48,6 +48,9 @@ def lib():
         l.dqo_hll_registers.restype = None
         l.dqo_hll_registers.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p]
+        l.dqo_hll_registers_mt.restype = None
+        l.dqo_hll_registers_mt.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_int]
         l.dqo_xxh64.restype = ctypes.c_uint64
         l.dqo_xxh64.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64]
         _lib = l
@@ -101,4 +104,15 @@ def hll_registers(kind: str, values, validity=None, offsets=None):
     lib().dqo_hll_registers(code, len(values) if offsets is None else len(offsets) - 1,
                             values.ctypes.data, None if offsets is None else offsets.ctypes.data,
                             None if validity is None else validity.ctypes.data, regs.ctypes.data)
+    return regs
+
+
+def hll_registers_int64(values, validity, threads: int = 1):
+    """The 512 HLL registers (uint8) of an int64 column (Spark hashLong, seed 42), NULL rows
+    skipped (validity: LSB-first bitmap or None), on `threads` threads (register max merge)."""
+    v = np.ascontiguousarray(values, dtype=np.int64)
+    bm = None if validity is None else np.ascontiguousarray(validity, dtype=np.uint8)
+    regs = np.zeros(512, dtype=np.uint8)
+    lib().dqo_hll_registers_mt(5, len(v), v.ctypes.data, None if bm is None else bm.ctypes.data,
+                               regs.ctypes.data, int(threads))
     return regs
