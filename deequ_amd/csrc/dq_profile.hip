@@ -287,7 +287,7 @@ __device__ __forceinline__ void load24_fix(uint64_t (&w)[3], uint32_t s) {
 // DT = false: the HLL alone (an ApproxCountDistinct without a DataType on the column), through
 // the same batched word loads.
 template <bool DT>
-__global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* __restrict__ tasks,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void dq_string_pass_kernel(const StrTask* __restrict__ tasks,
                                                                 const DevColumn* __restrict__ cols,
                                                                 const DevMask* __restrict__ masks, int64_t n_rows,
                                                                 uint32_t* registers, unsigned long long* counts) {
@@ -315,6 +315,21 @@ __global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* _
   uint64_t packed = 0ull;
   uint32_t since_fold = 0u;
   constexpr int U = DQ_STR_U;
+  // the offset pairs of a step's U rows (rows past the block read row r0's); the next step's are
+  // loaded while this step's strings load and are hashed (round 5, as the cast kernel does), so
+  // the offsets -> string bytes round trip is paid once per step, not twice
+  int32_t ob[U], oe[U];
+  auto load_offs = [&](int64_t base) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = base + (int64_t)u * kBlock;
+      const int64_t rr = row < r1 ? row : r0;
+      const auto o = __builtin_amdgcn_raw_buffer_load_b64(ro, (int)(4u * (uint32_t)(rr - r0)), 0, 0);
+      ob[u] = (int32_t)o[0];
+      oe[u] = (int32_t)o[1];
+    }
+  };
+  if (r0 + (int64_t)threadIdx.x < r1) load_offs(r0 + threadIdx.x);
   for (int64_t base = r0 + threadIdx.x; base < r1; base += U * kBlock) {
     if constexpr (DT) {
       if (since_fold >= 4096u - U) {
@@ -325,7 +340,6 @@ __global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* _
       }
       since_fold += U;
     }
-    int32_t ob[U], oe[U];
     uint32_t sel[U], sh[U];
     uint64_t w[U][3];
 #pragma unroll
@@ -333,18 +347,21 @@ __global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* _
       const int64_t row = base + (int64_t)u * kBlock;
       const bool in = row < r1;
       const int64_t rr = in ? row : r0;
-      const auto o = __builtin_amdgcn_raw_buffer_load_b64(ro, (int)(4u * (uint32_t)(rr - r0)), 0, 0);
-      ob[u] = (int32_t)o[0];
-      oe[u] = (int32_t)o[1];
       sel[u] = (in && (col.validity == nullptr || bit_at(col.validity, rr)) && (wt == nullptr || bit_at(wt, rr))) ? 1u : 0u;
     }
+    int32_t cb[U], ce[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) sh[u] = load24(rs, vals, heap_end, (uint32_t)ob[u], (uint32_t)(oe[u] - ob[u]), w[u]);
+    for (int u = 0; u < U; ++u) {
+      cb[u] = ob[u];
+      ce[u] = oe[u];
+      sh[u] = load24(rs, vals, heap_end, (uint32_t)cb[u], (uint32_t)(ce[u] - cb[u]), w[u]);
+    }
+    if (base + U * kBlock < r1) load_offs(base + U * kBlock);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t row = base + (int64_t)u * kBlock;
       if (row >= r1) break;
-      const int32_t n = oe[u] - ob[u];
+      const int32_t n = ce[u] - cb[u];
       int k;
       W64 h;
       if (n <= 24) {
@@ -353,8 +370,8 @@ __global__ __launch_bounds__(kBlock) void dq_string_pass_kernel(const StrTask* _
         k = (DT && sel[u]) ? classify_shifted(s[0], s[1], s[2], n) : DT_NULL;
         h = xxh64_words_dev(s, (uint32_t)n);
       } else {
-        k = (DT && sel[u]) ? classify_utf8(PtrSrc{vals + ob[u]}, n) : DT_NULL;
-        h = xxh64_utf8_dev(vals + ob[u], (uint32_t)n);
+        k = (DT && sel[u]) ? classify_utf8(PtrSrc{vals + cb[u]}, n) : DT_NULL;
+        h = xxh64_utf8_dev(vals + cb[u], (uint32_t)n);
       }
       if constexpr (DT) packed += 1ull << (12u * (uint32_t)k);
       uint32_t idx, nlz, r;
