@@ -99,6 +99,44 @@ __global__ void probe_scatter8(uint64_t* __restrict__ out, uint64_t out_n, uint6
     out[mix(i) % out_n] = i;
 }
 
+// 11-14. the C2 value scan's exact access shape (dq_scan_fast.hip fast_load): each workgroup owns
+//    a contiguous chunk addressed through its own buffer descriptors; per iteration a lane loads
+//    4 x 16 B of values (2 rows each) and the validity BYTE of each pair (4 lanes share a byte, a
+//    wave reads 16 contiguous validity bytes per instruction); iteration it + 1 is loaded while it
+//    is consumed, so the last look-ahead falls past the chunk (range-checked to 0).  AUX is the
+//    cache-policy operand (2 = non-temporal, as the scan uses for large passes).
+typedef uint32_t pv4u __attribute__((ext_vector_type(4)));
+template <int AUX, bool VALUES, bool VALID>
+__global__ __launch_bounds__(256) void probe_scan_shape(const uint64_t* __restrict__ values, const uint8_t* __restrict__ valid,
+                                                        uint64_t n_rows, uint32_t* sink) {
+  const uint64_t per = n_rows / gridDim.x;  // host: n_rows % (gridDim.x * 2048) == 0
+  const uint64_t r_begin = (uint64_t)blockIdx.x * per;
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(values + r_begin), 0, (int)(per * 8), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(valid + r_begin / 8), 0, (int)(per / 8), 0x00020000);
+  const uint32_t iters = (uint32_t)(per / 2048);
+  uint32_t acc = 0;
+  pv4u v[4];
+  uint32_t b[4];
+  auto load = [&](uint32_t it) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t r0 = it * 2048u + ((uint32_t)u * 256u + threadIdx.x) * 2u;
+      if (VALUES) v[u] = __builtin_amdgcn_raw_buffer_load_b128(rv, (int)(r0 * 8u), 0, AUX);
+      if (VALID) b[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rb, (int)(r0 >> 3), 0, AUX);
+    }
+  };
+  load(0);
+  for (uint32_t it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (VALUES) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+      if (VALID) acc += b[u];
+    }
+    load(it + 1);
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
 int main() {
   const uint64_t GB = 1ull << 30;
   const uint64_t big = 2 * GB;
@@ -114,8 +152,9 @@ int main() {
   CHK(hipDeviceSynchronize());
   const dim3 grid(256 * 8), block(256);
   auto fence = [&]() { CHK(hipDeviceSynchronize()); };
-  auto line = [](const char* k, double rd, double wr, const char* shape) {
-    printf("{\"kernel\": \"%s\", \"read_bytes\": %.0f, \"write_bytes\": %.0f, \"shape\": \"%s\"}\n", k, rd, wr, shape);
+  auto line = [](const char* k, double rd, double wr, const char* shape, const char* kname = nullptr) {
+    printf("{\"kernel\": \"%s\", \"kname\": \"%s\", \"read_bytes\": %.0f, \"write_bytes\": %.0f, \"shape\": \"%s\"}\n", k,
+           kname ? kname : k, rd, wr, shape);
   };
   // reads (each from a fresh half so no probe reads what the previous one left in the caches)
   probe_read_wide16<<<grid, block>>>((const uint4*)a, GB / 16, sink); fence();
@@ -143,6 +182,22 @@ int main() {
   const uint64_t n_scatter = 1ull << 26;
   probe_scatter8<<<grid, block>>>((uint64_t*)(t), 4 * GB / 8, n_scatter); fence();
   line("probe_scatter8", 0, 8.0 * n_scatter, "random 8-B stores into a 4 GiB buffer");
+  // the scan's shape: 2^27 rows of 8-byte values (1 GiB) + their 16 MiB validity bitmap, 1024
+  // workgroups; values in a, validity in b (fresh: the write probes left t / b / a behind, and the
+  // values region alternates so no probe reads what the previous one touched)
+  const uint64_t rows = 1ull << 27;
+  const double vbytes = 8.0 * rows, bbytes = rows / 8.0;
+  const dim3 sgrid(1024);
+  probe_scan_shape<2, true, true><<<sgrid, block>>>((const uint64_t*)a, b, rows, sink); fence();
+  line("probe_scan_shape_nt", vbytes + bbytes, 0, "the C2 scan's loads: 16 B values + 1 validity byte per lane, chunk descriptors, aux=nt", "probe_scan_shape<2, true, true>");
+  probe_scan_shape<0, true, true><<<sgrid, block>>>((const uint64_t*)(a + GB), b + GB / 2, rows, sink); fence();
+  line("probe_scan_shape_default", vbytes + bbytes, 0, "the same loads, default cache policy", "probe_scan_shape<0, true, true>");
+  probe_scan_shape<2, true, false><<<sgrid, block>>>((const uint64_t*)t, nullptr, rows, sink); fence();
+  line("probe_scan_values_nt", vbytes, 0, "the scan's value loads only, aux=nt", "probe_scan_shape<2, true, false>");
+  probe_scan_shape<2, false, true><<<sgrid, block>>>(nullptr, t + 2 * GB, rows, sink); fence();
+  line("probe_scan_validity_nt", 0 + bbytes, 0, "the scan's validity-byte loads only (16 B per wave instruction), aux=nt", "probe_scan_shape<2, false, true>");
+  probe_scan_shape<0, false, true><<<sgrid, block>>>(nullptr, t + 3 * GB, rows, sink); fence();
+  line("probe_scan_validity_default", 0 + bbytes, 0, "the scan's validity-byte loads only, default policy", "probe_scan_shape<0, false, true>");
   CHK(hipFree(a));
   CHK(hipFree(b));
   CHK(hipFree(t));

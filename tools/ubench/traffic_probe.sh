@@ -17,19 +17,20 @@ want = {}
 for ln in open("gpurun_out/traffic_probe_bytes.jsonl"):
     if ln.startswith("{"):
         d = json.loads(ln)
-        want[d["kernel"]] = d
+        want[d.get("kname", d["kernel"])] = d
 got = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     for f in glob.glob("gpurun_out/tprobe_%s/**/*counter_collection.csv" % c, recursive=True):
         for row in csv.DictReader(open(f)):
             k = row["Kernel_Name"].split("(")[0]
+            k = k[5:] if k.startswith("void ") else k
             if row.get("Counter_Name") == c and k in want:
                 got.setdefault(k, {}).setdefault(c, 0.0)
                 got[k][c] += float(row["Counter_Value"])
 out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (KiB), one pass each, over tools/ubench/traffic_probe",
        "probes": {}}
-for k, d in want.items():
-    g = got.get(k, {})
+for kn, d in want.items():
+    g, k = got.get(kn, {}), d["kernel"]
     fr, wr = g.get("FETCH_SIZE", 0.0) * 1024, g.get("WRITE_SIZE", 0.0) * 1024
     out["probes"][k] = {"shape": d["shape"], "read_bytes": d["read_bytes"], "write_bytes": d["write_bytes"],
                         "fetch_size_bytes": fr, "write_size_bytes": wr,
