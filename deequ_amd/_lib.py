@@ -34,6 +34,7 @@ DQ_CMP_AS_INT64, DQ_CMP_AS_FLOAT64 = 0, 1
 
 DQ_HLL_NUM_WORDS = 52
 DQ_FREQ_NULL_AS_KEY = 0x1
+DQ_FREQ_FEW_ONLY = 0x2
 DQ_FLAT_DEVICE = 0x1
 
 TYPE_CODES = {
@@ -66,6 +67,14 @@ class DqState(Structure):
                 ("count", c_int64), ("sum", c_double), ("n", c_double), ("avg", c_double),
                 ("m2", c_double), ("value", c_double), ("words", c_int64 * DQ_HLL_NUM_WORDS),
                 ("y_avg", c_double), ("ck", c_double), ("x_mk", c_double), ("y_mk", c_double)]
+
+
+DQ_FEW_MAX_GROUPS = 1024
+
+
+class DqFewResult(Structure):
+    _fields_ = [("ok", c_int32), ("n_groups", c_int32), ("n_nulls", c_int64),
+                ("completeness", DqState), ("hll", DqState), ("dtype", DqState)]
 
 
 class DqFreqSummary(Structure):
@@ -164,6 +173,10 @@ SIGNATURES = {
     "dq_cast_utf8": (c_int, [c_void_p, POINTER(DqColumn), c_int64, c_int32, c_void_p, c_void_p, POINTER(c_int64)]),
     "dq_cast_utf8_batch": (c_int, [c_void_p, c_int32, POINTER(DqColumn), c_int64, POINTER(c_int32),
                                    POINTER(c_void_p), POINTER(c_void_p)]),
+    "dq_profile_few_strings": (c_int, [c_void_p, c_int32, POINTER(DqColumn), c_int64, POINTER(DqFewResult),
+                                       c_void_p, c_void_p, c_void_p]),
+    "dq_profile_string_groups": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int,
+                                         POINTER(DqState), POINTER(DqState)]),
     "dq_freq_partition": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_void_p, c_int64, POINTER(c_int64),
                                   POINTER(c_int64), POINTER(c_int64)]),
     "dq_freq_import_parts": (c_int, [c_void_p, c_int, c_void_p, POINTER(c_int64), POINTER(c_int64), c_void_p,

@@ -678,11 +678,17 @@ class Histogram(Analyzer):
             dtype = state.table.dtypes[0]
             n_rows = state.numRows
             counts, keys = state.table.top(self.maxDetailBins)
-            items = []
-            for k, c in zip(keys, counts.tolist()):
-                v = decode_key(k, [dtype], histogram=True)[0]
-                items.append((NULL_FIELD_REPLACEMENT if v is None else spark_cast_to_string(v, dtype), c))
-            items.sort(key=lambda kv: (-kv[1], kv[0].encode("utf-8")))
+            if dtype == "string":
+                # a string key's encoding is its UTF-8 bytes, and top() is already ordered by
+                # (count desc, encoded key asc) -- the order below: decode only what is kept
+                items = [(k.decode("utf-8"), c) for k, c in zip(keys[:self.maxDetailBins],
+                                                               counts[:self.maxDetailBins].tolist())]
+            else:
+                items = []
+                for k, c in zip(keys, counts.tolist()):
+                    v = decode_key(k, [dtype], histogram=True)[0]
+                    items.append((NULL_FIELD_REPLACEMENT if v is None else spark_cast_to_string(v, dtype), c))
+                items.sort(key=lambda kv: (-kv[1], kv[0].encode("utf-8")))
             values = {k: DistributionValue(c, c / n_rows) for k, c in items[:self.maxDetailBins]}
             return HistogramMetric(self.column, _S(Distribution(values, state.summary().num_groups)))
         except Exception as e:  # noqa: BLE001
@@ -711,14 +717,24 @@ class Histogram(Analyzer):
             literal = state.table.lookup(null_key) if dtype == "string" else 0
             null_bin = (n_rows - s.grouped_rows) + literal
             counts, keys = state.table.top(self.maxDetailBins)
-            items = []
-            for k, c in zip(keys, counts.tolist()):
-                if dtype == "string" and k == null_key:
-                    continue  # merged into the NULL bin
-                items.append((spark_cast_to_string(decode_key(k, [dtype])[0], dtype), c))
-            if null_bin:
-                items.append((NULL_FIELD_REPLACEMENT, null_bin))
-            items.sort(key=lambda kv: (-kv[1], kv[0].encode("utf-8")))
+            if dtype == "string":
+                # top() is ordered by (count desc, UTF-8 key asc), the order below: decode only the
+                # keys that can be kept (one more for the literal "NullValue" key, skipped here),
+                # and put the NULL bin in its place
+                m = self.maxDetailBins + 1
+                items = [(k.decode("utf-8"), c) for k, c in zip(keys[:m], counts[:m].tolist()) if k != null_key]
+                if null_bin:
+                    import bisect
+                    pos = bisect.bisect_left([(-c, k.encode("utf-8")) for k, c in items],
+                                             (-null_bin, null_key))
+                    items.insert(pos, (NULL_FIELD_REPLACEMENT, null_bin))
+            else:
+                items = []
+                for k, c in zip(keys, counts.tolist()):
+                    items.append((spark_cast_to_string(decode_key(k, [dtype])[0], dtype), c))
+                if null_bin:
+                    items.append((NULL_FIELD_REPLACEMENT, null_bin))
+                items.sort(key=lambda kv: (-kv[1], kv[0].encode("utf-8")))
             bins = s.num_groups + (1 if null_bin and not literal else 0)
             values = {k: DistributionValue(c, c / n_rows) for k, c in items[:self.maxDetailBins]}
             return HistogramMetric(self.column, _S(Distribution(values, bins)))

@@ -1983,6 +1983,186 @@ extern "C" dq_status dq_cast_utf8_batch(dq_ctx* ctx, int32_t n, const dq_column*
   return DQ_OK;
 }
 
+extern "C" dq_status dq_profile_string_groups(dq_ctx* ctx, const int64_t* counts, const int64_t* key_offsets,
+                                              const uint8_t* key_bytes, int64_t n_groups, int64_t n_nulls, int flags,
+                                              dq_state* hll_out, dq_state* dtype_out) {
+  if (!ctx || !hll_out || !dtype_out || n_groups < 0 || n_nulls < 0 || (n_groups > 0 && (!counts || !key_offsets)))
+    return fail(DQ_ERR_INVALID, "bad argument");
+  if (flags & ~DQ_FLAT_DEVICE) return fail(DQ_ERR_INVALID, "unknown flag");
+  const bool dev = (flags & DQ_FLAT_DEVICE) != 0;
+  DQ_HIP(hipSetDevice(ctx->device));
+  hipStream_t stream = nullptr;
+  DQ_HIP(StreamPool::get().acquire(ctx->device, &stream));
+  struct Release {
+    int d;
+    hipStream_t s;
+    ~Release() { StreamPool::get().release(d, s); }
+  } rel{ctx->device, stream};
+  int64_t n_bytes = 0;
+  if (n_groups > 0) {
+    if (dev)
+      DQ_HIP(hipMemcpyAsync(&n_bytes, key_offsets + n_groups, 8, hipMemcpyDeviceToHost, stream));
+    else
+      n_bytes = key_offsets[n_groups];
+    DQ_HIP(hipStreamSynchronize(stream));
+    if (n_bytes < 0 || (n_bytes > 0 && !key_bytes)) return fail(DQ_ERR_INVALID, "bad key bytes");
+  }
+  const size_t a = (size_t)n_groups * 8, b = ((size_t)n_groups + 1) * 8, c = (size_t)n_bytes;
+  const size_t scratch = kHllM * sizeof(uint32_t) + 8 * sizeof(unsigned long long);
+  DevBuf buf;
+  DQ_TRY(buf.ensure(scratch + (dev ? 0 : a + b + c + 16)));
+  uint8_t* base = static_cast<uint8_t*>(buf.ptr);
+  uint32_t* d_regs = reinterpret_cast<uint32_t*>(base);
+  unsigned long long* d_dtc = reinterpret_cast<unsigned long long*>(base + kHllM * sizeof(uint32_t));
+  DQ_HIP(hipMemsetAsync(base, 0, scratch, stream));
+  const int64_t* d_cnt = counts;
+  const int64_t* d_off = key_offsets;
+  const uint8_t* d_bytes = key_bytes;
+  if (!dev && n_groups > 0) {
+    uint8_t* in = base + scratch;
+    DQ_HIP(hipMemcpyAsync(in, counts, a, hipMemcpyHostToDevice, stream));
+    DQ_HIP(hipMemcpyAsync(in + a, key_offsets, b, hipMemcpyHostToDevice, stream));
+    if (c) DQ_HIP(hipMemcpyAsync(in + a + b, key_bytes, c, hipMemcpyHostToDevice, stream));
+    d_cnt = reinterpret_cast<const int64_t*>(in);
+    d_off = reinterpret_cast<const int64_t*>(in + a);
+    d_bytes = in + a + b;
+  }
+  DQ_HIP(launch_string_groups(d_cnt, d_off, d_bytes, n_groups, d_regs, d_dtc, stream));
+  std::vector<uint32_t> regs(kHllM);
+  unsigned long long dtc[5];
+  DQ_HIP(hipMemcpyAsync(regs.data(), d_regs, kHllM * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+  DQ_HIP(hipMemcpyAsync(dtc, d_dtc, sizeof(dtc), hipMemcpyDeviceToHost, stream));
+  DQ_HIP(hipStreamSynchronize(stream));
+  std::memset(hll_out, 0, sizeof(*hll_out));
+  hll_out->kind = DQ_OP_APPROX_COUNT_DISTINCT;
+  hll_out->has_value = 1;  // never NULL (StatefulHyperloglogPlus.nullable = false)
+  pack_hll(regs.data(), hll_out->words);
+  std::memset(dtype_out, 0, sizeof(*dtype_out));
+  dtype_out->kind = DQ_OP_DATATYPE;
+  dtype_out->has_value = 1;  // the StatefulDataType UDAF never returns NULL
+  for (int k = 0; k < 5; ++k) dtype_out->words[k] = (int64_t)dtc[k];
+  dtype_out->words[0] += n_nulls;  // (DtPos: NULL first, dq_profile.hip)
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_profile_few_strings(dq_ctx* ctx, int32_t n, const dq_column* cols, int64_t n_rows,
+                                            dq_few_result* results, int64_t* group_counts, uint8_t* group_keys,
+                                            int32_t* group_lens) {
+  static_assert(DQ_FEW_MAX_GROUPS == kFreqSmallSlots, "the few-groups kernel's LDS table size");
+  if (!ctx || n < 0 || (n > 0 && (!cols || !results || !group_counts || !group_keys || !group_lens)))
+    return fail(DQ_ERR_INVALID, "NULL argument");
+  if (n_rows < 0) return fail(DQ_ERR_INVALID, "bad n_rows");
+  for (int32_t i = 0; i < n; ++i) {
+    if (cols[i].type != DQ_T_UTF8) return fail(DQ_ERR_INVALID, "dq_profile_few_strings needs utf8 columns");
+    if (cols[i].length < n_rows) return fail(DQ_ERR_INVALID, "bad n_rows");
+  }
+  std::memset(results, 0, sizeof(dq_few_result) * (size_t)std::max(0, n));
+  if (n == 0 || n_rows == 0) return DQ_OK;  // (no rows: every column goes to the per-row pass)
+  DQ_HIP(hipSetDevice(ctx->device));
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(2 * (int64_t)cus, n_rows / 4096));
+  constexpr int kLanes = 4;
+  const int lanes = std::min<int>(kLanes, n);
+  // per lane: the workgroups' lists; per column: its compact list, count, flag, registers, counts
+  const size_t lists = (size_t)blocks * kFreqSmallSlots * (8 + 8 + 4) + (size_t)blocks * 4;
+  const size_t out_col = (size_t)kFreqSmallSlots * 24 + 8 + kHllM * sizeof(uint32_t) + 8 * sizeof(unsigned long long);
+  DevBuf scratch, outs, dcols;
+  DQ_TRY(scratch.ensure(lists * (size_t)lanes));
+  DQ_TRY(outs.ensure(out_col * (size_t)n));
+  DQ_TRY(dcols.ensure(sizeof(DevColumn) * (size_t)n));
+  Stager st[kLanes];
+  dq_status s = DQ_OK;
+  hipError_t e = hipSuccess;
+  int acquired = 0;
+  for (; acquired < lanes; ++acquired) {
+    e = StreamPool::get().acquire(ctx->device, &st[acquired].stream);
+    if (e != hipSuccess) break;
+    st[acquired].col_types.assign((size_t)n, DQ_T_UTF8);
+    st[acquired].resize_stage(n);
+  }
+  uint8_t* ob = static_cast<uint8_t*>(outs.ptr);
+  auto col_out = [&](int32_t i) { return ob + out_col * (size_t)i; };
+  if (e == hipSuccess) e = hipMemsetAsync(ob, 0, out_col * (size_t)n, st[0].stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(st[0].stream);  // (the other lanes use them)
+  std::vector<DevColumn> hc((size_t)n);
+  for (int32_t i = 0; i < n && e == hipSuccess && s == DQ_OK; ++i) {
+    s = prepare_column(&st[i % lanes], i, cols[i], n_rows, &hc[(size_t)i]);
+  }
+  if (s == DQ_OK && e == hipSuccess)
+    e = hipMemcpy(dcols.ptr, hc.data(), sizeof(DevColumn) * (size_t)n, hipMemcpyHostToDevice);
+  FreqKeySpec ks{};
+  ks.key_cols[0] = 0;
+  ks.n_keys = 1;
+  ks.null_as_key = 0;
+  for (int32_t i = 0; i < n && e == hipSuccess && s == DQ_OK; ++i) {
+    Stager& L = st[i % lanes];
+    uint8_t* lb = static_cast<uint8_t*>(scratch.ptr) + lists * (size_t)(i % lanes);
+    const size_t per = (size_t)blocks * kFreqSmallSlots;
+    unsigned long long* k0 = reinterpret_cast<unsigned long long*>(lb);
+    unsigned long long* k1 = k0 + per;
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(k1 + per);
+    uint32_t* nused = cnt + per;
+    uint8_t* o = col_out(i);
+    unsigned long long* ok0 = reinterpret_cast<unsigned long long*>(o);
+    unsigned long long* ok1 = ok0 + kFreqSmallSlots;
+    unsigned long long* oc = ok1 + kFreqSmallSlots;
+    uint32_t* on = reinterpret_cast<uint32_t*>(oc + kFreqSmallSlots);
+    unsigned int* bad = on + 1;
+    uint32_t* regs = on + 2;
+    unsigned long long* dtc = reinterpret_cast<unsigned long long*>(regs + kHllM);
+    e = launch_freq_small_flat(true, ks, static_cast<const DevColumn*>(dcols.ptr) + i, n_rows, blocks, k0, k1, cnt, nused,
+                               bad, ok0, ok1, oc, on, L.stream);
+    if (e == hipSuccess) e = launch_string_groups_words(ok0, ok1, oc, on, kFreqSmallSlots, regs, dtc, L.stream);
+  }
+  for (int k = 0; k < acquired; ++k) {
+    const hipError_t w = hipStreamSynchronize(st[k].stream);
+    if (e == hipSuccess) e = w;
+    StreamPool::get().release(ctx->device, st[k].stream);
+    st[k].stream = nullptr;
+  }
+  if (s != DQ_OK) return s;
+  if (e != hipSuccess) return fail(DQ_ERR_DEVICE, std::string("dq_profile_few_strings: ") + hipGetErrorString(e));
+  std::vector<uint8_t> host(out_col * (size_t)n);
+  DQ_HIP(hipMemcpy(host.data(), ob, host.size(), hipMemcpyDeviceToHost));
+  for (int32_t i = 0; i < n; ++i) {
+    const uint8_t* o = host.data() + out_col * (size_t)i;
+    const unsigned long long* hk0 = reinterpret_cast<const unsigned long long*>(o);
+    const unsigned long long* hk1 = hk0 + kFreqSmallSlots;
+    const unsigned long long* hc2 = hk1 + kFreqSmallSlots;
+    const uint32_t ng = *reinterpret_cast<const uint32_t*>(hc2 + kFreqSmallSlots);
+    const unsigned int bad = *(reinterpret_cast<const uint32_t*>(hc2 + kFreqSmallSlots) + 1);
+    const uint32_t* regs = reinterpret_cast<const uint32_t*>(hc2 + kFreqSmallSlots) + 2;
+    const unsigned long long* dtc = reinterpret_cast<const unsigned long long*>(regs + kHllM);
+    dq_few_result& r = results[i];
+    if (bad) continue;  // (more groups, a longer key, or a heap under 16 bytes: the per-row pass)
+    uint64_t grouped = 0;
+    for (uint32_t g = 0; g < ng; ++g) {
+      const size_t at = (size_t)i * kFreqSmallSlots + g;
+      group_counts[at] = (int64_t)hc2[g];
+      group_lens[at] = (int32_t)(hk1[g] >> 56);
+      for (int b = 0; b < 8; ++b) group_keys[at * 16 + b] = (uint8_t)(hk0[g] >> (8 * b));
+      for (int b = 0; b < 8; ++b) group_keys[at * 16 + 8 + b] = b < 7 ? (uint8_t)(hk1[g] >> (8 * b)) : 0;
+      grouped += hc2[g];
+    }
+    r.ok = 1;
+    r.n_groups = (int32_t)ng;
+    r.n_nulls = n_rows - (int64_t)grouped;
+    r.completeness.kind = DQ_OP_COMPLETENESS;
+    r.completeness.has_value = 1;  // (n_rows > 0)
+    r.completeness.num_matches = (int64_t)grouped;
+    r.completeness.count = n_rows;
+    r.hll.kind = DQ_OP_APPROX_COUNT_DISTINCT;
+    r.hll.has_value = 1;
+    pack_hll(regs, r.hll.words);
+    r.dtype.kind = DQ_OP_DATATYPE;
+    r.dtype.has_value = 1;
+    for (int k = 0; k < 5; ++k) r.dtype.words[k] = (int64_t)dtc[k];
+    r.dtype.words[0] += r.n_nulls;  // (DtPos: NULL first, dq_profile.hip)
+  }
+  return DQ_OK;
+}
+
 // The frequency group-by shares the staging helpers above.
 #include "dq_freq_api.inc"
 

@@ -2681,6 +2681,32 @@ hipError_t launch_freq_pack_probe(const FreqKeySpec& ks, const DevColumn* d_cols
   return hipGetLastError();
 }
 
+// The rollback image of a region staging, taken on the device before the batch's kernels: the
+// level-1 fills, the sizing sketch and the overflow count, and the batch's longest-key counter
+// cleared -- one launch instead of three copies and a memset per batch.
+__global__ __launch_bounds__(kBlock) void dq_freq_stage_save_kernel(const unsigned long long* __restrict__ fill,
+                                                                    unsigned long long* __restrict__ fill_save, uint32_t n_fill,
+                                                                    const uint32_t* __restrict__ sketch,
+                                                                    uint32_t* __restrict__ sketch_save,
+                                                                    const unsigned long long* __restrict__ ovf_n,
+                                                                    unsigned long long* __restrict__ ovf_save,
+                                                                    unsigned long long* __restrict__ long_key) {
+  for (uint32_t i = threadIdx.x; i < n_fill; i += kBlock) fill_save[i] = fill[i];
+  for (uint32_t i = threadIdx.x; i < (uint32_t)kHllM; i += kBlock) sketch_save[i] = sketch[i];
+  if (threadIdx.x == 0) {
+    *ovf_save = *ovf_n;
+    *long_key = 0ull;
+  }
+}
+
+hipError_t launch_freq_stage_save(const unsigned long long* d_fill, unsigned long long* d_fill_save, uint32_t n_fill,
+                                  const uint32_t* d_sketch, uint32_t* d_sketch_save, const unsigned long long* d_ovf_n,
+                                  unsigned long long* d_ovf_save, unsigned long long* d_long_key, hipStream_t stream) {
+  hipLaunchKernelGGL(dq_freq_stage_save_kernel, dim3(1), dim3(kBlock), 0, stream, d_fill, d_fill_save, n_fill, d_sketch,
+                     d_sketch_save, d_ovf_n, d_ovf_save, d_long_key);
+  return hipGetLastError();
+}
+
 hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, bool packed, const DevColumn* d_cols,
                                   int64_t n_rows, int b1, void* d_out,
                                   uint64_t cap1, unsigned long long* d_fill1, FreqRec* d_ovf, unsigned long long* d_ovf_n,
@@ -3862,27 +3888,21 @@ __global__ __launch_bounds__(kSmallThreads) void dq_freq_small_kernel(FreqKeySpe
   if (t == 0) out_n[blockIdx.x] = L.n_used;
 }
 
-// Sums the workgroups' staging lists (one workgroup, an LDS table) and inserts each group into the
-// table once (global_insert: the table may already hold groups).
-__global__ __launch_bounds__(kSmallThreads) void dq_freq_small_merge_kernel(const unsigned long long* __restrict__ in_k0,
-                                                                            const unsigned long long* __restrict__ in_k1,
-                                                                            const uint32_t* __restrict__ in_c,
-                                                                            const uint32_t* __restrict__ in_n, int n_blocks,
-                                                                            FreqTable T, unsigned int* bad) {
-  __shared__ unsigned long long K0[kSmallSlots], K1[kSmallSlots];
-  __shared__ unsigned long long C[kSmallSlots];
+// Sums the workgroups' staging lists into one LDS table (K0 / K1 / C, kSmallSlots keys; one
+// workgroup): thread t merges the lists of blocks t, t + kSmallThreads, ..., 8 entries at a time
+// with their loads issued together (one list per thread: the lists' loads all in flight at once).
+// Returns (to every thread) whether more keys than the table holds arrived.
+__device__ bool small_merge_lists(unsigned long long* K0, unsigned long long* K1, unsigned long long* C,
+                                  const unsigned long long* __restrict__ in_k0, const unsigned long long* __restrict__ in_k1,
+                                  const uint32_t* __restrict__ in_c, const uint32_t* __restrict__ in_n, int n_blocks,
+                                  unsigned int* any_fail) {
   const uint32_t t = threadIdx.x;
-  if (*bad) return;  // (the counting kernel failed: the host takes the general path)
   for (uint32_t i = t; i < (uint32_t)kSmallSlots; i += kSmallThreads) {
     K1[i] = kLdsEmpty;
     C[i] = 0ull;
   }
+  if (t == 0) *any_fail = 0u;
   __syncthreads();
-  __shared__ unsigned int any_fail;
-  if (t == 0) any_fail = 0u;
-  __syncthreads();
-  // thread t merges the lists of blocks t, t + kSmallThreads, ..., 8 entries at a time with
-  // their loads issued together (one list per thread: the lists' loads all in flight at once)
   bool fail = false;
   constexpr int U = 8;
   for (int b = (int)t; b < n_blocks; b += kSmallThreads) {
@@ -3932,9 +3952,25 @@ __global__ __launch_bounds__(kSmallThreads) void dq_freq_small_merge_kernel(cons
       }
     }
   }
-  if (fail) any_fail = 1u;
+  if (fail) *any_fail = 1u;
   __syncthreads();
-  if (any_fail) {  // more keys than the image holds: nothing is inserted, the host regroups
+  return *any_fail != 0u;
+}
+
+// Sums the workgroups' staging lists and inserts each group into the table once (global_insert:
+// the table may already hold groups).
+__global__ __launch_bounds__(kSmallThreads) void dq_freq_small_merge_kernel(const unsigned long long* __restrict__ in_k0,
+                                                                            const unsigned long long* __restrict__ in_k1,
+                                                                            const uint32_t* __restrict__ in_c,
+                                                                            const uint32_t* __restrict__ in_n, int n_blocks,
+                                                                            FreqTable T, unsigned int* bad) {
+  __shared__ unsigned long long K0[kSmallSlots], K1[kSmallSlots];
+  __shared__ unsigned long long C[kSmallSlots];
+  __shared__ unsigned int any_fail;
+  const uint32_t t = threadIdx.x;
+  if (*bad) return;  // (the counting kernel failed: the host takes the general path)
+  if (small_merge_lists(K0, K1, C, in_k0, in_k1, in_c, in_n, n_blocks, &any_fail)) {
+    // more keys than the image holds: nothing is inserted, the host regroups
     if (t == 0) atomicOr(bad, 1u);
     return;
   }
@@ -3948,6 +3984,68 @@ __global__ __launch_bounds__(kSmallThreads) void dq_freq_small_merge_kernel(cons
     k.hash = hash_inline(k.k0, k.k1, k.len);
     global_insert(T, k, C[i]);
   }
+}
+
+// The same sum written as ONE compact list (out_k0 / out_k1 / out_c [0, *out_n); K1 = key bytes
+// 8..14 | length << 56) instead of into a table: the profiler's few-valued string columns
+// (dq_profile_few_strings).  *out_n stays 0 and *bad is raised when the column did not fit.
+__global__ __launch_bounds__(kSmallThreads) void dq_freq_small_merge_flat_kernel(
+    const unsigned long long* __restrict__ in_k0, const unsigned long long* __restrict__ in_k1,
+    const uint32_t* __restrict__ in_c, const uint32_t* __restrict__ in_n, int n_blocks, unsigned long long* out_k0,
+    unsigned long long* out_k1, unsigned long long* out_c, uint32_t* out_n, unsigned int* bad) {
+  __shared__ unsigned long long K0[kSmallSlots], K1[kSmallSlots];
+  __shared__ unsigned long long C[kSmallSlots];
+  __shared__ unsigned int any_fail;
+  __shared__ uint32_t n_used;
+  const uint32_t t = threadIdx.x;
+  if (t == 0) n_used = 0u;
+  if (*bad) {
+    if (t == 0) *out_n = 0u;
+    return;
+  }
+  if (small_merge_lists(K0, K1, C, in_k0, in_k1, in_c, in_n, n_blocks, &any_fail)) {
+    if (t == 0) {
+      atomicOr(bad, 1u);
+      *out_n = 0u;
+    }
+    return;
+  }
+  for (uint32_t i = t; i < (uint32_t)kSmallSlots; i += kSmallThreads) {
+    const bool used = C[i] != 0ull;
+    const uint64_t m = __ballot(used);
+    uint32_t at = 0;
+    if (m) {
+      const uint32_t lane = t & 63u;
+      uint32_t base_w = 0;
+      if (lane == (uint32_t)__builtin_ctzll(m)) base_w = atomicAdd(&n_used, (uint32_t)__popcll(m));
+      base_w = __shfl(base_w, __builtin_ctzll(m), 64);
+      at = base_w + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    }
+    if (used) {
+      out_k0[at] = K0[i];
+      out_k1[at] = K1[i];
+      out_c[at] = C[i];
+    }
+  }
+  __syncthreads();
+  if (t == 0) *out_n = n_used;
+}
+
+hipError_t launch_freq_small_flat(bool string_key, const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
+                                  int blocks, unsigned long long* d_k0, unsigned long long* d_k1, uint32_t* d_c,
+                                  uint32_t* d_n, unsigned int* d_bad, unsigned long long* d_out_k0,
+                                  unsigned long long* d_out_k1, unsigned long long* d_out_c, uint32_t* d_out_n,
+                                  hipStream_t stream) {
+  if (n_rows <= 0) return hipErrorInvalidValue;
+  if (string_key)
+    hipLaunchKernelGGL(dq_freq_small_kernel<true>, dim3((unsigned)blocks), dim3(kSmallThreads), 0, stream, ks, d_cols, n_rows,
+                       d_k0, d_k1, d_c, d_n, d_bad);
+  else
+    hipLaunchKernelGGL(dq_freq_small_kernel<false>, dim3((unsigned)blocks), dim3(kSmallThreads), 0, stream, ks, d_cols,
+                       n_rows, d_k0, d_k1, d_c, d_n, d_bad);
+  hipLaunchKernelGGL(dq_freq_small_merge_flat_kernel, dim3(1), dim3(kSmallThreads), 0, stream, d_k0, d_k1, d_c, d_n, blocks,
+                     d_out_k0, d_out_k1, d_out_c, d_out_n, d_bad);
+  return hipGetLastError();
 }
 
 hipError_t launch_freq_small(const FreqKeySpec& ks, bool string_key, const DevColumn* d_cols, int64_t n_rows, int blocks,

@@ -335,6 +335,23 @@ hipError_t launch_freq_part(const void* d_in, uint64_t in_n, const unsigned long
 // one_string): digit keys staged as packed words, other keys onto the overflow list.
 hipError_t launch_freq_pack_probe(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, unsigned long long* d_out,
                                   hipStream_t stream);
+// dq_profile.hip: ApproxCountDistinct registers (ranks, 512) and the five DataType counts of a
+// utf8 column from its flat groups (dq_profile_string_groups); both zeroed by the caller.
+hipError_t launch_string_groups(const int64_t* d_counts, const int64_t* d_offs, const uint8_t* d_bytes, int64_t n,
+                                uint32_t* d_regs, unsigned long long* d_dtc, hipStream_t stream);
+hipError_t launch_string_groups_words(const unsigned long long* d_k0, const unsigned long long* d_k1,
+                                      const unsigned long long* d_counts, const uint32_t* d_n, uint32_t max_n,
+                                      uint32_t* d_regs, unsigned long long* d_dtc, hipStream_t stream);
+// dq_freq.hip: the few-groups kernel of one column + its lists summed into one compact list
+// (out_*[0, *out_n), at most kFreqSmallSlots groups; *bad raised when the column did not fit).
+hipError_t launch_freq_small_flat(bool string_key, const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
+                                  int blocks, unsigned long long* d_k0, unsigned long long* d_k1, uint32_t* d_c,
+                                  uint32_t* d_n, unsigned int* d_bad, unsigned long long* d_out_k0,
+                                  unsigned long long* d_out_k1, unsigned long long* d_out_c, uint32_t* d_out_n,
+                                  hipStream_t stream);
+hipError_t launch_freq_stage_save(const unsigned long long* d_fill, unsigned long long* d_fill_save, uint32_t n_fill,
+                                  const uint32_t* d_sketch, uint32_t* d_sketch_save, const unsigned long long* d_ovf_n,
+                                  unsigned long long* d_ovf_save, unsigned long long* d_long_key, hipStream_t stream);
 hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, bool packed, const DevColumn* d_cols,
                                   int64_t n_rows, int b1, void* d_out,
                                   uint64_t cap1, unsigned long long* d_fill1, FreqRec* d_ovf, unsigned long long* d_ovf_n,

@@ -560,6 +560,67 @@ hipError_t launch_string_pass(const StrTask* d_tasks, int n_tasks, const DevColu
   return hipGetLastError();
 }
 
+// ApproxCountDistinct + DataType of a utf8 column from its distinct strings (dq_profile_string_groups):
+// one thread per group hashes and classifies the key once; the DataType count is weighted by the
+// group's count, the register update is the same maximum the per-row pass takes.
+__global__ __launch_bounds__(kBlock) void dq_string_groups_kernel(const int64_t* __restrict__ counts,
+                                                                  const int64_t* __restrict__ offs,
+                                                                  const uint8_t* __restrict__ bytes, int64_t n,
+                                                                  uint32_t* __restrict__ regs,
+                                                                  unsigned long long* __restrict__ dtc) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* p = bytes + offs[i];
+  const int64_t len = offs[i + 1] - offs[i];
+  const int cls = classify_utf8(p, (int32_t)len);
+  atomicAdd(&dtc[cls], (unsigned long long)counts[i]);
+  uint32_t idx, pw;
+  hll_idx_rank(xxh64_bytes(p, len, 42), &idx, &pw);
+  atomicMax(&regs[idx], pw);
+}
+
+hipError_t launch_string_groups(const int64_t* d_counts, const int64_t* d_offs, const uint8_t* d_bytes, int64_t n,
+                                uint32_t* d_regs, unsigned long long* d_dtc, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(dq_string_groups_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
+                     d_counts, d_offs, d_bytes, n, d_regs, d_dtc);
+  return hipGetLastError();
+}
+
+// The same from the few-groups kernel's compact list (dq_freq_small_merge_flat_kernel: key bytes
+// 0..7 in k0, 8..14 and the length << 56 in k1, *n groups).
+__global__ __launch_bounds__(kBlock) void dq_string_groups_words_kernel(const unsigned long long* __restrict__ k0,
+                                                                        const unsigned long long* __restrict__ k1,
+                                                                        const unsigned long long* __restrict__ counts,
+                                                                        const uint32_t* __restrict__ n,
+                                                                        uint32_t* __restrict__ regs,
+                                                                        unsigned long long* __restrict__ dtc) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= *n) return;
+  const uint64_t w0 = k0[i], w1 = k1[i];
+  const uint32_t len = (uint32_t)(w1 >> 56);
+  uint8_t b[16];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    b[j] = (uint8_t)(w0 >> (8 * j));
+    b[8 + j] = j < 7 ? (uint8_t)(w1 >> (8 * j)) : 0u;
+  }
+  const uint8_t* p = b;
+  const int cls = classify_utf8(p, (int32_t)len);
+  atomicAdd(&dtc[cls], counts[i]);
+  uint32_t idx, pw;
+  hll_idx_rank(xxh64_bytes(p, (int64_t)len, 42), &idx, &pw);
+  atomicMax(&regs[idx], pw);
+}
+
+hipError_t launch_string_groups_words(const unsigned long long* d_k0, const unsigned long long* d_k1,
+                                      const unsigned long long* d_counts, const uint32_t* d_n, uint32_t max_n,
+                                      uint32_t* d_regs, unsigned long long* d_dtc, hipStream_t stream) {
+  hipLaunchKernelGGL(dq_string_groups_words_kernel, dim3((max_n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, d_k0,
+                     d_k1, d_counts, d_n, d_regs, d_dtc);
+  return hipGetLastError();
+}
+
 hipError_t launch_datatype(const HllTask* d_tasks, int n_tasks, const DevColumn* d_cols, const DevMask* d_masks,
                            int64_t n_rows, int blocks_per_task, unsigned long long* d_counts, hipStream_t stream) {
   if (n_tasks <= 0 || n_rows <= 0) return hipSuccess;

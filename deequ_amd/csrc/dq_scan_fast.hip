@@ -225,6 +225,13 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 #ifndef DQ_FAST_WAVES
 #define DQ_FAST_WAVES 1  // amdgpu_waves_per_eu minimum (register budget: 8 -> 64 VGPRs, 6 -> 80)
 #endif
+// The validity bytes keep the default policy: a 128-B bitmap line serves 1024 rows, i.e. eight
+// wave-instructions of one workgroup, and read non-temporally it is fetched about twice (the
+// known-bytes probes, tools/ubench/traffic_probe.hip: 0.508 vs 0.501 of the bytes; C2's PMC
+// reads 33.3 -> 32.5 GB per launch, exactly the algorithmic bytes).
+#ifndef DQ_VALID_AUX
+#define DQ_VALID_AUX 0
+#endif
 constexpr int kFastUnroll = DQ_FAST_UNROLL;  // 16-byte loads (2 rows) per lane per iteration
 
 // Streaming loads of a large pass go non-temporal (aux = 2: the bytes are read once and are far
@@ -251,7 +258,7 @@ __device__ inline void fast_load(FastLoad& L, __amdgpu_buffer_rsrc_t rv, __amdgp
     const uint32_t r0 = it * ROWS_PER_ITER + ((uint32_t)u * kBlock + tid) * 2u;
     if (nt) {  // (wave-uniform)
       L.vec[u] = __builtin_amdgcn_raw_buffer_load_b128(rv, (int)(r0 * 8u), 0, 2);
-      L.vb[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rvalid, (int)(r0 >> 3), 0, 2);
+      L.vb[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rvalid, (int)(r0 >> 3), 0, DQ_VALID_AUX);
     } else {
       L.vec[u] = __builtin_amdgcn_raw_buffer_load_b128(rv, (int)(r0 * 8u), 0, 0);
       L.vb[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rvalid, (int)(r0 >> 3), 0, 0);

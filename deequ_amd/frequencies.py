@@ -81,10 +81,12 @@ class FrequencyTable:
     """A dq_freq handle: device-resident (group key -> count) table plus numRows.
 
     `schema` is the batch schema handed to `consume` (defaults to the key columns alone);
-    `histogram=True` is Histogram's NULL-as-"NullValue" grouping (DQ_FREQ_NULL_AS_KEY)."""
+    `histogram=True` is Histogram's NULL-as-"NullValue" grouping (DQ_FREQ_NULL_AS_KEY);
+    `few_only=True` groups with the few-groups kernel alone (DQ_FREQ_FEW_ONLY): a batch with more
+    distinct keys than it holds raises DeequAmdError with status DQ_ERR_SPACE."""
 
     def __init__(self, key_columns: Sequence[str], schema: Dict[str, str], histogram: bool = False,
-                 device: Optional[int] = None):
+                 device: Optional[int] = None, few_only: bool = False):
         from .engine import current_device
         self.key_columns = list(key_columns)
         self.schema = dict(schema)
@@ -96,8 +98,9 @@ class FrequencyTable:
         idx = (ctypes.c_int32 * len(self.key_columns))(*[self.names.index(c) for c in self.key_columns])
         types = (ctypes.c_int32 * len(self.names))(*[L.TYPE_CODES[self.schema[n]] for n in self.names])
         h = ctypes.c_void_p()
-        L.check(L.lib().dq_freq_create(ctx.handle, idx, len(self.key_columns), types, len(self.names),
-                                       L.DQ_FREQ_NULL_AS_KEY if histogram else 0, ctypes.byref(h)))
+        flags = (L.DQ_FREQ_NULL_AS_KEY if histogram else 0) | (L.DQ_FREQ_FEW_ONLY if few_only else 0)
+        L.check(L.lib().dq_freq_create(ctx.handle, idx, len(self.key_columns), types, len(self.names), flags,
+                                       ctypes.byref(h)))
         self.handle = h
 
     @classmethod

@@ -167,14 +167,49 @@ class ColumnProfiler:
             return [Minimum(c), Maximum(c), Mean(c), StandardDeviation(c), Sum(c)]
 
         early = [c for c in relevant if _fixed_numeric(c)]
-        first = []
-        for c in relevant:
-            first += [Completeness(c), ApproxCountDistinct(c)]
-            if schema[c] == "string" and c not in predefined:
-                first.append(DataType(c))
-        for c in early:
-            first += _stats(c)
-        ctx1 = AnalysisRunner.onData(data).addAnalyzers(first).addAnalyzer(Size()).run()
+        strings = [c for c in relevant if schema[c] == "string" and c not in predefined]
+
+        def _first(cols):
+            out = []
+            for c in cols:
+                out += [Completeness(c), ApproxCountDistinct(c)]
+                if c in strings:
+                    out.append(DataType(c))
+            return out + [a for c in early if c in cols for a in _stats(c)]
+
+        from concurrent.futures import ThreadPoolExecutor
+        from .distributed import is_sharded
+        from .runner import AnalyzerContext
+        overlap = os.environ.get("DEEQU_AMD_PROFILE_SERIAL", "0") != "1"  # (A/B and debugging knob)
+        sharded = is_sharded(data)
+        casted, few = None, {}
+        if sharded or not overlap or not strings:
+            # one fused pass over every column (over a ShardedTable every pass is collective)
+            ctx1 = AnalysisRunner.onData(data).addAnalyzers(_first(relevant)).addAnalyzer(Size()).run()
+        else:
+            # Pass 1 in three steps.  First every string column is tried as a few-valued column
+            # (_few_group_strings): one that fits gets Completeness, ApproxCountDistinct and
+            # DataType from its distinct values weighted by their counts -- the same states as
+            # the per-row pass -- and, should it become a histogram target, its groups are pass
+            # 3's histogram.  Then two plans run side by side: the columns that need no string
+            # pass (every non-string column, predefined string columns) on a thread of their own,
+            # the other string columns' per-row string pass here.  As soon as the string
+            # columns' types are known, pass 2's casts start: they need nothing else from pass 1.
+            # (The metrics are those of the one fused pass; only the failure scope of an error
+            # inside a plan is the plan's columns.)
+            others = [c for c in relevant if c not in strings]
+            few = _few_group_strings(data, strings)  # (first: its latency-bound kernels starve beside the scans)
+            rest = [c for c in strings if c not in few]
+            pool = ThreadPoolExecutor(max_workers=1)
+            fut = pool.submit(lambda: AnalysisRunner.onData(data).addAnalyzers(_first(others)).addAnalyzer(Size()).run())
+            try:
+                ctx_s = AnalysisRunner.onData(data).addAnalyzers(_first(rest)).run() if rest else AnalyzerContext()
+                ctx_s = ctx_s + _few_group_metrics(few)
+                casted = _cast_numeric_string_columns(relevant, data,
+                                                      _extract_generic_statistics(strings, schema, ctx_s, predefined))
+                ctx1 = fut.result() + ctx_s
+            finally:
+                pool.shutdown(wait=True)
         generic = _extract_generic_statistics(relevant, schema, ctx1, predefined)
 
         if printStatusUpdates:
@@ -184,16 +219,15 @@ class ColumnProfiler:
         # the library releases the GIL).  Over a ShardedTable both passes are collective, so
         # they stay in order there.  A pass-2 failure is raised as the sequential run would.
         targets = _find_target_columns_for_histograms(schema, generic, lowCardinalityHistogramThreshold)
-        from concurrent.futures import ThreadPoolExecutor
-        from .distributed import is_sharded
-        overlap = os.environ.get("DEEQU_AMD_PROFILE_SERIAL", "0") != "1"  # (A/B and debugging knob)
-        side = ThreadPoolExecutor(max_workers=1) if overlap and targets and not is_sharded(data) else None
+        side = ThreadPoolExecutor(max_workers=1) if overlap and targets and not sharded else None
         if side and printStatusUpdates:
             print("### PROFILING: Computing histograms of low-cardinality columns in pass (3/3), beside pass 2...")
-        pending = (side.submit(compute_histograms, data, targets, generic.approximateNumDistincts)
+        known = {c: few[c].histogram() for c in targets if c in few}
+        pending = (side.submit(compute_histograms, data, targets, generic.approximateNumDistincts, known)
                    if side else None)
         try:
-            casted = _cast_numeric_string_columns(relevant, data, generic)
+            if casted is None:
+                casted = _cast_numeric_string_columns(relevant, data, generic)
             second = []
             for c in relevant:
                 if c not in early and generic.typeOf(c) in numeric_types:
@@ -219,8 +253,95 @@ class ColumnProfiler:
             finally:
                 side.shutdown(wait=True)
         else:
-            histograms = compute_histograms(data, targets, generic.approximateNumDistincts)
+            histograms = compute_histograms(data, targets, generic.approximateNumDistincts, known)
         return _create_profiles(relevant, generic, numeric, histograms)
+
+
+class _FewGroups:
+    """A string column pass 1 found few-valued (dq_profile_few_strings): its distinct non-NULL
+    strings with their counts, its NULL count, and its pass-1 states (Completeness,
+    ApproxCountDistinct, DataType) computed from them."""
+
+    def __init__(self, groups: Dict[bytes, int], nulls: int, comp, hll, dtype):
+        self.groups, self.nulls = groups, int(nulls)
+        self.comp, self.hll, self.dtype = comp, hll, dtype
+
+    def merge(self, other: "_FewGroups") -> "_FewGroups":
+        """The union of two batches' results (State.sum of each state; group counts added)."""
+        for k, c in other.groups.items():
+            self.groups[k] = self.groups.get(k, 0) + c
+        self.nulls += other.nulls
+        for name in ("comp", "hll", "dtype"):
+            out = L.DqState()
+            L.check(L.lib().dq_state_merge(getattr(self, name), getattr(other, name), out))
+            setattr(self, name, out)
+        return self
+
+    def histogram(self) -> Distribution:
+        """computeHistograms' distribution (NULL -> "NullValue", merged with that literal)."""
+        keys, counts = list(self.groups.keys()), list(self.groups.values())
+        if self.nulls:
+            keys.append(NULL_FIELD_REPLACEMENT.encode("utf-8"))
+            counts.append(self.nulls)
+        return _histogram_distribution(counts, keys, "string")
+
+
+def _few_group_metrics(few: Dict[str, "_FewGroups"]):
+    """Pass 1's metrics of the few-valued string columns from their states."""
+    from .runner import AnalyzerContext
+    out = OrderedDict()
+    for c, g in few.items():
+        for a, st in ((Completeness(c), g.comp), (ApproxCountDistinct(c), g.hll), (DataType(c), g.dtype)):
+            try:
+                out[a] = a.metricFromAggregationResult(st, None, None)
+            except Exception as e:  # noqa: BLE001
+                out[a] = a.toFailureMetric(e)
+    return AnalyzerContext(out)
+
+
+def _few_group_strings(data, columns: Sequence[str]) -> Dict[str, _FewGroups]:
+    """Pass 1's string columns tried as few-valued columns, all in one library call per batch
+    (dq_profile_few_strings: the few-groups kernel and a merge per column, launches overlapped,
+    one wait); a column must fit in every batch.  Not over a ShardedTable (its passes are
+    collective) and off with DEEQU_AMD_PROFILE_FEW=0."""
+    from .distributed import is_sharded
+    if not columns or is_sharded(data) or os.environ.get("DEEQU_AMD_PROFILE_FEW", "1") == "0":
+        return {}
+    from .arrow import ArrowBatch
+    from .engine import current_device
+    from .table import Table
+    ctx = L.Context.get(current_device())
+    import numpy as np
+    out: Dict[str, _FewGroups] = {}
+    live = list(columns)
+    first = True
+    for batch in data.batches():
+        if not live:
+            break
+        if isinstance(batch, ArrowBatch):  # zero-copy host view of the record batch
+            batch = Table.from_arrow(batch.batch)
+        n, rows = len(live), batch.num_rows
+        res = (L.DqFewResult * n)()
+        counts = np.zeros(n * L.DQ_FEW_MAX_GROUPS, dtype=np.int64)
+        keys = np.zeros(n * L.DQ_FEW_MAX_GROUPS * 16, dtype=np.uint8)
+        lens = np.zeros(n * L.DQ_FEW_MAX_GROUPS, dtype=np.int32)
+        cols = (L.DqColumn * n)(*[batch.columns[c].to_dq() for c in live])
+        L.check(L.lib().dq_profile_few_strings(ctx.handle, n, cols, rows, res, counts.ctypes.data, keys.ctypes.data,
+                                               lens.ctypes.data))
+        kept = []
+        for i, c in enumerate(live):
+            r = res[i]
+            if not r.ok or (not first and c not in out):
+                out.pop(c, None)
+                continue
+            base = i * L.DQ_FEW_MAX_GROUPS
+            raw = keys[base * 16:(base + r.n_groups) * 16].tobytes()
+            g = {raw[16 * j:16 * j + int(lens[base + j])]: int(counts[base + j]) for j in range(r.n_groups)}
+            got = _FewGroups(g, r.n_nulls, r.completeness, r.hll, r.dtype)
+            out[c] = out[c].merge(got) if c in out else got
+            kept.append(c)
+        live, first = kept, False
+    return out
 
 
 def _extract_generic_statistics(columns, schema, ctx, predefined) -> GenericColumnStatistics:
@@ -381,14 +502,18 @@ def _bool_histograms(data, columns: Sequence[str]) -> Dict[str, Distribution]:
 
 
 def compute_histograms(data, target_columns: Sequence[str],
-                       expected_groups: Optional[Dict[str, int]] = None) -> Dict[str, Distribution]:
+                       expected_groups: Optional[Dict[str, int]] = None,
+                       known: Optional[Dict[str, Distribution]] = None) -> Dict[str, Distribution]:
     """computeHistograms (:564-606): exact (column, value.toString) counts, NULL -> "NullValue",
-    one GPU group-by per target column; ratio = count / (sum of the column's counts)."""
+    one GPU group-by per target column; ratio = count / (sum of the column's counts).  `known`:
+    histograms already computed (pass 1's few-groups string columns)."""
     from .frequencies import FrequencyTable
     schema = data.schema
-    out = {}
+    out = dict(known or {})
+    target_columns = [c for c in target_columns if c not in out]
+    order = [c for c in out]
     bool_cols = [c for c in target_columns if schema[c] == "bool" and _IDENT.match(c)]
-    order = list(bool_cols)  # (the boolean columns' histograms first, as computed sequentially)
+    order += bool_cols  # (the boolean columns' histograms first, as computed sequentially)
     from .distributed import is_sharded
     from .engine import current_device
     rest = [c for c in target_columns if c not in bool_cols]

@@ -343,6 +343,40 @@ dq_status dq_cast_utf8(dq_ctx* ctx, const dq_column* src, int64_t n_rows, int32_
 dq_status dq_cast_utf8_batch(dq_ctx* ctx, int32_t n, const dq_column* srcs, int64_t n_rows,
                              const int32_t* to_types, void* const* d_values, uint8_t* const* d_validity);
 
+/* ApproxCountDistinct and DataType of a utf8 column from its groups instead of its rows: the
+ * column's distinct non-NULL strings (flat, as dq_freq_export_flat lists them: counts[i], key
+ * bytes [key_offsets[i], key_offsets[i + 1])) and its NULL count.  Every group is hashed and
+ * classified once and weighted by its count -- the same registers (a maximum does not see
+ * duplicates) and the same five DataType counts as the per-row pass (StatefulHyperloglogPlus
+ * .update, StatefulDataType.update over every row).  hll_out / dtype_out receive what
+ * dq_plan_finish gives ApproxCountDistinct and DataType on that column.  DQ_FLAT_DEVICE: the
+ * three buffers are device memory on the context's device. */
+dq_status dq_profile_string_groups(dq_ctx* ctx, const int64_t* counts, const int64_t* key_offsets,
+                                   const uint8_t* key_bytes, int64_t n_groups, int64_t n_nulls, int flags,
+                                   dq_state* hll_out, dq_state* dtype_out);
+
+/* ColumnProfiler pass 1 on n utf8 columns of one batch, each tried as a few-valued column: the
+ * few-groups kernel (per-workgroup LDS tables of DQ_FEW_MAX_GROUPS keys of at most 15 bytes) and
+ * one merge per column, all columns in one call (their launches overlap; one wait).  Column i
+ * fits when it has at most DQ_FEW_MAX_GROUPS distinct non-NULL strings, none longer than 15
+ * bytes (and a string heap of at least 16 bytes); then results[i].ok = 1 and:
+ *   - results[i].completeness / .hll / .dtype are what dq_plan_finish gives Completeness,
+ *     ApproxCountDistinct and DataType on the column (states from the groups weighted by their
+ *     counts: the same registers and counts as the per-row pass);
+ *   - its groups are group_counts / group_keys (16 bytes each, zero padded) / group_lens
+ *     [i * DQ_FEW_MAX_GROUPS, + results[i].n_groups), non-NULL strings only (NULLs are
+ *     results[i].n_nulls).
+ * A column that does not fit has ok = 0 and nothing else set. */
+#define DQ_FEW_MAX_GROUPS 1024
+typedef struct dq_few_result {
+  int32_t ok;
+  int32_t n_groups;
+  int64_t n_nulls;
+  dq_state completeness, hll, dtype;
+} dq_few_result;
+dq_status dq_profile_few_strings(dq_ctx* ctx, int32_t n, const dq_column* cols, int64_t n_rows, dq_few_result* results,
+                                 int64_t* group_counts, uint8_t* group_keys, int32_t* group_lens);
+
 /* ---------------------------------------------------------------- frequency group-by
  * Replaces FrequencyBasedAnalyzer.computeFrequencies (GroupingAnalyzers.scala:53-80) and the
  * group-by of Histogram (Histogram.scala:54-69).  A dq_freq is the device-resident state
@@ -358,6 +392,13 @@ dq_status dq_cast_utf8_batch(dq_ctx* ctx, int32_t n, const dq_column* srcs, int6
 typedef struct dq_freq dq_freq;
 
 #define DQ_FREQ_NULL_AS_KEY 0x1
+/* Few groups or nothing: one key column, grouped only by the few-groups kernel (per-workgroup
+ * LDS tables of 1024 keys of at most 15 bytes).  A batch it cannot hold -- more distinct keys, a
+ * longer key -- fails dq_freq_consume with DQ_ERR_SPACE, and every later consume fails alike: the
+ * caller drops the table.  ColumnProfiler uses it to try every string column as a
+ * low-cardinality histogram in pass 1 (no reference counterpart: a speculative schedule of the
+ * same aggregations). */
+#define DQ_FREQ_FEW_ONLY 0x2
 
 typedef struct dq_freq_summary {
   int64_t num_rows;      /* FrequenciesAndNumRows.numRows: every consumed row          */
