@@ -182,7 +182,7 @@ class ColumnProfiler:
         from .runner import AnalyzerContext
         overlap = os.environ.get("DEEQU_AMD_PROFILE_SERIAL", "0") != "1"  # (A/B and debugging knob)
         sharded = is_sharded(data)
-        casted, few = None, {}
+        casted, few, ctx2_s, bool_hist = None, {}, None, {}
         if sharded or not overlap or not strings:
             # one fused pass over every column (over a ShardedTable every pass is collective)
             ctx1 = AnalysisRunner.onData(data).addAnalyzers(_first(relevant)).addAnalyzer(Size()).run()
@@ -198,16 +198,28 @@ class ColumnProfiler:
             # (The metrics are those of the one fused pass; only the failure scope of an error
             # inside a plan is the plan's columns.)
             others = [c for c in relevant if c not in strings]
-            few = _few_group_strings(data, strings)  # (first: its latency-bound kernels starve beside the scans)
+            # (first and alone: the few-groups kernels are latency-bound, beside the VALU-bound
+            # scans they starve)
+            few = _few_group_strings(data, strings)
             rest = [c for c in strings if c not in few]
-            pool = ThreadPoolExecutor(max_workers=1)
+            pool = ThreadPoolExecutor(max_workers=2)
             fut = pool.submit(lambda: AnalysisRunner.onData(data).addAnalyzers(_first(others)).addAnalyzer(Size()).run())
+            # a boolean column has at most three values, so it is a histogram target unless the
+            # threshold is below that: its histogram scan runs now, beside pass 1, and is used if so
+            bools = [c for c in relevant if schema[c] == "bool" and _IDENT.match(c)]
+            fut_bool = pool.submit(_bool_histograms, data, bools) if bools else None
             try:
                 ctx_s = AnalysisRunner.onData(data).addAnalyzers(_first(rest)).run() if rest else AnalyzerContext()
                 ctx_s = ctx_s + _few_group_metrics(few)
-                casted = _cast_numeric_string_columns(relevant, data,
-                                                      _extract_generic_statistics(strings, schema, ctx_s, predefined))
+                gen_s = _extract_generic_statistics(strings, schema, ctx_s, predefined)
+                casted = _cast_numeric_string_columns(relevant, data, gen_s)
+                # pass 2's statistics of the string columns typed numeric: they need only the casts
+                early_s = [a for c in strings if gen_s.typeOf(c) in numeric_types for a in _stats(c)]
+                if early_s:
+                    ctx2_s = AnalysisRunner.onData(casted).addAnalyzers(early_s).run()
                 ctx1 = fut.result() + ctx_s
+                if fut_bool is not None:
+                    bool_hist = fut_bool.result()
             finally:
                 pool.shutdown(wait=True)
         generic = _extract_generic_statistics(relevant, schema, ctx1, predefined)
@@ -223,16 +235,21 @@ class ColumnProfiler:
         if side and printStatusUpdates:
             print("### PROFILING: Computing histograms of low-cardinality columns in pass (3/3), beside pass 2...")
         known = {c: few[c].histogram() for c in targets if c in few}
+        known.update({c: bool_hist[c] for c in targets if c in bool_hist})
         pending = (side.submit(compute_histograms, data, targets, generic.approximateNumDistincts, known)
                    if side else None)
         try:
             if casted is None:
                 casted = _cast_numeric_string_columns(relevant, data, generic)
             second = []
+            done = set(ctx2_s.metricMap) if ctx2_s is not None else set()
             for c in relevant:
                 if c not in early and generic.typeOf(c) in numeric_types:
-                    second += _stats(c)
+                    second += [a for a in _stats(c) if a not in done]
             numeric = _extract_numeric_statistics(ctx1)
+            if ctx2_s is not None:
+                for k, v in _extract_numeric_statistics(ctx2_s).items():
+                    numeric[k].update(v)
             if second:
                 ctx2 = AnalysisRunner.onData(casted).addAnalyzers(second).run()
                 for k, v in _extract_numeric_statistics(ctx2).items():

@@ -61,6 +61,8 @@ if os.environ.get("SPANS") == "1":  # wall-clock spans of the profiler's host st
     for mod, name in [(profiles, "_extract_generic_statistics"), (profiles, "_cast_numeric_string_columns"),
                       (profiles, "compute_histograms"), (profiles, "_create_profiles"),
                       (profiles, "_extract_numeric_statistics"), (profiles, "cast_string_column"),
+                      (profiles, "_few_group_strings"), (profiles, "_few_group_metrics"),
+                      (profiles, "cast_string_columns"),
                       (engine, "run_scan_raw"), (engine, "_scan_local"), (engine, "op_supported")]:
         wrap(mod, name)
     R = runner.AnalysisRunner
