@@ -2051,7 +2051,7 @@ extern "C" dq_status dq_profile_few_strings(dq_ctx* ctx, int32_t n, const dq_col
   static_assert(DQ_FEW_MAX_GROUPS == kFreqSmallSlots, "the few-groups kernel's LDS table size");
   if (!ctx || n < 0 || (n > 0 && (!cols || !results || !group_counts || !group_keys || !group_lens)))
     return fail(DQ_ERR_INVALID, "NULL argument");
-  if (n_rows < 0) return fail(DQ_ERR_INVALID, "bad n_rows");
+  if (n_rows < 0 || n > 65535) return fail(DQ_ERR_INVALID, "bad n_rows or column count");
   for (int32_t i = 0; i < n; ++i) {
     if (cols[i].type != DQ_T_UTF8) return fail(DQ_ERR_INVALID, "dq_profile_few_strings needs utf8 columns");
     if (cols[i].length < n_rows) return fail(DQ_ERR_INVALID, "bad n_rows");
@@ -2061,89 +2061,71 @@ extern "C" dq_status dq_profile_few_strings(dq_ctx* ctx, int32_t n, const dq_col
   DQ_HIP(hipSetDevice(ctx->device));
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
+  // every column in ONE launch of each kernel (blockIdx.y = column): the few-groups kernel (its
+  // workgroups' lists), the per-column merge into one compact list, the states from the groups
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(2 * (int64_t)cus, n_rows / 4096));
-  constexpr int kLanes = 4;
-  const int lanes = std::min<int>(kLanes, n);
-  // per lane: the workgroups' lists; per column: its compact list, count, flag, registers, counts
-  const size_t lists = (size_t)blocks * kFreqSmallSlots * (8 + 8 + 4) + (size_t)blocks * 4;
-  const size_t out_col = (size_t)kFreqSmallSlots * 24 + 8 + kHllM * sizeof(uint32_t) + 8 * sizeof(unsigned long long);
+  const size_t nc = (size_t)n, per = (size_t)blocks * kFreqSmallSlots, S = kFreqSmallSlots;
+  const size_t lists = nc * per * (8 + 8 + 4) + nc * (size_t)blocks * 4;
+  const size_t outs_bytes = nc * S * 24 + nc * 8 + nc * kHllM * sizeof(uint32_t) + nc * 8 * sizeof(unsigned long long);
   DevBuf scratch, outs, dcols;
-  DQ_TRY(scratch.ensure(lists * (size_t)lanes));
-  DQ_TRY(outs.ensure(out_col * (size_t)n));
-  DQ_TRY(dcols.ensure(sizeof(DevColumn) * (size_t)n));
-  Stager st[kLanes];
-  dq_status s = DQ_OK;
-  hipError_t e = hipSuccess;
-  int acquired = 0;
-  for (; acquired < lanes; ++acquired) {
-    e = StreamPool::get().acquire(ctx->device, &st[acquired].stream);
-    if (e != hipSuccess) break;
-    st[acquired].col_types.assign((size_t)n, DQ_T_UTF8);
-    st[acquired].resize_stage(n);
-  }
+  DQ_TRY(scratch.ensure(lists));
+  DQ_TRY(outs.ensure(outs_bytes));
+  DQ_TRY(dcols.ensure(sizeof(DevColumn) * nc));
+  Stager st;
+  DQ_HIP(StreamPool::get().acquire(ctx->device, &st.stream));
+  struct Release {
+    int d;
+    Stager* s;
+    ~Release() { StreamPool::get().release(d, s->stream); s->stream = nullptr; }
+  } rel{ctx->device, &st};
+  st.col_types.assign(nc, DQ_T_UTF8);
+  st.resize_stage(n);
+  std::vector<DevColumn> hc(nc);
+  for (int32_t i = 0; i < n; ++i) DQ_TRY(prepare_column(&st, i, cols[i], n_rows, &hc[(size_t)i]));
+  DQ_HIP(hipMemcpyAsync(dcols.ptr, hc.data(), sizeof(DevColumn) * nc, hipMemcpyHostToDevice, st.stream));
+  uint8_t* lb = static_cast<uint8_t*>(scratch.ptr);
+  unsigned long long* k0 = reinterpret_cast<unsigned long long*>(lb);
+  unsigned long long* k1 = k0 + nc * per;
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(k1 + nc * per);
+  uint32_t* nused = cnt + nc * per;
   uint8_t* ob = static_cast<uint8_t*>(outs.ptr);
-  auto col_out = [&](int32_t i) { return ob + out_col * (size_t)i; };
-  if (e == hipSuccess) e = hipMemsetAsync(ob, 0, out_col * (size_t)n, st[0].stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(st[0].stream);  // (the other lanes use them)
-  std::vector<DevColumn> hc((size_t)n);
-  for (int32_t i = 0; i < n && e == hipSuccess && s == DQ_OK; ++i) {
-    s = prepare_column(&st[i % lanes], i, cols[i], n_rows, &hc[(size_t)i]);
-  }
-  if (s == DQ_OK && e == hipSuccess)
-    e = hipMemcpy(dcols.ptr, hc.data(), sizeof(DevColumn) * (size_t)n, hipMemcpyHostToDevice);
+  unsigned long long* ok0 = reinterpret_cast<unsigned long long*>(ob);
+  unsigned long long* ok1 = ok0 + nc * S;
+  unsigned long long* oc = ok1 + nc * S;
+  uint32_t* on = reinterpret_cast<uint32_t*>(oc + nc * S);
+  unsigned int* bad = on + nc;
+  uint32_t* regs = bad + nc;
+  unsigned long long* dtc = reinterpret_cast<unsigned long long*>(regs + nc * kHllM);
+  DQ_HIP(hipMemsetAsync(on, 0, nc * 8 + nc * kHllM * sizeof(uint32_t) + nc * 8 * sizeof(unsigned long long), st.stream));
   FreqKeySpec ks{};
   ks.key_cols[0] = 0;
   ks.n_keys = 1;
   ks.null_as_key = 0;
-  for (int32_t i = 0; i < n && e == hipSuccess && s == DQ_OK; ++i) {
-    Stager& L = st[i % lanes];
-    uint8_t* lb = static_cast<uint8_t*>(scratch.ptr) + lists * (size_t)(i % lanes);
-    const size_t per = (size_t)blocks * kFreqSmallSlots;
-    unsigned long long* k0 = reinterpret_cast<unsigned long long*>(lb);
-    unsigned long long* k1 = k0 + per;
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(k1 + per);
-    uint32_t* nused = cnt + per;
-    uint8_t* o = col_out(i);
-    unsigned long long* ok0 = reinterpret_cast<unsigned long long*>(o);
-    unsigned long long* ok1 = ok0 + kFreqSmallSlots;
-    unsigned long long* oc = ok1 + kFreqSmallSlots;
-    uint32_t* on = reinterpret_cast<uint32_t*>(oc + kFreqSmallSlots);
-    unsigned int* bad = on + 1;
-    uint32_t* regs = on + 2;
-    unsigned long long* dtc = reinterpret_cast<unsigned long long*>(regs + kHllM);
-    e = launch_freq_small_flat(true, ks, static_cast<const DevColumn*>(dcols.ptr) + i, n_rows, blocks, k0, k1, cnt, nused,
-                               bad, ok0, ok1, oc, on, L.stream);
-    if (e == hipSuccess) e = launch_string_groups_words(ok0, ok1, oc, on, kFreqSmallSlots, regs, dtc, L.stream);
-  }
-  for (int k = 0; k < acquired; ++k) {
-    const hipError_t w = hipStreamSynchronize(st[k].stream);
-    if (e == hipSuccess) e = w;
-    StreamPool::get().release(ctx->device, st[k].stream);
-    st[k].stream = nullptr;
-  }
-  if (s != DQ_OK) return s;
-  if (e != hipSuccess) return fail(DQ_ERR_DEVICE, std::string("dq_profile_few_strings: ") + hipGetErrorString(e));
-  std::vector<uint8_t> host(out_col * (size_t)n);
-  DQ_HIP(hipMemcpy(host.data(), ob, host.size(), hipMemcpyDeviceToHost));
+  DQ_HIP(launch_freq_small_flat(true, ks, static_cast<const DevColumn*>(dcols.ptr), n, n_rows, blocks, k0, k1, cnt, nused,
+                                bad, ok0, ok1, oc, on, st.stream));
+  DQ_HIP(launch_string_groups_words(ok0, ok1, oc, on, kFreqSmallSlots, n, regs, dtc, st.stream));
+  std::vector<uint8_t> host(outs_bytes);
+  DQ_HIP(hipMemcpyAsync(host.data(), ob, outs_bytes, hipMemcpyDeviceToHost, st.stream));
+  DQ_HIP(hipStreamSynchronize(st.stream));
+  const unsigned long long* hk0 = reinterpret_cast<const unsigned long long*>(host.data());
+  const unsigned long long* hk1 = hk0 + nc * S;
+  const unsigned long long* hcn = hk1 + nc * S;
+  const uint32_t* hn = reinterpret_cast<const uint32_t*>(hcn + nc * S);
+  const uint32_t* hbad = hn + nc;
+  const uint32_t* hregs = hbad + nc;
+  const unsigned long long* hdtc = reinterpret_cast<const unsigned long long*>(hregs + nc * kHllM);
   for (int32_t i = 0; i < n; ++i) {
-    const uint8_t* o = host.data() + out_col * (size_t)i;
-    const unsigned long long* hk0 = reinterpret_cast<const unsigned long long*>(o);
-    const unsigned long long* hk1 = hk0 + kFreqSmallSlots;
-    const unsigned long long* hc2 = hk1 + kFreqSmallSlots;
-    const uint32_t ng = *reinterpret_cast<const uint32_t*>(hc2 + kFreqSmallSlots);
-    const unsigned int bad = *(reinterpret_cast<const uint32_t*>(hc2 + kFreqSmallSlots) + 1);
-    const uint32_t* regs = reinterpret_cast<const uint32_t*>(hc2 + kFreqSmallSlots) + 2;
-    const unsigned long long* dtc = reinterpret_cast<const unsigned long long*>(regs + kHllM);
+    if (hbad[i]) continue;  // (more groups, a longer key, or a heap under 16 bytes: the per-row pass)
     dq_few_result& r = results[i];
-    if (bad) continue;  // (more groups, a longer key, or a heap under 16 bytes: the per-row pass)
+    const uint32_t ng = hn[i];
     uint64_t grouped = 0;
     for (uint32_t g = 0; g < ng; ++g) {
-      const size_t at = (size_t)i * kFreqSmallSlots + g;
-      group_counts[at] = (int64_t)hc2[g];
-      group_lens[at] = (int32_t)(hk1[g] >> 56);
-      for (int b = 0; b < 8; ++b) group_keys[at * 16 + b] = (uint8_t)(hk0[g] >> (8 * b));
-      for (int b = 0; b < 8; ++b) group_keys[at * 16 + 8 + b] = b < 7 ? (uint8_t)(hk1[g] >> (8 * b)) : 0;
-      grouped += hc2[g];
+      const size_t at = (size_t)i * S + g;
+      group_counts[at] = (int64_t)hcn[at];
+      group_lens[at] = (int32_t)(hk1[at] >> 56);
+      for (int b = 0; b < 8; ++b) group_keys[at * 16 + b] = (uint8_t)(hk0[at] >> (8 * b));
+      for (int b = 0; b < 8; ++b) group_keys[at * 16 + 8 + b] = b < 7 ? (uint8_t)(hk1[at] >> (8 * b)) : 0;
+      grouped += hcn[at];
     }
     r.ok = 1;
     r.n_groups = (int32_t)ng;
@@ -2154,10 +2136,10 @@ extern "C" dq_status dq_profile_few_strings(dq_ctx* ctx, int32_t n, const dq_col
     r.completeness.count = n_rows;
     r.hll.kind = DQ_OP_APPROX_COUNT_DISTINCT;
     r.hll.has_value = 1;
-    pack_hll(regs, r.hll.words);
+    pack_hll(hregs + (size_t)i * kHllM, r.hll.words);
     r.dtype.kind = DQ_OP_DATATYPE;
     r.dtype.has_value = 1;
-    for (int k = 0; k < 5; ++k) r.dtype.words[k] = (int64_t)dtc[k];
+    for (int k = 0; k < 5; ++k) r.dtype.words[k] = (int64_t)hdtc[(size_t)i * 8 + k];
     r.dtype.words[0] += r.n_nulls;  // (DtPos: NULL first, dq_profile.hip)
   }
   return DQ_OK;

@@ -3752,6 +3752,16 @@ __global__ __launch_bounds__(kSmallThreads) void dq_freq_small_kernel(FreqKeySpe
                                                                       uint32_t* out_n, unsigned int* bad) {
   __shared__ SmallLds L;
   const uint32_t t = threadIdx.x;
+  {  // a launch over several columns (dq_profile_few_strings): blockIdx.y picks the column and
+     // its lists (gridDim.y = 1 otherwise)
+    const uint64_t y = blockIdx.y;
+    cols += y;
+    out_k0 += y * gridDim.x * kSmallSlots;
+    out_k1 += y * gridDim.x * kSmallSlots;
+    out_c += y * gridDim.x * kSmallSlots;
+    out_n += y * gridDim.x;
+    bad += y;
+  }
   for (uint32_t i = t; i < (uint32_t)kSmallSlots; i += kSmallThreads) {
     L.K1[i] = kLdsEmpty;
     L.C[i] = 0u;
@@ -3998,6 +4008,18 @@ __global__ __launch_bounds__(kSmallThreads) void dq_freq_small_merge_flat_kernel
   __shared__ unsigned int any_fail;
   __shared__ uint32_t n_used;
   const uint32_t t = threadIdx.x;
+  {  // one workgroup per column (blockIdx.x), each over that column's lists
+    const uint64_t y = blockIdx.x;
+    in_k0 += y * (uint64_t)n_blocks * kSmallSlots;
+    in_k1 += y * (uint64_t)n_blocks * kSmallSlots;
+    in_c += y * (uint64_t)n_blocks * kSmallSlots;
+    in_n += y * (uint64_t)n_blocks;
+    out_k0 += y * kSmallSlots;
+    out_k1 += y * kSmallSlots;
+    out_c += y * kSmallSlots;
+    out_n += y;
+    bad += y;
+  }
   if (t == 0) n_used = 0u;
   if (*bad) {
     if (t == 0) *out_n = 0u;
@@ -4031,20 +4053,21 @@ __global__ __launch_bounds__(kSmallThreads) void dq_freq_small_merge_flat_kernel
   if (t == 0) *out_n = n_used;
 }
 
-hipError_t launch_freq_small_flat(bool string_key, const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
-                                  int blocks, unsigned long long* d_k0, unsigned long long* d_k1, uint32_t* d_c,
-                                  uint32_t* d_n, unsigned int* d_bad, unsigned long long* d_out_k0,
+hipError_t launch_freq_small_flat(bool string_key, const FreqKeySpec& ks, const DevColumn* d_cols, int n_cols,
+                                  int64_t n_rows, int blocks, unsigned long long* d_k0, unsigned long long* d_k1,
+                                  uint32_t* d_c, uint32_t* d_n, unsigned int* d_bad, unsigned long long* d_out_k0,
                                   unsigned long long* d_out_k1, unsigned long long* d_out_c, uint32_t* d_out_n,
                                   hipStream_t stream) {
-  if (n_rows <= 0) return hipErrorInvalidValue;
+  if (n_rows <= 0 || n_cols <= 0 || n_cols > 65535) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)blocks, (unsigned)n_cols);
   if (string_key)
-    hipLaunchKernelGGL(dq_freq_small_kernel<true>, dim3((unsigned)blocks), dim3(kSmallThreads), 0, stream, ks, d_cols, n_rows,
-                       d_k0, d_k1, d_c, d_n, d_bad);
+    hipLaunchKernelGGL(dq_freq_small_kernel<true>, grid, dim3(kSmallThreads), 0, stream, ks, d_cols, n_rows, d_k0, d_k1,
+                       d_c, d_n, d_bad);
   else
-    hipLaunchKernelGGL(dq_freq_small_kernel<false>, dim3((unsigned)blocks), dim3(kSmallThreads), 0, stream, ks, d_cols,
-                       n_rows, d_k0, d_k1, d_c, d_n, d_bad);
-  hipLaunchKernelGGL(dq_freq_small_merge_flat_kernel, dim3(1), dim3(kSmallThreads), 0, stream, d_k0, d_k1, d_c, d_n, blocks,
-                     d_out_k0, d_out_k1, d_out_c, d_out_n, d_bad);
+    hipLaunchKernelGGL(dq_freq_small_kernel<false>, grid, dim3(kSmallThreads), 0, stream, ks, d_cols, n_rows, d_k0, d_k1,
+                       d_c, d_n, d_bad);
+  hipLaunchKernelGGL(dq_freq_small_merge_flat_kernel, dim3((unsigned)n_cols), dim3(kSmallThreads), 0, stream, d_k0, d_k1,
+                     d_c, d_n, blocks, d_out_k0, d_out_k1, d_out_c, d_out_n, d_bad);
   return hipGetLastError();
 }
 

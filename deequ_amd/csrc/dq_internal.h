@@ -339,14 +339,18 @@ hipError_t launch_freq_pack_probe(const FreqKeySpec& ks, const DevColumn* d_cols
 // utf8 column from its flat groups (dq_profile_string_groups); both zeroed by the caller.
 hipError_t launch_string_groups(const int64_t* d_counts, const int64_t* d_offs, const uint8_t* d_bytes, int64_t n,
                                 uint32_t* d_regs, unsigned long long* d_dtc, hipStream_t stream);
+// ... and over n_cols such lists (column y: d_k0 / d_k1 / d_counts + y * max_n, d_n[y], registers
+// d_regs + y * kHllM, counts d_dtc + y * 8).
 hipError_t launch_string_groups_words(const unsigned long long* d_k0, const unsigned long long* d_k1,
-                                      const unsigned long long* d_counts, const uint32_t* d_n, uint32_t max_n,
+                                      const unsigned long long* d_counts, const uint32_t* d_n, uint32_t max_n, int n_cols,
                                       uint32_t* d_regs, unsigned long long* d_dtc, hipStream_t stream);
-// dq_freq.hip: the few-groups kernel of one column + its lists summed into one compact list
-// (out_*[0, *out_n), at most kFreqSmallSlots groups; *bad raised when the column did not fit).
-hipError_t launch_freq_small_flat(bool string_key, const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
-                                  int blocks, unsigned long long* d_k0, unsigned long long* d_k1, uint32_t* d_c,
-                                  uint32_t* d_n, unsigned int* d_bad, unsigned long long* d_out_k0,
+// dq_freq.hip: the few-groups kernel over n_cols columns (d_cols[0 .. n_cols), one launch,
+// blockIdx.y = column) + each column's lists summed into one compact list: column y's groups at
+// out_*[y * kFreqSmallSlots ..][0, out_n[y]), bad[y] raised when it did not fit.  The lists:
+// d_k0 / d_k1 / d_c hold n_cols * blocks * kFreqSmallSlots entries, d_n n_cols * blocks.
+hipError_t launch_freq_small_flat(bool string_key, const FreqKeySpec& ks, const DevColumn* d_cols, int n_cols,
+                                  int64_t n_rows, int blocks, unsigned long long* d_k0, unsigned long long* d_k1,
+                                  uint32_t* d_c, uint32_t* d_n, unsigned int* d_bad, unsigned long long* d_out_k0,
                                   unsigned long long* d_out_k1, unsigned long long* d_out_c, uint32_t* d_out_n,
                                   hipStream_t stream);
 hipError_t launch_freq_stage_save(const unsigned long long* d_fill, unsigned long long* d_fill_save, uint32_t n_fill,

@@ -594,9 +594,16 @@ __global__ __launch_bounds__(kBlock) void dq_string_groups_words_kernel(const un
                                                                         const unsigned long long* __restrict__ counts,
                                                                         const uint32_t* __restrict__ n,
                                                                         uint32_t* __restrict__ regs,
-                                                                        unsigned long long* __restrict__ dtc) {
+                                                                        unsigned long long* __restrict__ dtc,
+                                                                        uint32_t max_n) {
+  const uint64_t y = blockIdx.y;  // the column
+  k0 += y * max_n;
+  k1 += y * max_n;
+  counts += y * max_n;
+  regs += y * kHllM;
+  dtc += y * 8;
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= *n) return;
+  if (i >= n[y]) return;
   const uint64_t w0 = k0[i], w1 = k1[i];
   const uint32_t len = (uint32_t)(w1 >> 56);
   uint8_t b[16];
@@ -614,10 +621,11 @@ __global__ __launch_bounds__(kBlock) void dq_string_groups_words_kernel(const un
 }
 
 hipError_t launch_string_groups_words(const unsigned long long* d_k0, const unsigned long long* d_k1,
-                                      const unsigned long long* d_counts, const uint32_t* d_n, uint32_t max_n,
+                                      const unsigned long long* d_counts, const uint32_t* d_n, uint32_t max_n, int n_cols,
                                       uint32_t* d_regs, unsigned long long* d_dtc, hipStream_t stream) {
-  hipLaunchKernelGGL(dq_string_groups_words_kernel, dim3((max_n + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, d_k0,
-                     d_k1, d_counts, d_n, d_regs, d_dtc);
+  if (n_cols <= 0 || n_cols > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dq_string_groups_words_kernel, dim3((max_n + kBlock - 1) / kBlock, (unsigned)n_cols), dim3(kBlock), 0,
+                     stream, d_k0, d_k1, d_counts, d_n, d_regs, d_dtc, max_n);
   return hipGetLastError();
 }
 
