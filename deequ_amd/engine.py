@@ -7,6 +7,7 @@ fused pass of the gfx950 kernels, and `dq_plan_finish` returns one POD state per
 """
 from __future__ import annotations
 
+import contextvars
 import ctypes
 import os
 from typing import Dict, List, Optional, Sequence
@@ -231,9 +232,18 @@ class OpUnsupported:
         self.error = error
 
 
+# A threading.Event the scans of this context wait on before their first launch: the
+# profiler plans pass 1's first scan on a thread while its few-groups launch still has the
+# device to itself (a latency-bound kernel starves beside the VALU-bound scans).
+LAUNCH_GATE: "contextvars.ContextVar" = contextvars.ContextVar("deequ_amd_launch_gate", default=None)
+
+
 def _scan_local(specs: Sequence[OpSpec], data) -> List:
     plan = Plan(specs, data.schema)
     try:
+        gate = LAUNCH_GATE.get()
+        if gate is not None:
+            gate.wait()
         for batch in data.batches():
             plan.consume(batch)
         out = plan.finish_raw()

@@ -198,17 +198,33 @@ class ColumnProfiler:
             # (The metrics are those of the one fused pass; only the failure scope of an error
             # inside a plan is the plan's columns.)
             others = [c for c in relevant if c not in strings]
-            # (first and alone: the few-groups kernels are latency-bound, beside the VALU-bound
-            # scans they starve)
-            few = _few_group_strings(data, strings)
-            rest = [c for c in strings if c not in few]
+            import threading
+            from .engine import LAUNCH_GATE
+            gate = threading.Event()
+            if os.environ.get("DEEQU_AMD_PROFILE_GATE", "1") == "0":  # (A/B knob)
+                gate.set()
+
+            def gated(fn, *args):
+                token = LAUNCH_GATE.set(gate)
+                try:
+                    return fn(*args)
+                finally:
+                    LAUNCH_GATE.reset(token)
             pool = ThreadPoolExecutor(max_workers=2)
-            fut = pool.submit(lambda: AnalysisRunner.onData(data).addAnalyzers(_first(others)).addAnalyzer(Size()).run())
+            # the other plan is planned now but launches after the few-groups launch: that
+            # launch is latency-bound, beside the VALU-bound scans it would starve
+            fut = pool.submit(gated, lambda: AnalysisRunner.onData(data).addAnalyzers(_first(others))
+                              .addAnalyzer(Size()).run())
             # a boolean column has at most three values, so it is a histogram target unless the
-            # threshold is below that: its histogram scan runs now, beside pass 1, and is used if so
+            # threshold is below that: its histogram scan runs beside pass 1 and is used if so
             bools = [c for c in relevant if schema[c] == "bool" and _IDENT.match(c)]
-            fut_bool = pool.submit(_bool_histograms, data, bools) if bools else None
+            fut_bool = pool.submit(gated, _bool_histograms, data, bools) if bools else None
             try:
+                try:
+                    few = _few_group_strings(data, strings)
+                finally:
+                    gate.set()
+                rest = [c for c in strings if c not in few]
                 ctx_s = AnalysisRunner.onData(data).addAnalyzers(_first(rest)).run() if rest else AnalyzerContext()
                 ctx_s = ctx_s + _few_group_metrics(few)
                 gen_s = _extract_generic_statistics(strings, schema, ctx_s, predefined)
