@@ -232,10 +232,11 @@ class OpUnsupported:
         self.error = error
 
 
-# A threading.Event the scans of this context wait on before their first launch: the
-# profiler plans pass 1's first scan on a thread while its few-groups launch still has the
-# device to itself (a latency-bound kernel starves beside the VALU-bound scans).
+# A threading.Event the scans of this context wait on before their first launch (LAUNCH_GATE),
+# and one they set once their kernels are queued (LAUNCH_SIGNAL): the profiler orders pass 1's
+# launches across its threads with them (profiles.py).
 LAUNCH_GATE: "contextvars.ContextVar" = contextvars.ContextVar("deequ_amd_launch_gate", default=None)
+LAUNCH_SIGNAL: "contextvars.ContextVar" = contextvars.ContextVar("deequ_amd_launch_signal", default=None)
 
 
 def _scan_local(specs: Sequence[OpSpec], data) -> List:
@@ -246,6 +247,9 @@ def _scan_local(specs: Sequence[OpSpec], data) -> List:
             gate.wait()
         for batch in data.batches():
             plan.consume(batch)
+        signal = LAUNCH_SIGNAL.get()
+        if signal is not None:
+            signal.set()
         out = plan.finish_raw()
         res = []
         for i in range(plan.n_ops):

@@ -182,7 +182,7 @@ class ColumnProfiler:
         from .runner import AnalyzerContext
         overlap = os.environ.get("DEEQU_AMD_PROFILE_SERIAL", "0") != "1"  # (A/B and debugging knob)
         sharded = is_sharded(data)
-        casted, few, ctx2_s, bool_hist = None, {}, None, {}
+        casted, few, ctx2_s, bool_hist, few_hist = None, {}, None, {}, {}
         if sharded or not overlap or not strings:
             # one fused pass over every column (over a ShardedTable every pass is collective)
             ctx1 = AnalysisRunner.onData(data).addAnalyzers(_first(relevant)).addAnalyzer(Size()).run()
@@ -210,22 +210,38 @@ class ColumnProfiler:
                     return fn(*args)
                 finally:
                     LAUNCH_GATE.reset(token)
-            pool = ThreadPoolExecutor(max_workers=2)
-            # the other plan is planned now but launches after the few-groups launch: that
-            # launch is latency-bound, beside the VALU-bound scans it would starve
-            fut = pool.submit(gated, lambda: AnalysisRunner.onData(data).addAnalyzers(_first(others))
-                              .addAnalyzer(Size()).run())
-            # a boolean column has at most three values, so it is a histogram target unless the
-            # threshold is below that: its histogram scan runs beside pass 1 and is used if so
+            pool = ThreadPoolExecutor(max_workers=3)
             bools = [c for c in relevant if schema[c] == "bool" and _IDENT.match(c)]
-            fut_bool = pool.submit(gated, _bool_histograms, data, bools) if bools else None
+            started = {}
+
+            def start_others():
+                # the other plan is planned while the few-groups launch runs (the library call
+                # holds no GIL) and launches once the string pass is queued: the few-groups launch
+                # is latency-bound and would starve beside its VALU-bound scans
+                started["fut"] = pool.submit(gated, lambda: AnalysisRunner.onData(data).addAnalyzers(_first(others))
+                                             .addAnalyzer(Size()).run())
+                # a boolean column has at most three values, so it is a histogram target unless
+                # the threshold is below that: its histogram scan runs beside pass 1, used if so
+                started["bool"] = pool.submit(gated, _bool_histograms, data, bools) if bools else None
             try:
                 try:
-                    few = _few_group_strings(data, strings)
+                    few = _few_group_strings(data, strings, before_launch=start_others)
                 finally:
-                    gate.set()
+                    if "fut" not in started:
+                        start_others()
+                fut, fut_bool = started["fut"], started["bool"]
                 rest = [c for c in strings if c not in few]
-                ctx_s = AnalysisRunner.onData(data).addAnalyzers(_first(rest)).run() if rest else AnalyzerContext()
+                # the string pass is the head of the critical path (its types -> the casts -> their
+                # statistics): it is queued first, the other plan's scans after it
+                from .engine import LAUNCH_SIGNAL
+                token = LAUNCH_SIGNAL.set(gate)
+                try:
+                    ctx_s = AnalysisRunner.onData(data).addAnalyzers(_first(rest)).run() if rest else AnalyzerContext()
+                finally:
+                    LAUNCH_SIGNAL.reset(token)
+                    gate.set()
+                # the few-valued columns' histograms, built while the casts run
+                fut_hist = pool.submit(lambda: {c: g.histogram() for c, g in few.items()}) if few else None
                 ctx_s = ctx_s + _few_group_metrics(few)
                 gen_s = _extract_generic_statistics(strings, schema, ctx_s, predefined)
                 casted = _cast_numeric_string_columns(relevant, data, gen_s)
@@ -236,6 +252,8 @@ class ColumnProfiler:
                 ctx1 = fut.result() + ctx_s
                 if fut_bool is not None:
                     bool_hist = fut_bool.result()
+                if fut_hist is not None:
+                    few_hist = fut_hist.result()
             finally:
                 pool.shutdown(wait=True)
         generic = _extract_generic_statistics(relevant, schema, ctx1, predefined)
@@ -247,11 +265,12 @@ class ColumnProfiler:
         # the library releases the GIL).  Over a ShardedTable both passes are collective, so
         # they stay in order there.  A pass-2 failure is raised as the sequential run would.
         targets = _find_target_columns_for_histograms(schema, generic, lowCardinalityHistogramThreshold)
-        side = ThreadPoolExecutor(max_workers=1) if overlap and targets and not sharded else None
+        known = {c: few_hist[c] if c in few_hist else few[c].histogram() for c in targets if c in few}
+        known.update({c: bool_hist[c] for c in targets if c in bool_hist})
+        todo = [c for c in targets if c not in known]
+        side = ThreadPoolExecutor(max_workers=1) if overlap and todo and not sharded else None
         if side and printStatusUpdates:
             print("### PROFILING: Computing histograms of low-cardinality columns in pass (3/3), beside pass 2...")
-        known = {c: few[c].histogram() for c in targets if c in few}
-        known.update({c: bool_hist[c] for c in targets if c in bool_hist})
         pending = (side.submit(compute_histograms, data, targets, generic.approximateNumDistincts, known)
                    if side else None)
         try:
@@ -332,13 +351,15 @@ def _few_group_metrics(few: Dict[str, "_FewGroups"]):
     return AnalyzerContext(out)
 
 
-def _few_group_strings(data, columns: Sequence[str]) -> Dict[str, _FewGroups]:
+def _few_group_strings(data, columns: Sequence[str], before_launch=None) -> Dict[str, _FewGroups]:
     """Pass 1's string columns tried as few-valued columns, all in one library call per batch
     (dq_profile_few_strings: the few-groups kernel and a merge per column, launches overlapped,
     one wait); a column must fit in every batch.  Not over a ShardedTable (its passes are
     collective) and off with DEEQU_AMD_PROFILE_FEW=0."""
     from .distributed import is_sharded
     if not columns or is_sharded(data) or os.environ.get("DEEQU_AMD_PROFILE_FEW", "1") == "0":
+        if before_launch is not None:
+            before_launch()
         return {}
     from .arrow import ArrowBatch
     from .engine import current_device
@@ -359,6 +380,9 @@ def _few_group_strings(data, columns: Sequence[str]) -> Dict[str, _FewGroups]:
         keys = np.zeros(n * L.DQ_FEW_MAX_GROUPS * 16, dtype=np.uint8)
         lens = np.zeros(n * L.DQ_FEW_MAX_GROUPS, dtype=np.int32)
         cols = (L.DqColumn * n)(*[batch.columns[c].to_dq() for c in live])
+        if before_launch is not None:  # (once: the caller's other threads start here, while the
+            before_launch()            # library call below holds no GIL)
+            before_launch = None
         L.check(L.lib().dq_profile_few_strings(ctx.handle, n, cols, rows, res, counts.ctypes.data, keys.ctypes.data,
                                                lens.ctypes.data))
         kept = []
