@@ -3697,8 +3697,17 @@ hipError_t launch_import_global(const FreqTable& T, const ImportRun* d_runs, int
 // LDS table holds, raises `bad` and the host takes the general insert path instead.
 // =============================================================================================
 constexpr int kSmallSlots = 1024;
-constexpr int kSmallThreads = 512;
-constexpr int kSmallPer = 8;  // rows per thread per iteration
+// Rows per thread per step: 4 (70 VGPRs, 7 waves per SIMD) measured 4.64 ms for C5's 20-column
+// launch against 5.13 with 8 (109 VGPRs, 4 waves); 2 / 3 / 6 rows and 256 threads per block were
+// within 0.1 ms of 4, 1024 threads 5.96 (profiles/r05_c5_small_per_ab.txt)
+#ifndef DQ_SMALL_PER
+#define DQ_SMALL_PER 4
+#endif
+#ifndef DQ_SMALL_THREADS
+#define DQ_SMALL_THREADS 512
+#endif
+constexpr int kSmallThreads = DQ_SMALL_THREADS;
+constexpr int kSmallPer = DQ_SMALL_PER;  // rows per thread per iteration
 
 struct SmallLds {
   unsigned long long K0[kSmallSlots], K1[kSmallSlots];  // K1 = key bytes 8..14 | length << 56
