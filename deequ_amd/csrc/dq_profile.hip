@@ -464,6 +464,12 @@ __device__ inline bool cast_one(const Src& p, int32_t n, int64_t* lv, double* dv
 #ifndef DQ_CAST_PIPE
 #define DQ_CAST_PIPE 1
 #endif
+// Rows per lane per step of the cast: 2 (62 VGPRs, 8 waves per SIMD) measured 0.55 ms per
+// 1e8-row column alone against 0.71 with 4 (114 VGPRs, 4 waves); 3 0.62, 6 0.85
+// (profiles/r05_c5_cast_rows_ab.txt)
+#ifndef DQ_CAST_U
+#define DQ_CAST_U 2
+#endif
 template <int TO>
 __global__ __launch_bounds__(kBlock) void dq_cast_utf8_kernel(DevColumn src, int64_t n_rows, void* values,
                                                               uint8_t* validity) {
@@ -471,7 +477,7 @@ __global__ __launch_bounds__(kBlock) void dq_cast_utf8_kernel(DevColumn src, int
   // pair (one 8-byte load), its validity byte, and the first 24 bytes of the string (load24: a 16-
   // and an 8-byte unaligned buffer load).  Longer strings take the byte-pointer parser.
   constexpr int to_type = TO;
-  constexpr int U = 4;
+  constexpr int U = DQ_CAST_U;
   const uint32_t lane = threadIdx.x & 63u;
   const uint8_t* vals = static_cast<const uint8_t*>(src.values);
   const uint32_t heap_end = (uint32_t)src.offsets[n_rows];
@@ -647,7 +653,7 @@ hipError_t launch_cast_utf8(const DevColumn& src, int64_t n_rows, int to_type, v
     c.offsets = src.offsets + start;  // (offsets stay absolute into the bytes)
     if (c.validity) c.validity = src.validity + (start >> 3);
     uint8_t* vout = d_validity + (start >> 3);
-    int64_t blocks = (m + 4 * kBlock - 1) / (4 * kBlock);  // (4 rows per lane per step)
+    int64_t blocks = (m + DQ_CAST_U * kBlock - 1) / (DQ_CAST_U * kBlock);  // (DQ_CAST_U rows per lane per step)
     if (blocks > 8192) blocks = 8192;
     if (to_type == DQ_T_INT64)
       hipLaunchKernelGGL(dq_cast_utf8_kernel<DQ_T_INT64>, dim3((unsigned)blocks), dim3(kBlock), 0, stream, c, m,
