@@ -27,6 +27,7 @@ DQ_COL_DEVICE = 0x1
 
 DQ_P_COLUMN, DQ_P_LIT_INT, DQ_P_LIT_FLOAT, DQ_P_LIT_NULL, DQ_P_COALESCE, DQ_P_LIT_STRING = 1, 2, 3, 4, 5, 6
 DQ_P_CAST_DOUBLE = 7
+DQ_P_CAST = 8  # arg = target dq_type (TYPE_CODES)
 DQ_P_EQ, DQ_P_NE, DQ_P_LT, DQ_P_LE, DQ_P_GT, DQ_P_GE, DQ_P_EQ_NULLSAFE = 10, 11, 12, 13, 14, 15, 16
 DQ_P_IS_NULL, DQ_P_IS_NOT_NULL = 20, 21
 DQ_P_AND, DQ_P_OR, DQ_P_NOT, DQ_P_TRUE, DQ_P_FALSE = 30, 31, 32, 33, 34
@@ -118,6 +119,7 @@ DIAG_SIGNATURES = {
     "dq_diag_parse_double": (c_int, [c_char_p, c_int64, POINTER(c_double), POINTER(c_int32)]),
     "dq_diag_table_hash": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "dq_diag_key_pack": (c_int, [c_char_p, c_int32, POINTER(c_uint64), c_char_p, POINTER(c_int32), POINTER(c_int32)]),
+    "dq_diag_eval_predicate": (c_int, [POINTER(DqPredicate), POINTER(DqColumn), c_int, c_int64, c_void_p]),
 }
 
 

@@ -220,12 +220,14 @@ class Compliance(StandardScanShareableAnalyzer):
     def preconditions(self):
         # Spark fails the aggregation (AnalysisException) on an unknown column; deequ turns
         # it into a failure metric.  Checked on the schema here, before any data is touched.
-        from .predicates import referenced_columns
+        from .predicates import referenced_columns, resolve_column
 
         def check(schema):
             for c in referenced_columns(self.predicate) + (
                     referenced_columns(self.where) if self.where else []):
-                if c not in schema:
+                try:  # case-insensitive, as Spark 2.2 resolves names
+                    resolve_column(c, schema)
+                except KeyError:
                     raise NoSuchColumnException("Input data does not include column %s!" % c)
         return [check]
 

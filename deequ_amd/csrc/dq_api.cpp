@@ -23,6 +23,7 @@
 #include "dq_internal.h"
 #include "dq_keypack.h"
 #include "dq_numparse.h"
+#include "dq_predeval.h"
 #include "../../include/deequ_amd_diag.h"
 #include "hll_p9_tables.h"
 
@@ -403,7 +404,10 @@ extern "C" dq_status dq_ctx_destroy(dq_ctx* ctx) {
 }
 
 // ------------------------------------------------------------------------------ predicates
-enum VT { V_INT = 0, V_FLT = 1, V_BOOL = 2, V_STR = 3 };
+// Value types of the validator.  V_F32 is a FloatType value (a FLOAT32 column or a cast to
+// FLOAT32; the device holds it as the fp64 of the same value); V_NULL the untyped NULL literal,
+// compatible with every type (Spark types it by the other side).
+enum VT { V_INT = 0, V_FLT = 1, V_BOOL = 2, V_STR = 3, V_F32 = 4, V_NULL = 5 };
 
 struct Program {
   std::vector<PredInsn> code;
@@ -411,6 +415,20 @@ struct Program {
   std::string pool;          // string literals (DQ_P_LIT_STRING), offsets relative to this
   std::string key;           // byte image for de-duplication
 };
+
+static bool vt_fractional(int t) { return t == V_FLT || t == V_F32; }
+
+// The binary-operand rules of the header's "Type rules" (include/deequ_amd.h): a pair the IR
+// cannot evaluate exactly as Spark 2.2 would is DQ_ERR_UNSUPPORTED.
+static dq_status check_pair(int a, int b, const char* what) {
+  if (a == V_NULL || b == V_NULL) return DQ_OK;
+  if ((a == V_STR) != (b == V_STR))  // Spark casts the string: only DQ_P_CAST_DOUBLE does that
+    return fail(DQ_ERR_UNSUPPORTED, std::string(what) + " of a string with a non-string");
+  if ((a == V_F32 && b == V_INT) || (a == V_INT && b == V_F32))
+    return fail(DQ_ERR_UNSUPPORTED, std::string(what) + " of a FloatType value with an integral value: Spark "
+                "compares in FloatType, so the integral side needs a DQ_P_CAST to FLOAT32");
+  return DQ_OK;
+}
 
 static dq_status validate_predicate(const dq_predicate& p, const int32_t* types, int n_cols,
                                     Program* out) {
@@ -425,7 +443,8 @@ static dq_status validate_predicate(const dq_predicate& p, const int32_t* types,
       case DQ_P_COLUMN: {
         if (in.arg < 0 || in.arg >= n_cols) return fail(DQ_ERR_INVALID, "predicate column out of range");
         const int t = types[in.arg];
-        st.push_back(t == DQ_T_UTF8 ? V_STR : t == DQ_T_BOOL ? V_BOOL : (is_integral(t) ? V_INT : V_FLT));
+        st.push_back(t == DQ_T_UTF8 ? V_STR : t == DQ_T_BOOL ? V_BOOL : t == DQ_T_FLOAT32 ? V_F32
+                     : (is_integral(t) ? V_INT : V_FLT));
         prog.columns.push_back(in.arg);
         break;
       }
@@ -437,20 +456,45 @@ static dq_status validate_predicate(const dq_predicate& p, const int32_t* types,
       }
       case DQ_P_LIT_INT: st.push_back(V_INT); break;
       case DQ_P_LIT_FLOAT: st.push_back(V_FLT); break;
-      case DQ_P_LIT_NULL: st.push_back(V_INT); break;
+      case DQ_P_LIT_NULL: st.push_back(V_NULL); break;
       case DQ_P_CAST_DOUBLE:  // Cast(-> DoubleType) of a string or a number
         if (st.empty()) return fail(DQ_ERR_INVALID, "predicate stack underflow");
         if (st.back() == V_BOOL) return fail(DQ_ERR_UNSUPPORTED, "cast of a boolean to double");
-        st.back() = V_FLT;
+        if (st.back() != V_NULL) st.back() = V_FLT;
         break;
+      case DQ_P_CAST: {  // Cast(numeric / boolean -> arg)
+        if (st.empty()) return fail(DQ_ERR_INVALID, "predicate stack underflow");
+        const int to = in.arg;
+        int vt;
+        switch (to) {
+          case DQ_T_INT8: case DQ_T_INT16: case DQ_T_INT32: case DQ_T_INT64: vt = V_INT; break;
+          case DQ_T_FLOAT32: vt = V_F32; break;
+          case DQ_T_FLOAT64: vt = V_FLT; break;
+          case DQ_T_BOOL: vt = V_BOOL; break;
+          default:
+            return fail(DQ_ERR_UNSUPPORTED, "DQ_P_CAST to type " + std::to_string(to) +
+                        " (only INT8..INT64, FLOAT32, FLOAT64 and BOOL are evaluated on the GPU)");
+        }
+        if (st.back() == V_STR)
+          return fail(DQ_ERR_UNSUPPORTED, "DQ_P_CAST of a string (Spark's UTF8String casts stay on Spark)");
+        if (st.back() != V_NULL) st.back() = vt;
+        break;
+      }
       case DQ_P_TRUE: case DQ_P_FALSE: st.push_back(V_BOOL); break;
       case DQ_P_COALESCE: {
         if (st.size() < 2) return fail(DQ_ERR_INVALID, "predicate stack underflow");
         const int b = st.back(); st.pop_back();
         const int a = st.back(); st.pop_back();
-        if ((a == V_BOOL) != (b == V_BOOL)) return fail(DQ_ERR_UNSUPPORTED, "COALESCE of mixed boolean/numeric");
-        if ((a == V_STR) != (b == V_STR)) return fail(DQ_ERR_UNSUPPORTED, "COALESCE of mixed string/numeric");
-        st.push_back((a == V_FLT || b == V_FLT) ? V_FLT : a);
+        if (a != V_NULL && b != V_NULL && (a == V_BOOL) != (b == V_BOOL))
+          return fail(DQ_ERR_UNSUPPORTED, "COALESCE of mixed boolean/numeric");
+        DQ_TRY(check_pair(a, b, "COALESCE"));
+        int r;
+        if (a == V_NULL) r = b;
+        else if (b == V_NULL) r = a;
+        else if (a == V_FLT || b == V_FLT) r = V_FLT;
+        else if (a == V_F32 || b == V_F32) r = V_F32;  // (F32, F32): the device keeps the value
+        else r = a;
+        st.push_back(r);
         break;
       }
       case DQ_P_EQ: case DQ_P_NE: case DQ_P_LT: case DQ_P_LE: case DQ_P_GT: case DQ_P_GE:
@@ -460,10 +504,10 @@ static dq_status validate_predicate(const dq_predicate& p, const int32_t* types,
         const int a = st.back(); st.pop_back();
         if (in.arg != DQ_CMP_AS_INT64 && in.arg != DQ_CMP_AS_FLOAT64)
           return fail(DQ_ERR_INVALID, "comparison type must be DQ_CMP_AS_INT64 or DQ_CMP_AS_FLOAT64");
-        if (in.arg == DQ_CMP_AS_INT64 && (a == V_FLT || b == V_FLT))
-          return fail(DQ_ERR_INVALID, "int64 comparison of a floating-point operand");
-        if ((a == V_STR) != (b == V_STR))  // Spark would cast the string to double: not here
-          return fail(DQ_ERR_UNSUPPORTED, "comparison of a string with a non-string");
+        if (in.arg == DQ_CMP_AS_INT64 && (vt_fractional(a) || vt_fractional(b)))
+          return fail(DQ_ERR_UNSUPPORTED, "int64 comparison of a floating-point operand (Spark compares "
+                      "that pair in a fractional type: cast it or compare as DQ_CMP_AS_FLOAT64)");
+        DQ_TRY(check_pair(a, b, "comparison"));
         st.push_back(V_BOOL);
         break;
       }
@@ -1889,6 +1933,33 @@ extern "C" dq_status dq_diag_parse_double(const uint8_t* s, int64_t n, double* o
   return DQ_OK;
 }
 
+// Host build of the predicate interpreter (dq_predeval.h, the same source dq_pred_kernel runs):
+// validates `p` against the columns' types exactly as plan creation does, then evaluates it row
+// by row over host columns.  out[r] = 0 FALSE, 1 TRUE, 2 NULL.
+extern "C" dq_status dq_diag_eval_predicate(const dq_predicate* p, const dq_column* cols, int n_cols,
+                                            int64_t n_rows, uint8_t* out) {
+  if (!p || (n_cols > 0 && !cols) || n_cols < 0 || n_rows < 0 || (n_rows > 0 && !out))
+    return fail(DQ_ERR_INVALID, "bad argument");
+  std::vector<int32_t> types((size_t)n_cols);
+  std::vector<DevColumn> dc((size_t)n_cols);
+  for (int c = 0; c < n_cols; ++c) {
+    if (cols[c].flags & DQ_COL_DEVICE) return fail(DQ_ERR_INVALID, "host columns only");
+    if (cols[c].offset != 0) return fail(DQ_ERR_INVALID, "column offset must be 0");
+    if (cols[c].length < n_rows) return fail(DQ_ERR_INVALID, "column shorter than n_rows");
+    types[c] = cols[c].type;
+    dc[c] = DevColumn{cols[c].validity, cols[c].values, cols[c].offsets, cols[c].type, 0};
+  }
+  Program prog;
+  DQ_TRY(validate_predicate(*p, types.data(), n_cols, &prog));
+  const uint8_t* pool = reinterpret_cast<const uint8_t*>(prog.pool.data());
+  for (int64_t r = 0; r < n_rows; ++r) {
+    bool t = false, nn = false;
+    pred::eval_program<true>(prog.code.data(), (int)prog.code.size(), pool, dc.data(), r, t, nn);
+    out[r] = nn ? (t ? 1 : 0) : 2;
+  }
+  return DQ_OK;
+}
+
 // Host build of the group-by's digit-key packing (dq_keypack.h): the record word of a key of
 // <= 15 bytes, and the key bytes it unpacks to.
 extern "C" dq_status dq_diag_key_pack(const uint8_t* key, int32_t len, uint64_t* packed, uint8_t* back,
@@ -2045,20 +2116,10 @@ extern "C" dq_status dq_profile_string_groups(dq_ctx* ctx, const int64_t* counts
   return DQ_OK;
 }
 
-extern "C" dq_status dq_profile_few_strings(dq_ctx* ctx, int32_t n, const dq_column* cols, int64_t n_rows,
-                                            dq_few_result* results, int64_t* group_counts, uint8_t* group_keys,
-                                            int32_t* group_lens) {
-  static_assert(DQ_FEW_MAX_GROUPS == kFreqSmallSlots, "the few-groups kernel's LDS table size");
-  if (!ctx || n < 0 || (n > 0 && (!cols || !results || !group_counts || !group_keys || !group_lens)))
-    return fail(DQ_ERR_INVALID, "NULL argument");
-  if (n_rows < 0 || n > 65535) return fail(DQ_ERR_INVALID, "bad n_rows or column count");
-  for (int32_t i = 0; i < n; ++i) {
-    if (cols[i].type != DQ_T_UTF8) return fail(DQ_ERR_INVALID, "dq_profile_few_strings needs utf8 columns");
-    if (cols[i].length < n_rows) return fail(DQ_ERR_INVALID, "bad n_rows");
-  }
-  std::memset(results, 0, sizeof(dq_few_result) * (size_t)std::max(0, n));
-  if (n == 0 || n_rows == 0) return DQ_OK;  // (no rows: every column goes to the per-row pass)
-  DQ_HIP(hipSetDevice(ctx->device));
+// One chunk of dq_profile_few_strings' columns (arguments checked, results zeroed by the caller).
+static dq_status few_strings_chunk(dq_ctx* ctx, int32_t n, const dq_column* cols, int64_t n_rows,
+                                   dq_few_result* results, int64_t* group_counts, uint8_t* group_keys,
+                                   int32_t* group_lens) {
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
   // every column in ONE launch of each kernel (blockIdx.y = column): the few-groups kernel (its
@@ -2141,6 +2202,39 @@ extern "C" dq_status dq_profile_few_strings(dq_ctx* ctx, int32_t n, const dq_col
     r.dtype.has_value = 1;
     for (int k = 0; k < 5; ++k) r.dtype.words[k] = (int64_t)hdtc[(size_t)i * 8 + k];
     r.dtype.words[0] += r.n_nulls;  // (DtPos: NULL first, dq_profile.hip)
+  }
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_profile_few_strings(dq_ctx* ctx, int32_t n, const dq_column* cols, int64_t n_rows,
+                                            dq_few_result* results, int64_t* group_counts, uint8_t* group_keys,
+                                            int32_t* group_lens) {
+  static_assert(DQ_FEW_MAX_GROUPS == kFreqSmallSlots, "the few-groups kernel's LDS table size");
+  if (!ctx || n < 0 || (n > 0 && (!cols || !results || !group_counts || !group_keys || !group_lens)))
+    return fail(DQ_ERR_INVALID, "NULL argument");
+  if (n_rows < 0 || n > 65535) return fail(DQ_ERR_INVALID, "bad n_rows or column count");
+  for (int32_t i = 0; i < n; ++i) {
+    if (cols[i].type != DQ_T_UTF8) return fail(DQ_ERR_INVALID, "dq_profile_few_strings needs utf8 columns");
+    if (cols[i].length < n_rows) return fail(DQ_ERR_INVALID, "bad n_rows");
+  }
+  std::memset(results, 0, sizeof(dq_few_result) * (size_t)std::max(0, n));
+  if (n == 0 || n_rows == 0) return DQ_OK;  // (no rows: every column goes to the per-row pass)
+  DQ_HIP(hipSetDevice(ctx->device));
+  // Bounded chunks: the workgroup lists take blocks x 1024 x 20 B per column (~12 MB on 304
+  // CUs), so a wide table is grouped 32 columns at a time.  A chunk whose scratch cannot be
+  // allocated is not an error: its columns stay ok = 0 and take the per-row string pass.
+  constexpr int32_t kChunk = 32;
+  const size_t S = kFreqSmallSlots;
+  for (int32_t i0 = 0; i0 < n; i0 += kChunk) {
+    const int32_t m = std::min(kChunk, n - i0);
+    const dq_status st = few_strings_chunk(ctx, m, cols + i0, n_rows, results + i0, group_counts + (size_t)i0 * S,
+                                           group_keys + (size_t)i0 * S * 16, group_lens + (size_t)i0 * S);
+    if (st == DQ_ERR_OOM) {
+      (void)hipGetLastError();  // (clear the runtime's sticky allocation error)
+      std::memset(results + i0, 0, sizeof(dq_few_result) * (size_t)m);
+      continue;
+    }
+    if (st != DQ_OK) return st;
   }
   return DQ_OK;
 }

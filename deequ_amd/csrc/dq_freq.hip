@@ -1412,10 +1412,6 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
     room[k] = 0ull;
     if (b < nb) {
       const uint32_t c = L.hist[b];
-#ifdef DQ_X_NORES  // (timing experiment, results wrong: no reservation round trip)
-      if (REC_LDS) room[k] = (unsigned long long)(blockIdx.x & 63u) * 64ull;
-      else
-#endif
       if (c) room[k] = atomicAdd(&out_fill[base_id + b], (unsigned long long)c);
     }
   }
@@ -1467,9 +1463,6 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
       const uint32_t pos = r0 + j;  // the record's tile position
       const R r = L.rec[j];
       if (pos < L.lim[b]) {
-#ifdef DQ_X_NOWRITE  // (timing experiment, results wrong: no record stores)
-        if (!REC_LDS)
-#endif
         out[L.gbase[b] + pos] = r;
       } else {  // the region is full: the overflow list (16-B records, aggregated by the sort path)
         const unsigned long long k = atomicAdd(ovf_n, 1ull);
@@ -1987,11 +1980,7 @@ __global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(D
             packed = kp_pack_record(k0, k1, len, &p);
           }
           if (packed) {
-#ifdef DQ_X_NOPARK  // (experiment: records stay in registers)
-            rec[j] = p;
-#else
             L.rec[j * kStageThreads + t] = p;  // (row order; part_tile sorts it)
-#endif
             h = hash_record_packed(p);
           } else {  // not a digit key: a 16-B record on the overflow list
             h = hash_raw(k0, k1, len);
@@ -2055,25 +2044,9 @@ __global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(D
       if constexpr (PACK)
         if (t == 0) abort_v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
-#ifdef DQ_X_NOSPLIT  // (timing experiment, results wrong: no multi-split, nothing written)
-#ifdef DQ_X_ROWWRITE  // (... but the records written in row order, coalesced)
-    if constexpr (PACK) {
-#pragma unroll
-      for (int j = 0; j < kStagePer; ++j) out[(uint64_t)tile * kStageTile + (uint64_t)j * kStageThreads + t] = L.rec[j * kStageThreads + t];
-    }
-#else
-    if (t == 0 && bin[0] == 0xFFFFFFFEu) out[0] = L.rec[0];
-#endif
-#else
     part_tile<kStagePer, (1 << kStageBinBits), R, (PACK ? kStageSubP : kPartSub), kProf, DQ_STAGE_WOUT_UNROLL,
-#ifdef DQ_X_NOPARK
-              false,
-#else
-              PACK,
-#endif
-              kStageThreads, decltype(flag_read)>(
+              PACK, kStageThreads, decltype(flag_read)>(
         L, rec, bin, nb, 0, out, cap1, fill1, ovf, ovf_n, ovf_cap, flag, staged, nullptr, prof_t_, flag_read);
-#endif
   }
   if (PACK && n_side) atomicAdd(staged, (unsigned long long)n_side);
 #ifdef DQ_STAGE_PROF

@@ -7,183 +7,11 @@
 // postfix interpreter (the plan's validated dq_pred_insn program).  Each wave evaluates 64
 // consecutive rows and writes two 64-bit ballot words: TRUE bits and NOT-NULL bits.  The scan
 // kernel then reads those masks (2 bits per row instead of the referenced columns' bytes).
-#include "dq_parse.h"
+// The interpreter itself (types, three-valued logic, Spark 2.2's casts) is dq_predeval.h, shared
+// with the host build the CPU tests check against the oracle.
+#include "dq_predeval.h"
 
 namespace dq {
-
-namespace {
-
-enum ValType : uint8_t { VT_INT = 0, VT_FLT = 1, VT_BOOL = 2, VT_STR = 3 };
-
-struct Val {
-  int64_t i;      // int / bool value; string length for VT_STR
-  double f;
-  uint8_t type;
-  uint8_t null;
-  const uint8_t* s;  // VT_STR bytes
-};
-
-// UTF8String.compareTo: unsigned byte-wise, then shorter first.
-__device__ inline int ord_str(const Val& a, const Val& b) {
-  const int64_t n = a.i < b.i ? a.i : b.i;
-  for (int64_t k = 0; k < n; ++k) {
-    const int d = (int)a.s[k] - (int)b.s[k];
-    if (d) return d < 0 ? -1 : 1;
-  }
-  return (int)(a.i > b.i) - (int)(a.i < b.i);
-}
-
-__device__ inline bool col_valid(const DevColumn& c, int64_t row) {
-  return c.validity == nullptr || ((c.validity[row >> 3] >> (row & 7)) & 1u);
-}
-
-__device__ inline Val load_col(const DevColumn& c, int64_t row) {
-  Val v;
-  v.null = col_valid(c, row) ? 0 : 1;
-  v.i = 0;
-  v.f = 0.0;
-  v.type = VT_INT;
-  v.s = nullptr;
-  switch (c.type) {
-    case DQ_T_UTF8: {
-      const int32_t b = c.offsets[row], e = c.offsets[row + 1];
-      v.s = static_cast<const uint8_t*>(c.values) + b;
-      v.i = e - b;
-      v.type = VT_STR;
-      break;
-    }
-    case DQ_T_BOOL: {
-      const uint8_t* b = static_cast<const uint8_t*>(c.values);
-      v.i = (b[row >> 3] >> (row & 7)) & 1u;
-      v.type = VT_BOOL;
-      break;
-    }
-    case DQ_T_INT8: v.i = static_cast<const int8_t*>(c.values)[row]; break;
-    case DQ_T_INT16: v.i = static_cast<const int16_t*>(c.values)[row]; break;
-    case DQ_T_INT32: v.i = static_cast<const int32_t*>(c.values)[row]; break;
-    case DQ_T_INT64: v.i = static_cast<const int64_t*>(c.values)[row]; break;
-    case DQ_T_FLOAT32: v.f = static_cast<const float*>(c.values)[row]; v.type = VT_FLT; break;
-    case DQ_T_FLOAT64: v.f = static_cast<const double*>(c.values)[row]; v.type = VT_FLT; break;
-    default: v.null = 1; break;
-  }
-  return v;
-}
-
-__device__ inline double as_f64(const Val& v) { return v.type == VT_FLT ? v.f : (double)v.i; }
-
-__device__ inline int ord_f64(double a, double b) {
-  const bool an = a != a, bn = b != b;
-  if (an | bn) return (int)an - (int)bn;
-  return (int)(a > b) - (int)(a < b);
-}
-
-__device__ inline bool cmp_result(int opcode, int ord) {
-  switch (opcode) {
-    case DQ_P_EQ: return ord == 0;
-    case DQ_P_NE: return ord != 0;
-    case DQ_P_LT: return ord < 0;
-    case DQ_P_LE: return ord <= 0;
-    case DQ_P_GT: return ord > 0;
-    case DQ_P_GE: return ord >= 0;
-    default: return ord == 0;
-  }
-}
-
-// CAST: the program may cast a string to double (Double.parseDouble, whose exact slow path
-// carries ~1 KB of private scratch per lane); programs without one run a kernel without it.
-template <bool CAST>
-__device__ void eval_program(const PredInsn* code, int n, const uint8_t* pool, const DevColumn* cols, int64_t row,
-                             bool& t, bool& nn) {
-  Val st[kMaxStack];
-  int sp = 0;
-  for (int pc = 0; pc < n; ++pc) {
-    const PredInsn ins = code[pc];
-    switch (ins.opcode) {
-      case DQ_P_COLUMN: st[sp++] = load_col(cols[ins.arg], row); break;
-      case DQ_P_LIT_INT: st[sp++] = Val{ins.i64, 0.0, VT_INT, 0}; break;
-      case DQ_P_LIT_FLOAT: st[sp++] = Val{0, ins.f64, VT_FLT, 0}; break;
-      case DQ_P_LIT_NULL: st[sp++] = Val{0, 0.0, VT_INT, 1}; break;
-      case DQ_P_LIT_STRING: st[sp++] = Val{(int64_t)ins.arg, 0.0, VT_STR, 0, pool + ins.i64}; break;
-      case DQ_P_CAST_DOUBLE: {  // Spark 2.2 Cast(-> DoubleType): parseDouble of a string
-        Val& a = st[sp - 1];
-        if (CAST && a.type == VT_STR) {
-          double v = 0.0;
-          int r = 0;
-          if constexpr (CAST) r = a.null ? 0 : parse_double(PtrSrc{a.s}, (int32_t)a.i, &v);
-          a.null = (r == 1) ? a.null : 1;
-          a.f = v;
-        } else {
-          a.f = as_f64(a);
-        }
-        a.type = VT_FLT;
-        break;
-      }
-      case DQ_P_TRUE: st[sp++] = Val{1, 0.0, VT_BOOL, 0}; break;
-      case DQ_P_FALSE: st[sp++] = Val{0, 0.0, VT_BOOL, 0}; break;
-      case DQ_P_COALESCE: {
-        Val b = st[--sp];
-        Val a = st[sp - 1];
-        Val r = a.null ? b : a;
-        if ((a.type == VT_FLT) != (b.type == VT_FLT)) {  // common type is fp64
-          r.f = as_f64(r);
-          r.type = VT_FLT;
-        }
-        st[sp - 1] = r;
-        break;
-      }
-      case DQ_P_EQ: case DQ_P_NE: case DQ_P_LT: case DQ_P_LE: case DQ_P_GT: case DQ_P_GE:
-      case DQ_P_EQ_NULLSAFE: {
-        Val b = st[--sp];
-        Val a = st[sp - 1];
-        Val r{0, 0.0, VT_BOOL, 0};
-        if (a.null || b.null) {
-          if (ins.opcode == DQ_P_EQ_NULLSAFE) r.i = (a.null && b.null) ? 1 : 0;
-          else r.null = 1;
-        } else {
-          int ord;
-          if (a.type == VT_STR) ord = ord_str(a, b);
-          else if (ins.arg == DQ_CMP_AS_FLOAT64) ord = ord_f64(as_f64(a), as_f64(b));
-          else ord = (int)(a.i > b.i) - (int)(a.i < b.i);
-          r.i = cmp_result(ins.opcode, ord) ? 1 : 0;
-        }
-        st[sp - 1] = r;
-        break;
-      }
-      case DQ_P_IS_NULL: st[sp - 1] = Val{st[sp - 1].null ? 1 : 0, 0.0, VT_BOOL, 0}; break;
-      case DQ_P_IS_NOT_NULL: st[sp - 1] = Val{st[sp - 1].null ? 0 : 1, 0.0, VT_BOOL, 0}; break;
-      case DQ_P_NOT: {
-        Val a = st[sp - 1];
-        if (!a.null) a.i = a.i ? 0 : 1;
-        st[sp - 1] = a;
-        break;
-      }
-      case DQ_P_AND: case DQ_P_OR: {
-        Val b = st[--sp];
-        Val a = st[sp - 1];
-        Val r{0, 0.0, VT_BOOL, 0};
-        const bool at = !a.null && a.i, af = !a.null && !a.i;
-        const bool bt = !b.null && b.i, bf = !b.null && !b.i;
-        if (ins.opcode == DQ_P_AND) {
-          if (af || bf) r.i = 0;
-          else if (a.null || b.null) r.null = 1;
-          else r.i = 1;
-        } else {
-          if (at || bt) r.i = 1;
-          else if (a.null || b.null) r.null = 1;
-          else r.i = 0;
-        }
-        st[sp - 1] = r;
-        break;
-      }
-      default: break;
-    }
-  }
-  const Val top = st[sp - 1];
-  nn = !top.null;
-  t = nn && top.i != 0;
-}
-
-}  // namespace
 
 template <bool CAST>
 __global__ __launch_bounds__(kBlock) void dq_pred_kernel(const PredProgram* __restrict__ progs,
@@ -202,7 +30,7 @@ __global__ __launch_bounds__(kBlock) void dq_pred_kernel(const PredProgram* __re
        w += (int64_t)gridDim.x * (kBlock / 64)) {
     const int64_t row = (w << 6) + lane;
     bool t = false, nn = false;
-    if (row < n_rows) eval_program<CAST>(code, prog.n, pool, cols, row, t, nn);
+    if (row < n_rows) pred::eval_program<CAST>(code, prog.n, pool, cols, row, t, nn);
     const uint64_t bt = __ballot(t);
     const uint64_t bn = __ballot(nn);
     if (lane == 0) {

@@ -167,7 +167,16 @@ class FrequencyTable:
         if len(offsets) != n + 1:
             raise ValueError("offsets must hold one more value than counts")
         if hasattr(counts, "data_ptr"):
-            c, o, b = counts.contiguous(), offsets.contiguous(), blob.contiguous()
+            import torch
+            for name, t in (("counts", counts), ("offsets", offsets), ("blob", blob)):
+                if not hasattr(t, "data_ptr") or not t.is_cuda or t.device != self.torch_device:
+                    raise ValueError("import_flat: %s must be a tensor on %s (got %s)"
+                                     % (name, self.torch_device, getattr(t, "device", type(t).__name__)))
+            # the library reads int64 counts / offsets and uint8 bytes (Arrow string offsets are
+            # often int32): convert rather than let it misread the buffers
+            c = counts.to(torch.int64).contiguous()
+            o = offsets.to(torch.int64).contiguous()
+            b = blob.to(torch.uint8).contiguous()
             L.check(L.lib().dq_freq_import_flat(self.handle, c.data_ptr(), o.data_ptr(), b.data_ptr() if b.numel() else None,
                                                 n, int(num_rows), L.DQ_FLAT_DEVICE))
             return

@@ -9,10 +9,19 @@ Spark 2.2.2's literal typing and coercion:
 * `3` is an integer literal, `3.5` a DECIMAL literal, `3.5e2` / `3.5D` a DOUBLE literal;
 * long vs decimal compares exactly (DecimalPrecision); here that is rewritten into an exact
   int64 comparison (x > 3.5  ==>  x >= 4;  x = 3.5  ==>  false-or-NULL);
-* anything vs double / float column compares in fp64 with Spark's NaN-safe ordering.
+* anything vs double / float column compares in fp64 with Spark's NaN-safe ordering;
+* float vs int / long compares in FloatType: the integral side is rounded to float (a literal on
+  the host, a column per row through DQ_P_CAST to FLOAT32);
+* `CAST(x AS type)` to TINYINT/SMALLINT/INT/BIGINT, FLOAT, DOUBLE or BOOLEAN becomes DQ_P_CAST
+  (the library evaluates Spark 2.2's Cast semantics: narrowing wraps, fractional -> integral is
+  Java's saturating d2i / d2l); CAST(string AS DOUBLE) is DQ_P_CAST_DOUBLE.
 
-Strings, arithmetic, functions and UDFs raise UnsupportedPredicate: the reference's JNI
-shim would leave such an analyzer on Spark (SURVEY §8(b) "Eligibility").
+Column names resolve case-insensitively, as Spark 2.2 does by default
+(`spark.sql.caseSensitive=false`); two columns equal but for case make a reference ambiguous.
+
+Arithmetic, functions other than COALESCE / CAST, other casts of strings and UDFs raise
+UnsupportedPredicate: the reference's JNI shim would leave such an analyzer on Spark
+(SURVEY §8(b) "Eligibility").
 """
 from __future__ import annotations
 
@@ -21,14 +30,17 @@ from decimal import Decimal, InvalidOperation
 from fractions import Fraction
 from typing import Dict, List, Tuple
 
-import numpy as np
-
 from . import _lib as L
 
 Insn = Tuple[int, int, int, float]  # (opcode, arg, i64, f64)
 
 _INTEGRAL = {"int8", "int16", "int32", "int64"}
 _FRACTIONAL = {"float32", "float64"}
+
+# Spark 2.2 SQL type names (SqlBase.g4 primitive types) -> dq_type names the IR casts to
+_CAST_TYPES = {"TINYINT": "int8", "BYTE": "int8", "SMALLINT": "int16", "SHORT": "int16",
+               "INT": "int32", "INTEGER": "int32", "BIGINT": "int64", "LONG": "int64",
+               "FLOAT": "float32", "REAL": "float32", "DOUBLE": "float64", "BOOLEAN": "bool"}
 
 
 class UnsupportedPredicate(ValueError):
@@ -95,7 +107,7 @@ def _tokenize(text: str):
             toks.append(("ID", text[i:j]))
             i = j
             continue
-        for op in ("<=>", "<=", ">=", "!=", "<>", "==", "<", ">", "=", "(", ")", ",", "-", "+"):
+        for op in ("<=>", "<=", ">=", "!=", "<>", "==", "<", ">", "=", "(", ")", ",", "-", "+", "*", "/", "%"):
             if text.startswith(op, i):
                 toks.append(("OP", op))
                 i += len(op)
@@ -190,10 +202,17 @@ class _Parser:
         return ("truth", left)
 
     def value(self):
+        node = self._operand()
+        t = self.peek()
+        if t[0] == "OP" and t[1] in ("+", "-", "*", "/", "%"):
+            raise UnsupportedPredicate("arithmetic (%s) is not GPU-eligible in %r" % (t[1], self.text))
+        return node
+
+    def _operand(self):
         t = self.take()
         kind, text = t
         if kind == "OP" and text in ("-", "+"):
-            inner = self.value()
+            inner = self._operand()
             if inner[0] != "lit" or inner[1] not in ("int", "dec", "dbl"):
                 raise UnsupportedPredicate("unary %s on a non-literal in %r" % (text, self.text))
             if text == "-":
@@ -221,6 +240,21 @@ class _Parser:
                 return ("lit", "bool", up == "TRUE")
             if up == "NULL":
                 return ("lit", "null", None)
+            if self.peek() == ("OP", "(") and up == "CAST":
+                self.take()
+                inner = self.value()
+                if not self.keyword("AS"):
+                    raise PredicateSyntaxError("expected AS in CAST of %r" % self.text)
+                t2 = self.take()
+                if t2[0] != "ID":
+                    raise PredicateSyntaxError("expected a type name in CAST of %r" % self.text)
+                if self.peek() == ("OP", "("):  # DECIMAL(p, s), VARCHAR(n), ...
+                    raise UnsupportedPredicate("CAST to %s(...) is not GPU-eligible" % t2[1])
+                target = _CAST_TYPES.get(t2[1].upper())
+                if target is None:
+                    raise UnsupportedPredicate("CAST to %s is not GPU-eligible" % t2[1])
+                self.expect_op(")")
+                return ("cast", inner, target)
             if self.peek() == ("OP", "("):
                 if up != "COALESCE":
                     raise UnsupportedPredicate("function %s() is not GPU-eligible" % text)
@@ -242,21 +276,38 @@ class _Compiler:
         self.code: List[Insn] = []
         self.pool = bytearray()  # DQ_P_LIT_STRING bytes
 
+    def column(self, name: str) -> Tuple[int, str]:
+        return self.schema[resolve_column(name, self.schema)]
+
+    def stype(self, node) -> str:
+        """Spark type class of a value: int / f32 / f64 / dec / str / bool / null."""
+        t = node[0]
+        if t == "col":
+            dtype = self.column(node[1])[1]
+            return ("int" if dtype in _INTEGRAL else "f32" if dtype == "float32" else
+                    "f64" if dtype == "float64" else "bool" if dtype == "bool" else "str")
+        if t == "cast":
+            return {"float32": "f32", "float64": "f64", "bool": "bool"}.get(node[2], "int")
+        if t == "coalesce":
+            kinds = {self.stype(a) for a in node[1]} - {"null"}
+            if "str" in kinds:
+                return "str"
+            if "f64" in kinds or ("f32" in kinds and "dec" in kinds):
+                return "f64"
+            for k in ("f32", "dec", "int", "bool"):
+                if k in kinds:
+                    return k
+            return "null"
+        if t == "lit":
+            return {"dbl": "f64"}.get(node[1], node[1])
+        return "bool"
+
     def vtype(self, node) -> str:
         t = node[0]
         if t == "lit":
             return node[1]
-        if t == "col":
-            if node[1] not in self.schema:
-                raise KeyError(node[1])
-            dtype = self.schema[node[1]][1]
-            if dtype in _INTEGRAL:
-                return "int"
-            if dtype in _FRACTIONAL:
-                return "dbl"
-            if dtype == "bool":
-                return "bool"
-            return "str"
+        if t in ("col", "cast"):
+            return {"f32": "dbl", "f64": "dbl"}.get(self.stype(node), self.stype(node))
         if t == "coalesce":
             kinds = [self.vtype(a) for a in node[1]]
             kinds = [k for k in kinds if k != "null"] or ["null"]
@@ -269,31 +320,60 @@ class _Compiler:
         return "bool"
 
     def _has_f32(self, node) -> bool:
-        """A FloatType column, directly or inside a COALESCE."""
-        if node[0] == "col":
-            return node[1] in self.schema and self.schema[node[1]][1] == "float32"
-        if node[0] == "coalesce":
-            return any(self._has_f32(x) for x in node[1])
-        return False
+        """A FloatType value: a FLOAT column, a CAST to FLOAT, or a COALESCE typed FloatType."""
+        return self.stype(node) == "f32"
 
     def emit(self, opcode, arg=0, i64=0, f64=0.0):
         self.code.append((opcode, arg, int(i64), float(f64)))
 
     def emit_value(self, node, target: str):
+        """Push `node`; target is the comparison's type class (int / dbl / str, or f32: Spark
+        coerces an integral operand to FloatType, so it is rounded to float first)."""
         t = node[0]
         if t == "col":
-            idx, dtype = self.schema[node[1]]
+            idx, dtype = self.column(node[1])
             if dtype == "string" and target != "str":
                 raise UnsupportedPredicate("string column %s in a numeric context" % node[1])
             self.emit(L.DQ_P_COLUMN, idx)
+            if target == "f32" and dtype in _INTEGRAL | {"bool"}:
+                self.emit(L.DQ_P_CAST, L.TYPE_CODES["float32"])
+        elif t == "cast":
+            inner, to = node[1], node[2]
+            ik = self.stype(inner)
+            if ik == "str":
+                if to != "float64":
+                    raise UnsupportedPredicate("CAST of a string to %s stays on Spark" % to)
+                self.emit_value(inner, "str")
+                self.emit(L.DQ_P_CAST_DOUBLE)
+            elif ik == "dec":  # a decimal literal: Decimal.toDouble is correctly rounded
+                if inner[0] != "lit" or to == "float32":
+                    raise UnsupportedPredicate("CAST of a decimal-typed expression to %s" % to)
+                v = inner[2]
+                if to == "float64":
+                    self.emit(L.DQ_P_LIT_FLOAT, f64=float(v))
+                else:  # Decimal.toLong truncates toward zero (the low 64 bits); != 0 for boolean
+                    w = (1 if v != 0 else 0) if to == "bool" else (math.trunc(v) + 2 ** 63) % 2 ** 64 - 2 ** 63
+                    self.emit(L.DQ_P_LIT_INT, i64=w)
+                    self.emit(L.DQ_P_CAST, L.TYPE_CODES[to])
+            elif ik == "null":
+                self.emit(L.DQ_P_LIT_NULL)
+            else:
+                self.emit_value(inner, "dbl" if ik in ("f32", "f64") else "int")
+                self.emit(L.DQ_P_CAST, L.TYPE_CODES[to])
+            if target == "f32" and to in _INTEGRAL | {"bool"}:
+                self.emit(L.DQ_P_CAST, L.TYPE_CODES["float32"])
         elif t == "lit":
             kind, v = node[1], node[2]
             if kind == "null":
                 self.emit(L.DQ_P_LIT_NULL)
             elif kind == "bool":
                 self.emit(L.DQ_P_LIT_INT, i64=1 if v else 0)
+                if target == "f32":
+                    self.emit(L.DQ_P_CAST, L.TYPE_CODES["float32"])
             elif kind == "int":
-                if target == "dbl":
+                if target == "f32":
+                    self.emit(L.DQ_P_LIT_FLOAT, f64=int_to_float32(v))
+                elif target == "dbl":
                     self.emit(L.DQ_P_LIT_FLOAT, f64=float(v))
                 else:
                     self.emit(L.DQ_P_LIT_INT, i64=v)
@@ -314,6 +394,8 @@ class _Compiler:
                 raise UnsupportedPredicate("string literal in a numeric context")
         elif t == "coalesce":
             args = node[1]
+            if target == "dbl" and self.stype(node) == "f32":  # COALESCE typed FloatType
+                target = "f32"
             self.emit_value(args[0], target)
             for a in args[1:]:
                 self.emit_value(a, target)
@@ -359,17 +441,10 @@ class _Compiler:
             return
         if "int" in (ta, tb) and (self._has_f32(a) or self._has_f32(b)):
             # Spark 2.2 coerces float vs int / long to FloatType: the integral side is rounded to
-            # float first.  Exact here for a literal (rounded once on the host, then compared in
-            # fp64, which orders float values the same); an integral column would need a rounding
-            # per row, which the IR does not have.
-            f32_side, int_side = (a, b) if self._has_f32(a) else (b, a)
-            if f32_side[0] != "col" or int_side[0] != "lit":
-                raise UnsupportedPredicate("float column compared with an integral expression (FloatType)")
-            for node in (a, b):
-                if node is int_side:
-                    self.emit(L.DQ_P_LIT_FLOAT, f64=float(np.float32(int_side[2])))
-                else:
-                    self.emit_value(node, "dbl")
+            # float first (a literal once on the host, anything else per row by DQ_P_CAST), then
+            # compared in fp64, which orders float values as FloatType does
+            self.emit_value(a, "f32")
+            self.emit_value(b, "f32")
             self.emit(self._OPS[op], L.DQ_CMP_AS_FLOAT64)
             return
         if "dbl" in (ta, tb):
@@ -428,7 +503,7 @@ class _Compiler:
             self.emit(L.DQ_P_NOT)
         elif t in ("isnull", "isnotnull"):
             vt = self.vtype(node[1])
-            if node[1][0] in ("col", "lit", "coalesce"):
+            if node[1][0] in ("col", "lit", "coalesce", "cast"):
                 self.emit_value(node[1], vt if vt in ("dbl", "str") else "int")
             else:
                 self.emit_bool(node[1])
@@ -449,7 +524,9 @@ class _Compiler:
             if v[0] == "lit" and v[1] == "bool":
                 self.emit(L.DQ_P_TRUE if v[2] else L.DQ_P_FALSE)
             elif v[0] == "col" and self.vtype(v) == "bool":
-                self.emit(L.DQ_P_COLUMN, self.schema[v[1]][0])
+                self.emit(L.DQ_P_COLUMN, self.column(v[1])[0])
+            elif v[0] == "cast" and v[2] == "bool":
+                self.emit_value(v, "int")
             elif v[0] in ("or", "and", "not", "cmp", "in", "isnull", "isnotnull", "truth"):
                 self.emit_bool(v)
             else:
@@ -460,6 +537,35 @@ class _Compiler:
 
 def parse(text: str):
     return _Parser(text).parse()
+
+
+def int_to_float32(v: int) -> float:
+    """Java l2f / i2f: the integer rounded to the nearest float (ties to even), exactly."""
+    if v == 0:
+        return 0.0
+    a = abs(v)
+    sh = a.bit_length() - 24
+    if sh > 0:
+        q, rem = divmod(a, 1 << sh)
+        half = 1 << (sh - 1)
+        if rem > half or (rem == half and q & 1):
+            q += 1
+        a = q << sh
+    return float(a if v > 0 else -a)
+
+
+def resolve_column(name: str, schema) -> str:
+    """Spark 2.2 resolves column references case-insensitively by default: the schema's own
+    name for `name`.  KeyError when none matches (AnalysisException), ValueError when two
+    columns match (an ambiguous reference)."""
+    if name in schema and sum(1 for k in schema if k.lower() == name.lower()) == 1:
+        return name
+    hits = [k for k in schema if k.lower() == name.lower()]
+    if not hits:
+        raise KeyError(name)
+    if len(hits) > 1:
+        raise ValueError("Reference '%s' is ambiguous, could be: %s" % (name, ", ".join(sorted(hits))))
+    return hits[0]
 
 
 def referenced_columns(text: str) -> List[str]:

@@ -224,11 +224,9 @@ class ColumnProfiler:
                 # the threshold is below that: its histogram scan runs beside pass 1, used if so
                 started["bool"] = pool.submit(gated, _bool_histograms, data, bools) if bools else None
             try:
-                try:
-                    few = _few_group_strings(data, strings, before_launch=start_others)
-                finally:
-                    if "fut" not in started:
-                        start_others()
+                few = _few_group_strings(data, strings, before_launch=start_others)
+                if "fut" not in started:
+                    start_others()
                 fut, fut_bool = started["fut"], started["bool"]
                 rest = [c for c in strings if c not in few]
                 # the string pass is the head of the critical path (its types -> the casts -> their
@@ -255,7 +253,12 @@ class ColumnProfiler:
                 if fut_hist is not None:
                     few_hist = fut_hist.result()
             finally:
-                pool.shutdown(wait=True)
+                # every exit path opens the gate: a pass-1 plan already submitted (start_others
+                # runs before the few-groups launch) waits on it, and an error raised before the
+                # string pass must surface instead of leaving that thread -- and this shutdown --
+                # blocked forever
+                gate.set()
+                pool.shutdown(wait=True, cancel_futures=True)
         generic = _extract_generic_statistics(relevant, schema, ctx1, predefined)
 
         if printStatusUpdates:

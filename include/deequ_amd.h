@@ -98,6 +98,17 @@ typedef enum dq_op_kind {
  * boolean instructions pop/push three-valued booleans.  Numeric comparisons compare in the type
  * given by `arg` (DQ_CMP_AS_INT64 / DQ_CMP_AS_FLOAT64), converting operands first; two strings
  * compare byte-wise (unsigned, then by length), as Spark's UTF8String.compareTo.
+ *
+ * Type rules the library enforces (anything it cannot evaluate exactly as Spark would is
+ * DQ_ERR_UNSUPPORTED, so the caller routes the analyzer to Spark; a malformed program -- stack
+ * underflow, a column out of range -- is DQ_ERR_INVALID):
+ *   - DQ_CMP_AS_INT64 with a floating-point operand;
+ *   - a FloatType value (a FLOAT32 column or DQ_P_CAST to FLOAT32) compared or COALESCEd with an
+ *     integral operand: Spark coerces that pair to FloatType, so the integral side must carry an
+ *     explicit DQ_P_CAST to FLOAT32 (an integral literal may instead be rounded to float by the
+ *     encoder and pushed with DQ_P_LIT_FLOAT);
+ *   - a string compared with a non-string (only DQ_P_CAST_DOUBLE converts strings);
+ *   - DQ_P_CAST of a string.
  */
 typedef enum dq_pred_opcode {
   DQ_P_COLUMN = 1,     /* push value of batch column `arg`                                  */
@@ -111,6 +122,15 @@ typedef enum dq_pred_opcode {
                            through java.lang.Double.parseDouble of its trimmed text, NULL when
                            unparsable; correctly rounded for every input (decimal of any
                            length and exponent, hexadecimal, NaN / Infinity, f/d suffix).   */
+  DQ_P_CAST = 8,       /* pop value; push Cast(value -> `arg`), `arg` a dq_type: INT8..INT64,
+                           FLOAT32, FLOAT64 or BOOL, of a numeric or boolean value (Spark 2.2.2
+                           Cast, non-ANSI: integral narrowing keeps the low bits; fractional ->
+                           int/long is Java d2i/d2l, NaN -> 0, saturating; -> short/byte is d2i
+                           then the low bits; integral -> float rounds the integer itself (l2f);
+                           -> boolean is value != 0; boolean -> numeric 1/0).  The analyzer's
+                           Cast nodes (`cast(l as int) > 3`, the FloatType side of `f = 16777217`)
+                           map 1:1 onto it.  A cast of a string other than DQ_P_CAST_DOUBLE is
+                           DQ_ERR_UNSUPPORTED (route the analyzer to Spark).                     */
   DQ_P_EQ = 10, DQ_P_NE = 11, DQ_P_LT = 12, DQ_P_LE = 13, DQ_P_GT = 14, DQ_P_GE = 15,
   DQ_P_EQ_NULLSAFE = 16, /* <=>                                                             */
   DQ_P_IS_NULL = 20,   /* pop value; push boolean (never NULL)                              */
@@ -366,7 +386,9 @@ dq_status dq_profile_string_groups(dq_ctx* ctx, const int64_t* counts, const int
  *   - its groups are group_counts / group_keys (16 bytes each, zero padded) / group_lens
  *     [i * DQ_FEW_MAX_GROUPS, + results[i].n_groups), non-NULL strings only (NULLs are
  *     results[i].n_nulls).
- * A column that does not fit has ok = 0 and nothing else set. */
+ * A column that does not fit has ok = 0 and nothing else set.  Columns are grouped 32 at a time
+ * (bounded scratch); a chunk whose device scratch cannot be allocated leaves its columns at ok = 0
+ * (the caller's per-row pass handles them) instead of failing the call. */
 #define DQ_FEW_MAX_GROUPS 1024
 typedef struct dq_few_result {
   int32_t ok;

@@ -43,6 +43,13 @@ dq_status dq_diag_freq_test_flags(dq_freq* f, int32_t flags);
  * Spark).  Lets CPU tests check it against a reference parser on millions of strings. */
 dq_status dq_diag_parse_double(const uint8_t* s, int64_t n, double* out, int32_t* ok);
 
+/* Host build of the predicate interpreter (the source dq_pred_kernel runs on the device,
+ * deequ_amd/csrc/dq_predeval.h): validates `p` against the columns' types as plan creation does
+ * (same status codes), then evaluates it over `n_rows` rows of HOST columns (offset 0):
+ * out[r] = 0 FALSE, 1 TRUE, 2 NULL.  CPU tests check it against the oracle's SQL evaluator. */
+dq_status dq_diag_eval_predicate(const dq_predicate* p, const dq_column* columns, int n_columns, int64_t n_rows,
+                                 uint8_t* out);
+
 /* Host build of the group-by's record packing of digit-string keys (<= 15 ASCII digits, or
  * Histogram's "NullValue"; deequ_amd/csrc/dq_keypack.h): *ok = 1, *packed = the 8-byte record
  * word and back[0 .. *back_len) = the key bytes it unpacks to; *ok = 0 for any other key. */

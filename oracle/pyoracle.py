@@ -629,6 +629,85 @@ def java_parse_double(s: str) -> Optional[float]:
     return None
 
 
+_SQL_TYPES = {"TINYINT": "int8", "BYTE": "int8", "SMALLINT": "int16", "SHORT": "int16", "INT": "int32",
+              "INTEGER": "int32", "BIGINT": "int64", "LONG": "int64", "FLOAT": "float32", "REAL": "float32",
+              "DOUBLE": "float64", "BOOLEAN": "bool"}
+_INT_BITS = {"int8": 8, "int16": 16, "int32": 32, "int64": 64}
+
+
+def _wrap_bits(v: int, bits: int) -> int:
+    """Scala .toByte / .toShort / .toInt / .toLong of an integral value: the low bits, signed."""
+    v &= (1 << bits) - 1
+    return v - (1 << bits) if v >= (1 << (bits - 1)) else v
+
+
+def _java_f2int(x: float, bits: int) -> int:
+    """Java d2i (bits 32) / d2l (bits 64): NaN -> 0, saturating, truncation toward zero."""
+    if x != x:
+        return 0
+    lo, hi = -(1 << (bits - 1)), (1 << (bits - 1)) - 1
+    if x >= hi:
+        return hi
+    if x <= lo:
+        return lo
+    return int(x)
+
+
+def int_to_f32(v: int) -> float:
+    """Java i2f / l2f: the exact integer rounded to the nearest float, ties to even."""
+    if v == 0:
+        return 0.0
+    a = abs(v)
+    sh = a.bit_length() - 24
+    if sh > 0:
+        q, rem = divmod(a, 1 << sh)
+        if rem > (1 << (sh - 1)) or (rem == (1 << (sh - 1)) and q & 1):
+            q += 1
+        a = q << sh
+    return float(a if v > 0 else -a)
+
+
+def spark_cast(v, src: str, to: str):
+    """Spark 2.2.2 Cast (non-ANSI) of one value of kind `src` (int / float / double / decimal /
+    bool / string) to `to` (a dq type name): Cast.castToByte/Short/Int/Long (integral values keep
+    their low bits; fractional ones go through Java d2i -- then the low bits for byte/short -- or
+    d2l), castToFloat (l2f rounds the integer itself; a double rounds to nearest), castToDouble,
+    castToBoolean (value != 0).  NULL stays NULL."""
+    if v is None:
+        return None
+    if src == "bool":
+        v = 1 if v else 0
+        src = "int"
+    if to in _INT_BITS:
+        if src in ("float", "double"):
+            x = _java_f2int(float(v), 64 if to == "int64" else 32)
+            return _wrap_bits(x, _INT_BITS[to])
+        if src == "decimal":  # Decimal.toLong (truncation), then the low bits
+            from fractions import Fraction
+            return _wrap_bits(math.trunc(Fraction(v)), _INT_BITS[to])
+        if src == "int":
+            return _wrap_bits(int(v), _INT_BITS[to])
+        raise ValueError("cast of %s to %s is outside the restated subset" % (src, to))
+    if to == "float32":
+        if src == "int":
+            return int_to_f32(int(v))
+        if src in ("float", "double"):
+            import warnings
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore")
+                return float(np.float32(float(v)))
+        raise ValueError("cast of %s to float is outside the restated subset" % src)
+    if to == "float64":
+        if src == "string":
+            return java_parse_double(v)
+        return float(v)
+    if to == "bool":
+        if src == "string":
+            raise ValueError("cast of a string to boolean is outside the restated subset")
+        return float(v) != 0.0 if src in ("float", "double") else v != 0
+    raise ValueError(to)
+
+
 def eval_predicate(text: str, table: OTable) -> List[Optional[bool]]:
     """Evaluate a deequ SQL predicate string (the numeric subset deequ's checks emit:
     comparisons, IN, BETWEEN, IS [NOT] NULL, COALESCE, AND/OR/NOT, string equality)
@@ -654,6 +733,13 @@ def eval_predicate(text: str, table: OTable) -> List[Optional[bool]]:
                 v += tk.next()[1]
             return ("lit", "string", v)
         if t[0] == "id":
+            if t[1].upper() == "CAST" and tk.peek() == ("op", "("):
+                tk.next()
+                inner = operand()
+                assert tk.kw("AS"), "CAST without AS in %r" % text
+                tname = tk.next()[1].upper()
+                assert tk.next() == ("op", ")")
+                return ("cast", inner, _SQL_TYPES[tname])
             if t[1].upper() == "COALESCE":
                 assert tk.next() == ("op", "(")
                 args = [operand()]
@@ -744,6 +830,11 @@ def eval_predicate(text: str, table: OTable) -> List[Optional[bool]]:
             return kind, lambda r, c=col: c.values[r]
         if node[0] == "paren":
             return typed(node[1])
+        if node[0] == "cast":
+            k, g = typed(node[1])
+            to = node[2]
+            kind = {"float32": "float", "float64": "double", "bool": "bool"}.get(to, "int")
+            return kind, lambda r: spark_cast(g(r), k, to)
         if node[0] == "neg":
             k, g = typed(node[1])
             return k, lambda r: None if g(r) is None else -g(r)
@@ -778,9 +869,10 @@ def eval_predicate(text: str, table: OTable) -> List[Optional[bool]]:
             return None
         if dst == "double":
             return float(v)
-        if dst == "float":
-            import numpy as _np
-            return float(_np.float32(v))
+        if dst == "float":  # Java i2f / l2f round the integer itself (no double rounding)
+            if isinstance(v, int) and not isinstance(v, bool):
+                return int_to_f32(v)
+            return float(np.float32(v))
         if dst == "decimal":
             from fractions import Fraction
             return Fraction(v) if not isinstance(v, float) else Fraction(v)

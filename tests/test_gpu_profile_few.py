@@ -171,3 +171,53 @@ def test_profiles_equal_with_and_without(gpu, monkeypatch):
     for c in cols:
         a, b = on.profiles[c], off.profiles[c]
         assert a == b, c
+
+
+def test_wide_table_chunks(gpu):
+    """More string columns than one library chunk (32): every column comes back, each chunk's
+    columns with the per-row pass's states (bounded scratch per call)."""
+    rng = np.random.default_rng(17)
+    n = 20_000
+    cols = {"c%02d" % k: _column(rng, n, _VALUES[:3 + k % 10]) for k in range(70)}
+    cols["c05"] = ["k%d" % i for i in range(n)]  # one that does not fit, in the first chunk
+    table = _table(cols)
+    got = _batched_few(table, list(cols))
+    for c, vals in cols.items():
+        ok, groups, nulls, comp, hll, dt = got[c]
+        if c == "c05":
+            assert ok == 0
+            continue
+        assert ok == 1, c
+        assert sum(groups.values()) + nulls == n
+        assert hll.words == d.ApproxCountDistinct(c).computeStateFrom(table).words, c
+
+
+def test_profiler_raises_when_few_groups_fail(gpu, monkeypatch):
+    """An error in the few-groups step (after the other pass-1 plan was submitted, gated) is
+    raised by the profiler, not turned into a hang."""
+    import threading
+    import deequ_amd.profiles as P
+
+    def boom(data, columns, before_launch=None):
+        if before_launch is not None:
+            before_launch()
+        raise RuntimeError("injected few-groups failure")
+    monkeypatch.setattr(P, "_few_group_strings", boom)
+    rng = np.random.default_rng(3)
+    n = 10_000
+    table = d.Table({"s": d.Column.from_pylist(_column(rng, n, _VALUES), "string"),
+                     "i": d.Column.from_numpy(rng.integers(0, 9, n))}).to_device(0)
+    done = threading.Event()
+    result = {}
+
+    def run():
+        try:
+            ColumnProfilerRunner().onData(table).run()
+        except BaseException as e:  # noqa: BLE001
+            result["e"] = e
+        finally:
+            done.set()
+    th = threading.Thread(target=run, daemon=True)
+    th.start()
+    assert done.wait(60), "the profiler hung after a few-groups failure"
+    assert isinstance(result.get("e"), RuntimeError) and "injected" in str(result["e"])
