@@ -982,6 +982,7 @@ struct AggTrack {
   unsigned long long big_cap;
   uint32_t* smax;             // per slice
   int write_all;
+  FreqCompact cmp;            // cmp.slots != nullptr: write the occupied slots only (packed aggregation)
 };
 
 __device__ inline void track_count(AggLds& L, const AggTrack& tr, uint32_t c) {
@@ -2307,12 +2308,39 @@ __global__ __launch_bounds__(kAggRegionThreads) __attribute__((amdgpu_waves_per_
 struct AggLdsP {
   unsigned long long K[kFreqSliceSlots];
   uint32_t C[kFreqSliceSlots];
+  uint16_t map[kFreqSliceSlots];  // compact write-out: the slot of the slice's i-th group
+  uint32_t wsum[4];
   int overflow;
   uint32_t fresh;
   uint32_t cmax;
   unsigned long long retry_base;
+  unsigned long long cbase;
   uint32_t hist[kAggLdsHist];
 };
+
+// Exclusive prefix of v over a workgroup of NT threads (NT / 64 <= 4 waves); *total = the sum.
+// Every thread must call it (it holds a barrier).
+template <int NT>
+__device__ inline uint32_t block_prefix(uint32_t v, uint32_t* wsum, uint32_t* total) {
+  static_assert(NT % 64 == 0 && NT / 64 <= 4, "block_prefix: up to four waves");
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63u) wsum[wave] = x;
+  lds_barrier();
+  uint32_t before = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) {
+    before += (uint32_t)w < wave ? wsum[w] : 0u;
+    tot += wsum[w];
+  }
+  *total = tot;
+  return before + x - v;
+}
 
 // Count packed record p from LDS slot s on (probe `first` of its run); false if the image is full.
 __device__ inline bool lds_count_packed(unsigned long long* K, uint32_t* C, uint64_t p, uint32_t s, uint32_t first = 0) {
@@ -2349,6 +2377,7 @@ __global__ __launch_bounds__(kAggPThreads) __attribute__((amdgpu_waves_per_eu(DQ
   constexpr int NT = kAggPThreads;
   __shared__ AggLdsP L;
   const bool track = tr.hist != nullptr;
+  const bool compact = tr.cmp.slots != nullptr;  // (an empty table only)
   if (track) {
     for (int i = threadIdx.x; i < kAggLdsHist; i += NT) L.hist[i] = 0u;
     lds_barrier();
@@ -2366,8 +2395,11 @@ __global__ __launch_bounds__(kAggPThreads) __attribute__((amdgpu_waves_per_eu(DQ
       if (i < r1) touch = *reinterpret_cast<const uint32_t*>(recs + i);
     }
     if (r1 == r0) {
-      if (tr.write_all)
+      if (compact) {
+        if (threadIdx.x == 0) tr.cmp.num[b] = 0u;
+      } else if (tr.write_all) {
         for (uint32_t s = threadIdx.x; s < S; s += NT) slice[s] = FreqSlot{0ull, 0ull, 0ull, 0ull};
+      }
       if (tr.smax && threadIdx.x == 0) tr.smax[b] = 0u;
       asm volatile("" ::"v"(touch));
       continue;
@@ -2425,9 +2457,68 @@ __global__ __launch_bounds__(kAggPThreads) __attribute__((amdgpu_waves_per_eu(DQ
       if (threadIdx.x == 0) L.retry_base = atomicAdd(n_retry, (unsigned long long)(r1 - r0));
       lds_barrier();
       for (uint64_t i = r0 + threadIdx.x; i < r1; i += NT) retry[L.retry_base + (i - r0)] = rec_raw(recs[i]);
-      if (tr.write_all)  // (the table was not cleared: the slice starts out empty)
+      if (compact) {
+        if (threadIdx.x == 0) tr.cmp.num[b] = 0u;  // (the slice starts out empty)
+      } else if (tr.write_all) {  // (the table was not cleared: the slice starts out empty)
         for (uint32_t q = threadIdx.x; q < 2 * S; q += NT) halves[q] = ulonglong2{0ull, 0ull};
+      }
       if (tr.smax && threadIdx.x == 0) tr.smax[b] = 0xFFFFFFFFu;  // unknown: never skipped
+    } else if (compact) {
+      // Only the occupied slots are written (C4: ~0.37 of the slice), in slot order, at a place
+      // reserved with one atomic per slice; the slice's occupancy bitmap (256 B) lets
+      // dq_freq_expand_kernel rebuild the slot image exactly when a probing operation needs it.
+      static_assert(S == 8u * NT, "eight slots per thread");
+      const uint32_t t = threadIdx.x;
+      const uint4 c0 = *reinterpret_cast<const uint4*>(&L.C[8u * t]);
+      const uint4 c1 = *reinterpret_cast<const uint4*>(&L.C[8u * t + 4u]);
+      const uint32_t cs[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      uint32_t occ = 0u;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (!cs[j]) continue;
+        occ |= 1u << j;
+        if (track || tr.smax) {
+          atomicMax(&L.cmax, cs[j]);
+          if (track) {
+            if (cs[j] < (uint32_t)kAggLdsHist) atomicAdd(&L.hist[cs[j]], 1u);
+            else if (cs[j] < (uint32_t)kFreqHist) atomicAdd(&tr.hist[cs[j]], 1ull);
+            else {
+              const unsigned long long i = atomicAdd(tr.n_big, 1ull);
+              if (i < tr.big_cap) tr.big[i] = cs[j];
+            }
+          }
+        }
+      }
+      uint32_t tot;
+      uint32_t k = block_prefix<NT>((uint32_t)__builtin_popcount(occ), L.wsum, &tot);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (occ & (1u << j)) L.map[k++] = (uint16_t)(8u * t + (uint32_t)j);
+      tr.cmp.bits[(b << 8) + t] = (uint8_t)occ;
+      if (t == 0) {
+        const unsigned long long at = atomicAdd(tr.cmp.cursor, (unsigned long long)tot);
+        L.cbase = at;
+        tr.cmp.base[b] = at;
+        tr.cmp.num[b] = tot;
+        if (tot) atomicAdd(new_groups, (unsigned long long)tot);
+      }
+      lds_barrier();
+      ulonglong2* out = reinterpret_cast<ulonglong2*>(tr.cmp.slots + L.cbase);
+      for (uint32_t q = t; q < 2u * tot; q += NT) {
+        const uint32_t s = L.map[q >> 1];
+        const uint64_t p = L.K[s];
+        if (!(q & 1u)) {
+          const uint32_t len = p == kPackNull ? 9u : (uint32_t)(p >> 60);
+          out[q] = ulonglong2{((unsigned long long)tag_of(hash_record_packed(p)) << 32) | kReady | len,
+                              (unsigned long long)L.C[s]};
+        } else {
+          uint64_t k0, k1;
+          uint32_t len;
+          kp_unpack(p, &k0, &k1, &len);
+          out[q] = ulonglong2{k0, k1};
+        }
+      }
+      if (tr.smax && t == 0) tr.smax[b] = L.cmax;
     } else {
       for (uint32_t q = threadIdx.x; q < 2 * S; q += NT) {
         const uint32_t s = q >> 1;
@@ -2483,6 +2574,62 @@ __global__ __launch_bounds__(kAggPThreads) __attribute__((amdgpu_waves_per_eu(DQ
     lds_barrier();
     for (int i = threadIdx.x; i < kAggLdsHist; i += NT)
       if (L.hist[i]) atomicAdd(&tr.hist[i], (unsigned long long)L.hist[i]);
+  }
+}
+
+// The slot image of a compacted table (AggTrack::cmp) rebuilt in T: slice b's groups, stored in
+// slot order from cmp.base[b], go back to the slots its occupancy bitmap names; every other slot
+// is written empty (T is not cleared first).  One workgroup per slice, whole 1 KiB stores.
+__global__ __launch_bounds__(kAggPThreads) void dq_freq_expand_kernel(FreqTable T, FreqCompact cmp, uint64_t n_slices) {
+  constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
+  constexpr int NT = kAggPThreads;
+  __shared__ uint16_t pos[kFreqSliceSlots];  // slot -> its group's index in the slice, 0xFFFF empty
+  __shared__ uint32_t wsum[4];
+  static_assert(S == 8u * NT, "eight slots per thread");
+  const uint32_t t = threadIdx.x;
+  for (uint64_t b = blockIdx.x; b < n_slices; b += gridDim.x) {
+    ulonglong2* halves = reinterpret_cast<ulonglong2*>(T.slots + (b << kFreqSliceLog));
+    const uint32_t n = cmp.num[b];
+    if (n == 0u) {
+      for (uint32_t q = t; q < 2u * S; q += NT) halves[q] = ulonglong2{0ull, 0ull};
+      continue;
+    }
+    const uint32_t occ = cmp.bits[(b << 8) + t];
+    uint32_t tot;
+    uint32_t k = block_prefix<NT>((uint32_t)__builtin_popcount(occ), wsum, &tot);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pos[8u * t + (uint32_t)j] = (occ & (1u << j)) ? (uint16_t)(k++) : (uint16_t)0xFFFFu;
+    lds_barrier();
+    const ulonglong2* src = reinterpret_cast<const ulonglong2*>(cmp.slots + cmp.base[b]);
+    for (uint32_t q = t; q < 2u * S; q += NT) {
+      const uint32_t g = pos[q >> 1];
+      halves[q] = g == 0xFFFFu ? ulonglong2{0ull, 0ull} : src[2u * g + (q & 1u)];
+    }
+    lds_barrier();  // (pos and wsum are rewritten by the next slice)
+  }
+}
+
+// dq_freq_export_slices_kernel over a compacted table: slice b's groups are the cmp.num[b]
+// records from cmp.base[b]; slices whose largest count (smax) is below min_count are skipped.
+__global__ __launch_bounds__(kBlock) void dq_freq_export_compact_kernel(FreqCompact cmp, uint64_t n_slices,
+                                                                        unsigned long long min_count,
+                                                                        const uint32_t* __restrict__ smax, FreqOut out) {
+  for (uint64_t b = blockIdx.x; b < n_slices; b += gridDim.x) {
+    if (smax && (unsigned long long)smax[b] < min_count) continue;
+    const FreqSlot* g = cmp.slots + cmp.base[b];
+    const uint32_t n = cmp.num[b];
+    for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
+      const FreqSlot e = g[i];
+      if (e.count >= min_count) {
+        const unsigned long long j = atomicAdd(out.n, 1ull);
+        if (j < out.cap) {
+          out.ctrl[j] = e.ctrl;
+          out.count[j] = e.count;
+          out.k0[j] = e.k0;
+          out.k1[j] = e.k1;
+        }
+      }
+    }
   }
 }
 
@@ -2791,11 +2938,13 @@ hipError_t launch_freq_agg_region(const FreqTable& T, const void* d_recs, bool p
                                   uint64_t cap, uint64_t n_slices, int table_empty, FreqRec* d_retry,
                                   unsigned long long* d_n_retry, unsigned long long* d_new_groups,
                                   unsigned long long* d_hist, unsigned long long* d_big, unsigned long long* d_n_big,
-                                  unsigned long long big_cap, uint32_t* d_smax, int write_all, hipStream_t stream) {
+                                  unsigned long long big_cap, uint32_t* d_smax, int write_all, hipStream_t stream,
+                                  const FreqCompact* compact) {
   uint64_t blocks = n_slices < 65536 ? n_slices : 65536;
   if (blocks < 1) blocks = 1;
   if (!table_empty && (d_hist || d_smax || write_all)) return hipErrorInvalidValue;
-  AggTrack tr{d_hist, d_big, d_n_big, big_cap, d_smax, write_all};
+  if (compact && (!packed || !table_empty)) return hipErrorInvalidValue;
+  AggTrack tr{d_hist, d_big, d_n_big, big_cap, d_smax, write_all, compact ? *compact : FreqCompact{}};
   if (packed)
     hipLaunchKernelGGL(dq_freq_agg_packed_kernel, dim3((unsigned)blocks), dim3(kAggPThreads), 0, stream, T,
                        static_cast<const uint64_t*>(d_recs), d_fill, cap, n_slices, table_empty, d_retry, d_n_retry,
@@ -2804,6 +2953,23 @@ hipError_t launch_freq_agg_region(const FreqTable& T, const void* d_recs, bool p
     hipLaunchKernelGGL(dq_freq_agg_region_kernel, dim3((unsigned)blocks), dim3(kAggRegionThreads), 0, stream, T,
                        static_cast<const FreqRec*>(d_recs), d_fill, cap, n_slices, table_empty, d_retry, d_n_retry,
                        d_new_groups, tr);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_expand(const FreqTable& T, const FreqCompact& cmp, hipStream_t stream) {
+  const uint64_t n_slices = (T.mask + 1) >> kFreqSliceLog;
+  uint64_t blocks = n_slices < 65536 ? n_slices : 65536;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(dq_freq_expand_kernel, dim3((unsigned)blocks), dim3(kAggPThreads), 0, stream, T, cmp, n_slices);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_export_compact(const FreqCompact& cmp, uint64_t n_slices, unsigned long long min_count,
+                                      const FreqOut& out, const uint32_t* d_smax, hipStream_t stream) {
+  uint64_t blocks = n_slices < 16384 ? n_slices : 16384;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(dq_freq_export_compact_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, cmp, n_slices,
+                     min_count, d_smax, out);
   return hipGetLastError();
 }
 

@@ -191,6 +191,18 @@ struct FreqTable {
 constexpr unsigned int kFreqWaitTimeout = 8u;
 constexpr int32_t kFreqTestNoPublish = 1;  // dq_diag_freq_test_flags (tests only): claimed slots never turn READY
 
+// A compacted table (the packed aggregation into an empty table, round 6): the occupied slots
+// only, each slice's groups in slot order from base[b] (num[b] of them), and per slice a 2048-bit
+// occupancy bitmap (bits + 256 b: bit j of byte t = slot 8 t + j) from which dq_freq_expand
+// rebuilds the slot image when an operation needs to probe.
+struct FreqCompact {
+  FreqSlot* slots;
+  unsigned long long* base;
+  uint32_t* num;
+  uint8_t* bits;
+  unsigned long long* cursor;
+};
+
 struct FreqKeySpec {
   int32_t key_cols[kMaxKeyCols];
   int32_t n_keys;
@@ -368,7 +380,13 @@ hipError_t launch_freq_agg_region(const FreqTable& T, const void* d_recs, bool p
                                   uint64_t cap, uint64_t n_slices, int table_empty, FreqRec* d_retry,
                                   unsigned long long* d_n_retry, unsigned long long* d_new_groups,
                                   unsigned long long* d_hist, unsigned long long* d_big, unsigned long long* d_n_big,
-                                  unsigned long long big_cap, uint32_t* d_smax, int write_all, hipStream_t stream);
+                                  unsigned long long big_cap, uint32_t* d_smax, int write_all, hipStream_t stream,
+                                  const FreqCompact* compact = nullptr);
+// A compacted table's slot image rebuilt into T (every slot written), and its groups exported
+// (as launch_freq_export with slice maxima).
+hipError_t launch_freq_expand(const FreqTable& T, const FreqCompact& cmp, hipStream_t stream);
+hipError_t launch_freq_export_compact(const FreqCompact& cmp, uint64_t n_slices, unsigned long long min_count,
+                                      const FreqOut& out, const uint32_t* d_smax, hipStream_t stream);
 hipError_t launch_freq_rehash(const FreqSlot* d_old, uint64_t old_n, const FreqTable& T, hipStream_t stream);
 
 // ---------------------------------------------------------------- launchers (.hip files)

@@ -261,3 +261,37 @@ def test_packed_paths_equal_unpacked(gpu, part, monkeypatch, mode):
         assert res["1paths"]["packed_runs"] >= (2 if mode == "budget" else 1), res["1paths"]
     if mode == "load":
         assert res["1paths"]["sort_records"] > 0, res["1paths"]  # slices overflowed LDS
+
+
+def test_compacted_table_equals_slot_image(gpu, part, monkeypatch):
+    """Round 6: the packed aggregation into a fresh table writes only its occupied slots
+    (compacted); summary() and top() read that form, every other operation rebuilds the slot
+    image first (dq_freq_expand_kernel).  The same operations with DQ_FREQ_COMPACT=0: identical
+    summaries, top groups, exports, lookups, and results of further batches, imports and merges."""
+    rng = np.random.default_rng(31)
+    n = 1_200_000  # ~650k groups: 2^21 slots, level-2 split on, packed records
+    keys = ["%011d" % v if i % 53 else None for i, v in enumerate(rng.integers(0, 1_000_000, n))]
+    more = ["%011d" % v for v in rng.integers(500_000, 1_500_000, 300_000)]
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DQ_FREQ_COMPACT", mode)
+        out = {}
+        t = _consume_batches(keys, True, 3)
+        s = t.summary()
+        out["summary"] = (s.num_groups, s.num_unique, s.grouped_rows, s.num_rows, s.entropy)
+        out["top"] = t.top(9)[0].tolist(), sorted(t.top(9)[1])
+        out["export"] = _export(t)
+        out["lookup"] = [t.lookup(k.encode()) for k in keys[:50] if k is not None]
+        t.consume(d.Table.from_pydict({"key": ("string", more)}))
+        out["after_consume"] = _export(t)
+        src = _consume_batches(more[:100_000], True, 1)
+        t.merge_from(src)
+        src.close()
+        out["after_merge"] = _export(t)
+        out["paths"] = t.paths()["packed_runs"]
+        t.close()
+        res[mode] = out
+    for k in ("summary", "top", "export", "lookup", "after_consume", "after_merge"):
+        assert res["0"][k] == res["1"][k], k
+    assert res["1"]["export"] == _count(keys, True)
+    assert res["1"]["paths"] >= 1

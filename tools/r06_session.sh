@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round-6 GPU sessions.  PART=tests: a subset of the GPU tests (TESTS) in one pytest process;
+# PART=ab: same-box A/B of environment knobs (tools/r05_envab.sh; VARIANTS / WL / STEPS);
+# PART=c2pmc: the C2 scan kernels' issue / wait counters (one rocprofv3 --pmc pass per group).
+# Parts run in the order given (PARTS="tests ab"); any failure ends the script.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TAG=${TAG:-r06}
+for P in ${PARTS:-tests}; do
+  case $P in
+    tests)
+      timeout -k 10 ${LIMIT:-900} python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 600 --timeout-method thread \
+        > gpurun_out/${TAG}_tests.log 2>&1
+      st=$?
+      grep -E "passed|failed|error" gpurun_out/${TAG}_tests.log | tail -5
+      [ $st -ne 0 ] && { grep -E "FAILED|Error" gpurun_out/${TAG}_tests.log | head -20; exit $st; } ;;
+    ab)
+      bash tools/r05_envab.sh || exit $? ;;
+    c2pmc)
+      WL=c2 KERNEL=dq_scan_fast_kernel TAG=$TAG TL=240 \
+        PASSES="SQ_ACTIVE_INST_VALU,SQ_INSTS_VALU,SQ_WAIT_INST_ANY,SQ_BUSY_CYCLES,SQ_WAVE_CYCLES,SQ_ACTIVE_INST_ANY,SQ_WAIT_ANY,SQ_ACTIVE_INST_VALU2,GRBM_GUI_ACTIVE;SQ_THREAD_CYCLES_VALU,SQ_BUSY_CU_CYCLES,SQ_ACTIVE_INST_LDS,SQ_INSTS_LDS,SQ_INSTS_SALU,SQ_ACTIVE_INST_SCA,SQ_WAVES,SQ_INSTS_VMEM_RD,GRBM_GUI_ACTIVE" \
+        bash tools/pmc_kernel.sh || exit $? ;;
+  esac
+done
+echo "SESSION DONE"
