@@ -63,9 +63,13 @@ def parse_args():
     p.add_argument("--c4-rows", type=int, default=1_000_000_000, help="rows per GPU")
     p.add_argument("--c4-batch", type=int, default=125_000_000, help="rows per string batch")
     p.add_argument("--c4-distinct", type=int, default=201_500_000)
-    p.add_argument("--c4-keys", default="digits", choices=["digits", "alnum"],
-                   help="C4 key text: 12 decimal digits (packs into one word: 8-byte records) or 'k' + 11 "
-                        "digits (not a digit string: the 16-byte record path, after the packed staging gives up)")
+    p.add_argument("--c4-keys", default="digits", choices=["digits", "alnum", "uuid", "pair"],
+                   help="C4 key text: 12 decimal digits (packs into one word: 8-byte records), 'k' + 11 "
+                        "digits (not a digit string: the 16-byte record path, after the packed staging gives up), "
+                        "uuid (36-character UUID text of the same ids: the hashed record path, isPrimaryKey's "
+                        "shape) or pair (a two-column key (int64 id / 1000, 8-digit id % 1000): 20 encoded "
+                        "bytes, the hashed record path; Uniqueness / Distinctness / UniqueValueRatio / "
+                        "CountDistinct of the pair)")
     p.add_argument("--c4-verify", action="store_true",
                    help="after timing, check the C4 metrics against torch.unique over the integer ids on the "
                         "device (an independent sort-based group-by; 1 rank); adds `verify` to the line")
@@ -397,12 +401,18 @@ def c4_verify(args, metrics, dist_metric, analyzers):
            "uniqueness_ok": got[str(analyzers[0])] == unique / n,
            "distinctness_ok": got[str(analyzers[1])] == groups / n,
            "entropy_rel_err": abs(got[str(analyzers[2])] - ent) / ent}
+    if dist_metric is None:  # pair keys: the pair's metrics only (UniqueValueRatio in place of Entropy)
+        del out["entropy_rel_err"]
+        out["unique_value_ratio_ok"] = got[str(analyzers[2])] == unique / groups
+        out["ok"] = all(out[k] for k in out if k.endswith("_ok"))
+        return out
     uh, ch = u.cpu().numpy(), c.cpu().numpy()
     vals = {k: v.absolute for k, v in dist_metric.values.items()}
     nonnull = {k: a for k, a in vals.items() if k != "NullValue"}
     # (alnum keys: 'k' + the id's last 11 digits -- the first digit of a 12-digit id below 1e11 is
     # always 0, so the map is one to one)
-    idx = np.array([int(k[1:]) if args.c4_keys == "alnum" else int(k) for k in nonnull], dtype=np.int64)
+    idx = np.array([int(k[1:]) if args.c4_keys == "alnum" else uuid_to_id(k) if args.c4_keys == "uuid" else int(k)
+                    for k in nonnull], dtype=np.int64)
     cnt = np.array(list(nonnull.values()), dtype=np.int64)
     pos = np.clip(np.searchsorted(uh, idx), 0, len(uh) - 1)
     out["detail_bins"] = len(nonnull)
@@ -414,33 +424,77 @@ def c4_verify(args, metrics, dist_metric, analyzers):
     return out
 
 
-def make_c4_batches(rows: int, batch: int, distinct: int, rank: int, device: int, alnum: bool = False):
+# UUID text of an id (--c4-keys uuid): the 32 hex digits of x = id * A + B and y = (id ^ C) * D
+# (mod 2^64), as 8-4-4-4-12.  x is a bijection of the id, so the keys group exactly as the ids.
+_UUID_A, _UUID_B = 0x9E3779B97F4A7C15, 0x632BE59BD9B4E019
+_UUID_C, _UUID_D = 0x5DEECE66D, 0xC2B2AE3D27D4EB4F
+
+
+def _s64(v: int) -> int:
+    v %= 2 ** 64
+    return v - 2 ** 64 if v >= 2 ** 63 else v
+
+
+def _uuid_chars(ids, dev):
+    """(n, 36) uint8 UUID text of int64 ids (torch int64 arithmetic wraps mod 2^64)."""
+    import torch
+    x = ids * _s64(_UUID_A) + _s64(_UUID_B)
+    y = (ids ^ _UUID_C) * _s64(_UUID_D)
+    sh = torch.arange(60, -4, -4, dtype=torch.int64, device=dev)
+    nib = torch.cat([(x[:, None] >> sh[None, :]) & 15, (y[:, None] >> sh[None, :]) & 15], dim=1)
+    hexd = torch.where(nib < 10, nib + 48, nib + 87).to(torch.uint8)  # 0-9, a-f
+    dash = torch.full((ids.numel(), 1), ord("-"), dtype=torch.uint8, device=dev)
+    return torch.cat([hexd[:, :8], dash, hexd[:, 8:12], dash, hexd[:, 12:16], dash, hexd[:, 16:20], dash,
+                      hexd[:, 20:32]], dim=1)
+
+
+def uuid_to_id(key: str) -> int:
+    """The id behind a --c4-keys uuid key (inverting x = id * A + B mod 2^64)."""
+    x = int(key.replace("-", "")[:16], 16)
+    return ((x - _UUID_B) * pow(_UUID_A, -1, 2 ** 64)) % 2 ** 64
+
+
+def make_c4_batches(rows: int, batch: int, distinct: int, rank: int, device: int, keys_kind: str = "digits"):
     """C4: a string key = 12-digit zero-padded decimal of a uniform int in [0, distinct), 1% NULL,
     as Arrow utf8 batches of `batch` rows (int32 offsets cap one batch at 2 GiB of chars).
-    alnum: the first digit replaced by 'k' (same groups, keys that are not digit strings)."""
+    alnum: the first digit replaced by 'k' (same groups, keys that are not digit strings); uuid:
+    the id's 36-character UUID text; pair: two columns a = id // 1000 (int64, NULL where the key is)
+    and b = the 8 digits of id % 1000 (utf8).  The ids are the same draws in every case."""
     import torch
     import deequ_amd as d
     dev = torch.device("cuda", device)
     gen = torch.Generator(device=dev)
     gen.manual_seed(7 + 1000 * rank)
     pow10 = torch.tensor([10 ** (11 - i) for i in range(12)], dtype=torch.int64, device=dev)
+    width = {"uuid": 36, "pair": 8}.get(keys_kind, 12)
     parts = []
     for b0 in range(0, rows, batch):
         m = min(batch, rows - b0)
-        chars = torch.empty(m * 12 + 16, dtype=torch.uint8, device=dev)
+        chars = torch.empty(m * width + 16, dtype=torch.uint8, device=dev)
         valid = torch.empty((m + 7) // 8 + 64, dtype=torch.uint8, device=dev)
+        avals = torch.empty(m, dtype=torch.int64, device=dev) if keys_kind == "pair" else None
         sub = 1 << 24
         for s in range(0, m, sub):
             e = min(m, s + sub)
             keys = torch.randint(0, distinct, (e - s,), generator=gen, device=dev, dtype=torch.int64)
-            digits = (keys[:, None] // pow10[None, :]) % 10 + 48
-            if alnum:
-                digits[:, 0] = ord("k")
-            chars[s * 12: e * 12] = digits.to(torch.uint8).reshape(-1)
+            if keys_kind == "uuid":
+                chars[s * width: e * width] = _uuid_chars(keys, dev).reshape(-1)
+            elif keys_kind == "pair":
+                avals[s:e] = keys // 1000
+                chars[s * width: e * width] = _strings_from_ints(keys % 1000, 8, b"", dev)
+            else:
+                digits = (keys[:, None] // pow10[None, :]) % 10 + 48
+                if keys_kind == "alnum":
+                    digits[:, 0] = ord("k")
+                chars[s * 12: e * 12] = digits.to(torch.uint8).reshape(-1)
             packed = _valid_bits(e - s, gen, dev, 0.01)
             valid[s // 8: s // 8 + packed.numel()] = packed
-        offsets = torch.arange(0, 12 * (m + 1), 12, dtype=torch.int32, device=dev)
-        parts.append(d.Table({"key": d.Column("string", m, chars, valid, offsets=offsets, device=True)}))
+        offsets = torch.arange(0, width * (m + 1), width, dtype=torch.int32, device=dev)
+        if keys_kind == "pair":
+            parts.append(d.Table({"a": d.Column("int64", m, avals, valid, device=True),
+                                  "b": d.Column("string", m, chars, None, offsets=offsets, device=True)}))
+        else:
+            parts.append(d.Table({"key": d.Column("string", m, chars, valid, offsets=offsets, device=True)}))
     torch.cuda.synchronize(dev)
     return d.PartitionedTable(parts)
 
@@ -644,21 +698,26 @@ def run_c4(args, world, rank, local):
     GPUs every rank groups its own shard and the tables meet in the key-hash all-to-all."""
     import deequ_amd as d
     from deequ_amd.distributed import ShardedTable
-    shard = make_c4_batches(args.c4_rows, args.c4_batch, args.c4_distinct, rank, local, args.c4_keys == "alnum")
+    shard = make_c4_batches(args.c4_rows, args.c4_batch, args.c4_distinct, rank, local, args.c4_keys)
     data = ShardedTable(shard) if world > 1 else shard
-    analyzers = [d.Uniqueness(["key"]), d.Distinctness(["key"]), d.Entropy("key"),
-                 d.CountDistinct(["key"]), d.Histogram("key")]
+    pair = args.c4_keys == "pair"
+    if pair:  # a composite key: the pair's frequency analyzers (Check.hasUniqueness / isPrimaryKey shape)
+        cols = ["a", "b"]
+        analyzers = [d.Uniqueness(cols), d.Distinctness(cols), d.UniqueValueRatio(cols), d.CountDistinct(cols)]
+    else:
+        analyzers = [d.Uniqueness(["key"]), d.Distinctness(["key"]), d.Entropy("key"),
+                     d.CountDistinct(["key"]), d.Histogram("key")]
 
     def step(ev=None):
         return d.AnalysisRunner.onData(data).addAnalyzers(analyzers).run()
     elapsed, _, ctx = _timed(args, world, step)
     metrics = {str(a): ctx.metric(a).value.get() for a in analyzers[:4]}
-    hist = ctx.metric(analyzers[4]).value.get()
+    hist = None if pair else ctx.metric(analyzers[4]).value.get()
     verify = None
     if args.c4_verify and world == 1:
         del ctx
         verify = c4_verify(args, {a: metrics[str(a)] for a in analyzers[:4]}, hist, analyzers)
-    in_bytes = sum(_column_bytes(b.columns["key"]) for b in shard.batches())
+    in_bytes = sum(_column_bytes(c) for b in shard.batches() for c in b.columns.values())
     groups = metrics[str(analyzers[3])] / world  # the groups this rank's share of the table holds
     # SURVEY §8(d) C4: input + one write of the final table (8 B hash + 8 B count + 8 B key ref)
     algo = in_bytes + 24.0 * groups
@@ -669,13 +728,17 @@ def run_c4(args, world, rank, local):
         "unit": "rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": step_s * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "utf8 keys, int64 counts",
-        "data": "synthetic %s keys uniform in [0, %d), 1%% NULL, generated in HBM"
-                % ("12-digit" if args.c4_keys == "digits" else "'k' + 11-digit", args.c4_distinct),
-        "config": {"workload": "C4: %d rows/GPU in %d-row utf8 batches; Uniqueness, Distinctness, Entropy, "
-                               "CountDistinct + Histogram, all from one GPU group-by of the key (the "
-                               "reference runs Histogram as a second job)%s"
+        "data": "synthetic %s keys of ids uniform in [0, %d), 1%% NULL, generated in HBM"
+                % ({"digits": "12-digit", "alnum": "'k' + 11-digit", "uuid": "36-character UUID",
+                    "pair": "(int64, 8-digit utf8) pair"}[args.c4_keys], args.c4_distinct),
+        "config": {"workload": ("C4: %d rows/GPU in %d-row batches; Uniqueness, Distinctness, UniqueValueRatio, "
+                                "CountDistinct of the two-column key (a, b), one GPU group-by%s" if pair else
+                                "C4: %d rows/GPU in %d-row utf8 batches; Uniqueness, Distinctness, Entropy, "
+                                "CountDistinct + Histogram, all from one GPU group-by of the key (the "
+                                "reference runs Histogram as a second job)%s")
                                % (args.c4_rows, args.c4_batch,
-                                  "; key-hash all-to-all over %d ranks" % world if world > 1 else "")},
+                                  "; key-hash all-to-all over %d ranks" % world if world > 1 else ""),
+                   "keys": args.c4_keys},
         "roofline": _step_roofline(algo, step_s, "one whole group-by step per GPU (stage + level-1 partition, "
                                                  "level-2 partition, slice aggregation, top-N), HBM-bound by design",
                                    workload="c4" if world == 1 else None,
@@ -686,9 +749,8 @@ def run_c4(args, world, rank, local):
         # read + write, aggregation read) -- 8 B for these digit-string keys (packed words), 16 B
         # for other keys -- and touches the HBM table only in whole-slice writes: no per-row table
         # probe (the probes are in LDS).
-        "table_access": {"record_passes_per_row": 3, "record_bytes": 8, "global_table_probes_per_row": 0,
-                         "table_slots_written_per_row": _c4_table_slots(groups) / float(args.c4_rows)},
-        "check": dict(metrics, histogram_bins=hist.numberOfBins),
+        "table_access": _c4_table_access(args.c4_keys, groups, args.c4_rows),
+        "check": dict(metrics, **({} if pair else {"histogram_bins": hist.numberOfBins})),
         **({"verify": verify} if verify is not None else {}),
         **({"exchange": _exchange_stats(world, local)} if world > 1 else {}),
     }
@@ -711,6 +773,26 @@ def _exchange_stats(world: int, local: int):
     out.update({"max_" + k: v for k, v in zip(keys, t.cpu().tolist())})
     out["exchange_bytes"] = st.get("bytes_sent")
     return out
+
+
+def _c4_table_access(keys: str, groups: float, rows: int):
+    """SURVEY §8(d) C4 asks for the table accesses per row beside the streaming fraction.  A staged
+    row's record is written by the row-order stage, read and written by the level-1 split (into its
+    region), read and written by the level-2 split (into its slice region) and read by the slice
+    aggregation: 3 writes + 3 reads for packed and hashed records; 16-B records keep one fused
+    stage-and-split kernel, 2 writes + 2 reads.  Probes are in LDS; the table is written once,
+    occupied slots only (compacted) for packed and hashed records.  Hashed records (long /
+    composite keys) also copy each key's bytes into the key heap once, and re-read a record and two
+    keys per row that joins an existing hash group (the exact compare)."""
+    slot_bytes = 32.0
+    rec = {"digits": 8, "alnum": 16, "uuid": 16, "pair": 16}[keys]
+    passes = {"digits": (3, 3), "alnum": (2, 2), "uuid": (3, 3), "pair": (3, 3)}[keys]
+    compacted = keys != "alnum"
+    return {"record_bytes": rec, "record_writes_per_row": passes[0], "record_reads_per_row": passes[1],
+            "global_table_probes_per_row": 0,
+            "table_bytes_written_per_row": (groups if compacted else _c4_table_slots(groups)) * slot_bytes / float(rows),
+            "table_write": "occupied slots only" if compacted else "whole slot image",
+            "key_heap_copy": keys in ("uuid", "pair")}
 
 
 def _c4_table_slots(groups: float) -> float:

@@ -35,7 +35,6 @@ constexpr unsigned long long kHeapKey = 1ull << 30;
 constexpr unsigned long long kLenMask = (1ull << 24) - 1;
 constexpr int kLdsSlots = 1024;       // LDS pre-aggregation slots per workgroup
 constexpr int kLdsProbe = 8;          // linear probes in LDS before going global
-constexpr int kMaxLocalKey = 64;      // encoded multi-column keys are built in registers/scratch
 #ifndef DQ_INSERT_R
 #define DQ_INSERT_R 4
 #endif
@@ -346,7 +345,9 @@ __device__ bool heap_equal(const FreqTable& T, uint64_t off, const uint8_t* p, u
 // Insert `cnt` rows of key k into the global table.  Returns false on table/heap overflow.
 // kFlagOverflow = false: a full slice is reported only by the return value (the sorted path
 // hands such rows back for a retry after the table grows).
-template <bool kFlagOverflow = true>
+// kKeyInHeap: a long key's bytes already lie in T's heap at k.ptr (the hashed path's stage put
+// them there): a claimed slot refers to them instead of copying them again.
+template <bool kFlagOverflow = true, bool kKeyInHeap = false>
 __device__ bool global_insert(const FreqTable& T, const Key& k, unsigned long long cnt) {
   // Every action happens inside the loop iteration and the loop ends only through `state`: a
   // lane that waits for another lane of its own wave to publish a slot must see that publish in
@@ -368,6 +369,8 @@ __device__ bool global_insert(const FreqTable& T, const Key& k, unsigned long lo
       if (inl) {
         atomicExch(&e->k0, (unsigned long long)k.k0);
         atomicExch(&e->k1, (unsigned long long)k.k1);
+      } else if (kKeyInHeap) {
+        atomicExch(&e->k0, (unsigned long long)(k.ptr - T.heap));
       } else {
         const unsigned long long bytes = ((unsigned long long)k.len + 7ull) & ~7ull;
         const unsigned long long off = atomicAdd(T.heap_used, bytes);
@@ -1275,8 +1278,20 @@ __device__ inline uint64_t rec_hash(uint64_t p, bool* hole) {
   return hash_record_packed(p);
 }
 
-// A record in the 16-byte form (what the overflow and retry lists and the sort path hold).
+__device__ inline uint64_t rec_hash(const HashRec& r, bool* hole) {
+  *hole = r.ref == kHashHole;
+  return r.h;
+}
+
+// A record in the 16-byte form (what the overflow and retry lists and the sort path hold; a
+// hashed record keeps its bits: the hashed path's lists are read by dq_freq_insert_hashed_kernel).
 __device__ inline FreqRec rec_raw(const FreqRec& r) { return r; }
+__device__ inline FreqRec rec_raw(const HashRec& r) {
+  FreqRec f;
+  f.k0 = r.h;
+  f.k1 = r.ref;
+  return f;
+}
 __device__ inline FreqRec rec_raw(uint64_t p) {
   uint64_t k0, k1;
   uint32_t len;
@@ -2577,6 +2592,348 @@ __global__ __launch_bounds__(kAggPThreads) __attribute__((amdgpu_waves_per_eu(DQ
   }
 }
 
+// ---- Long and multi-column keys on the partition path (round 6).  The reference groups any key
+// in one hash aggregate (GroupingAnalyzers.scala:67-71): isUnique / isPrimaryKey / hasUniqueness
+// (Check.scala:140-230) on UUID-like ids or composite keys.  Such a key does not fit a 16-byte
+// record, so the stage copies its bytes into the table's key heap once and stages a HashRec
+// {table hash, heap reference}; the records travel the same two-level split as the other record
+// forms, and each slice is aggregated in LDS by hash (dq_freq_agg_hashed_kernel), with every
+// record of a hash group compared byte for byte against the group's first record, so the
+// grouping is exact: a slice holding two different keys of one 64-bit hash (about 0.03 such
+// pairs per 1e9 distinct keys) hands its records to the global inserts, which compare keys.
+
+// Exact heap bytes the hashed stage appends for rows [0, n_rows): sum of 8-aligned key lengths.
+__global__ __launch_bounds__(kBlock) void dq_freq_key_bytes_kernel(FreqKeySpec ks, const DevColumn* __restrict__ cols,
+                                                                   int64_t n_rows, unsigned long long* out) {
+  unsigned long long local = 0;
+  for (int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x; row < n_rows; row += (int64_t)gridDim.x * kBlock) {
+    uint32_t n = 0;
+    bool key = true;
+    for (int i = 0; i < ks.n_keys; ++i) {
+      const DevColumn& c = cols[ks.key_cols[i]];
+      const bool valid = col_valid(c, row);
+      if (!valid) {
+        if (ks.n_keys == 1 && ks.null_as_key) {
+          n = c.type == DQ_T_UTF8 ? 9u : 0u;  // "NullValue" / the empty key
+          continue;
+        }
+        key = false;
+        break;
+      }
+      if (c.type == DQ_T_UTF8) n += (uint32_t)(c.offsets[row + 1] - c.offsets[row]) + (ks.n_keys > 1 ? 4u : 0u);
+      else n += (uint32_t)width_of(c.type);
+    }
+    if (key) local += ((unsigned long long)n + 7ull) & ~7ull;
+  }
+  for (int d = 32; d >= 1; d >>= 1) local += __shfl_xor(local, d, 64);
+  if ((threadIdx.x & 63u) == 0 && local) atomicAdd(out, local);
+}
+
+__global__ __launch_bounds__(kBlock) void dq_freq_stage_hashed_kernel(FreqKeySpec ks, const DevColumn* __restrict__ cols,
+                                                                      int64_t n_rows, HashRec* __restrict__ out, FreqTable T,
+                                                                      uint32_t* hll, unsigned long long* too_long,
+                                                                      unsigned long long* staged,
+                                                                      unsigned long long* max_len) {
+  __shared__ uint32_t regs[kHllM];
+  for (uint32_t i = threadIdx.x; i < (uint32_t)kHllM; i += kBlock) regs[i] = 0xFFFFFFFFu;  // (stage_sketch)
+  __syncthreads();
+  alignas(8) uint8_t scratch[kMaxLocalKey];
+  const uint32_t lane = threadIdx.x & 63u;
+  unsigned long long n_keys = 0;
+  uint32_t longest = 0u;
+  bool tl_any = false;
+  // wave-uniform trip count: every lane takes part in each iteration's scan
+  for (int64_t base = (int64_t)blockIdx.x * kBlock; base < n_rows; base += (int64_t)gridDim.x * kBlock) {
+    const int64_t row = base + threadIdx.x;
+    Key k;
+    bool tl = false, ok = false;
+    if (row < n_rows) ok = make_key(ks, cols, row, k, scratch, tl);
+    tl_any |= tl;
+    const uint32_t a = ok ? ((k.len + 7u) & ~7u) : 0u;
+    uint32_t x = a;  // inclusive scan of the aligned lengths over the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d, 64);
+      if (lane >= (uint32_t)d) x += y;
+    }
+    unsigned long long wbase = 0ull;
+    if (lane == 63u && x) wbase = atomicAdd(T.heap_used, (unsigned long long)x);
+    wbase = __shfl(wbase, 63, 64);
+    const unsigned long long off = wbase + (x - a);
+    HashRec r;
+    r.h = 0ull;
+    r.ref = kHashHole;
+    if (ok) {
+      if (off + a > T.heap_cap) {
+        atomicOr(T.overflow, 2u);  // (the host sized the heap for the batch: never expected)
+      } else {
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(T.heap + off);
+        if (k.ptr == nullptr) {  // an inline key (<= 16 bytes) in k0 / k1, zero padded
+          if (k.len) dst[0] = k.k0;
+          if (k.len > 8) dst[1] = k.k1;
+        } else {
+          for (uint32_t i = 0; i < k.len; i += 8) dst[i >> 3] = ld_partial(k.ptr + i, k.len - i < 8 ? k.len - i : 8);
+        }
+        r.h = k.hash;
+        r.ref = (off << 24) | k.len;
+        stage_sketch(regs, k.hash);
+        ++n_keys;
+        longest = max(longest, k.len);
+      }
+    }
+    if (row < n_rows) out[row] = r;
+  }
+  for (int d = 32; d >= 1; d >>= 1) n_keys += __shfl_xor(n_keys, d, 64);
+  if (staged && lane == 0u && n_keys) atomicAdd(staged, n_keys);
+  if (max_len && longest) atomicMax(max_len, (unsigned long long)longest);
+  if (tl_any) atomicMax(too_long, (unsigned long long)kMaxLocalKey + 1ull);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < (uint32_t)kHllM; i += kBlock)
+    if (regs[i] != 0xFFFFFFFFu) atomicMax(&hll[i], stage_sketch_rank(regs[i]));
+}
+
+// The key of a hashed record, its bytes read from (and, when long, left in) T's heap.
+__device__ inline Key hashed_key(const FreqTable& T, const FreqRec& r) {
+  Key k;
+  k.len = (uint32_t)(r.k1 & kLenMask);
+  k.hash = r.k0;
+  const uint8_t* p = T.heap + (r.k1 >> 24);
+  k.k0 = k.k1 = 0ull;
+  k.ptr = nullptr;
+  if (k.len > 16) {
+    k.ptr = p;
+  } else {
+    const unsigned long long* w = reinterpret_cast<const unsigned long long*>(p);
+    if (k.len) k.k0 = w[0];
+    if (k.len > 8) k.k1 = w[1];
+  }
+  return k;
+}
+
+__global__ __launch_bounds__(kBlock) void dq_freq_insert_hashed_kernel(FreqTable T, const FreqRec* __restrict__ recs,
+                                                                       uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    const FreqRec r = recs[i];
+    if (r.k1 == kHashHole) continue;
+    if (!global_insert<true, true>(T, hashed_key(T, r), 1ull)) return;
+  }
+}
+
+// Two heap keys (8-byte aligned, zero padded) equal byte for byte.
+__device__ inline bool heap_refs_equal(const uint8_t* heap, unsigned long long ra, unsigned long long rb) {
+  if (ra == rb) return true;
+  if ((ra & kLenMask) != (rb & kLenMask)) return false;
+  const uint32_t words = (uint32_t)(((ra & kLenMask) + 7ull) >> 3);
+  const unsigned long long* a = reinterpret_cast<const unsigned long long*>(heap + (ra >> 24));
+  const unsigned long long* b = reinterpret_cast<const unsigned long long*>(heap + (rb >> 24));
+  for (uint32_t i = 0; i < words; ++i)
+    if (a[i] != b[i]) return false;
+  return true;
+}
+
+// The owner aggregation of slice regions of hashed records into a FRESH table.  LDS image: the
+// hash (0 kept as 1), the reference of the group's first record, the count.  A workgroup takes
+// a region's records 64 per thread at a time: they are counted by hash (one CAS per probe), then
+// -- after a barrier, when every group's first reference is in place -- each record that joined an
+// existing hash group is compared with that group's first record byte for byte.  A full image
+// or a mismatch (two keys of one hash) hands the slice's records to the retry list; the caller
+// inserts them globally.  Write-out as the packed aggregation: the slot image, or (tr.cmp) the
+// occupied slots only; keys of <= 16 bytes inline, longer ones referring to their heap bytes.
+constexpr int kAggHThreads = 256;
+struct AggLdsH {
+  unsigned long long K[kFreqSliceSlots];
+  unsigned long long R[kFreqSliceSlots];
+  uint32_t C[kFreqSliceSlots];
+  uint16_t map[kFreqSliceSlots];
+  uint32_t wsum[4];
+  int overflow;
+  uint32_t fresh;
+  uint32_t cmax;
+  unsigned long long retry_base;
+  unsigned long long cbase;
+  uint32_t hist[kAggLdsHist];
+};
+
+__device__ inline uint32_t lds_find_hash(const unsigned long long* K, unsigned long long kk, uint32_t s) {
+  constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
+  for (uint32_t probe = 0; probe < S; ++probe) {
+    if (K[s] == kk) return s;
+    s = (s + 1u) & (S - 1u);
+  }
+  return S;
+}
+
+__global__ __launch_bounds__(kAggHThreads) void dq_freq_agg_hashed_kernel(FreqTable T, const HashRec* __restrict__ recs,
+                                                                          const unsigned long long* __restrict__ fill,
+                                                                          uint64_t cap, uint64_t n_slices, FreqRec* retry,
+                                                                          unsigned long long* n_retry,
+                                                                          unsigned long long* new_groups, AggTrack tr) {
+  constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
+  constexpr int NT = kAggHThreads;
+  constexpr uint32_t kChunk = 64u * NT;  // records per round (a 64-bit mask of joins per thread)
+  __shared__ AggLdsH L;
+  const bool track = tr.hist != nullptr;
+  const bool compact = tr.cmp.slots != nullptr;
+  const uint32_t t = threadIdx.x;
+  if (track) {
+    for (int i = t; i < kAggLdsHist; i += NT) L.hist[i] = 0u;
+    lds_barrier();
+  }
+  for (uint64_t b = blockIdx.x; b < n_slices; b += gridDim.x) {
+    const uint64_t r0 = b * cap;
+    const unsigned long long f = fill[b];
+    const uint64_t r1 = r0 + (f < cap ? f : cap);
+    FreqSlot* slice = T.slots + (b << kFreqSliceLog);
+    ulonglong2* halves = reinterpret_cast<ulonglong2*>(slice);
+    if (r1 == r0) {
+      if (compact) {
+        if (t == 0) tr.cmp.num[b] = 0u;
+      } else if (tr.write_all) {
+        for (uint32_t q = t; q < 2u * S; q += NT) halves[q] = ulonglong2{0ull, 0ull};
+      }
+      if (tr.smax && t == 0) tr.smax[b] = 0u;
+      continue;
+    }
+    for (uint32_t s = t; s < S; s += NT) {
+      L.K[s] = 0ull;
+      L.C[s] = 0u;
+    }
+    if (t == 0) {
+      L.overflow = 0;
+      L.cmax = 0u;
+    }
+    lds_barrier();
+    for (uint64_t c0 = r0; c0 < r1; c0 += kChunk) {
+      const uint64_t c1 = c0 + kChunk < r1 ? c0 + kChunk : r1;
+      unsigned long long joined = 0ull;
+      for (uint32_t i = 0; i < 64u; i += 4u) {
+        HashRec rb[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint64_t idx = c0 + (uint64_t)(i + j) * NT + t;
+          rb[j].ref = kHashHole;
+          if (idx < c1) rb[j] = recs[idx];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (rb[j].ref == kHashHole) continue;
+          const unsigned long long kk = rb[j].h ? rb[j].h : 1ull;
+          uint32_t s = (uint32_t)rb[j].h & (S - 1u);
+          uint32_t probe = 0;
+          for (; probe < S; ++probe) {
+            const unsigned long long c = atomicCAS(&L.K[s], 0ull, kk);
+            if (c == 0ull) {
+              L.R[s] = rb[j].ref;
+              atomicAdd(&L.C[s], 1u);
+              break;
+            }
+            if (c == kk) {
+              atomicAdd(&L.C[s], 1u);
+              joined |= 1ull << (i + j);
+              break;
+            }
+            s = (s + 1u) & (S - 1u);
+          }
+          if (probe == S) L.overflow = 1;
+        }
+      }
+      lds_barrier();  // every group's first reference is in place
+      if (!L.overflow) {
+        while (joined) {
+          const uint32_t i = (uint32_t)__builtin_ctzll(joined);
+          joined &= joined - 1ull;
+          const HashRec r = recs[c0 + (uint64_t)i * NT + t];
+          const unsigned long long kk = r.h ? r.h : 1ull;
+          const uint32_t s = lds_find_hash(L.K, kk, (uint32_t)r.h & (S - 1u));
+          if (s == S || !heap_refs_equal(T.heap, L.R[s], r.ref)) L.overflow = 2;  // two keys, one hash
+        }
+      }
+      lds_barrier();
+    }
+    if (L.overflow) {  // hand the region's records back (inserted globally, keys compared)
+      if (t == 0) L.retry_base = atomicAdd(n_retry, (unsigned long long)(r1 - r0));
+      lds_barrier();
+      for (uint64_t i = r0 + t; i < r1; i += NT) retry[L.retry_base + (i - r0)] = rec_raw(recs[i]);
+      if (compact) {
+        if (t == 0) tr.cmp.num[b] = 0u;
+      } else if (tr.write_all) {
+        for (uint32_t q = t; q < 2u * S; q += NT) halves[q] = ulonglong2{0ull, 0ull};
+      }
+      if (tr.smax && t == 0) tr.smax[b] = 0xFFFFFFFFu;
+      lds_barrier();
+      continue;
+    }
+    // the group of slot s as its two 16-byte halves
+    auto half = [&](uint32_t s, bool hi) -> ulonglong2 {
+      const unsigned long long ref = L.R[s];
+      const uint32_t len = (uint32_t)(ref & kLenMask);
+      const unsigned long long off = ref >> 24;
+      if (!hi) {
+        const unsigned long long ctrl = ((unsigned long long)tag_of(L.K[s]) << 32) | kReady |  // (tag_of(1) == tag_of(0))
+                                        (len > 16u ? kHeapKey : 0ull) | len;
+        return ulonglong2{ctrl, (unsigned long long)L.C[s]};
+      }
+      if (len > 16u) return ulonglong2{off, 0ull};
+      const unsigned long long* w = reinterpret_cast<const unsigned long long*>(T.heap + off);
+      return ulonglong2{len ? w[0] : 0ull, len > 8u ? w[1] : 0ull};
+    };
+    static_assert(S == 8u * NT, "eight slots per thread");
+    const uint4 c0v = *reinterpret_cast<const uint4*>(&L.C[8u * t]);
+    const uint4 c1v = *reinterpret_cast<const uint4*>(&L.C[8u * t + 4u]);
+    const uint32_t cs[8] = {c0v.x, c0v.y, c0v.z, c0v.w, c1v.x, c1v.y, c1v.z, c1v.w};
+    uint32_t occ = 0u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (!cs[j]) continue;
+      occ |= 1u << j;
+      if (track || tr.smax) {
+        atomicMax(&L.cmax, cs[j]);
+        if (track) {
+          if (cs[j] < (uint32_t)kAggLdsHist) atomicAdd(&L.hist[cs[j]], 1u);
+          else if (cs[j] < (uint32_t)kFreqHist) atomicAdd(&tr.hist[cs[j]], 1ull);
+          else {
+            const unsigned long long i = atomicAdd(tr.n_big, 1ull);
+            if (i < tr.big_cap) tr.big[i] = cs[j];
+          }
+        }
+      }
+    }
+    uint32_t tot;
+    uint32_t k = block_prefix<NT>((uint32_t)__builtin_popcount(occ), L.wsum, &tot);
+    if (compact) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (occ & (1u << j)) L.map[k++] = (uint16_t)(8u * t + (uint32_t)j);
+      tr.cmp.bits[(b << 8) + t] = (uint8_t)occ;
+      if (t == 0) {
+        const unsigned long long at = atomicAdd(tr.cmp.cursor, (unsigned long long)tot);
+        L.cbase = at;
+        tr.cmp.base[b] = at;
+        tr.cmp.num[b] = tot;
+      }
+      lds_barrier();
+      ulonglong2* out = reinterpret_cast<ulonglong2*>(tr.cmp.slots + L.cbase);
+      for (uint32_t q = t; q < 2u * tot; q += NT) out[q] = half(L.map[q >> 1], (q & 1u) != 0u);
+    } else {
+      for (uint32_t q = t; q < 2u * S; q += NT) {
+        const uint32_t s = q >> 1;
+        if (L.C[s]) halves[q] = half(s, (q & 1u) != 0u);
+        else if (tr.write_all) halves[q] = ulonglong2{0ull, 0ull};
+      }
+    }
+    if (t == 0) {
+      if (tot) atomicAdd(new_groups, (unsigned long long)tot);
+      if (tr.smax) tr.smax[b] = L.cmax;
+    }
+    lds_barrier();  // LDS is reused by the next slice
+  }
+  if (track) {
+    lds_barrier();
+    for (int i = t; i < kAggLdsHist; i += NT)
+      if (L.hist[i]) atomicAdd(&tr.hist[i], (unsigned long long)L.hist[i]);
+  }
+}
+
 // The slot image of a compacted table (AggTrack::cmp) rebuilt in T: slice b's groups, stored in
 // slot order from cmp.base[b], go back to the slots its occupancy bitmap names; every other slot
 // is written empty (T is not cleared first).  One workgroup per slice, whole 1 KiB stores.
@@ -2734,9 +3091,10 @@ hipError_t launch_freq_agg(const FreqTable& T, const FreqRec* d_recs, const uint
 hipError_t launch_freq_part(const void* d_in, uint64_t in_n, const unsigned long long* d_in_fill, uint64_t in_cap,
                             uint64_t n_in_regions, int id_bits, int bin_bits, void* d_out, uint64_t out_cap,
                             unsigned long long* d_out_fill, FreqRec* d_ovf, unsigned long long* d_ovf_n,
-                            uint64_t ovf_cap, unsigned int* d_flag, bool packed, hipStream_t stream,
+                            uint64_t ovf_cap, unsigned int* d_flag, int rec_kind, hipStream_t stream,
                             unsigned long long* d_staged) {
   if (bin_bits < 0 || bin_bits > kPartMaxBinBits || id_bits < bin_bits || id_bits > 32) return hipErrorInvalidValue;
+  const bool packed = rec_kind == kRecPacked;
   const uint64_t tile = packed ? kPartTileP : kPartTile;  // (the kernel's records per workgroup)
   dim3 grid;
   if (d_in_fill) {
@@ -2754,6 +3112,10 @@ hipError_t launch_freq_part(const void* d_in, uint64_t in_n, const unsigned long
     hipLaunchKernelGGL((dq_freq_part_kernel<uint64_t, (1 << kPartMaxBinBits)>), grid, dim3(kPartThreads), 0, stream,
                        static_cast<const uint64_t*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
                        static_cast<uint64_t*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag, d_staged);
+  else if (rec_kind == kRecHashed)
+    hipLaunchKernelGGL((dq_freq_part_kernel<HashRec, (1 << kPartMaxBinBits)>), grid, dim3(kPartThreads), 0, stream,
+                       static_cast<const HashRec*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
+                       static_cast<HashRec*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag, d_staged);
   else
     hipLaunchKernelGGL((dq_freq_part_kernel<FreqRec, (1 << kPartMaxBinBits)>), grid, dim3(kPartThreads), 0, stream,
                        static_cast<const FreqRec*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
@@ -2934,7 +3296,7 @@ hipError_t launch_freq_compact(const void* d_in, bool packed, const unsigned lon
   return hipGetLastError();
 }
 
-hipError_t launch_freq_agg_region(const FreqTable& T, const void* d_recs, bool packed, const unsigned long long* d_fill,
+hipError_t launch_freq_agg_region(const FreqTable& T, const void* d_recs, int rec_kind, const unsigned long long* d_fill,
                                   uint64_t cap, uint64_t n_slices, int table_empty, FreqRec* d_retry,
                                   unsigned long long* d_n_retry, unsigned long long* d_new_groups,
                                   unsigned long long* d_hist, unsigned long long* d_big, unsigned long long* d_n_big,
@@ -2943,9 +3305,14 @@ hipError_t launch_freq_agg_region(const FreqTable& T, const void* d_recs, bool p
   uint64_t blocks = n_slices < 65536 ? n_slices : 65536;
   if (blocks < 1) blocks = 1;
   if (!table_empty && (d_hist || d_smax || write_all)) return hipErrorInvalidValue;
-  if (compact && (!packed || !table_empty)) return hipErrorInvalidValue;
+  const bool packed = rec_kind == kRecPacked;
+  if (compact && (rec_kind == kRecFree || !table_empty)) return hipErrorInvalidValue;
+  if (rec_kind == kRecHashed && !table_empty) return hipErrorInvalidValue;  // (fresh tables only)
   AggTrack tr{d_hist, d_big, d_n_big, big_cap, d_smax, write_all, compact ? *compact : FreqCompact{}};
-  if (packed)
+  if (rec_kind == kRecHashed)
+    hipLaunchKernelGGL(dq_freq_agg_hashed_kernel, dim3((unsigned)blocks), dim3(kAggHThreads), 0, stream, T,
+                       static_cast<const HashRec*>(d_recs), d_fill, cap, n_slices, d_retry, d_n_retry, d_new_groups, tr);
+  else if (packed)
     hipLaunchKernelGGL(dq_freq_agg_packed_kernel, dim3((unsigned)blocks), dim3(kAggPThreads), 0, stream, T,
                        static_cast<const uint64_t*>(d_recs), d_fill, cap, n_slices, table_empty, d_retry, d_n_retry,
                        d_new_groups, tr);
@@ -2961,6 +3328,34 @@ hipError_t launch_freq_expand(const FreqTable& T, const FreqCompact& cmp, hipStr
   uint64_t blocks = n_slices < 65536 ? n_slices : 65536;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(dq_freq_expand_kernel, dim3((unsigned)blocks), dim3(kAggPThreads), 0, stream, T, cmp, n_slices);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_key_bytes(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
+                                 unsigned long long* d_out, hipStream_t stream) {
+  if (n_rows <= 0) return hipSuccess;
+  int64_t blocks = (n_rows + kBlock * 8 - 1) / (kBlock * 8);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(dq_freq_key_bytes_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, ks, d_cols, n_rows, d_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_stage_hashed(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, HashRec* d_out,
+                                    const FreqTable& T, uint32_t* d_hll, unsigned long long* d_too_long,
+                                    unsigned long long* d_staged, unsigned long long* d_max_len, hipStream_t stream) {
+  if (n_rows <= 0) return hipSuccess;
+  int64_t blocks = (n_rows + kBlock * 4 - 1) / (kBlock * 4);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(dq_freq_stage_hashed_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, ks, d_cols, n_rows,
+                     d_out, T, d_hll, d_too_long, d_staged, d_max_len);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_insert_hashed(const FreqTable& T, const FreqRec* d_recs, uint64_t n, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  uint64_t blocks = (n + kBlock - 1) / kBlock;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(dq_freq_insert_hashed_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, d_recs, n);
   return hipGetLastError();
 }
 

@@ -153,6 +153,7 @@ struct PredProgram {
 
 // ---------------------------------------------------------------- frequency group-by
 constexpr int kMaxKeyCols = 8;
+constexpr int kMaxLocalKey = 64;     // encoded multi-column keys are built in registers/scratch
 constexpr int kFreqHist = 1 << 16;   // count-of-counts bins kept on the device
 constexpr int kFreqLdsHist = 2048;   // ... of which the first are aggregated in LDS
 
@@ -175,6 +176,14 @@ constexpr int kPartMaxBits = 11;
 struct alignas(16) FreqRec {
   unsigned long long k0, k1;
 };
+
+// A staged row of a long or multi-column key (the hashed partition path, round 6): the key's
+// table hash and a reference to its bytes, which the stage copied into the table's key heap
+// (8-byte aligned, zero padded): ref = heap offset << 24 | key length.  A hole: ref = ~0.
+struct alignas(16) HashRec {
+  unsigned long long h, ref;
+};
+constexpr unsigned long long kHashHole = ~0ull;
 
 struct FreqTable {
   FreqSlot* slots;
@@ -336,8 +345,9 @@ hipError_t launch_freq_agg(const FreqTable& T, const FreqRec* d_recs, const uint
 hipError_t launch_freq_part(const void* d_in, uint64_t in_n, const unsigned long long* d_in_fill, uint64_t in_cap,
                             uint64_t n_in_regions, int id_bits, int bin_bits, void* d_out, uint64_t out_cap,
                             unsigned long long* d_out_fill, FreqRec* d_ovf, unsigned long long* d_ovf_n,
-                            uint64_t ovf_cap, unsigned int* d_flag, bool packed, hipStream_t stream,
+                            uint64_t ovf_cap, unsigned int* d_flag, int rec_kind, hipStream_t stream,
                             unsigned long long* d_staged = nullptr);
+constexpr int kRecFree = 0, kRecPacked = 1, kRecHashed = 2;  // FreqRec, packed word, HashRec
 // With an empty table it can also produce the count-of-counts histogram (d_hist, counts >=
 // kFreqHist into d_big), each slice's largest count (d_smax) and write every slot (write_all:
 // the table needs no clearing).
@@ -374,9 +384,21 @@ hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, bool p
                                   uint64_t ovf_cap, unsigned int* d_flag, uint32_t* d_hll, unsigned long long* d_long_key,
                                   unsigned long long* d_staged, hipStream_t stream,
                                   void* d_rows = nullptr);
+// The hashed partition path (dq_freq.hip, round 6).  Stage: every row's key (make_key: long
+// strings, several columns) is copied to the key heap (one atomic per wave) and written as a
+// HashRec in row order (holes for NULL keys); too_long: a multi-column key over kMaxLocalKey.
+hipError_t launch_freq_stage_hashed(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, HashRec* d_out,
+                                    const FreqTable& T, uint32_t* d_hll, unsigned long long* d_too_long,
+                                    unsigned long long* d_staged, unsigned long long* d_max_len, hipStream_t stream);
+// Exact bytes the stage will append to the heap for n_rows rows (sum of 8-aligned key lengths).
+hipError_t launch_freq_key_bytes(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
+                                 unsigned long long* d_out, hipStream_t stream);
+// Global inserts of n hashed records (the list form: FreqRec bits of HashRec), their key bytes
+// already in T's heap: the retry / overflow records and the fall-back of the hashed path.
+hipError_t launch_freq_insert_hashed(const FreqTable& T, const FreqRec* d_recs, uint64_t n, hipStream_t stream);
 hipError_t launch_freq_compact(const void* d_in, bool packed, const unsigned long long* d_fill, uint64_t cap,
                                uint64_t n_regions, const unsigned long long* d_prefix, FreqRec* d_out, hipStream_t stream);
-hipError_t launch_freq_agg_region(const FreqTable& T, const void* d_recs, bool packed, const unsigned long long* d_fill,
+hipError_t launch_freq_agg_region(const FreqTable& T, const void* d_recs, int rec_kind, const unsigned long long* d_fill,
                                   uint64_t cap, uint64_t n_slices, int table_empty, FreqRec* d_retry,
                                   unsigned long long* d_n_retry, unsigned long long* d_new_groups,
                                   unsigned long long* d_hist, unsigned long long* d_big, unsigned long long* d_n_big,

@@ -28,7 +28,10 @@ dq_status dq_diag_hash_rate(int device, int with_hll, int reps, double* hashes_p
  * the few-groups kernel (dq_freq_small_kernel), out[6] = 1 if a wait for another lane's slot
  * publish ever timed out (an error every API call also reports), out[7] = imported wire runs
  * that were in order only by coarser slices than the table's (merged from the enclosing ranges),
- * out[8] = imported wire runs out of order (inserted group by group).  `out` holds 9 values. */
+ * out[8] = imported wire runs out of order (inserted group by group), out[9] = partition-path
+ * aggregations of hashed records (long or multi-column keys), out[10] = hashed records inserted
+ * globally (slices handed back, tables that already held groups), out[11] = 1 while the table is
+ * compacted (occupied slots only).  `out` holds 12 values. */
 dq_status dq_diag_freq_paths(dq_freq* f, int64_t* out);
 
 /* Test hooks of one table (tests only; never set by the product): flags = 1 makes claimed

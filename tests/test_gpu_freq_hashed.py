@@ -1,0 +1,156 @@
+"""Long (> 15 B) and multi-column grouping keys on the partition path (round 6): hashed records.
+
+The reference groups any key type in one hash aggregate (GroupingAnalyzers.scala:67-71); its
+most common callers on such keys are isUnique / isPrimaryKey / hasUniqueness (Check.scala:140-230)
+on UUID-like ids and composite keys.  Here a batch holding a key that does not fit a 16-byte
+record switches the table to hashed records: the stage copies every key's bytes into the key heap
+and stages {table hash, heap reference}; the two-level split and an LDS aggregation by hash follow,
+each record of a hash group compared byte for byte with the group's first.  Checked exactly
+(every group and count) against Python counts / the oracle, for:
+
+* 36-character UUID strings with duplicates and NULLs, Histogram's "NullValue" included;
+* composite (int64, utf8) keys whose encoding is longer than 15 bytes (oracle);
+* tables that already hold groups (early aggregations, or short keys first): the global inserts;
+* every operation after it (summary, top, export, lookup, merge, further batches).
+"""
+import numpy as np
+import pytest
+
+import deequ_amd as d
+import pyoracle as O
+from deequ_amd.frequencies import FrequencyTable, encode_key
+from helpers import oracle_table, product_table
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def part(monkeypatch):
+    monkeypatch.setenv("DQ_FREQ_PART_MIN", "1")
+    monkeypatch.setenv("DQ_FREQ_PATH", "sorted")
+
+
+def _uuid(v: int) -> str:
+    x = (v * 0x9E3779B97F4A7C15 + 0x632BE59BD9B4E019) % 2 ** 64
+    y = ((v ^ 0x5DEECE66D) * 0xC2B2AE3D27D4EB4F) % 2 ** 64
+    h = "%016x%016x" % (x, y)
+    return "%s-%s-%s-%s-%s" % (h[:8], h[8:12], h[12:16], h[16:20], h[20:32])
+
+
+def _count(keys, hist=False):
+    want = {}
+    for k in keys:
+        if k is None and not hist:
+            continue
+        kb = b"NullValue" if k is None else k.encode()
+        want[kb] = want.get(kb, 0) + 1
+    return want
+
+
+def _export(t):
+    counts, keys = t.export()
+    return dict(zip(keys, counts.tolist()))
+
+
+def _consume(keys, hist, batches, **kw):
+    t = FrequencyTable(["key"], {"key": "string"}, histogram=hist, **kw)
+    step = (len(keys) + batches - 1) // batches
+    for s in range(0, len(keys), step):
+        t.consume(d.Table.from_pydict({"key": ("string", keys[s:s + step])}))
+    return t
+
+
+@pytest.mark.parametrize("hist", [False, True])
+def test_uuid_keys_exact(gpu, part, hist):
+    rng = np.random.default_rng(41)
+    n = 600_000
+    ids = rng.integers(0, 250_000, n)
+    keys = [None if i % 41 == 0 else _uuid(int(v)) for i, v in enumerate(ids)]
+    t = _consume(keys, hist, 3)
+    want = _count(keys, hist)
+    s = t.summary()
+    assert (s.num_groups, s.num_unique, s.grouped_rows) == (
+        len(want), sum(1 for c in want.values() if c == 1), sum(want.values()))
+    top_c, top_k = t.top(5)
+    best = sorted(want.items(), key=lambda kv: (-kv[1], kv[0]))
+    cut = best[4][1]
+    assert sorted(zip(top_c.tolist(), top_k)) == sorted((c, k) for k, c in want.items() if c >= cut)
+    paths = t.paths()
+    assert paths["hashed_runs"] >= 1 and paths["hashed_inserts"] == 0, paths
+    assert _export(t) == want
+    assert t.lookup(best[0][0]) == best[0][1]
+    t.close()
+
+
+def test_uuid_keys_unique_ids(gpu, part):
+    """isPrimaryKey-shaped: every id distinct (no hash group of two records to compare)."""
+    n = 500_000
+    keys = [_uuid(v) for v in range(n)]
+    t = _consume(keys, False, 2)
+    s = t.summary()
+    assert (s.num_groups, s.num_unique, s.grouped_rows) == (n, n, n)
+    assert t.paths()["hashed_runs"] >= 1
+    t.close()
+
+
+def test_composite_keys_against_oracle(gpu, part, monkeypatch):
+    """(int64, utf8) grouping keys of 8 + 4 + 9..12 encoded bytes: hashed records; groups equal
+    to the oracle's FrequenciesAndNumRows (GroupingAnalyzers.scala:53-80), NULL in either column
+    dropping the row."""
+    monkeypatch.setenv("DQ_FREQ_PART_SLOTS", str(1 << 20))  # (the LDS aggregation's slice layout)
+    rng = np.random.default_rng(43)
+    n = 120_000
+    a = rng.integers(0, 3000, n)
+    spec = {"id": ["int64", [None if i % 31 == 0 else int(a[i] % 700) for i in range(n)]],
+            "name": ["string", [None if i % 37 == 0 else "name-%05d" % (a[i] % 900) for i in range(n)]]}
+    table = product_table(spec)
+    t = FrequencyTable(["id", "name"], dict(table.schema))
+    t.consume(table)
+    got = _export(t)
+    st = O.frequencies_state(oracle_table(spec), ["id", "name"])
+    want = {encode_key(list(k), ["int64", "string"]): c for k, c in st.frequencies.items()}
+    assert got == want
+    assert t.paths()["hashed_runs"] >= 1
+    s = t.summary()
+    assert s.num_groups == len(want) and s.num_rows == n
+    t.close()
+
+
+@pytest.mark.parametrize("mode", ["budget", "short_first"])
+def test_hashed_into_table_with_groups(gpu, part, monkeypatch, mode):
+    """budget: an early aggregation fills the table, the next hashed regions go in by global
+    inserts; short_first: 12-digit keys first (packed records), then UUIDs.  Exact either way."""
+    rng = np.random.default_rng(47)
+    n = 300_000
+    uu = [_uuid(int(v)) for v in rng.integers(0, 80_000, n)]
+    if mode == "budget":
+        monkeypatch.setenv("DQ_FREQ_STAGE_BUDGET", "200000")
+        keys = uu
+    else:
+        keys = ["%012d" % v for v in rng.integers(0, 90_000, n)] + uu
+    t = _consume(keys, False, 4)
+    assert _export(t) == _count(keys)
+    assert t.paths()["hashed_inserts"] > 0
+    t.close()
+
+
+def test_hashed_operations_after(gpu, part):
+    """A hashed (compacted) table through every later operation: further batches, a merge from
+    another hashed table, imports; exact against Python counts."""
+    rng = np.random.default_rng(53)
+    k1 = [_uuid(int(v)) for v in rng.integers(0, 100_000, 250_000)]
+    k2 = [_uuid(int(v)) for v in rng.integers(50_000, 150_000, 150_000)]
+    t = _consume(k1, False, 2)
+    assert t.paths()["compacted"] == 1
+    t.consume(d.Table.from_pydict({"key": ("string", k2)}))
+    other = _consume(k2, False, 1)
+    t.merge_from(other)
+    other.close()
+    want = _count(k1 + k2 + k2)
+    assert _export(t) == want
+    counts, offs, blob = t.export_flat()
+    t2 = FrequencyTable(["key"], {"key": "string"})
+    t2.import_flat(counts, offs, blob, num_rows=5)
+    assert _export(t2) == want
+    t.close()
+    t2.close()
