@@ -1245,7 +1245,6 @@ constexpr int kStagePer = DQ_STAGE_PER;   // rows per thread per fused-stage til
 #define DQ_STAGE_NT 512
 #endif
 constexpr int kStageThreads = DQ_STAGE_NT;
-constexpr int kStageWaves = kStageThreads / 64;
 constexpr uint32_t kStageTile = (uint32_t)kStageThreads * kStagePer;
 #ifndef DQ_STAGEP_SUB
 #define DQ_STAGEP_SUB kStageTile
@@ -4243,14 +4242,24 @@ constexpr int kSmallSlots = 1024;
 constexpr int kSmallThreads = DQ_SMALL_THREADS;
 constexpr int kSmallPer = DQ_SMALL_PER;  // rows per thread per iteration
 
+// Counts in kSmallCopies copies per slot, a lane adding to copy (lane & 3): with ~100 keys most
+// of a wave's 64 rows fall on a few slots, and LDS atomics of one instruction to ONE address are
+// serialised (C5 round 5: 0.49 of the LDS-active cycles in bank conflicts); the copies of a slot
+// are adjacent words, so lanes of one key hit four banks.
+#ifndef DQ_SMALL_COPIES
+#define DQ_SMALL_COPIES 4
+#endif
+constexpr int kSmallCopies = DQ_SMALL_COPIES;
+static_assert(kSmallCopies == 1 || kSmallCopies == 2 || kSmallCopies == 4, "the write-out reads the copies as one load");
 struct SmallLds {
   unsigned long long K0[kSmallSlots], K1[kSmallSlots];  // K1 = key bytes 8..14 | length << 56
-  uint32_t C[kSmallSlots];
+  alignas(16) uint32_t C[kSmallSlots * kSmallCopies];
   uint32_t n_used;
 };
 
 __device__ inline bool small_count(SmallLds& L, uint64_t k0, uint64_t k1l) {
   uint32_t s = lds_hash(k0, k1l, 0) & (kSmallSlots - 1);
+  const uint32_t cp = threadIdx.x & (kSmallCopies - 1);
   // the common case once the few keys are in: the key in its first slot (both words read in
   // one LDS round trip; volatile keeps K1's read before K0's -- a wave's LDS reads execute in
   // order and a slot's K0 is written before its K1 is published -- so a matching K1 comes with
@@ -4259,7 +4268,7 @@ __device__ inline bool small_count(SmallLds& L, uint64_t k0, uint64_t k1l) {
     const unsigned long long c1 = *reinterpret_cast<volatile unsigned long long*>(&L.K1[s]);
     const unsigned long long c0 = *reinterpret_cast<volatile unsigned long long*>(&L.K0[s]);
     if (c1 == k1l && c0 == k0) {
-      atomicAdd(&L.C[s], 1u);
+      atomicAdd(&L.C[s * kSmallCopies + cp], 1u);
       return true;
     }
   }
@@ -4267,14 +4276,14 @@ __device__ inline bool small_count(SmallLds& L, uint64_t k0, uint64_t k1l) {
   for (uint32_t probe = 0; probe < (uint32_t)kSmallSlots && !done;) {  // (publish inside the iteration)
     const unsigned long long c = __hip_atomic_load(&L.K1[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (c == k1l && __hip_atomic_load(&L.K0[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == k0) {
-      atomicAdd(&L.C[s], 1u);
+      atomicAdd(&L.C[s * kSmallCopies + cp], 1u);
       done = true;
     } else if (c == kLdsEmpty) {
       if (atomicCAS(&L.K1[s], kLdsEmpty, kLdsBusy) == kLdsEmpty) {
         L.K0[s] = k0;
         __threadfence_block();
         atomicExch(&L.K1[s], k1l);
-        atomicAdd(&L.C[s], 1u);
+        atomicAdd(&L.C[s * kSmallCopies + cp], 1u);
         done = true;
       }
     } else if (c == kLdsBusy) {
@@ -4305,10 +4314,8 @@ __global__ __launch_bounds__(kSmallThreads) void dq_freq_small_kernel(FreqKeySpe
     out_n += y * gridDim.x;
     bad += y;
   }
-  for (uint32_t i = t; i < (uint32_t)kSmallSlots; i += kSmallThreads) {
-    L.K1[i] = kLdsEmpty;
-    L.C[i] = 0u;
-  }
+  for (uint32_t i = t; i < (uint32_t)kSmallSlots; i += kSmallThreads) L.K1[i] = kLdsEmpty;
+  for (uint32_t i = t; i < (uint32_t)(kSmallSlots * kSmallCopies); i += kSmallThreads) L.C[i] = 0u;
   if (t == 0) L.n_used = 0u;
   __syncthreads();
   const DevColumn& c0 = cols[ks.key_cols[0]];
@@ -4419,7 +4426,9 @@ __global__ __launch_bounds__(kSmallThreads) void dq_freq_small_kernel(FreqKeySpe
   __syncthreads();
   // this workgroup's groups, compacted into its staging list
   for (uint32_t i = t; i < (uint32_t)kSmallSlots; i += kSmallThreads) {
-    const uint32_t c = L.C[i];
+    uint32_t c = 0u;
+#pragma unroll
+    for (int k = 0; k < kSmallCopies; ++k) c += L.C[i * kSmallCopies + k];
     const bool used = c != 0u;
     const uint64_t m = __ballot(used);
     uint32_t at = 0;
