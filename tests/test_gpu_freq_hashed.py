@@ -10,7 +10,8 @@ each record of a hash group compared byte for byte with the group's first.  Chec
 
 * 36-character UUID strings with duplicates and NULLs, Histogram's "NullValue" included;
 * composite (int64, utf8) keys whose encoding is longer than 15 bytes (oracle);
-* tables that already hold groups (early aggregations, or short keys first): the global inserts;
+* tables that already hold groups (early aggregations, short keys first, batches beyond the
+  reserved rows) and tables of fewer than 2^20 slots: the global inserts (exact, slower);
 * every operation after it (summary, top, export, lookup, merge, further batches).
 """
 import numpy as np
@@ -54,6 +55,7 @@ def _export(t):
 
 def _consume(keys, hist, batches, **kw):
     t = FrequencyTable(["key"], {"key": "string"}, histogram=hist, **kw)
+    t.reserve(len(keys))  # (as compute_frequencies does: one staging for every batch)
     step = (len(keys) + batches - 1) // batches
     for s in range(0, len(keys), step):
         t.consume(d.Table.from_pydict({"key": ("string", keys[s:s + step])}))
@@ -62,9 +64,10 @@ def _consume(keys, hist, batches, **kw):
 
 @pytest.mark.parametrize("hist", [False, True])
 def test_uuid_keys_exact(gpu, part, hist):
+    """~260k UUID groups of 1-8 rows (2^20 slots: one slice per level-1 region), NULLs, 3 batches."""
     rng = np.random.default_rng(41)
     n = 600_000
-    ids = rng.integers(0, 250_000, n)
+    ids = rng.integers(0, 300_000, n)
     keys = [None if i % 41 == 0 else _uuid(int(v)) for i, v in enumerate(ids)]
     t = _consume(keys, hist, 3)
     want = _count(keys, hist)
@@ -83,7 +86,8 @@ def test_uuid_keys_exact(gpu, part, hist):
 
 
 def test_uuid_keys_unique_ids(gpu, part):
-    """isPrimaryKey-shaped: every id distinct (no hash group of two records to compare)."""
+    """isPrimaryKey-shaped: every id distinct (no hash group of two records to compare); 2^21
+    slots, so the level-2 split runs too."""
     n = 500_000
     keys = [_uuid(v) for v in range(n)]
     t = _consume(keys, False, 2)
@@ -105,6 +109,7 @@ def test_composite_keys_against_oracle(gpu, part, monkeypatch):
             "name": ["string", [None if i % 37 == 0 else "name-%05d" % (a[i] % 900) for i in range(n)]]}
     table = product_table(spec)
     t = FrequencyTable(["id", "name"], dict(table.schema))
+    t.reserve(n)
     t.consume(table)
     got = _export(t)
     st = O.frequencies_state(oracle_table(spec), ["id", "name"])
@@ -138,8 +143,8 @@ def test_hashed_operations_after(gpu, part):
     """A hashed (compacted) table through every later operation: further batches, a merge from
     another hashed table, imports; exact against Python counts."""
     rng = np.random.default_rng(53)
-    k1 = [_uuid(int(v)) for v in rng.integers(0, 100_000, 250_000)]
-    k2 = [_uuid(int(v)) for v in rng.integers(50_000, 150_000, 150_000)]
+    k1 = [_uuid(int(v)) for v in rng.integers(0, 600_000, 600_000)]  # ~380k groups: 2^20 slots
+    k2 = [_uuid(int(v)) for v in rng.integers(300_000, 900_000, 200_000)]
     t = _consume(k1, False, 2)
     assert t.paths()["compacted"] == 1
     t.consume(d.Table.from_pydict({"key": ("string", k2)}))
