@@ -2709,15 +2709,6 @@ __device__ inline Key hashed_key(const FreqTable& T, const FreqRec& r) {
   return k;
 }
 
-__global__ __launch_bounds__(kBlock) void dq_freq_insert_hashed_kernel(FreqTable T, const FreqRec* __restrict__ recs,
-                                                                       uint64_t n) {
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
-    const FreqRec r = recs[i];
-    if (r.k1 == kHashHole) continue;
-    if (!global_insert<true, true>(T, hashed_key(T, r), 1ull)) return;
-  }
-}
-
 // Two heap keys (8-byte aligned, zero padded) equal byte for byte.
 __device__ inline bool heap_refs_equal(const uint8_t* heap, unsigned long long ra, unsigned long long rb) {
   if (ra == rb) return true;
@@ -2844,7 +2835,7 @@ __global__ __launch_bounds__(kAggHThreads) void dq_freq_agg_hashed_kernel(FreqTa
           const HashRec r = recs[c0 + (uint64_t)i * NT + t];
           const unsigned long long kk = r.h ? r.h : 1ull;
           const uint32_t s = lds_find_hash(L.K, kk, (uint32_t)r.h & (S - 1u));
-          if (s == S || !heap_refs_equal(T.heap, L.R[s], r.ref)) L.overflow = 2;  // two keys, one hash
+          if (!heap_refs_equal(T.heap, L.R[s], r.ref)) L.overflow = 2;  // two keys, one hash (~never)
         }
       }
       lds_barrier();
@@ -2931,6 +2922,92 @@ __global__ __launch_bounds__(kAggHThreads) void dq_freq_agg_hashed_kernel(FreqTa
     for (int i = t; i < kAggLdsHist; i += NT)
       if (L.hist[i]) atomicAdd(&tr.hist[i], (unsigned long long)L.hist[i]);
   }
+}
+
+// Hashed records into the GLOBAL table (T may hold groups; any slice count): the fall-back of
+// the hashed path -- tables of fewer slices than level-1 regions, tables that already hold
+// groups, and the records a slice aggregation handed back.  Each workgroup pre-aggregates its
+// chunks of records in an LDS image by hash (as dq_freq_agg_hashed_kernel, joins compared byte
+// for byte with the group's first record) and inserts each LDS group ONCE with its count when the
+// image is half full and at the end, so a key repeated over many rows (few groups) costs one
+// global insert per workgroup flush, not one per row.  A record whose hash group holds another
+// key, or that finds the image full, is inserted on its own.
+__global__ __launch_bounds__(kAggHThreads) void dq_freq_insert_hashed_kernel(FreqTable T, const FreqRec* __restrict__ recs,
+                                                                             uint64_t n) {
+  constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
+  constexpr int NT = kAggHThreads;
+  constexpr uint32_t kChunk = 64u * NT;
+  __shared__ AggLdsH L;
+  const uint32_t t = threadIdx.x;
+  for (uint32_t s = t; s < S; s += NT) {
+    L.K[s] = 0ull;
+    L.C[s] = 0u;
+  }
+  if (t == 0) L.fresh = 0u;  // (groups in the image)
+  lds_barrier();
+  auto flush = [&]() {
+    for (uint32_t s = t; s < S; s += NT) {
+      const uint32_t c = L.C[s];
+      if (c) {
+        FreqRec r;
+        r.k0 = L.K[s];  // (kk: a hash of 0 was kept as 1 -- the key's own hash is recomputed below)
+        r.k1 = L.R[s];
+        Key k = hashed_key(T, r);
+        k.hash = k.len > 16 ? xxh64_any(k.ptr, k.len, 42) : hash_inline(k.k0, k.k1, k.len);
+        (void)global_insert<true, true>(T, k, (unsigned long long)c);
+      }
+      L.K[s] = 0ull;
+      L.C[s] = 0u;
+    }
+    if (t == 0) L.fresh = 0u;
+    lds_barrier();
+  };
+  for (uint64_t c0 = (uint64_t)blockIdx.x * kChunk; c0 < n; c0 += (uint64_t)gridDim.x * kChunk) {
+    const uint64_t c1 = c0 + kChunk < n ? c0 + kChunk : n;
+    unsigned long long joined = 0ull;
+    for (uint32_t i = 0; i < 64u; ++i) {
+      const uint64_t idx = c0 + (uint64_t)i * NT + t;
+      if (idx >= c1) break;
+      const FreqRec r = recs[idx];
+      if (r.k1 == kHashHole) continue;
+      const unsigned long long kk = r.k0 ? r.k0 : 1ull;
+      uint32_t s = (uint32_t)r.k0 & (S - 1u);
+      bool placed = false;
+      for (uint32_t probe = 0; probe < S / 2u; ++probe) {  // (half the image: the flush keeps room)
+        const unsigned long long c = atomicCAS(&L.K[s], 0ull, kk);
+        if (c == 0ull) {
+          L.R[s] = r.k1;
+          atomicAdd(&L.C[s], 1u);
+          atomicAdd(&L.fresh, 1u);
+          placed = true;
+          break;
+        }
+        if (c == kk) {
+          atomicAdd(&L.C[s], 1u);
+          joined |= 1ull << i;
+          placed = true;
+          break;
+        }
+        s = (s + 1u) & (S - 1u);
+      }
+      if (!placed) (void)global_insert<true, true>(T, hashed_key(T, r), 1ull);
+    }
+    lds_barrier();  // every group's first reference is in place
+    while (joined) {
+      const uint32_t i = (uint32_t)__builtin_ctzll(joined);
+      joined &= joined - 1ull;
+      const FreqRec r = recs[c0 + (uint64_t)i * NT + t];
+      const unsigned long long kk = r.k0 ? r.k0 : 1ull;
+      const uint32_t s = lds_find_hash(L.K, kk, (uint32_t)r.k0 & (S - 1u));
+      if (!heap_refs_equal(T.heap, L.R[s], r.k1)) {  // two keys, one hash: this record on its own
+        atomicSub(&L.C[s], 1u);
+        (void)global_insert<true, true>(T, hashed_key(T, r), 1ull);
+      }
+    }
+    lds_barrier();
+    if (L.fresh > S / 4u) flush();
+  }
+  flush();
 }
 
 // The slot image of a compacted table (AggTrack::cmp) rebuilt in T: slice b's groups, stored in
@@ -3352,9 +3429,12 @@ hipError_t launch_freq_stage_hashed(const FreqKeySpec& ks, const DevColumn* d_co
 
 hipError_t launch_freq_insert_hashed(const FreqTable& T, const FreqRec* d_recs, uint64_t n, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  uint64_t blocks = (n + kBlock - 1) / kBlock;
-  if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(dq_freq_insert_hashed_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, d_recs, n);
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const uint64_t chunk = 64ull * kAggHThreads;
+  uint64_t blocks = (n + chunk - 1) / chunk;
+  if (blocks > 2ull * (uint64_t)cus) blocks = 2ull * (uint64_t)cus;  // (each workgroup flushes its image once at the end)
+  hipLaunchKernelGGL(dq_freq_insert_hashed_kernel, dim3((unsigned)blocks), dim3(kAggHThreads), 0, stream, T, d_recs, n);
   return hipGetLastError();
 }
 

@@ -79,7 +79,10 @@ def test_uuid_keys_exact(gpu, part, hist):
     cut = best[4][1]
     assert sorted(zip(top_c.tolist(), top_k)) == sorted((c, k) for k, c in want.items() if c >= cut)
     paths = t.paths()
-    assert paths["hashed_runs"] >= 1 and paths["hashed_inserts"] == 0, paths
+    assert paths["hashed_runs"] >= 1, paths
+    # (Histogram: "NullValue" holds 1/41 of the rows, more than its region's room -- the rest
+    # takes the overflow list, inserted globally)
+    assert paths["hashed_inserts"] <= (keys.count(None) if hist else 0), paths
     assert _export(t) == want
     assert t.lookup(best[0][0]) == best[0][1]
     t.close()
