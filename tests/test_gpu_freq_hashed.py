@@ -162,3 +162,31 @@ def test_hashed_operations_after(gpu, part):
     assert _export(t2) == want
     t.close()
     t2.close()
+
+
+def test_composite_few_groups_many_rows(gpu):
+    """A composite key of few groups over many rows (a (region, city)-shaped pair, 24 encoded
+    bytes): the table stays below the partition path's slice count, so the hashed records are
+    inserted globally after the LDS pre-aggregation of dq_freq_insert_hashed_kernel -- exact, and
+    one global insert per workgroup flush, not per row."""
+    rng = np.random.default_rng(59)
+    n = 6_000_000
+    a = rng.integers(0, 40, n)
+    b = rng.integers(0, 25, n)
+    valid = rng.random(n) > 0.02
+    names = np.array(["city-%07d" % k for k in range(25)])
+    table = d.Table({"a": d.Column.from_numpy(a, valid, "int64"),
+                     "b": d.Column.from_pylist(names[b].tolist(), "string")})
+    t = FrequencyTable(["a", "b"], dict(table.schema))
+    t.reserve(n)
+    t.consume(table)
+    s = t.summary()
+    pairs, counts = np.unique(a[valid] * 100 + b[valid], return_counts=True)
+    assert (s.num_groups, s.grouped_rows, s.num_rows) == (len(pairs), int(valid.sum()), n)
+    assert s.num_unique == int((counts == 1).sum())
+    got = {(int.from_bytes(k[:8], "little", signed=True), k[12:].decode()): c for k, c in _export(t).items()}
+    want = {(int(p // 100), "city-%07d" % (p % 100)): int(c) for p, c in zip(pairs, counts)}
+    assert got == want
+    paths = t.paths()
+    assert paths["hashed_inserts"] == int(valid.sum()), paths
+    t.close()
