@@ -357,6 +357,15 @@ def make_c3_string_table(rows: int, n_cols: int, rank: int, device: int):
     return d.Table(cols)
 
 
+def c4_batch_rows(batch: int, keys_kind: str) -> int:
+    """Arrow utf8 offsets are int32: one batch holds at most 2^31 - 1 bytes of chars.  36-char
+    UUIDs fit 59.6M rows, so the 125M-row default is cut to 50M-row batches for them."""
+    width = {"uuid": 36, "pair": 8}.get(keys_kind, 12)
+    if batch * width >= 2 ** 31:
+        return 50_000_000 if width * 50_000_000 < 2 ** 31 else (2 ** 31 - 1) // width
+    return batch
+
+
 def c4_valid_ids(rows: int, batch: int, distinct: int, rank: int, device: int):
     """The integer ids behind make_c4_batches' non-NULL keys, regenerated from the same generator
     sequence (the keys are their 12-digit decimals), concatenated on the device."""
@@ -384,7 +393,8 @@ def c4_verify(args, metrics, dist_metric, analyzers):
     import math
     import numpy as np
     import torch
-    ids = c4_valid_ids(args.c4_rows, args.c4_batch, args.c4_distinct, 0, torch.cuda.current_device())
+    ids = c4_valid_ids(args.c4_rows, c4_batch_rows(args.c4_batch, args.c4_keys), args.c4_distinct, 0,
+                       torch.cuda.current_device())
     n_valid = int(ids.numel())
     u, c = torch.unique(ids, sorted=True, return_counts=True)
     del ids
@@ -467,6 +477,7 @@ def make_c4_batches(rows: int, batch: int, distinct: int, rank: int, device: int
     gen.manual_seed(7 + 1000 * rank)
     pow10 = torch.tensor([10 ** (11 - i) for i in range(12)], dtype=torch.int64, device=dev)
     width = {"uuid": 36, "pair": 8}.get(keys_kind, 12)
+    batch = c4_batch_rows(batch, keys_kind)
     parts = []
     for b0 in range(0, rows, batch):
         m = min(batch, rows - b0)
@@ -736,12 +747,13 @@ def run_c4(args, world, rank, local):
                                 "C4: %d rows/GPU in %d-row utf8 batches; Uniqueness, Distinctness, Entropy, "
                                 "CountDistinct + Histogram, all from one GPU group-by of the key (the "
                                 "reference runs Histogram as a second job)%s")
-                               % (args.c4_rows, args.c4_batch,
+                               % (args.c4_rows, c4_batch_rows(args.c4_batch, args.c4_keys),
                                   "; key-hash all-to-all over %d ranks" % world if world > 1 else ""),
                    "keys": args.c4_keys},
         "roofline": _step_roofline(algo, step_s, "one whole group-by step per GPU (stage + level-1 partition, "
                                                  "level-2 partition, slice aggregation, top-N), HBM-bound by design",
-                                   workload="c4" if world == 1 else None,
+                                   workload=("c4" if args.c4_keys == "digits" else "c4_" + args.c4_keys)
+                                   if world == 1 else None,
                                    default_size=(args.c4_rows, args.c4_batch, args.c4_distinct)
                                    == (1_000_000_000, 125_000_000, 201_500_000)),
         # SURVEY §8(d) C4 asks for the table accesses per row beside the streaming fraction: the
