@@ -795,7 +795,9 @@ __global__ __launch_bounds__(kBlock) void dq_freq_import_flat_kernel(FreqTable T
 }
 
 // Count of one encoded key (0 if absent): a single-thread probe of the key's slice.
-__global__ void dq_freq_lookup_kernel(FreqTable T, const uint8_t* key, uint32_t len, unsigned long long* out) {
+// cmp.slots != nullptr: a compacted table -- the key's slice's groups are scanned instead of probed.
+__global__ void dq_freq_lookup_kernel(FreqTable T, const uint8_t* key, uint32_t len, unsigned long long* out,
+                                      FreqCompact cmp) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   Key k;
   k.len = len;
@@ -811,8 +813,10 @@ __global__ void dq_freq_lookup_kernel(FreqTable T, const uint8_t* key, uint32_t 
   }
   const uint32_t tag = tag_of(k.hash);
   *out = 0ull;
-  for (uint64_t i = 0; i < kFreqSliceSlots; ++i) {
-    const FreqSlot& e = T.slots[probe_slot(T, k.hash, i)];
+  const uint64_t b = slice_of(T, k.hash);
+  const uint64_t n_scan = cmp.slots ? cmp.num[b] : kFreqSliceSlots;
+  for (uint64_t i = 0; i < n_scan; ++i) {
+    const FreqSlot& e = cmp.slots ? cmp.slots[cmp.base[b] + i] : T.slots[probe_slot(T, k.hash, i)];
     if (e.ctrl == 0ull) return;  // launch boundary: the table is complete and visible
     if ((uint32_t)(e.ctrl >> 32) != tag || (uint32_t)(e.ctrl & kLenMask) != len) continue;
     if (len <= 16 && !(e.ctrl & kHeapKey)) {
@@ -2322,7 +2326,6 @@ __global__ __launch_bounds__(kAggRegionThreads) __attribute__((amdgpu_waves_per_
 struct AggLdsP {
   unsigned long long K[kFreqSliceSlots];
   uint32_t C[kFreqSliceSlots];
-  uint16_t map[kFreqSliceSlots];  // compact write-out: the slot of the slice's i-th group
   uint32_t wsum[4];
   int overflow;
   uint32_t fresh;
@@ -2377,7 +2380,8 @@ __device__ inline bool lds_count_packed(unsigned long long* K, uint32_t* C, uint
 constexpr int kAggPBatch = DQ_AGGP_BATCH;  // packed records per thread loaded together
 
 #ifndef DQ_AGGP_WAVES
-#define DQ_AGGP_WAVES 8  // (registers allow 5: the compiler warns, the measured build)
+#define DQ_AGGP_WAVES 6  // (80 VGPRs, no spill; asking for 8 left the compiler at 84 VGPRs = 5 waves once
+                         // the compacted write-out was added -- round 5's build reached 6 at 77)
 #endif
 #ifndef DQ_AGGP_THREADS
 #define DQ_AGGP_THREADS 256
@@ -2504,10 +2508,7 @@ __global__ __launch_bounds__(kAggPThreads) __attribute__((amdgpu_waves_per_eu(DQ
         }
       }
       uint32_t tot;
-      uint32_t k = block_prefix<NT>((uint32_t)__builtin_popcount(occ), L.wsum, &tot);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (occ & (1u << j)) L.map[k++] = (uint16_t)(8u * t + (uint32_t)j);
+      const uint32_t k = block_prefix<NT>((uint32_t)__builtin_popcount(occ), L.wsum, &tot);
       tr.cmp.bits[(b << 8) + t] = (uint8_t)occ;
       if (t == 0) {
         const unsigned long long at = atomicAdd(tr.cmp.cursor, (unsigned long long)tot);
@@ -2517,20 +2518,18 @@ __global__ __launch_bounds__(kAggPThreads) __attribute__((amdgpu_waves_per_eu(DQ
         if (tot) atomicAdd(new_groups, (unsigned long long)tot);
       }
       lds_barrier();
-      ulonglong2* out = reinterpret_cast<ulonglong2*>(tr.cmp.slots + L.cbase);
-      for (uint32_t q = t; q < 2u * tot; q += NT) {
-        const uint32_t s = L.map[q >> 1];
-        const uint64_t p = L.K[s];
-        if (!(q & 1u)) {
-          const uint32_t len = p == kPackNull ? 9u : (uint32_t)(p >> 60);
-          out[q] = ulonglong2{((unsigned long long)tag_of(hash_record_packed(p)) << 32) | kReady | len,
-                              (unsigned long long)L.C[s]};
-        } else {
-          uint64_t k0, k1;
-          uint32_t len;
-          kp_unpack(p, &k0, &k1, &len);
-          out[q] = ulonglong2{k0, k1};
-        }
+      // each thread writes its own groups (~3 at C4's load), whole 32-B records at consecutive
+      // positions: every store fills whole sectors, and the wave's stores fill whole lines
+      FreqSlot* out = tr.cmp.slots + L.cbase + k;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (!(occ & (1u << j))) continue;
+        const uint64_t p = L.K[8u * t + (uint32_t)j];
+        uint64_t k0, k1;
+        uint32_t len;
+        kp_unpack(p, &k0, &k1, &len);
+        *out++ = FreqSlot{((unsigned long long)tag_of(hash_record_packed(p)) << 32) | kReady | len,
+                          (unsigned long long)L.C[8u * t + (uint32_t)j], k0, k1};  // (re-read: registers)
       }
       if (tr.smax && t == 0) tr.smax[b] = L.cmax;
     } else {
@@ -2734,7 +2733,6 @@ struct AggLdsH {
   unsigned long long K[kFreqSliceSlots];
   unsigned long long R[kFreqSliceSlots];
   uint32_t C[kFreqSliceSlots];
-  uint16_t map[kFreqSliceSlots];
   uint32_t wsum[4];
   int overflow;
   uint32_t fresh;
@@ -2889,11 +2887,8 @@ __global__ __launch_bounds__(kAggHThreads) void dq_freq_agg_hashed_kernel(FreqTa
       }
     }
     uint32_t tot;
-    uint32_t k = block_prefix<NT>((uint32_t)__builtin_popcount(occ), L.wsum, &tot);
+    const uint32_t k = block_prefix<NT>((uint32_t)__builtin_popcount(occ), L.wsum, &tot);
     if (compact) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (occ & (1u << j)) L.map[k++] = (uint16_t)(8u * t + (uint32_t)j);
       tr.cmp.bits[(b << 8) + t] = (uint8_t)occ;
       if (t == 0) {
         const unsigned long long at = atomicAdd(tr.cmp.cursor, (unsigned long long)tot);
@@ -2902,8 +2897,13 @@ __global__ __launch_bounds__(kAggHThreads) void dq_freq_agg_hashed_kernel(FreqTa
         tr.cmp.num[b] = tot;
       }
       lds_barrier();
-      ulonglong2* out = reinterpret_cast<ulonglong2*>(tr.cmp.slots + L.cbase);
-      for (uint32_t q = t; q < 2u * tot; q += NT) out[q] = half(L.map[q >> 1], (q & 1u) != 0u);
+      ulonglong2* out = reinterpret_cast<ulonglong2*>(tr.cmp.slots + L.cbase + k);  // (as the packed kernel)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (!(occ & (1u << j))) continue;
+        *out++ = half(8u * t + (uint32_t)j, false);
+        *out++ = half(8u * t + (uint32_t)j, true);
+      }
     } else {
       for (uint32_t q = t; q < 2u * S; q += NT) {
         const uint32_t s = q >> 1;
@@ -3549,8 +3549,9 @@ hipError_t launch_freq_hash(const uint64_t* d_k0, const uint64_t* d_k1, const ui
 }
 
 hipError_t launch_freq_lookup(const FreqTable& T, const uint8_t* d_key, uint32_t len, unsigned long long* d_out,
-                              hipStream_t stream) {
-  hipLaunchKernelGGL(dq_freq_lookup_kernel, dim3(1), dim3(64), 0, stream, T, d_key, len, d_out);
+                              hipStream_t stream, const FreqCompact* cmp) {
+  hipLaunchKernelGGL(dq_freq_lookup_kernel, dim3(1), dim3(64), 0, stream, T, d_key, len, d_out,
+                     cmp ? *cmp : FreqCompact{});
   return hipGetLastError();
 }
 

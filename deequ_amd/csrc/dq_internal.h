@@ -312,7 +312,7 @@ hipError_t launch_freq_import_flat(const FreqTable& T, const long long* d_counts
 hipError_t launch_freq_hash(const uint64_t* d_k0, const uint64_t* d_k1, const uint32_t* d_len, int64_t n, uint64_t* d_out,
                             hipStream_t stream);
 hipError_t launch_freq_lookup(const FreqTable& T, const uint8_t* d_key, uint32_t len, unsigned long long* d_out,
-                              hipStream_t stream);
+                              hipStream_t stream, const FreqCompact* cmp = nullptr);
 hipError_t launch_freq_heap_need(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
                                  unsigned long long* d_need, unsigned long long* d_max_len, hipStream_t stream);
 // Sorted-bucket path (dq_freq.hip): stage rows as FreqRec + an HLL sketch of their hashes (to size
