@@ -19,6 +19,18 @@ for P in ${PARTS:-tests}; do
       [ $st -ne 0 ] && { grep -E "FAILED|Error" gpurun_out/${TAG}_tests.log | head -20; exit $st; } ;;
     ab)
       bash tools/r05_envab.sh || exit $? ;;
+    ab2)  # a second A/B set: WL2 / VARIANTS2 / STEPS2
+      WL=$WL2 VARIANTS=$VARIANTS2 STEPS=${STEPS2:-3} bash tools/r05_envab.sh || exit $? ;;
+    prof)  # kernel trace + stats of one bench command (PROF_ARGS, "," for spaces), PROF_ENV "A=1,B=2"
+      env $(echo "${PROF_ENV:-}" | tr ',' ' ') timeout -k 10 ${PLIMIT:-400} rocprofv3 --kernel-trace --stats \
+        -d gpurun_out/${TAG}_prof -o run --output-format csv -- python3 -u bench.py $(echo "$PROF_ARGS" | tr ',' ' ') \
+        > gpurun_out/${TAG}_prof.log 2>&1
+      st=$?
+      tail -c 1200 gpurun_out/${TAG}_prof.log
+      f=$(find gpurun_out/${TAG}_prof -name "*kernel_stats.csv" | head -1)
+      [ -n "$f" ] && cp "$f" gpurun_out/${TAG}_kernel_stats.csv && cut -d, -f1-8 gpurun_out/${TAG}_kernel_stats.csv | head -16
+      find gpurun_out/${TAG}_prof -name "*kernel_trace.csv" -delete
+      [ $st -ne 0 ] && { echo "STOP prof (exit $st)"; exit $st; } ;;
     bench)  # one bench line per BENCH_SET entry ("name:args with , for spaces")
       for b in ${BENCH_SET:-c2:}; do
         name=${b%%:*}; a=$(echo "${b#*:}" | tr ',' ' ')
