@@ -795,10 +795,38 @@ __global__ __launch_bounds__(kBlock) void dq_freq_import_flat_kernel(FreqTable T
 }
 
 // Count of one encoded key (0 if absent): a single-thread probe of the key's slice.
-// cmp.slots != nullptr: a compacted table -- the key's slice's groups are scanned instead of probed.
+// cmp.slots != nullptr: a compacted table -- the key's slice's groups are scanned (by the wave's
+// 64 lanes) instead of probed.
 __global__ void dq_freq_lookup_kernel(FreqTable T, const uint8_t* key, uint32_t len, unsigned long long* out,
                                       FreqCompact cmp) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  if (blockIdx.x != 0) return;
+  if (cmp.slots) {
+    Key k;
+    k.len = len;
+    k.k0 = len <= 16 ? ld_partial(key, len < 8 ? len : 8) : 0ull;
+    k.k1 = len > 8 && len <= 16 ? ld_partial(key + 8, len - 8) : 0ull;
+    k.hash = len <= 16 ? hash_inline(k.k0, k.k1, len) : xxh64_any(key, len, 42);
+    const uint32_t tag = tag_of(k.hash);
+    const uint64_t b = slice_of(T, k.hash);
+    const FreqSlot* g = cmp.slots + cmp.base[b];
+    const uint32_t n = cmp.num[b];
+    if (threadIdx.x == 0) *out = 0ull;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+      const FreqSlot e = g[i];
+      if ((uint32_t)(e.ctrl >> 32) != tag || (uint32_t)(e.ctrl & kLenMask) != len) continue;
+      bool eq;
+      if (len <= 16 && !(e.ctrl & kHeapKey)) {
+        eq = e.k0 == k.k0 && e.k1 == k.k1;
+      } else {
+        eq = (e.ctrl & kHeapKey) != 0;
+        for (uint32_t j = 0; eq && j < len; ++j) eq = T.heap[e.k0 + j] == key[j];
+      }
+      if (eq) *out = e.count;  // (one group holds the key)
+    }
+    return;
+  }
+  if (threadIdx.x != 0) return;
   Key k;
   k.len = len;
   k.k0 = k.k1 = 0;
@@ -813,10 +841,8 @@ __global__ void dq_freq_lookup_kernel(FreqTable T, const uint8_t* key, uint32_t 
   }
   const uint32_t tag = tag_of(k.hash);
   *out = 0ull;
-  const uint64_t b = slice_of(T, k.hash);
-  const uint64_t n_scan = cmp.slots ? cmp.num[b] : kFreqSliceSlots;
-  for (uint64_t i = 0; i < n_scan; ++i) {
-    const FreqSlot& e = cmp.slots ? cmp.slots[cmp.base[b] + i] : T.slots[probe_slot(T, k.hash, i)];
+  for (uint64_t i = 0; i < kFreqSliceSlots; ++i) {
+    const FreqSlot& e = T.slots[probe_slot(T, k.hash, i)];
     if (e.ctrl == 0ull) return;  // launch boundary: the table is complete and visible
     if ((uint32_t)(e.ctrl >> 32) != tag || (uint32_t)(e.ctrl & kLenMask) != len) continue;
     if (len <= 16 && !(e.ctrl & kHeapKey)) {
@@ -2601,70 +2627,84 @@ __global__ __launch_bounds__(kAggPThreads) __attribute__((amdgpu_waves_per_eu(DQ
 // pairs per 1e9 distinct keys) hands its records to the global inserts, which compare keys.
 
 // Exact heap bytes the hashed stage appends for rows [0, n_rows): sum of 8-aligned key lengths.
+// The encoded key length of `row` (make_key's encoding) in *n; false when the row is no key.
+__device__ inline bool key_len_of(const FreqKeySpec& ks, const DevColumn* cols, int64_t row, uint32_t* n) {
+  uint32_t m = 0;
+  for (int i = 0; i < ks.n_keys; ++i) {
+    const DevColumn& c = cols[ks.key_cols[i]];
+    if (!col_valid(c, row)) {
+      if (ks.n_keys == 1 && ks.null_as_key) {  // "NullValue" / the empty key
+        *n = c.type == DQ_T_UTF8 ? 9u : 0u;
+        return true;
+      }
+      return false;
+    }
+    if (c.type == DQ_T_UTF8) m += (uint32_t)(c.offsets[row + 1] - c.offsets[row]) + (ks.n_keys > 1 ? 4u : 0u);
+    else m += (uint32_t)width_of(c.type);
+  }
+  *n = m;
+  return true;
+}
+
 __global__ __launch_bounds__(kBlock) void dq_freq_key_bytes_kernel(FreqKeySpec ks, const DevColumn* __restrict__ cols,
                                                                    int64_t n_rows, unsigned long long* out) {
   unsigned long long local = 0;
   for (int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x; row < n_rows; row += (int64_t)gridDim.x * kBlock) {
-    uint32_t n = 0;
-    bool key = true;
-    for (int i = 0; i < ks.n_keys; ++i) {
-      const DevColumn& c = cols[ks.key_cols[i]];
-      const bool valid = col_valid(c, row);
-      if (!valid) {
-        if (ks.n_keys == 1 && ks.null_as_key) {
-          n = c.type == DQ_T_UTF8 ? 9u : 0u;  // "NullValue" / the empty key
-          continue;
-        }
-        key = false;
-        break;
-      }
-      if (c.type == DQ_T_UTF8) n += (uint32_t)(c.offsets[row + 1] - c.offsets[row]) + (ks.n_keys > 1 ? 4u : 0u);
-      else n += (uint32_t)width_of(c.type);
-    }
-    if (key) local += ((unsigned long long)n + 7ull) & ~7ull;
+    uint32_t n;
+    if (key_len_of(ks, cols, row, &n)) local += ((unsigned long long)n + 7ull) & ~7ull;
   }
   for (int d = 32; d >= 1; d >>= 1) local += __shfl_xor(local, d, 64);
   if ((threadIdx.x & 63u) == 0 && local) atomicAdd(out, local);
 }
 
+// One tile = kHashTile rows (kHashPer per thread, rows t, t + NT, ...): the rows' key lengths
+// first, a workgroup prefix sum, ONE heap reservation per tile (a reservation per wave put 15M
+// atomics on one address per 1e9 rows: the stage ran at 0.5 TB/s), then each thread copies its
+// rows' keys to consecutive heap positions and writes their records in row order.
+constexpr int kHashPer = 16;
+constexpr uint32_t kHashTile = (uint32_t)kBlock * kHashPer;
 __global__ __launch_bounds__(kBlock) void dq_freq_stage_hashed_kernel(FreqKeySpec ks, const DevColumn* __restrict__ cols,
                                                                       int64_t n_rows, HashRec* __restrict__ out, FreqTable T,
                                                                       uint32_t* hll, unsigned long long* too_long,
                                                                       unsigned long long* staged,
                                                                       unsigned long long* max_len) {
+  static_assert(kBlock / 64 <= 4, "block_prefix: up to four waves");
   __shared__ uint32_t regs[kHllM];
+  __shared__ uint32_t wsum[4];
+  __shared__ unsigned long long tile_base;
   for (uint32_t i = threadIdx.x; i < (uint32_t)kHllM; i += kBlock) regs[i] = 0xFFFFFFFFu;  // (stage_sketch)
   __syncthreads();
   alignas(8) uint8_t scratch[kMaxLocalKey];
-  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t t = threadIdx.x;
   unsigned long long n_keys = 0;
   uint32_t longest = 0u;
   bool tl_any = false;
-  // wave-uniform trip count: every lane takes part in each iteration's scan
-  for (int64_t base = (int64_t)blockIdx.x * kBlock; base < n_rows; base += (int64_t)gridDim.x * kBlock) {
-    const int64_t row = base + threadIdx.x;
-    Key k;
-    bool tl = false, ok = false;
-    if (row < n_rows) ok = make_key(ks, cols, row, k, scratch, tl);
-    tl_any |= tl;
-    const uint32_t a = ok ? ((k.len + 7u) & ~7u) : 0u;
-    uint32_t x = a;  // inclusive scan of the aligned lengths over the wave
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(x, d, 64);
-      if (lane >= (uint32_t)d) x += y;
+  const int64_t n_tiles = (n_rows + kHashTile - 1) / kHashTile;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const int64_t row0 = tile * (int64_t)kHashTile;
+    uint32_t mine = 0u;  // this thread's heap bytes in the tile
+#pragma unroll 4
+    for (int j = 0; j < kHashPer; ++j) {
+      const int64_t row = row0 + (int64_t)j * kBlock + t;
+      uint32_t n;
+      if (row < n_rows && key_len_of(ks, cols, row, &n)) mine += (n + 7u) & ~7u;
     }
-    unsigned long long wbase = 0ull;
-    if (lane == 63u && x) wbase = atomicAdd(T.heap_used, (unsigned long long)x);
-    wbase = __shfl(wbase, 63, 64);
-    const unsigned long long off = wbase + (x - a);
-    HashRec r;
-    r.h = 0ull;
-    r.ref = kHashHole;
-    if (ok) {
-      if (off + a > T.heap_cap) {
-        atomicOr(T.overflow, 2u);  // (the host sized the heap for the batch: never expected)
-      } else {
+    uint32_t total;
+    const uint32_t before = block_prefix<kBlock>(mine, wsum, &total);
+    if (t == 0) tile_base = total ? atomicAdd(T.heap_used, (unsigned long long)total) : 0ull;
+    __syncthreads();
+    unsigned long long off = tile_base + before;
+    const bool room = tile_base + total <= T.heap_cap;  // (the host sized the heap: never false)
+    if (!room && t == 0) atomicOr(T.overflow, 2u);
+    for (int j = 0; j < kHashPer; ++j) {
+      const int64_t row = row0 + (int64_t)j * kBlock + t;
+      if (row >= n_rows) break;
+      Key k;
+      bool tl = false;
+      HashRec r;
+      r.h = 0ull;
+      r.ref = kHashHole;
+      if (make_key(ks, cols, row, k, scratch, tl) && room) {
         unsigned long long* dst = reinterpret_cast<unsigned long long*>(T.heap + off);
         if (k.ptr == nullptr) {  // an inline key (<= 16 bytes) in k0 / k1, zero padded
           if (k.len) dst[0] = k.k0;
@@ -2674,19 +2714,22 @@ __global__ __launch_bounds__(kBlock) void dq_freq_stage_hashed_kernel(FreqKeySpe
         }
         r.h = k.hash;
         r.ref = (off << 24) | k.len;
+        off += (k.len + 7u) & ~7u;
         stage_sketch(regs, k.hash);
         ++n_keys;
         longest = max(longest, k.len);
       }
+      tl_any |= tl;
+      out[row] = r;
     }
-    if (row < n_rows) out[row] = r;
+    __syncthreads();  // (wsum and tile_base are rewritten by the next tile)
   }
+  const uint32_t lane = t & 63u;
   for (int d = 32; d >= 1; d >>= 1) n_keys += __shfl_xor(n_keys, d, 64);
   if (staged && lane == 0u && n_keys) atomicAdd(staged, n_keys);
   if (max_len && longest) atomicMax(max_len, (unsigned long long)longest);
   if (tl_any) atomicMax(too_long, (unsigned long long)kMaxLocalKey + 1ull);
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < (uint32_t)kHllM; i += kBlock)
+  for (uint32_t i = t; i < (uint32_t)kHllM; i += kBlock)
     if (regs[i] != 0xFFFFFFFFu) atomicMax(&hll[i], stage_sketch_rank(regs[i]));
 }
 
@@ -3407,6 +3450,34 @@ hipError_t launch_freq_expand(const FreqTable& T, const FreqCompact& cmp, hipStr
   return hipGetLastError();
 }
 
+// The heap bytes of exported groups (ctrl / k0 as launch_freq_export writes them) gathered to
+// dst at off[i] (heap keys only): a top-N export of a table whose heap holds every row's key (the
+// hashed path) moves its few keys, not the whole heap.
+__global__ __launch_bounds__(kBlock) void dq_freq_gather_keys_kernel(const uint8_t* __restrict__ heap,
+                                                                     const unsigned long long* __restrict__ ctrl,
+                                                                     const unsigned long long* __restrict__ k0,
+                                                                     const unsigned long long* __restrict__ off,
+                                                                     uint64_t n, uint8_t* __restrict__ dst) {
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    const unsigned long long c = ctrl[i];
+    if (!(c & kHeapKey)) continue;
+    const uint32_t words = (uint32_t)(((c & kLenMask) + 7ull) >> 3);
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(heap + k0[i]);
+    unsigned long long* d = reinterpret_cast<unsigned long long*>(dst + off[i]);
+    for (uint32_t w = 0; w < words; ++w) d[w] = src[w];
+  }
+}
+
+hipError_t launch_freq_gather_keys(const uint8_t* d_heap, const unsigned long long* d_ctrl, const unsigned long long* d_k0,
+                                   const unsigned long long* d_off, uint64_t n, uint8_t* d_dst, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  uint64_t blocks = (n + kBlock - 1) / kBlock;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(dq_freq_gather_keys_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, d_heap, d_ctrl, d_k0,
+                     d_off, n, d_dst);
+  return hipGetLastError();
+}
+
 hipError_t launch_freq_key_bytes(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
                                  unsigned long long* d_out, hipStream_t stream) {
   if (n_rows <= 0) return hipSuccess;
@@ -3420,7 +3491,7 @@ hipError_t launch_freq_stage_hashed(const FreqKeySpec& ks, const DevColumn* d_co
                                     const FreqTable& T, uint32_t* d_hll, unsigned long long* d_too_long,
                                     unsigned long long* d_staged, unsigned long long* d_max_len, hipStream_t stream) {
   if (n_rows <= 0) return hipSuccess;
-  int64_t blocks = (n_rows + kBlock * 4 - 1) / (kBlock * 4);
+  int64_t blocks = (n_rows + kHashTile - 1) / kHashTile;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(dq_freq_stage_hashed_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, ks, d_cols, n_rows,
                      d_out, T, d_hll, d_too_long, d_staged, d_max_len);

@@ -390,6 +390,9 @@ hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, bool p
 hipError_t launch_freq_stage_hashed(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, HashRec* d_out,
                                     const FreqTable& T, uint32_t* d_hll, unsigned long long* d_too_long,
                                     unsigned long long* d_staged, unsigned long long* d_max_len, hipStream_t stream);
+// Heap bytes of exported groups gathered to d_dst at d_off[i] (8-byte aligned; heap keys only).
+hipError_t launch_freq_gather_keys(const uint8_t* d_heap, const unsigned long long* d_ctrl, const unsigned long long* d_k0,
+                                   const unsigned long long* d_off, uint64_t n, uint8_t* d_dst, hipStream_t stream);
 // Exact bytes the stage will append to the heap for n_rows rows (sum of 8-aligned key lengths).
 hipError_t launch_freq_key_bytes(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
                                  unsigned long long* d_out, hipStream_t stream);
