@@ -678,12 +678,18 @@ def _pmc_traffic(workload: str):
     other kernels is never quoted (None, with the reason in traffic_source)."""
     import glob
     digest = kernel_source_digest()
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic_%s*.json" % workload)), reverse=True):
+    base, _, keys = workload.partition("_")  # e.g. "c4_uuid": the c4 workload with --c4-keys uuid
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic_%s*.json" % base)), reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
         except Exception:  # noqa: BLE001
             continue
+        args = d.get("bench_args", "")
+        shape = args.split("--c4-keys", 1)[1].split()[0] if "--c4-keys" in args else ""
+        shape = "" if shape == "digits" else shape
+        if d.get("workload", base) != base or shape != keys:
+            continue  # (another workload, or the same one with another key shape)
         if d.get("kernel_src_digest") == digest:
             return d["hbm_bytes_per_step"], "copied from %s (PMC pass of this bench at its default size, kernel " \
                 "sources %s)" % (os.path.relpath(path, ROOT), digest)
