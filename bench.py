@@ -979,6 +979,12 @@ def run_c5(args, world, rank, local):
     few_path = world == 1 and os.environ.get("DEEQU_AMD_PROFILE_FEW", "1") != "0"
     pass3 = sum(_column_bytes(cols[n]) for n, c in p.items()
                 if c.histogram is not None and not (few_path and cols[n].dtype == "string"))
+    roof = _step_roofline(pass1 + pass2 + pass3, step_s,
+                          "one whole profile per GPU (3 passes; bytes = what each pass must read: pass 1 every column once, pass 2 the numeric-typed strings cast + re-scanned, pass 3 the histogram columns pass 1 did not group)",
+                          workload="c5" if world == 1 else None, default_size=args.c5_rows == 100_000_000)
+    # the same step priced as if every column were read from HBM exactly once (no pass re-reads a
+    # column, no cast output written and read back): the bound of a single-pass profiler
+    roof["one_read_per_column"] = {"bytes": pass1, "frac": pass1 / step_s / 1e9 / roof["peak"]}
     return {
         "metric": "rows/sec for ColumnProfilerRunner (C5)", "value": args.c5_rows * world * args.steps / elapsed,
         "unit": "rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -987,9 +993,7 @@ def run_c5(args, world, rank, local):
         "config": {"workload": "C5: %d rows/GPU x 100 columns (40 int64, 30 fp64, 10 low- and 10 high-cardinality "
                                "utf8, 10 bool); ColumnProfilerRunner, 3 passes, KLL off (reference default)"
                                % args.c5_rows},
-        "roofline": _step_roofline(pass1 + pass2 + pass3, step_s,
-                                   "one whole profile per GPU (3 passes; bytes = what each pass must read: pass 1 every column once, pass 2 the numeric-typed strings cast + re-scanned, pass 3 the histogram columns pass 1 did not group)",
-                                   workload="c5" if world == 1 else None, default_size=args.c5_rows == 100_000_000),
+        "roofline": roof,
         "check": {"columns": len(p), "histograms": n_hist,
                   "s00_distinct": p["s00"].approximateNumDistinctValues,
                   "l00_completeness": p["l00"].completeness, "numRecords": profiles.numRecords},

@@ -1001,8 +1001,48 @@ struct AggLds {
   uint32_t fresh;
   uint32_t cmax;
   unsigned long long retry_base;
+  unsigned long long cbase;     // (compacted write-out)
+  uint32_t wsum[8];
   uint32_t hist[kAggLdsHist];
 };
+
+// One tile's multi-split: each thread holds kPartPerThread records and their LDS bins (bin <
+// 2^bin_bits, or kPartNoBin for none); output region of a bin = base_id + bin.  Ranks come from
+// LDS atomics, the room in each region from ONE device atomic per (tile, non-empty bin), and the
+// records are written from an LDS image sorted by bin, kPartSub at a time (coalesced runs).
+// A workgroup barrier for LDS only: the LDS writes before it complete (lgkmcnt) but global loads
+// and stores stay in flight across it -- __syncthreads() would wait for every outstanding vector
+// memory operation (the write-out's stores, the reservation's no-return atomics, loads already
+// issued) at each of a tile's barriers.  Used where the barrier orders LDS data only.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Exclusive prefix of v over a workgroup of NT threads (NT / 64 <= 8 waves; wsum holds NT / 64); *total = the sum.
+// Every thread must call it (it holds a barrier).
+template <int NT>
+__device__ inline uint32_t block_prefix(uint32_t v, uint32_t* wsum, uint32_t* total) {
+  static_assert(NT % 64 == 0 && NT / 64 <= 8, "block_prefix: up to eight waves");
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63u) wsum[wave] = x;
+  lds_barrier();
+  uint32_t before = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) {
+    before += (uint32_t)w < wave ? wsum[w] : 0u;
+    tot += wsum[w];
+  }
+  *total = tot;
+  return before + x - v;
+}
 
 // What a partition-path aggregation into an EMPTY table also produces (nullptr / 0 = off):
 // the count-of-counts histogram of the new groups (so the metrics need no table scan), the
@@ -1166,9 +1206,52 @@ __device__ void agg_item(AggLds& L, const FreqTable& T, const FreqRec* __restric
       if (threadIdx.x == 0) retry_base = atomicAdd(n_retry, (unsigned long long)(r1 - r0));
       __syncthreads();
       for (uint64_t i = r0 + threadIdx.x; i < r1; i += NT) retry[retry_base + (i - r0)] = recs[i];
-      if (tr && tr->write_all)  // (the table was not cleared: the slice starts out empty)
+      if (tr && tr->cmp.slots) {
+        if (threadIdx.x == 0) tr->cmp.num[b] = 0u;  // (the slice starts out empty)
+      } else if (tr && tr->write_all) {  // (the table was not cleared: the slice starts out empty)
         for (uint32_t s = threadIdx.x; s < S; s += NT) slice[s] = FreqSlot{0ull, 0ull, 0ull, 0ull};
+      }
       if (tr && tr->smax && threadIdx.x == 0) tr->smax[b] = 0xFFFFFFFFu;  // unknown: never skipped
+    } else if (tr && tr->cmp.slots) {
+      // Occupied slots only (an empty table; as dq_freq_agg_packed_kernel): thread t owns slots
+      // PER t .. PER t + PER - 1, its groups stored at consecutive places in slot order.
+      constexpr uint32_t PER = S / (uint32_t)NT;
+      static_assert(PER == 4u || PER == 8u, "four or eight slots per thread");
+      const uint32_t t = threadIdx.x;
+      uint32_t occ = 0u;
+#pragma unroll
+      for (uint32_t j = 0; j < PER; ++j) {
+        const uint32_t c = C[PER * t + j];
+        if (!c) continue;
+        occ |= 1u << j;
+        track_count(L, *tr, c);
+      }
+      uint32_t tot;
+      const uint32_t k = block_prefix<NT>((uint32_t)__builtin_popcount(occ), L.wsum, &tot);
+      if constexpr (PER == 8u) {
+        tr->cmp.bits[(b << 8) + t] = (uint8_t)occ;
+      } else {
+        const uint32_t hi = __shfl_down(occ, 1, 64);
+        if (!(t & 1u)) tr->cmp.bits[(b << 8) + (t >> 1)] = (uint8_t)(occ | (hi << 4));
+      }
+      if (t == 0) {
+        const unsigned long long at = atomicAdd(tr->cmp.cursor, (unsigned long long)tot);
+        L.cbase = at;
+        tr->cmp.base[b] = at;
+        tr->cmp.num[b] = tot;
+        if (tot) atomicAdd(new_groups, (unsigned long long)tot);
+      }
+      __syncthreads();
+      FreqSlot* out = tr->cmp.slots + L.cbase + k;
+#pragma unroll
+      for (uint32_t j = 0; j < PER; ++j) {
+        if (!(occ & (1u << j))) continue;
+        const uint32_t s = PER * t + j;
+        const unsigned long long k1 = K1[s];
+        *out++ = FreqSlot{((unsigned long long)L.G[s] << 32) | kReady | (uint32_t)(k1 >> kRecLenShift),
+                          (unsigned long long)C[s], K0[s], k1 & kRecKeyMask};
+      }
+      if (tr->smax && t == 0) tr->smax[b] = L.cmax;
     } else {
       for (uint32_t s = threadIdx.x; s < S; s += NT) {
         const uint32_t c = C[s];
@@ -1349,19 +1432,6 @@ __device__ unsigned long long g_stage_blk[4096][2];  // per workgroup: wall-cloc
 #define DQ_PROF_MARK(PROF, i) do { } while (0)
 #endif
 
-// One tile's multi-split: each thread holds kPartPerThread records and their LDS bins (bin <
-// 2^bin_bits, or kPartNoBin for none); output region of a bin = base_id + bin.  Ranks come from
-// LDS atomics, the room in each region from ONE device atomic per (tile, non-empty bin), and the
-// records are written from an LDS image sorted by bin, kPartSub at a time (coalesced runs).
-// A workgroup barrier for LDS only: the LDS writes before it complete (lgkmcnt) but global loads
-// and stores stay in flight across it -- __syncthreads() would wait for every outstanding vector
-// memory operation (the write-out's stores, the reservation's no-return atomics, loads already
-// issued) at each of a tile's barriers.  Used where the barrier orders LDS data only.
-__device__ __forceinline__ void lds_barrier() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
 
 struct NoMid {
   __device__ void operator()() const {}
@@ -2325,14 +2395,16 @@ __global__ __launch_bounds__(kAggRegionThreads) __attribute__((amdgpu_waves_per_
       if (i < r1) touch = *reinterpret_cast<const uint32_t*>(recs + i);
     }
     if (r1 == r0) {
-      if (tr.write_all) {
+      if (tr.cmp.slots) {
+        if (threadIdx.x == 0) tr.cmp.num[b] = 0u;
+      } else if (tr.write_all) {
         FreqSlot* slice = T.slots + (b << kFreqSliceLog);
         for (uint32_t s = threadIdx.x; s < (uint32_t)kFreqSliceSlots; s += kAggRegionThreads) slice[s] = FreqSlot{0ull, 0ull, 0ull, 0ull};
       }
       if (tr.smax && threadIdx.x == 0) tr.smax[b] = 0u;
     } else {
       agg_item<kAggRegionThreads, true>(L, T, recs, r0, r1, b, true, table_empty, retry, n_retry, new_groups,
-                                        track || tr.write_all ? &tr : nullptr);
+                                        track || tr.write_all || tr.cmp.slots ? &tr : nullptr);
     }
     asm volatile("" ::"v"(touch));
   }
@@ -2360,30 +2432,6 @@ struct AggLdsP {
   unsigned long long cbase;
   uint32_t hist[kAggLdsHist];
 };
-
-// Exclusive prefix of v over a workgroup of NT threads (NT / 64 <= 4 waves); *total = the sum.
-// Every thread must call it (it holds a barrier).
-template <int NT>
-__device__ inline uint32_t block_prefix(uint32_t v, uint32_t* wsum, uint32_t* total) {
-  static_assert(NT % 64 == 0 && NT / 64 <= 4, "block_prefix: up to four waves");
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
-    if (lane >= (uint32_t)d) x += y;
-  }
-  if (lane == 63u) wsum[wave] = x;
-  lds_barrier();
-  uint32_t before = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < NT / 64; ++w) {
-    before += (uint32_t)w < wave ? wsum[w] : 0u;
-    tot += wsum[w];
-  }
-  *total = tot;
-  return before + x - v;
-}
 
 // Count packed record p from LDS slot s on (probe `first` of its run); false if the image is full.
 __device__ inline bool lds_count_packed(unsigned long long* K, uint32_t* C, uint64_t p, uint32_t s, uint32_t first = 0) {
@@ -2657,74 +2705,254 @@ __global__ __launch_bounds__(kBlock) void dq_freq_key_bytes_kernel(FreqKeySpec k
   if ((threadIdx.x & 63u) == 0 && local) atomicAdd(out, local);
 }
 
-// One tile = kHashTile rows (kHashPer per thread, rows t, t + NT, ...): the rows' key lengths
-// first, a workgroup prefix sum, ONE heap reservation per tile (a reservation per wave put 15M
-// atomics on one address per 1e9 rows: the stage ran at 0.5 TB/s), then each thread copies its
-// rows' keys to consecutive heap positions and writes their records in row order.
+// xxh64_any(p, len, seed) of a key held in registers: kw[i] = its bytes 8i .. 8i + 7 (little
+// endian, zero past len), len <= 8 * MW.  The same stripes, words and tail as xxh64_any.
+template <int MW>
+__device__ inline uint64_t xxh64_words(const uint64_t (&kw)[MW], uint32_t len, uint64_t seed) {
+  const uint32_t stripes = len >> 5, full = len >> 3;
+  uint64_t h;
+  if (stripes) {
+    uint64_t v1 = seed + kP1 + kP2, v2 = seed + kP2, v3 = seed, v4 = seed - kP1;
+#pragma unroll
+    for (int st = 0; st < MW / 4; ++st) {
+      if ((uint32_t)st < stripes) {
+        v1 = xxh_round(v1, kw[4 * st]);
+        v2 = xxh_round(v2, kw[4 * st + 1]);
+        v3 = xxh_round(v3, kw[4 * st + 2]);
+        v4 = xxh_round(v4, kw[4 * st + 3]);
+      }
+    }
+    h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+    h ^= xxh_round(0, v1); h = h * kP1 + kP4;
+    h ^= xxh_round(0, v2); h = h * kP1 + kP4;
+    h ^= xxh_round(0, v3); h = h * kP1 + kP4;
+    h ^= xxh_round(0, v4); h = h * kP1 + kP4;
+  } else {
+    h = seed + kP5;
+  }
+  h += (uint64_t)len;
+  uint64_t tail = 0ull;
+#pragma unroll
+  for (int i = 0; i < MW; ++i) {
+    if ((uint32_t)i >= 4u * stripes && (uint32_t)i < full) {
+      h ^= xxh_round(0, kw[i]);
+      h = rotl64(h, 27) * kP1 + kP4;
+    }
+    if ((uint32_t)i == full) tail = kw[i];
+  }
+  if (len & 7u) {
+    h ^= tail * kP5;
+    h = rotl64(h, 11) * kP1;
+  }
+  return xxh_avalanche(h);
+}
+
+// One row of the hashed stage the general way (make_key): its key bytes to heap + off, its
+// record in *r; the heap bytes it used (0 when the row is no key).  Multi-column keys, NULLs
+// and keys longer than the register path's 48 bytes.
+__device__ __noinline__ uint32_t stage_hashed_row(const FreqKeySpec& ks, const DevColumn* cols, int64_t row,
+                                                  const FreqTable& T, unsigned long long off, HashRec* r,
+                                                  bool* tl) {
+  alignas(8) uint8_t scratch[kMaxLocalKey];
+  Key k;
+  r->h = 0ull;
+  r->ref = kHashHole;
+  if (!make_key(ks, cols, row, k, scratch, *tl)) return 0u;
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(T.heap + off);
+  if (k.ptr == nullptr) {  // an inline key (<= 16 bytes) in k0 / k1, zero padded
+    if (k.len) dst[0] = k.k0;
+    if (k.len > 8) dst[1] = k.k1;
+  } else {
+    for (uint32_t i = 0; i < k.len; i += 8) dst[i >> 3] = ld_partial(k.ptr + i, k.len - i < 8 ? k.len - i : 8);
+  }
+  r->h = k.hash;
+  r->ref = (off << 24) | k.len;
+  return (k.len + 7u) & ~7u;
+}
+
+// A multi-column key (make_key's encoding: fixed-width values' little-endian bytes, strings as
+// a u32 length + their bytes) built in registers, kw[i] = bytes 8i .. 8i + 7, zero past *n.
+// False when a column is NULL (no key) or the key is longer than 8 * MW bytes (*n = 0: the
+// caller takes make_key).
+template <int MW>
+__device__ inline bool key_words(const FreqKeySpec& ks, const DevColumn* cols, int64_t row, uint64_t (&kw)[MW],
+                                 uint32_t* n_out) {
+  uint32_t n = 0;
+#pragma unroll
+  for (int i = 0; i < MW; ++i) kw[i] = 0ull;
+  *n_out = 0u;
+  // v's low nb (<= 8) bytes appended at byte n
+  auto put = [&](uint64_t v, uint32_t nb) {
+    if (nb < 8u) v &= (1ull << (8u * nb)) - 1ull;
+    const uint32_t wi = n >> 3, sh = 8u * (n & 7u);
+#pragma unroll
+    for (int i = 0; i < MW; ++i) {
+      if ((uint32_t)i == wi) kw[i] |= v << sh;
+      if (sh && (uint32_t)i == wi + 1u) kw[i] |= v >> (64u - sh);
+    }
+    n += nb;
+  };
+  for (int c = 0; c < ks.n_keys; ++c) {
+    const DevColumn& col = cols[ks.key_cols[c]];
+    if (!col_valid(col, row)) return false;
+    if (col.type == DQ_T_UTF8) {
+      const int32_t b = col.offsets[row], e = col.offsets[row + 1];
+      const uint32_t sl = (uint32_t)(e - b);
+      if (n + 4u + sl > 8u * MW) return false;
+      put(sl, 4u);
+      const uint8_t* p = static_cast<const uint8_t*>(col.values) + b;
+      for (uint32_t i = 0; i < sl; i += 8u) put(ld_partial(p + i, sl - i < 8u ? sl - i : 8u), sl - i < 8u ? sl - i : 8u);
+    } else {
+      const uint32_t w = (uint32_t)width_of(col.type);
+      if (n + w > 8u * MW) return false;
+      put(fixed_bits(col, row), w);
+    }
+  }
+  *n_out = n;
+  return true;
+}
+
+// One tile = kHashTile rows; wave w takes rows row0 + w * 64 * kHashPer + 64 j + lane (j <
+// kHashPer), so the heap, like the records, is in row order: the rows' key lengths first (one
+// wave prefix per j), a workgroup prefix over the waves, ONE heap reservation per tile (a
+// reservation per wave put 15M atomics on one address per 1e9 rows: the stage ran at 0.5 TB/s),
+// then each group of 64 rows copies its keys to consecutive heap bytes.  A single string key
+// column's keys of 17..48 bytes (UUIDs) take the register path: kHashG rows' offsets, then
+// their aligned words, loaded together; the key realigned in registers, hashed (xxh64_words)
+// and stored from them.  Every other row takes stage_hashed_row.
 constexpr int kHashPer = 16;
+constexpr int kHashG = 2;      // rows whose words are in flight together
+constexpr int kHashWords = 6;  // register path: keys of <= 48 bytes
 constexpr uint32_t kHashTile = (uint32_t)kBlock * kHashPer;
+template <bool ONE_STRING>
 __global__ __launch_bounds__(kBlock) void dq_freq_stage_hashed_kernel(FreqKeySpec ks, const DevColumn* __restrict__ cols,
                                                                       int64_t n_rows, HashRec* __restrict__ out, FreqTable T,
                                                                       uint32_t* hll, unsigned long long* too_long,
                                                                       unsigned long long* staged,
                                                                       unsigned long long* max_len) {
-  static_assert(kBlock / 64 <= 4, "block_prefix: up to four waves");
+  static_assert(kBlock / 64 <= 4, "four waves");
   __shared__ uint32_t regs[kHllM];
   __shared__ uint32_t wsum[4];
   __shared__ unsigned long long tile_base;
   for (uint32_t i = threadIdx.x; i < (uint32_t)kHllM; i += kBlock) regs[i] = 0xFFFFFFFFu;  // (stage_sketch)
   __syncthreads();
-  alignas(8) uint8_t scratch[kMaxLocalKey];
-  const uint32_t t = threadIdx.x;
+  const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+  constexpr bool one_string = ONE_STRING;  // (the host: ks.n_keys == 1 and a utf8 column)
+  const DevColumn c0 = cols[ks.key_cols[0]];
+  const uint8_t* bytes = static_cast<const uint8_t*>(c0.values);
   unsigned long long n_keys = 0;
   uint32_t longest = 0u;
   bool tl_any = false;
   const int64_t n_tiles = (n_rows + kHashTile - 1) / kHashTile;
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-    const int64_t row0 = tile * (int64_t)kHashTile;
-    uint32_t mine = 0u;  // this thread's heap bytes in the tile
-#pragma unroll 4
+    const int64_t rw = tile * (int64_t)kHashTile + (int64_t)wave * 64 * kHashPer + lane;  // row of j = 0
+    uint32_t off[kHashPer];  // heap offset of row j within the wave's run
+    uint32_t run = 0u;
+#pragma unroll
     for (int j = 0; j < kHashPer; ++j) {
-      const int64_t row = row0 + (int64_t)j * kBlock + t;
-      uint32_t n;
-      if (row < n_rows && key_len_of(ks, cols, row, &n)) mine += (n + 7u) & ~7u;
+      const int64_t row = rw + 64 * j;
+      uint32_t n = 0u, m8 = 0u;
+      if (row < n_rows && key_len_of(ks, cols, row, &n)) m8 = (n + 7u) & ~7u;
+      uint32_t x = m8;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+      }
+      off[j] = run + x - m8;
+      run += __shfl(x, 63, 64);
     }
-    uint32_t total;
-    const uint32_t before = block_prefix<kBlock>(mine, wsum, &total);
+    if (lane == 0u) wsum[wave] = run;
+    __syncthreads();
+    uint32_t before = 0u, total = 0u;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+      before += (uint32_t)w < wave ? wsum[w] : 0u;
+      total += wsum[w];
+    }
     if (t == 0) tile_base = total ? atomicAdd(T.heap_used, (unsigned long long)total) : 0ull;
     __syncthreads();
-    unsigned long long off = tile_base + before;
+    const unsigned long long base = tile_base + before;
     const bool room = tile_base + total <= T.heap_cap;  // (the host sized the heap: never false)
     if (!room && t == 0) atomicOr(T.overflow, 2u);
-    for (int j = 0; j < kHashPer; ++j) {
-      const int64_t row = row0 + (int64_t)j * kBlock + t;
-      if (row >= n_rows) break;
-      Key k;
-      bool tl = false;
-      HashRec r;
-      r.h = 0ull;
-      r.ref = kHashHole;
-      if (make_key(ks, cols, row, k, scratch, tl) && room) {
-        unsigned long long* dst = reinterpret_cast<unsigned long long*>(T.heap + off);
-        if (k.ptr == nullptr) {  // an inline key (<= 16 bytes) in k0 / k1, zero padded
-          if (k.len) dst[0] = k.k0;
-          if (k.len > 8) dst[1] = k.k1;
-        } else {
-          for (uint32_t i = 0; i < k.len; i += 8) dst[i >> 3] = ld_partial(k.ptr + i, k.len - i < 8 ? k.len - i : 8);
+#pragma unroll
+    for (int g = 0; g < kHashPer; g += kHashG) {
+      int32_t ob[kHashG], oe[kHashG];
+      bool fast[kHashG];
+#pragma unroll
+      for (int q = 0; q < kHashG; ++q) {
+        const int64_t row = rw + 64 * (g + q);
+        ob[q] = oe[q] = 0;
+        fast[q] = false;
+        if (one_string && row < n_rows && col_valid(c0, row)) {
+          ob[q] = c0.offsets[row];
+          oe[q] = c0.offsets[row + 1];
+          const uint32_t n = (uint32_t)(oe[q] - ob[q]);
+          fast[q] = n > 16u && n <= 8u * kHashWords;
         }
-        r.h = k.hash;
-        r.ref = (off << 24) | k.len;
-        off += (k.len + 7u) & ~7u;
-        stage_sketch(regs, k.hash);
-        ++n_keys;
-        longest = max(longest, k.len);
       }
-      tl_any |= tl;
-      out[row] = r;
+      uint64_t w[kHashG][kHashWords + 1];
+#pragma unroll
+      for (int q = 0; q < kHashG; ++q) {
+        const uintptr_t a = (uintptr_t)(bytes + ob[q]);
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(a & ~(uintptr_t)7);
+        const uint32_t span = (uint32_t)(a & 7) + (uint32_t)(oe[q] - ob[q]);
+#pragma unroll
+        for (int i = 0; i <= kHashWords; ++i) w[q][i] = fast[q] && 8u * (uint32_t)i < span ? src[i] : 0ull;
+      }
+#pragma unroll
+      for (int q = 0; q < kHashG; ++q) {
+        const int j = g + q;
+        const int64_t row = rw + 64 * j;
+        if (row >= n_rows) continue;
+        const unsigned long long at = base + off[j];
+        HashRec r;
+        uint64_t kwm[kHashWords];
+        uint32_t nm = 0u;
+        if (fast[q] && room) {
+          const uint32_t n = (uint32_t)(oe[q] - ob[q]);
+          const uint32_t sh = 8u * (uint32_t)(((uintptr_t)(bytes + ob[q])) & 7);
+          uint64_t kw[kHashWords];
+#pragma unroll
+          for (int i = 0; i < kHashWords; ++i) {
+            uint64_t v = sh ? (w[q][i] >> sh) | (w[q][i + 1] << (64u - sh)) : w[q][i];
+            const int rem = (int)n - 8 * i;  // key bytes from word i on
+            if (rem <= 0) v = 0ull;
+            else if (rem < 8) v &= (1ull << (8 * rem)) - 1ull;
+            kw[i] = v;
+          }
+          unsigned long long* dst = reinterpret_cast<unsigned long long*>(T.heap + at);
+#pragma unroll
+          for (int i = 0; i < kHashWords; ++i)
+            if (8u * (uint32_t)i < n) dst[i] = kw[i];
+          r.h = xxh64_words<kHashWords>(kw, n, 42);
+          r.ref = (at << 24) | n;
+          longest = max(longest, n);
+        } else if (!ONE_STRING && room && key_words<kHashWords>(ks, cols, row, kwm, &nm) && nm) {
+          // a multi-column key in registers (make_key's bytes without its scratch copy)
+          unsigned long long* dst = reinterpret_cast<unsigned long long*>(T.heap + at);
+#pragma unroll
+          for (int i = 0; i < kHashWords; ++i)
+            if (8u * (uint32_t)i < nm) dst[i] = kwm[i];
+          r.h = nm <= 16u ? hash_inline(kwm[0], kwm[1], nm) : xxh64_words<kHashWords>(kwm, nm, 42);
+          r.ref = (at << 24) | nm;
+          longest = max(longest, nm);
+        } else {
+          bool tl = false;
+          if (room) stage_hashed_row(ks, cols, row, T, at, &r, &tl);
+          else { r.h = 0ull; r.ref = kHashHole; }
+          tl_any |= tl;
+          if (r.ref != kHashHole) longest = max(longest, (uint32_t)(r.ref & kLenMask));
+        }
+        if (r.ref != kHashHole) {
+          stage_sketch(regs, r.h);
+          ++n_keys;
+        }
+        out[row] = r;
+      }
     }
     __syncthreads();  // (wsum and tile_base are rewritten by the next tile)
   }
-  const uint32_t lane = t & 63u;
   for (int d = 32; d >= 1; d >>= 1) n_keys += __shfl_xor(n_keys, d, 64);
   if (staged && lane == 0u && n_keys) atomicAdd(staged, n_keys);
   if (max_len && longest) atomicMax(max_len, (unsigned long long)longest);
@@ -2765,13 +2993,20 @@ __device__ inline bool heap_refs_equal(const uint8_t* heap, unsigned long long r
 
 // The owner aggregation of slice regions of hashed records into a FRESH table.  LDS image: the
 // hash (0 kept as 1), the reference of the group's first record, the count.  A workgroup takes
-// a region's records 64 per thread at a time: they are counted by hash (one CAS per probe), then
-// -- after a barrier, when every group's first reference is in place -- each record that joined an
-// existing hash group is compared with that group's first record byte for byte.  A full image
+// a region's records kAggHPer per thread at a time, all loaded together: they are counted by hash
+// (one CAS per probe, the slot remembered), then -- after a barrier, when every group's first
+// reference is in place -- each record that joined an existing hash group is compared with that
+// group's first record byte for byte, kAggHCmp records' key words loaded together (round 6's first
+// build compared word by word, one dependent heap read after another: 97 ms per 1e9 UUIDs).  A full image
 // or a mismatch (two keys of one hash) hands the slice's records to the retry list; the caller
 // inserts them globally.  Write-out as the packed aggregation: the slot image, or (tr.cmp) the
 // occupied slots only; keys of <= 16 bytes inline, longer ones referring to their heap bytes.
 constexpr int kAggHThreads = 256;
+constexpr int kAggHPer = 16;    // records per thread per chunk
+constexpr int kAggHCmp = 2;     // joined records compared together
+constexpr int kAggHWords = 6;   // key words loaded unconditionally (keys of <= 48 bytes: one round)
+static_assert(kAggHWords % 2 == 0, "key words in 16-byte pairs");
+typedef unsigned long long u64x2_a8 __attribute__((ext_vector_type(2), aligned(8)));  // (8-byte aligned pair)
 struct AggLdsH {
   unsigned long long K[kFreqSliceSlots];
   unsigned long long R[kFreqSliceSlots];
@@ -2794,14 +3029,14 @@ __device__ inline uint32_t lds_find_hash(const unsigned long long* K, unsigned l
   return S;
 }
 
-__global__ __launch_bounds__(kAggHThreads) void dq_freq_agg_hashed_kernel(FreqTable T, const HashRec* __restrict__ recs,
+__global__ __launch_bounds__(kAggHThreads) __attribute__((amdgpu_waves_per_eu(3))) void dq_freq_agg_hashed_kernel(FreqTable T, const HashRec* __restrict__ recs,
                                                                           const unsigned long long* __restrict__ fill,
                                                                           uint64_t cap, uint64_t n_slices, FreqRec* retry,
                                                                           unsigned long long* n_retry,
                                                                           unsigned long long* new_groups, AggTrack tr) {
   constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
   constexpr int NT = kAggHThreads;
-  constexpr uint32_t kChunk = 64u * NT;  // records per round (a 64-bit mask of joins per thread)
+  constexpr uint32_t kChunk = (uint32_t)kAggHPer * NT;  // records per round
   __shared__ AggLdsH L;
   const bool track = tr.hist != nullptr;
   const bool compact = tr.cmp.slots != nullptr;
@@ -2836,47 +3071,98 @@ __global__ __launch_bounds__(kAggHThreads) void dq_freq_agg_hashed_kernel(FreqTa
     lds_barrier();
     for (uint64_t c0 = r0; c0 < r1; c0 += kChunk) {
       const uint64_t c1 = c0 + kChunk < r1 ? c0 + kChunk : r1;
-      unsigned long long joined = 0ull;
-      for (uint32_t i = 0; i < 64u; i += 4u) {
-        HashRec rb[4];
+      // the chunk's records all loaded together; each counted by hash (its slot remembered)
+      HashRec rb[kAggHPer];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint64_t idx = c0 + (uint64_t)(i + j) * NT + t;
-          rb[j].ref = kHashHole;
-          if (idx < c1) rb[j] = recs[idx];
-        }
+      for (int j = 0; j < kAggHPer; ++j) {
+        const uint64_t idx = c0 + (uint64_t)j * NT + t;
+        rb[j].h = 0ull;
+        rb[j].ref = kHashHole;
+        if (idx < c1) rb[j] = recs[idx];
+      }
+      uint32_t joined = 0u;
+      uint32_t sl[kAggHPer];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (rb[j].ref == kHashHole) continue;
-          const unsigned long long kk = rb[j].h ? rb[j].h : 1ull;
-          uint32_t s = (uint32_t)rb[j].h & (S - 1u);
-          uint32_t probe = 0;
-          for (; probe < S; ++probe) {
-            const unsigned long long c = atomicCAS(&L.K[s], 0ull, kk);
-            if (c == 0ull) {
-              L.R[s] = rb[j].ref;
-              atomicAdd(&L.C[s], 1u);
-              break;
-            }
-            if (c == kk) {
-              atomicAdd(&L.C[s], 1u);
-              joined |= 1ull << (i + j);
-              break;
-            }
-            s = (s + 1u) & (S - 1u);
+      for (int j = 0; j < kAggHPer; ++j) {
+        sl[j] = 0u;
+        if (rb[j].ref == kHashHole) continue;
+        const unsigned long long kk = rb[j].h ? rb[j].h : 1ull;
+        uint32_t s = (uint32_t)rb[j].h & (S - 1u);
+        uint32_t probe = 0;
+        for (; probe < S; ++probe) {
+          const unsigned long long c = atomicCAS(&L.K[s], 0ull, kk);
+          if (c == 0ull) {
+            L.R[s] = rb[j].ref;
+            atomicAdd(&L.C[s], 1u);
+            break;
           }
-          if (probe == S) L.overflow = 1;
+          if (c == kk) {
+            atomicAdd(&L.C[s], 1u);
+            joined |= 1u << j;
+            sl[j] = s;
+            break;
+          }
+          s = (s + 1u) & (S - 1u);
         }
+        if (probe == S) L.overflow = 1;
       }
       lds_barrier();  // every group's first reference is in place
-      if (!L.overflow) {
-        while (joined) {
-          const uint32_t i = (uint32_t)__builtin_ctzll(joined);
-          joined &= joined - 1ull;
-          const HashRec r = recs[c0 + (uint64_t)i * NT + t];
-          const unsigned long long kk = r.h ? r.h : 1ull;
-          const uint32_t s = lds_find_hash(L.K, kk, (uint32_t)r.h & (S - 1u));
-          if (!heap_refs_equal(T.heap, L.R[s], r.ref)) L.overflow = 2;  // two keys, one hash (~never)
+      if (!L.overflow && joined) {
+        // each joined record compared with its group's first, kAggHCmp records' key words in
+        // flight together (a key's words are loaded unconditionally, not word by word)
+#pragma unroll
+        for (int g = 0; g < kAggHPer; g += kAggHCmp) {
+          if (!((joined >> g) & ((1u << kAggHCmp) - 1u))) continue;
+          unsigned long long ra[kAggHCmp], wa[kAggHCmp][kAggHWords], wb[kAggHCmp][kAggHWords];
+          bool todo[kAggHCmp];
+#pragma unroll
+          for (int q = 0; q < kAggHCmp; ++q) {
+            const int j = g + q;
+            todo[q] = false;
+            ra[q] = 0ull;
+            if (!((joined >> j) & 1u)) continue;
+            ra[q] = L.R[sl[j]];
+            const unsigned long long rr = rb[j].ref;
+            todo[q] = ra[q] != rr;
+            if ((ra[q] & kLenMask) != (rr & kLenMask)) {
+              L.overflow = 2;  // (a length mismatch: two keys, one hash)
+              todo[q] = false;
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < kAggHCmp; ++q) {
+            const int j = g + q;
+            const uint32_t words = (uint32_t)(((ra[q] & kLenMask) + 7ull) >> 3);
+            const unsigned long long* a = reinterpret_cast<const unsigned long long*>(T.heap + (ra[q] >> 24));
+            const unsigned long long* b = reinterpret_cast<const unsigned long long*>(T.heap + (rb[j].ref >> 24));
+            // 16-byte loads (a key's words in half the requests; heap keys are 8-byte aligned),
+            // a last odd word alone: nothing past the key's padded bytes is read
+#pragma unroll
+            for (int w = 0; w < kAggHWords; w += 2) {
+              wa[q][w] = wb[q][w] = wa[q][w + 1] = wb[q][w + 1] = 0ull;
+              if (todo[q] && (uint32_t)w + 1u < words) {
+                const u64x2_a8 x = *reinterpret_cast<const u64x2_a8*>(a + w);
+                const u64x2_a8 y = *reinterpret_cast<const u64x2_a8*>(b + w);
+                wa[q][w] = x.x;
+                wa[q][w + 1] = x.y;
+                wb[q][w] = y.x;
+                wb[q][w + 1] = y.y;
+              } else if (todo[q] && (uint32_t)w < words) {
+                wa[q][w] = a[w];
+                wb[q][w] = b[w];
+              }
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < kAggHCmp; ++q) {
+            if (!todo[q]) continue;
+            const int j = g + q;
+            bool eq = true;
+#pragma unroll
+            for (int w = 0; w < kAggHWords; ++w) eq &= wa[q][w] == wb[q][w];
+            if (eq && (ra[q] & kLenMask) > 8u * kAggHWords) eq = heap_refs_equal(T.heap, ra[q], rb[j].ref);  // (longer keys)
+            if (!eq) L.overflow = 2;  // two keys, one hash (~never)
+          }
         }
       }
       lds_barrier();
@@ -3425,7 +3711,7 @@ hipError_t launch_freq_agg_region(const FreqTable& T, const void* d_recs, int re
   if (blocks < 1) blocks = 1;
   if (!table_empty && (d_hist || d_smax || write_all)) return hipErrorInvalidValue;
   const bool packed = rec_kind == kRecPacked;
-  if (compact && (rec_kind == kRecFree || !table_empty)) return hipErrorInvalidValue;
+  if (compact && !table_empty) return hipErrorInvalidValue;
   if (rec_kind == kRecHashed && !table_empty) return hipErrorInvalidValue;  // (fresh tables only)
   AggTrack tr{d_hist, d_big, d_n_big, big_cap, d_smax, write_all, compact ? *compact : FreqCompact{}};
   if (rec_kind == kRecHashed)
@@ -3487,14 +3773,18 @@ hipError_t launch_freq_key_bytes(const FreqKeySpec& ks, const DevColumn* d_cols,
   return hipGetLastError();
 }
 
-hipError_t launch_freq_stage_hashed(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, HashRec* d_out,
+hipError_t launch_freq_stage_hashed(const FreqKeySpec& ks, bool one_string, const DevColumn* d_cols, int64_t n_rows, HashRec* d_out,
                                     const FreqTable& T, uint32_t* d_hll, unsigned long long* d_too_long,
                                     unsigned long long* d_staged, unsigned long long* d_max_len, hipStream_t stream) {
   if (n_rows <= 0) return hipSuccess;
   int64_t blocks = (n_rows + kHashTile - 1) / kHashTile;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(dq_freq_stage_hashed_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, ks, d_cols, n_rows,
-                     d_out, T, d_hll, d_too_long, d_staged, d_max_len);
+  if (one_string)
+    hipLaunchKernelGGL(dq_freq_stage_hashed_kernel<true>, dim3((unsigned)blocks), dim3(kBlock), 0, stream, ks, d_cols,
+                       n_rows, d_out, T, d_hll, d_too_long, d_staged, d_max_len);
+  else
+    hipLaunchKernelGGL(dq_freq_stage_hashed_kernel<false>, dim3((unsigned)blocks), dim3(kBlock), 0, stream, ks, d_cols,
+                       n_rows, d_out, T, d_hll, d_too_long, d_staged, d_max_len);
   return hipGetLastError();
 }
 

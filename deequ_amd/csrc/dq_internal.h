@@ -387,7 +387,7 @@ hipError_t launch_freq_stage_part(const FreqKeySpec& ks, bool one_string, bool p
 // The hashed partition path (dq_freq.hip, round 6).  Stage: every row's key (make_key: long
 // strings, several columns) is copied to the key heap (one atomic per wave) and written as a
 // HashRec in row order (holes for NULL keys); too_long: a multi-column key over kMaxLocalKey.
-hipError_t launch_freq_stage_hashed(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, HashRec* d_out,
+hipError_t launch_freq_stage_hashed(const FreqKeySpec& ks, bool one_string, const DevColumn* d_cols, int64_t n_rows, HashRec* d_out,
                                     const FreqTable& T, uint32_t* d_hll, unsigned long long* d_too_long,
                                     unsigned long long* d_staged, unsigned long long* d_max_len, hipStream_t stream);
 // Heap bytes of exported groups gathered to d_dst at d_off[i] (8-byte aligned; heap keys only).

@@ -20,7 +20,7 @@ for P in ${PARTS:-tests}; do
     ab)
       bash tools/r05_envab.sh || exit $? ;;
     ab2)  # a second A/B set: WL2 / VARIANTS2 / STEPS2
-      WL=$WL2 VARIANTS=$VARIANTS2 STEPS=${STEPS2:-3} bash tools/r05_envab.sh || exit $? ;;
+      WL=$WL2 VARIANTS=$VARIANTS2 STEPS=${STEPS2:-3} BENCH_ARGS=${BENCH_ARGS2:-${BENCH_ARGS:-}} bash tools/r05_envab.sh || exit $? ;;
     prof)  # kernel trace + stats of one bench command (PROF_ARGS, "," for spaces), PROF_ENV "A=1,B=2"
       env $(echo "${PROF_ENV:-}" | tr ',' ' ') timeout -k 10 ${PLIMIT:-400} rocprofv3 --kernel-trace --stats \
         -d gpurun_out/${TAG}_prof -o run --output-format csv -- python3 -u bench.py $(echo "$PROF_ARGS" | tr ',' ' ') \
