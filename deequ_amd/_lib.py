@@ -119,6 +119,7 @@ DIAG_SIGNATURES = {
     "dq_diag_parse_double": (c_int, [c_char_p, c_int64, POINTER(c_double), POINTER(c_int32)]),
     "dq_diag_table_hash": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "dq_diag_key_pack": (c_int, [c_char_p, c_int32, POINTER(c_uint64), c_char_p, POINTER(c_int32), POINTER(c_int32)]),
+    "dq_diag_uuid_pack": (c_int, [c_char_p, c_int32, POINTER(c_uint64), c_char_p, POINTER(c_int32)]),
     "dq_diag_eval_predicate": (c_int, [POINTER(DqPredicate), POINTER(DqColumn), c_int, c_int64, c_void_p]),
 }
 

@@ -22,6 +22,7 @@
 
 #include "dq_internal.h"
 #include "dq_keypack.h"
+#include "dq_uuidpack.h"
 #include "dq_numparse.h"
 #include "dq_predeval.h"
 #include "../../include/deequ_amd_diag.h"
@@ -1977,6 +1978,22 @@ extern "C" dq_status dq_diag_key_pack(const uint8_t* key, int32_t len, uint64_t*
   std::memcpy(back, u, n);
   *back_len = (int32_t)n;
   *packed = p;
+  *ok = 1;
+  return DQ_OK;
+}
+
+// Host build of the group-by's UUID packing (dq_uuidpack.h): the two words of a canonical UUID
+// key and the 36 text bytes they unpack to.
+extern "C" dq_status dq_diag_uuid_pack(const uint8_t* key, int32_t len, uint64_t* words, uint8_t* back, int32_t* ok) {
+  if ((!key && len > 0) || !words || !back || !ok || len < 0) return fail(DQ_ERR_INVALID, "bad argument");
+  *ok = 0;
+  uint64_t lo = 0, hi = 0;
+  if (!dq::uuid_pack_bytes(key, (uint32_t)len, &lo, &hi)) return DQ_OK;
+  uint32_t w[10];
+  dq::uuid_unpack(lo, hi, w);
+  std::memcpy(back, w, dq::kUuidLen);
+  words[0] = lo;
+  words[1] = hi;
   *ok = 1;
   return DQ_OK;
 }

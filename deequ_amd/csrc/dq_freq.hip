@@ -22,6 +22,7 @@
 // cost one global atomic per (workgroup, key) instead of one per row.
 #include "dq_internal.h"
 #include "dq_keypack.h"
+#include "dq_uuidpack.h"
 
 #include <cstdio>
 #include <type_traits>
@@ -129,6 +130,31 @@ __device__ inline uint64_t hash_inline(uint64_t k0, uint64_t k1, uint32_t len) {
   return hash_raw(k0, k1, len);
 }
 
+// The table hash of a canonical UUID key (dq_uuidpack.h) from its packed words: the partition
+// path stages, splits and aggregates such keys as {lo, hi} and hashes each record in every pass,
+// so -- as a digit key is hashed as its packed word -- a UUID is hashed as its words (three
+// multiplies) rather than as 36 bytes of XXH64 (~25).
+__device__ inline uint64_t hash_uuid(uint64_t lo, uint64_t hi) { return hash_raw(lo, hi, kUuidLen); }
+
+// The table hash of a key of more than 16 bytes, wherever one is hashed (make_key, lookups,
+// imports, rehash, inserts from the heap): a canonical UUID hashes as its packed words, any other
+// key by xxh64_any.  A function of the key bytes alone, so every path agrees.
+__device__ inline uint64_t hash_long(const uint8_t* p, uint32_t len) {
+  if (len == kUuidLen) {
+    uint32_t w[9];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint64_t v = ld_partial(p + 8 * i, 8);
+      w[2 * i] = (uint32_t)v;
+      w[2 * i + 1] = (uint32_t)(v >> 32);
+    }
+    w[8] = (uint32_t)ld_partial(p + 32, 4);
+    uint64_t lo, hi;
+    if (uuid_pack(w, &lo, &hi)) return hash_uuid(lo, hi);
+  }
+  return xxh64_any(p, len, 42);
+}
+
 // One row's grouping key.  Inline (len <= 16) keys live in k0/k1; longer keys point at their
 // bytes (`ptr`, in the batch or in thread-local scratch).
 struct Key {
@@ -197,7 +223,7 @@ __device__ bool make_key(const FreqKeySpec& ks, const DevColumn* cols, int64_t r
         k.hash = want_hash ? hash_inline(k.k0, k.k1, n) : 0;
       } else {
         k.ptr = p;
-        k.hash = xxh64_any(p, n, 42);
+        k.hash = hash_long(p, n);
       }
       return true;
     }
@@ -245,7 +271,7 @@ __device__ bool make_key(const FreqKeySpec& ks, const DevColumn* cols, int64_t r
     k.hash = hash_inline(k.k0, k.k1, n);
   } else {
     k.ptr = scratch;
-    k.hash = xxh64_any(scratch, n, 42);
+    k.hash = hash_long(scratch, n);
   }
   return true;
 }
@@ -665,7 +691,7 @@ __global__ __launch_bounds__(kBlock) void dq_freq_import_kernel(FreqTable T, Fre
     if (in.ctrl[j] & kHeapKey) {
       k.ptr = in.heap + in.k0[j];
       k.k0 = k.k1 = 0;
-      k.hash = xxh64_any(k.ptr, k.len, 42);
+      k.hash = hash_long(k.ptr, k.len);
     } else {
       k.ptr = nullptr;
       k.k0 = in.k0[j];
@@ -783,7 +809,7 @@ __global__ __launch_bounds__(kBlock) void dq_freq_import_flat_kernel(FreqTable T
     if (k.len > 16u) {
       k.ptr = bytes + o;
       k.k0 = k.k1 = 0;
-      k.hash = xxh64_any(k.ptr, k.len, 42);
+      k.hash = hash_long(k.ptr, k.len);
     } else {
       k.ptr = nullptr;
       k.k0 = ld_partial(bytes + o, k.len < 8u ? k.len : 8u);
@@ -805,7 +831,7 @@ __global__ void dq_freq_lookup_kernel(FreqTable T, const uint8_t* key, uint32_t 
     k.len = len;
     k.k0 = len <= 16 ? ld_partial(key, len < 8 ? len : 8) : 0ull;
     k.k1 = len > 8 && len <= 16 ? ld_partial(key + 8, len - 8) : 0ull;
-    k.hash = len <= 16 ? hash_inline(k.k0, k.k1, len) : xxh64_any(key, len, 42);
+    k.hash = len <= 16 ? hash_inline(k.k0, k.k1, len) : hash_long(key, len);
     const uint32_t tag = tag_of(k.hash);
     const uint64_t b = slice_of(T, k.hash);
     const FreqSlot* g = cmp.slots + cmp.base[b];
@@ -837,7 +863,7 @@ __global__ void dq_freq_lookup_kernel(FreqTable T, const uint8_t* key, uint32_t 
     k.hash = hash_inline(k.k0, k.k1, len);
   } else {
     k.ptr = key;
-    k.hash = xxh64_any(key, len, 42);
+    k.hash = hash_long(key, len);
   }
   const uint32_t tag = tag_of(k.hash);
   *out = 0ull;
@@ -866,7 +892,7 @@ __device__ inline uint32_t freq_owner(uint64_t h, uint32_t n_parts) {
 }
 
 __device__ inline uint64_t slot_hash(const FreqTable& T, const FreqSlot& e, uint32_t len) {
-  return (e.ctrl & kHeapKey) ? xxh64_any(T.heap + e.k0, len, 42) : hash_inline(e.k0, e.k1, len);
+  return (e.ctrl & kHeapKey) ? hash_long(T.heap + e.k0, len) : hash_inline(e.k0, e.k1, len);
 }
 
 // ---- sorted-bucket path ---------------------------------------------------------------------
@@ -1394,6 +1420,10 @@ __device__ inline uint64_t rec_hash(const HashRec& r, bool* hole) {
   *hole = r.ref == kHashHole;
   return r.h;
 }
+__device__ inline uint64_t rec_hash(const UuidRec& r, bool* hole) {
+  *hole = false;  // (the UUID stage is fused with the level-1 split: no row-order holes)
+  return hash_uuid(r.lo, r.hi);
+}
 
 // A record in the 16-byte form (what the overflow and retry lists and the sort path hold; a
 // hashed record keeps its bits: the hashed path's lists are read by dq_freq_insert_hashed_kernel).
@@ -1402,6 +1432,12 @@ __device__ inline FreqRec rec_raw(const HashRec& r) {
   FreqRec f;
   f.k0 = r.h;
   f.k1 = r.ref;
+  return f;
+}
+__device__ inline FreqRec rec_raw(const UuidRec& r) {  // (its bits; the host converts such lists)
+  FreqRec f;
+  f.k0 = r.lo;
+  f.k1 = r.hi;
   return f;
 }
 __device__ inline FreqRec rec_raw(uint64_t p) {
@@ -2747,6 +2783,25 @@ __device__ inline uint64_t xxh64_words(const uint64_t (&kw)[MW], uint32_t len, u
   return xxh_avalanche(h);
 }
 
+// hash_long of a key held in registers (kw as for xxh64_words).
+template <int MW>
+__device__ inline uint64_t hash_long_words(const uint64_t (&kw)[MW], uint32_t len) {
+  if constexpr (MW >= 5) {
+    if (len == kUuidLen) {
+      uint32_t w[9];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        w[2 * i] = (uint32_t)kw[i];
+        w[2 * i + 1] = (uint32_t)(kw[i] >> 32);
+      }
+      w[8] = (uint32_t)kw[4];
+      uint64_t lo, hi;
+      if (uuid_pack(w, &lo, &hi)) return hash_uuid(lo, hi);
+    }
+  }
+  return xxh64_words<MW>(kw, len, 42);
+}
+
 // One row of the hashed stage the general way (make_key): its key bytes to heap + off, its
 // record in *r; the heap bytes it used (0 when the row is no key).  Multi-column keys, NULLs
 // and keys longer than the register path's 48 bytes.
@@ -2925,7 +2980,7 @@ __global__ __launch_bounds__(kBlock) void dq_freq_stage_hashed_kernel(FreqKeySpe
 #pragma unroll
           for (int i = 0; i < kHashWords; ++i)
             if (8u * (uint32_t)i < n) dst[i] = kw[i];
-          r.h = xxh64_words<kHashWords>(kw, n, 42);
+          r.h = hash_long_words<kHashWords>(kw, n);
           r.ref = (at << 24) | n;
           longest = max(longest, n);
         } else if (!ONE_STRING && room && key_words<kHashWords>(ks, cols, row, kwm, &nm) && nm) {
@@ -2934,7 +2989,7 @@ __global__ __launch_bounds__(kBlock) void dq_freq_stage_hashed_kernel(FreqKeySpe
 #pragma unroll
           for (int i = 0; i < kHashWords; ++i)
             if (8u * (uint32_t)i < nm) dst[i] = kwm[i];
-          r.h = nm <= 16u ? hash_inline(kwm[0], kwm[1], nm) : xxh64_words<kHashWords>(kwm, nm, 42);
+          r.h = nm <= 16u ? hash_inline(kwm[0], kwm[1], nm) : hash_long_words<kHashWords>(kwm, nm);
           r.ref = (at << 24) | nm;
           longest = max(longest, nm);
         } else {
@@ -3282,7 +3337,7 @@ __global__ __launch_bounds__(kAggHThreads) void dq_freq_insert_hashed_kernel(Fre
         r.k0 = L.K[s];  // (kk: a hash of 0 was kept as 1 -- the key's own hash is recomputed below)
         r.k1 = L.R[s];
         Key k = hashed_key(T, r);
-        k.hash = k.len > 16 ? xxh64_any(k.ptr, k.len, 42) : hash_inline(k.k0, k.k1, k.len);
+        k.hash = k.len > 16 ? hash_long(k.ptr, k.len) : hash_inline(k.k0, k.k1, k.len);
         (void)global_insert<true, true>(T, k, (unsigned long long)c);
       }
       L.K[s] = 0ull;
@@ -3337,6 +3392,363 @@ __global__ __launch_bounds__(kAggHThreads) void dq_freq_insert_hashed_kernel(Fre
     if (L.fresh > S / 4u) flush();
   }
   flush();
+}
+
+// ---- Canonical UUID keys on the partition path (round 6, dq_uuidpack.h).  A table whose keys
+// are UUID text (isPrimaryKey's ids, Check.scala:140-230) stages each row as its 128-bit value
+// (UuidRec), straight into its level-1 region; the level-2 split moves the same 16-byte records;
+// the slice aggregation counts them by table hash in LDS and compares every record that joins a
+// hash group with the group's first key IN LDS (two words), so the grouping is exact with no
+// key-byte reads; and the write-out turns each GROUP's words back into its 36 text bytes in the
+// key heap.  Against the hashed records of round 6's first build (every row's bytes copied into
+// the heap, then two random heap reads per row in the aggregation) the path moves no key bytes
+// but the input and the groups' text.
+constexpr int kUuidPer = 8;    // rows per thread per stage tile
+constexpr int kUuidWin = 2;    // rows whose key loads are in flight
+constexpr uint32_t kUuidTile = (uint32_t)kStageThreads * kUuidPer;
+constexpr uint32_t kUuidHeap = 40;  // heap bytes of a group's text (36, 8-byte aligned)
+
+// The 36 bytes at ob as nine words (two 16-byte loads and one 4-byte load through the values'
+// descriptor; bytes past the values read 0, so a shorter key near the end never faults).
+__device__ __forceinline__ void uuid_load(__amdgpu_buffer_rsrc_t rs, uint32_t ob, uint32_t (&w)[9]) {
+  const auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)ob, 0, 0);
+  const auto b = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(ob + 16u), 0, 0);
+  w[0] = a[0];
+  w[1] = a[1];
+  w[2] = a[2];
+  w[3] = a[3];
+  w[4] = b[0];
+  w[5] = b[1];
+  w[6] = b[2];
+  w[7] = b[3];
+  w[8] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(ob + 32u), 0, 0);
+}
+
+// A group's text into the heap at off (five 8-byte stores: 36 bytes and 4 of zero padding).
+__device__ __forceinline__ void uuid_store_text(uint8_t* heap, unsigned long long off, uint64_t lo, uint64_t hi) {
+  uint32_t w[10];
+  uuid_unpack(lo, hi, w);
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(heap + off);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) dst[i] = (unsigned long long)w[2 * i] | ((unsigned long long)w[2 * i + 1] << 32);
+}
+
+// Stage + level-1 split of one utf8 key column of canonical UUIDs (the host probed the batch;
+// NULL rows stage nothing -- the table is not Histogram's NULL-as-key grouping).  A non-NULL key
+// that is not a canonical UUID is counted in bad_keys and staged nothing: the host rolls the batch
+// back and stages the table's keys as hashed records from then on.  Tiles of kUuidTile rows:
+// the offsets as (begin, end) pairs, then each row's 36 bytes with kUuidWin rows in flight.
+__global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(DQ_STAGEP_WAVES))) void dq_freq_stage_uuid_kernel(
+    FreqKeySpec ks, const DevColumn* __restrict__ cols, int64_t n_rows, int b1, UuidRec* __restrict__ out,
+    uint64_t cap1, unsigned long long* fill1, FreqRec* ovf, unsigned long long* ovf_n, uint64_t ovf_cap,
+    unsigned int* flag, uint32_t* hll, unsigned long long* bad_keys, unsigned long long* staged) {
+  __shared__ PartLdsT<(1 << kStageBinBits), UuidRec, kPartSub> L;
+  __shared__ uint32_t regs[kHllM];
+  const uint32_t t = threadIdx.x;
+  const uint32_t nb = 1u << b1;
+  for (uint32_t i = t; i < (uint32_t)kHllM; i += kStageThreads) regs[i] = 0xFFFFFFFFu;  // (stage_sketch)
+  lds_barrier();
+  const DevColumn& c0 = cols[ks.key_cols[0]];
+  const int32_t* offs = uniform_ptr(c0.offsets);
+  const uint32_t heap_end = __builtin_amdgcn_readfirstlane((uint32_t)offs[n_rows]);
+  const __amdgpu_buffer_rsrc_t rs_vals = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(static_cast<const uint8_t*>(uniform_ptr(c0.values))), 0, (int)heap_end, 0x00020000);
+  const uint8_t* validity = uniform_ptr(c0.validity);
+  const int64_t n_tiles = (n_rows + kUuidTile - 1) / kUuidTile;
+  uint32_t n_bad = 0u;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const int64_t r0 = tile * (int64_t)kUuidTile;
+    const int64_t left = n_rows - r0;
+    const uint32_t m = (uint32_t)(left < (int64_t)kUuidTile ? left : (int64_t)kUuidTile);
+    const uint32_t vword = tile_valid_word<kStageThreads, kUuidPer>(validity, r0, m);
+    const __amdgpu_buffer_rsrc_t rs_off =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(offs + r0), 0, (int)(4u * (m + 1u)), 0x00020000);
+    uint32_t pob[kUuidPer], len[kUuidPer];
+#pragma unroll
+    for (int j = 0; j < kUuidPer; ++j) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs_off, (int)(4u * ((uint32_t)j * kStageThreads + t)), 0, 0);
+      pob[j] = v[0];
+      len[j] = v[1] - v[0];
+    }
+    UuidRec rec[kUuidPer];
+    uint32_t bin[kUuidPer];
+    uint32_t kw[kUuidWin][9];
+#pragma unroll
+    for (int j = 0; j < kUuidWin; ++j) uuid_load(rs_vals, pob[j], kw[j]);
+#pragma unroll
+    for (int j = 0; j < kUuidPer; ++j) {
+      uint32_t w[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) w[i] = kw[j % kUuidWin][i];
+      if (j + kUuidWin < kUuidPer) uuid_load(rs_vals, pob[j + kUuidWin], kw[j % kUuidWin]);
+      bin[j] = kPartNoBin;
+      rec[j].lo = rec[j].hi = 0ull;
+      const uint32_t i = (uint32_t)j * kStageThreads + t;
+      const bool valid = validity == nullptr || ((stage_valid_mask(vword, j) >> (t & 63u)) & 1u);
+      if (i >= m || !valid) continue;
+      uint64_t lo, hi;
+      if (len[j] != kUuidLen || !uuid_pack(w, &lo, &hi)) {
+        ++n_bad;
+        continue;
+      }
+      rec[j].lo = lo;
+      rec[j].hi = hi;
+      const uint64_t h = hash_uuid(lo, hi);
+      bin[j] = (uint32_t)(h >> (64 - b1)) & (nb - 1u);
+      stage_sketch(regs, h);
+    }
+    part_tile<kUuidPer, (1 << kStageBinBits), UuidRec, kPartSub, false, DQ_STAGE_WOUT_UNROLL, false, kStageThreads>(
+        L, rec, bin, nb, 0, out, cap1, fill1, ovf, ovf_n, ovf_cap, flag, staged);
+  }
+  for (int d = 32; d >= 1; d >>= 1) n_bad += __shfl_xor(n_bad, d, 64);
+  if ((t & 63u) == 0u && n_bad) atomicAdd(bad_keys, (unsigned long long)n_bad);
+  lds_barrier();
+  for (uint32_t i = t; i < (uint32_t)kHllM; i += kStageThreads)
+    if (regs[i] != 0xFFFFFFFFu) atomicMax(&hll[i], stage_sketch_rank(regs[i]));
+}
+
+// The owner aggregation of slice regions of UUID records into a FRESH table.  LDS image: the
+// table hash (0 kept as 1; the claimed mark), the group's key words and its count.  A chunk of
+// kAggUPer records per thread is counted by hash (one CAS per probe; the claimer stores its key
+// words), then, after one barrier, every record that joined an existing hash group is compared
+// with the group's words in LDS.  A full image, two keys of one hash (a slice holding two UUIDs of
+// one 64-bit hash: ~never) or no heap room hands the slice's records to the retry list (their
+// bits; the host converts and inserts them globally).  Write-out: each thread's groups (it owns
+// eight consecutive slots) as whole 32-byte slots at one reserved place per slice (tr.cmp) or in
+// the slot image, and their text as 40 consecutive heap bytes each at one heap reservation per
+// slice.
+constexpr int kAggUThreads = 512;  // (the 58 KB image allows two workgroups per CU: 4 waves per SIMD)
+constexpr int kAggUPer = 8;
+struct AggLdsU {
+  unsigned long long K[kFreqSliceSlots];
+  unsigned long long KL[kFreqSliceSlots];
+  unsigned long long KH[kFreqSliceSlots];
+  uint32_t C[kFreqSliceSlots];
+  uint32_t wsum[8];
+  int overflow;
+  uint32_t cmax;
+  unsigned long long retry_base;
+  unsigned long long cbase;
+  unsigned long long hbase;
+  uint32_t hist[kAggLdsHist];
+};
+
+__global__ __launch_bounds__(kAggUThreads) void dq_freq_agg_uuid_kernel(
+    FreqTable T, const UuidRec* __restrict__ recs, const unsigned long long* __restrict__ fill, uint64_t cap,
+    uint64_t n_slices, FreqRec* retry, unsigned long long* n_retry, unsigned long long* new_groups, AggTrack tr) {
+  constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
+  constexpr int NT = kAggUThreads;
+  constexpr uint32_t kChunk = (uint32_t)kAggUPer * NT;
+  static_assert(S == 4u * NT, "four slots per thread");
+  __shared__ AggLdsU L;
+  const bool track = tr.hist != nullptr;
+  const bool compact = tr.cmp.slots != nullptr;
+  const uint32_t t = threadIdx.x;
+  if (track) {
+    for (int i = t; i < kAggLdsHist; i += NT) L.hist[i] = 0u;
+    lds_barrier();
+  }
+  for (uint64_t b = blockIdx.x; b < n_slices; b += gridDim.x) {
+    const uint64_t r0 = b * cap;
+    const unsigned long long f = fill[b];
+    const uint64_t r1 = r0 + (f < cap ? f : cap);
+    ulonglong2* halves = reinterpret_cast<ulonglong2*>(T.slots + (b << kFreqSliceLog));
+    if (r1 == r0) {
+      if (compact) {
+        if (t == 0) tr.cmp.num[b] = 0u;
+      } else if (tr.write_all) {
+        for (uint32_t q = t; q < 2u * S; q += NT) halves[q] = ulonglong2{0ull, 0ull};
+      }
+      if (tr.smax && t == 0) tr.smax[b] = 0u;
+      continue;
+    }
+    for (uint32_t s = t; s < S; s += NT) {
+      L.K[s] = 0ull;
+      L.C[s] = 0u;
+    }
+    if (t == 0) {
+      L.overflow = 0;
+      L.cmax = 0u;
+    }
+    lds_barrier();
+    for (uint64_t c0 = r0; c0 < r1; c0 += kChunk) {
+      UuidRec rb[kAggUPer];
+      uint32_t sl[kAggUPer];
+#pragma unroll
+      for (int j = 0; j < kAggUPer; ++j) {
+        const uint64_t idx = c0 + (uint64_t)j * NT + t;
+        if (idx < r1) rb[j] = recs[idx];
+      }
+      uint32_t joined = 0u;
+#pragma unroll
+      for (int j = 0; j < kAggUPer; ++j) {
+        sl[j] = 0u;
+        if (c0 + (uint64_t)j * NT + t >= r1) continue;
+        const uint64_t h = hash_uuid(rb[j].lo, rb[j].hi);
+        const unsigned long long kk = h ? h : 1ull;
+        uint32_t s = (uint32_t)h & (S - 1u);
+        uint32_t probe = 0;
+        for (; probe < S; ++probe) {
+          const unsigned long long c = atomicCAS(&L.K[s], 0ull, kk);
+          if (c == 0ull) {
+            L.KL[s] = rb[j].lo;
+            L.KH[s] = rb[j].hi;
+            atomicAdd(&L.C[s], 1u);
+            break;
+          }
+          if (c == kk) {
+            atomicAdd(&L.C[s], 1u);
+            joined |= 1u << j;
+            sl[j] = s;
+            break;
+          }
+          s = (s + 1u) & (S - 1u);
+        }
+        if (probe == S) L.overflow = 1;
+      }
+      lds_barrier();  // every group's first key words are in place (later claims touch other slots)
+#pragma unroll
+      for (int j = 0; j < kAggUPer; ++j)
+        if (((joined >> j) & 1u) && (L.KL[sl[j]] != rb[j].lo || L.KH[sl[j]] != rb[j].hi)) L.overflow = 2;
+    }
+    lds_barrier();
+    // this thread's eight slots: occupancy, the slice's group count, one heap reservation
+    const uint4 cv = *reinterpret_cast<const uint4*>(&L.C[4u * t]);
+    const uint32_t cs[4] = {cv.x, cv.y, cv.z, cv.w};
+    uint32_t occ = 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) occ |= (cs[j] ? 1u : 0u) << j;
+    uint32_t tot;
+    const uint32_t k = block_prefix<NT>((uint32_t)__builtin_popcount(occ), L.wsum, &tot);
+    if (t == 0 && !L.overflow) {
+      const unsigned long long need = (unsigned long long)tot * kUuidHeap;
+      const unsigned long long hb = atomicAdd(T.heap_used, need);
+      if (hb + need > T.heap_cap) L.overflow = 3;  // (the host sized the heap from the sketch; it clamps heap_used)
+      L.hbase = hb;
+    }
+    lds_barrier();
+    if (L.overflow) {  // hand the region's records back (their bits: the host converts, then inserts globally)
+      if (t == 0) L.retry_base = atomicAdd(n_retry, (unsigned long long)(r1 - r0));
+      lds_barrier();
+      for (uint64_t i = r0 + t; i < r1; i += NT) retry[L.retry_base + (i - r0)] = rec_raw(recs[i]);
+      if (compact) {
+        if (t == 0) tr.cmp.num[b] = 0u;
+      } else if (tr.write_all) {
+        for (uint32_t q = t; q < 2u * S; q += NT) halves[q] = ulonglong2{0ull, 0ull};
+      }
+      if (tr.smax && t == 0) tr.smax[b] = 0xFFFFFFFFu;
+      lds_barrier();
+      continue;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!cs[j] || !(track || tr.smax)) continue;
+      atomicMax(&L.cmax, cs[j]);
+      if (track) {
+        if (cs[j] < (uint32_t)kAggLdsHist) atomicAdd(&L.hist[cs[j]], 1u);
+        else if (cs[j] < (uint32_t)kFreqHist) atomicAdd(&tr.hist[cs[j]], 1ull);
+        else {
+          const unsigned long long i = atomicAdd(tr.n_big, 1ull);
+          if (i < tr.big_cap) tr.big[i] = cs[j];
+        }
+      }
+    }
+    if (compact) {
+      const uint32_t pair = occ | ((uint32_t)__shfl_down((int)occ, 1, 64) << 4);  // (byte t / 2: slots 4t .. 4t + 7)
+      if (!(t & 1u)) tr.cmp.bits[(b << 8) + (t >> 1)] = (uint8_t)pair;
+      if (t == 0) {
+        const unsigned long long at = atomicAdd(tr.cmp.cursor, (unsigned long long)tot);
+        L.cbase = at;
+        tr.cmp.base[b] = at;
+        tr.cmp.num[b] = tot;
+      }
+    }
+    lds_barrier();  // (L.cbase; every thread's cmax update before thread 0 reads it)
+    unsigned long long hoff = L.hbase + (unsigned long long)k * kUuidHeap;
+    FreqSlot* out = compact ? tr.cmp.slots + L.cbase + k : nullptr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t s = 4u * t + (uint32_t)j;
+      if (!cs[j]) {
+        if (!compact && tr.write_all) {
+          halves[2u * s] = ulonglong2{0ull, 0ull};
+          halves[2u * s + 1u] = ulonglong2{0ull, 0ull};
+        }
+        continue;
+      }
+      const uint64_t lo = L.KL[s], hi = L.KH[s];
+      uuid_store_text(T.heap, hoff, lo, hi);
+      const unsigned long long ctrl = ((unsigned long long)tag_of(hash_uuid(lo, hi)) << 32) | kReady | kHeapKey | kUuidLen;
+      if (compact) {
+        *out++ = FreqSlot{ctrl, (unsigned long long)cs[j], hoff, 0ull};
+      } else {
+        halves[2u * s] = ulonglong2{ctrl, (unsigned long long)cs[j]};
+        halves[2u * s + 1u] = ulonglong2{hoff, 0ull};
+      }
+      hoff += kUuidHeap;
+    }
+    if (t == 0) {
+      if (tot) atomicAdd(new_groups, (unsigned long long)tot);
+      if (tr.smax) tr.smax[b] = L.cmax;
+    }
+    lds_barrier();  // LDS is reused by the next slice
+  }
+  if (track) {
+    lds_barrier();
+    for (int i = t; i < kAggLdsHist; i += NT)
+      if (L.hist[i]) atomicAdd(&tr.hist[i], (unsigned long long)L.hist[i]);
+  }
+}
+
+// A list of UUID records' bits (FreqRec {lo, hi}: the retry / overflow lists of the UUID path)
+// turned in place into hashed records {table hash, heap reference}: each key's text written to
+// the heap (one reservation per wave), so dq_freq_insert_hashed_kernel can insert them.  The host
+// reserved the room; a record that finds none raises the heap-full bit.
+__global__ __launch_bounds__(kBlock) void dq_freq_uuid_to_hashed_kernel(FreqTable T, FreqRec* recs, uint64_t n) {
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * kBlock; i0 < n; i0 += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t i = i0 + threadIdx.x;
+    const bool act = i < n;
+    const uint64_t ball = __ballot(act);
+    if (!ball) continue;
+    const uint32_t first = (uint32_t)__builtin_ctzll(ball);
+    unsigned long long base = 0ull;
+    if (lane == first) base = atomicAdd(T.heap_used, (unsigned long long)__popcll(ball) * kUuidHeap);
+    base = __shfl(base, (int)first, 64);
+    if (!act) continue;
+    const FreqRec r = recs[i];
+    const unsigned long long off = base + (unsigned long long)__popcll(ball & ((1ull << lane) - 1ull)) * kUuidHeap;
+    if (off + kUuidHeap > T.heap_cap) {
+      atomicOr(T.overflow, 2u);
+      continue;
+    }
+    uuid_store_text(T.heap, off, r.k0, r.k1);
+    FreqRec o;
+    o.k0 = hash_uuid(r.k0, r.k1);
+    o.k1 = (off << 24) | kUuidLen;
+    recs[i] = o;
+  }
+}
+
+// Whether a single-utf8-key staging holds canonical UUIDs: out[0] counts the sampled non-NULL keys
+// (kPackProbe scattered rows, as dq_freq_pack_probe_kernel) that are not, out[1] those that are.
+__global__ __launch_bounds__(kBlock) void dq_freq_uuid_probe_kernel(FreqKeySpec ks, const DevColumn* __restrict__ cols,
+                                                                    int64_t n_rows, unsigned long long* out) {
+  const DevColumn& c = cols[ks.key_cols[0]];
+  constexpr int64_t kProbe = 16384;  // (as kPackProbe)
+  const int64_t samples = n_rows < kProbe ? n_rows : kProbe;
+  uint32_t bad = 0u, good = 0u;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < samples; i += (int64_t)gridDim.x * kBlock) {
+    const int64_t row = samples == n_rows ? i : (int64_t)(((uint64_t)i * 11400714819323198485ull) % (uint64_t)n_rows);
+    if (c.validity != nullptr && !((c.validity[row >> 3] >> (row & 7)) & 1u)) continue;
+    const uint8_t* v = static_cast<const uint8_t*>(c.values) + c.offsets[row];
+    const uint32_t n = (uint32_t)(c.offsets[row + 1] - c.offsets[row]);
+    uint64_t lo, hi;
+    if (uuid_pack_bytes(v, n, &lo, &hi)) ++good;
+    else ++bad;
+  }
+  if (bad) atomicAdd(&out[0], (unsigned long long)bad);
+  if (good) atomicAdd(&out[1], (unsigned long long)good);
 }
 
 // The slot image of a compacted table (AggTrack::cmp) rebuilt in T: slice b's groups, stored in
@@ -3403,7 +3815,7 @@ __global__ __launch_bounds__(kBlock) void dq_freq_rehash_kernel(const FreqSlot* 
     const FreqSlot e = old_slots[i];
     if (!(e.ctrl & kReady)) continue;
     const uint32_t len = (uint32_t)(e.ctrl & kLenMask);
-    const uint64_t h = (e.ctrl & kHeapKey) ? xxh64_any(T.heap + e.k0, len, 42) : hash_inline(e.k0, e.k1, len);
+    const uint64_t h = (e.ctrl & kHeapKey) ? hash_long(T.heap + e.k0, len) : hash_inline(e.k0, e.k1, len);
     uint64_t it = 0;
     for (; it < kFreqSliceSlots; ++it) {
       const uint64_t slot = probe_slot(T, h, it);
@@ -3521,6 +3933,10 @@ hipError_t launch_freq_part(const void* d_in, uint64_t in_n, const unsigned long
     hipLaunchKernelGGL((dq_freq_part_kernel<HashRec, (1 << kPartMaxBinBits)>), grid, dim3(kPartThreads), 0, stream,
                        static_cast<const HashRec*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
                        static_cast<HashRec*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag, d_staged);
+  else if (rec_kind == kRecUuid)
+    hipLaunchKernelGGL((dq_freq_part_kernel<UuidRec, (1 << kPartMaxBinBits)>), grid, dim3(kPartThreads), 0, stream,
+                       static_cast<const UuidRec*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
+                       static_cast<UuidRec*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag, d_staged);
   else
     hipLaunchKernelGGL((dq_freq_part_kernel<FreqRec, (1 << kPartMaxBinBits)>), grid, dim3(kPartThreads), 0, stream,
                        static_cast<const FreqRec*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
@@ -3712,9 +4128,12 @@ hipError_t launch_freq_agg_region(const FreqTable& T, const void* d_recs, int re
   if (!table_empty && (d_hist || d_smax || write_all)) return hipErrorInvalidValue;
   const bool packed = rec_kind == kRecPacked;
   if (compact && !table_empty) return hipErrorInvalidValue;
-  if (rec_kind == kRecHashed && !table_empty) return hipErrorInvalidValue;  // (fresh tables only)
+  if ((rec_kind == kRecHashed || rec_kind == kRecUuid) && !table_empty) return hipErrorInvalidValue;  // (fresh tables only)
   AggTrack tr{d_hist, d_big, d_n_big, big_cap, d_smax, write_all, compact ? *compact : FreqCompact{}};
-  if (rec_kind == kRecHashed)
+  if (rec_kind == kRecUuid)
+    hipLaunchKernelGGL(dq_freq_agg_uuid_kernel, dim3((unsigned)blocks), dim3(kAggUThreads), 0, stream, T,
+                       static_cast<const UuidRec*>(d_recs), d_fill, cap, n_slices, d_retry, d_n_retry, d_new_groups, tr);
+  else if (rec_kind == kRecHashed)
     hipLaunchKernelGGL(dq_freq_agg_hashed_kernel, dim3((unsigned)blocks), dim3(kAggHThreads), 0, stream, T,
                        static_cast<const HashRec*>(d_recs), d_fill, cap, n_slices, d_retry, d_n_retry, d_new_groups, tr);
   else if (packed)
@@ -3725,6 +4144,40 @@ hipError_t launch_freq_agg_region(const FreqTable& T, const void* d_recs, int re
     hipLaunchKernelGGL(dq_freq_agg_region_kernel, dim3((unsigned)blocks), dim3(kAggRegionThreads), 0, stream, T,
                        static_cast<const FreqRec*>(d_recs), d_fill, cap, n_slices, table_empty, d_retry, d_n_retry,
                        d_new_groups, tr);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_stage_uuid(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, int b1, void* d_out,
+                                  uint64_t cap1, unsigned long long* d_fill1, FreqRec* d_ovf, unsigned long long* d_ovf_n,
+                                  uint64_t ovf_cap, unsigned int* d_flag, uint32_t* d_hll, unsigned long long* d_bad,
+                                  unsigned long long* d_staged, hipStream_t stream) {
+  if (n_rows <= 0) return hipSuccess;
+  if (b1 < 1 || b1 > kStageBinBits) return hipErrorInvalidValue;
+  const int64_t tiles = (n_rows + kUuidTile - 1) / kUuidTile;
+  int dev = 0, cus = 256, per_cu = 2;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dq_freq_stage_uuid_kernel, kStageThreads, 0);
+  const int64_t resident = (int64_t)cus * (per_cu > 0 ? per_cu : 1);
+  const int64_t blocks = tiles < resident ? tiles : resident;  // (one resident round, grid-stride over the tiles)
+  hipLaunchKernelGGL(dq_freq_stage_uuid_kernel, dim3((unsigned)blocks), dim3(kStageThreads), 0, stream, ks, d_cols, n_rows,
+                     b1, static_cast<UuidRec*>(d_out), cap1, d_fill1, d_ovf, d_ovf_n, ovf_cap, d_flag, d_hll, d_bad,
+                     d_staged);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_uuid_to_hashed(const FreqTable& T, FreqRec* d_recs, uint64_t n, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  uint64_t blocks = (n + kBlock - 1) / kBlock;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(dq_freq_uuid_to_hashed_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, d_recs, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_uuid_probe(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, unsigned long long* d_out,
+                                  hipStream_t stream) {
+  if (n_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(dq_freq_uuid_probe_kernel, dim3((16384 + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, ks, d_cols,
+                     n_rows, d_out);
   return hipGetLastError();
 }
 
@@ -4005,7 +4458,7 @@ hipError_t launch_freq_heap_need(const FreqKeySpec& ks, const DevColumn* d_cols,
 __device__ inline uint64_t slot_key_hash(const FreqTable& T, const FreqSlot& e, uint32_t len, uint64_t* packed,
                                          int* kind) {
   *kind = 1;
-  if (e.ctrl & kHeapKey) return xxh64_any(T.heap + e.k0, len, 42);
+  if (e.ctrl & kHeapKey) return hash_long(T.heap + e.k0, len);
   uint64_t p;
   if (kp_pack_record(e.k0, e.k1, len, &p)) {
     *packed = p;
@@ -4146,7 +4599,7 @@ __device__ inline void imp_load(const ImportRun& R, uint64_t i, ImpRec& r) {
   r.k1 = e.k1;
   r.p = 0;
   if (!r.present) return;
-  r.hash = r.heap ? xxh64_any(R.heap + e.k0, r.len, 42) : hash_inline(e.k0, e.k1, r.len);
+  r.hash = r.heap ? hash_long(R.heap + e.k0, r.len) : hash_inline(e.k0, e.k1, r.len);
 }
 
 __device__ inline uint64_t dst_slice(uint64_t h, int rb) { return rb ? (h >> (64 - rb)) : 0ull; }

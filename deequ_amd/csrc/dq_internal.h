@@ -185,6 +185,14 @@ struct alignas(16) HashRec {
 };
 constexpr unsigned long long kHashHole = ~0ull;
 
+// A staged row of a canonical UUID key (round 6, dq_uuidpack.h): its 36 text bytes packed into
+// 128 bits.  The record is the key itself, so the splits and the slice aggregation group it in
+// registers and LDS; the overflow and retry lists hold its bits as a FreqRec {lo, hi}, which
+// dq_freq_uuid_to_hashed turns into a hashed record (text into the key heap) before a global insert.
+struct alignas(16) UuidRec {
+  unsigned long long lo, hi;
+};
+
 struct FreqTable {
   FreqSlot* slots;
   uint64_t mask;                   // capacity - 1 (capacity: a power of two >= kFreqSliceSlots)
@@ -347,7 +355,7 @@ hipError_t launch_freq_part(const void* d_in, uint64_t in_n, const unsigned long
                             unsigned long long* d_out_fill, FreqRec* d_ovf, unsigned long long* d_ovf_n,
                             uint64_t ovf_cap, unsigned int* d_flag, int rec_kind, hipStream_t stream,
                             unsigned long long* d_staged = nullptr);
-constexpr int kRecFree = 0, kRecPacked = 1, kRecHashed = 2;  // FreqRec, packed word, HashRec
+constexpr int kRecFree = 0, kRecPacked = 1, kRecHashed = 2, kRecUuid = 3;  // FreqRec, packed word, HashRec, UuidRec
 // With an empty table it can also produce the count-of-counts histogram (d_hist, counts >=
 // kFreqHist into d_big), each slice's largest count (d_smax) and write every slot (write_all:
 // the table needs no clearing).
@@ -396,6 +404,18 @@ hipError_t launch_freq_gather_keys(const uint8_t* d_heap, const unsigned long lo
 // Exact bytes the stage will append to the heap for n_rows rows (sum of 8-aligned key lengths).
 hipError_t launch_freq_key_bytes(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
                                  unsigned long long* d_out, hipStream_t stream);
+// The UUID partition path (dq_freq.hip, round 6; dq_uuidpack.h).  Stage + level-1 split of a
+// single utf8 key column of canonical UUIDs into UuidRec regions (d_bad: non-NULL keys that are
+// not canonical UUIDs -- the caller rolls such a batch back); in-place conversion of a list of
+// UuidRec bits (retry / overflow) into hashed records, their text written to T's heap; the probe
+// of a batch's keys (d_out[0] non-canonical, d_out[1] canonical, of a sample).
+hipError_t launch_freq_stage_uuid(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, int b1, void* d_out,
+                                  uint64_t cap1, unsigned long long* d_fill1, FreqRec* d_ovf, unsigned long long* d_ovf_n,
+                                  uint64_t ovf_cap, unsigned int* d_flag, uint32_t* d_hll, unsigned long long* d_bad,
+                                  unsigned long long* d_staged, hipStream_t stream);
+hipError_t launch_freq_uuid_to_hashed(const FreqTable& T, FreqRec* d_recs, uint64_t n, hipStream_t stream);
+hipError_t launch_freq_uuid_probe(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, unsigned long long* d_out,
+                                  hipStream_t stream);
 // Global inserts of n hashed records (the list form: FreqRec bits of HashRec), their key bytes
 // already in T's heap: the retry / overflow records and the fall-back of the hashed path.
 hipError_t launch_freq_insert_hashed(const FreqTable& T, const FreqRec* d_recs, uint64_t n, hipStream_t stream);

@@ -31,7 +31,8 @@ dq_status dq_diag_hash_rate(int device, int with_hll, int reps, double* hashes_p
  * out[8] = imported wire runs out of order (inserted group by group), out[9] = partition-path
  * aggregations of hashed records (long or multi-column keys), out[10] = hashed records inserted
  * globally (slices handed back, tables that already held groups), out[11] = 1 while the table is
- * compacted (occupied slots only).  `out` holds 12 values. */
+ * compacted (occupied slots only), out[12] = partition-path aggregations of canonical UUID records
+ * (dq_uuidpack.h).  `out` holds 13 values. */
 dq_status dq_diag_freq_paths(dq_freq* f, int64_t* out);
 
 /* Test hooks of one table (tests only; never set by the product): flags = 1 makes claimed
@@ -64,6 +65,11 @@ dq_status dq_diag_table_hash(int device, const uint64_t* k0, const uint64_t* k1,
 
 dq_status dq_diag_key_pack(const uint8_t* key, int32_t len, uint64_t* packed, uint8_t* back, int32_t* back_len,
                            int32_t* ok);
+
+/* Host build of the group-by's canonical-UUID packing (dq_uuidpack.h): *ok = 1 and words[0..1] =
+ * the key's 128-bit value, back[0..36) = the text it unpacks to, when key[0..len) is a canonical
+ * lowercase UUID ("xxxxxxxx-xxxx-xxxx-xxxx-xxxxxxxxxxxx"); else *ok = 0. */
+dq_status dq_diag_uuid_pack(const uint8_t* key, int32_t len, uint64_t* words, uint8_t* back, int32_t* ok);
 
 #ifdef __cplusplus
 }

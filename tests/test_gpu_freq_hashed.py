@@ -190,3 +190,79 @@ def test_composite_few_groups_many_rows(gpu):
     paths = t.paths()
     assert paths["hashed_runs"] == 0 and paths["wait_timeouts"] == 0, paths
     t.close()
+
+
+# ---- canonical UUID keys (dq_uuidpack.h): the table stages each UUID as its 128 bits (UuidRec)
+# and compares keys in LDS; the text is written once per group.  Other key shapes keep the
+# hashed records above.
+
+def test_uuid_records_against_hashed(gpu, part, monkeypatch):
+    """The same UUID batches grouped with UuidRec records and, DQ_FREQ_UUID=0, with hashed
+    records: equal exports, summaries, top-N and lookups, both exact against Python counts."""
+    rng = np.random.default_rng(61)
+    keys = [None if i % 53 == 0 else _uuid(int(v)) for i, v in enumerate(rng.integers(0, 400_000, 900_000))]
+    want = _count(keys)
+    got = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("DQ_FREQ_UUID", mode)
+        t = _consume(keys, False, 3)
+        paths = t.paths()
+        assert (paths["uuid_runs"] >= 1) == (mode == "1"), paths
+        assert paths["hashed_inserts"] == 0, paths
+        s = t.summary()
+        got[mode] = (_export(t), (s.num_groups, s.num_unique, s.grouped_rows, s.num_rows),
+                     sorted(zip(t.top(7)[0].tolist(), t.top(7)[1])))
+        k = next(iter(want))
+        assert t.lookup(k) == want[k]
+        assert t.lookup(k.upper()) == 0
+        t.close()
+    assert got["1"][0] == want
+    assert got["1"] == got["0"]
+
+
+def test_uuid_batch_with_other_keys_rolls_back(gpu, part):
+    """Batch 1 holds canonical UUIDs only (UuidRec regions); batch 2 adds an uppercase UUID and a
+    40-byte string: it is rolled back, the UUID regions are aggregated, and the table stages
+    hashed records from then on.  Exact."""
+    rng = np.random.default_rng(67)
+    b1 = [_uuid(int(v)) for v in rng.integers(0, 150_000, 300_000)]
+    b2 = [_uuid(int(v)) for v in rng.integers(100_000, 250_000, 300_000)]
+    b2[17] = b2[17].upper()
+    b2[99] = "x" * 40
+    t = FrequencyTable(["key"], {"key": "string"})
+    t.reserve(len(b1) + len(b2))
+    t.consume(d.Table.from_pydict({"key": ("string", b1)}))
+    t.consume(d.Table.from_pydict({"key": ("string", b2)}))
+    assert _export(t) == _count(b1 + b2)
+    paths = t.paths()
+    assert paths["uuid_runs"] >= 1 and paths["hashed_runs"] >= 2, paths
+    t.close()
+
+
+def test_uuid_uppercase_keeps_hashed_records(gpu, part):
+    """Uppercase UUID text is not canonical: the probe keeps the hashed records.  Exact."""
+    rng = np.random.default_rng(71)
+    keys = [_uuid(int(v)).upper() for v in rng.integers(0, 100_000, 250_000)]
+    t = _consume(keys, False, 2)
+    assert _export(t) == _count(keys)
+    paths = t.paths()
+    assert paths["uuid_runs"] == 0 and paths["hashed_runs"] >= 1, paths
+    t.close()
+
+
+def test_uuid_slices_handed_back(gpu, part, monkeypatch):
+    """More groups than a 2^20-slot table's slices hold in LDS (2048 each): every slice hands its
+    UUID records back; they are turned into hashed records (text into the heap) and inserted
+    globally into a grown table.  Exact."""
+    monkeypatch.setenv("DQ_FREQ_PART_SLOTS", str(1 << 20))
+    n = 1_300_000
+    keys = [_uuid(v) for v in range(n)] + [_uuid(v) for v in range(0, n, 7)]
+    t = _consume(keys, False, 2)
+    s = t.summary()
+    assert (s.num_groups, s.grouped_rows) == (n, len(keys))
+    assert s.num_unique == n - len(range(0, n, 7))
+    paths = t.paths()
+    assert paths["uuid_runs"] >= 1 and paths["hashed_inserts"] > 0, paths
+    c, k = t.top(3)
+    assert c.tolist() == [2, 2, 2] and all(len(x) == 36 for x in k)
+    t.close()
