@@ -794,32 +794,24 @@ def _exchange_stats(world: int, local: int):
 
 
 def _c4_table_access(keys: str, groups: float, rows: int):
-    """SURVEY §8(d) C4 asks for the table accesses per row beside the streaming fraction.  A staged
-    row's record is written by the row-order stage, read and written by the level-1 split (into its
-    region), read and written by the level-2 split (into its slice region) and read by the slice
-    aggregation: 3 writes + 3 reads for packed and hashed records; 16-B records keep one fused
-    stage-and-split kernel, 2 writes + 2 reads.  Probes are in LDS; the table is written once,
-    occupied slots only (compacted) for packed and hashed records.  Hashed records (long /
-    composite keys) also copy each key's bytes into the key heap once, and re-read a record and two
-    keys per row that joins an existing hash group (the exact compare)."""
+    """SURVEY §8(d) C4 asks for the table accesses per row beside the streaming fraction.  Digit
+    keys (packed 8-B records): written by the row-order stage, read and written by the level-1
+    split, read and written by the level-2 split, read by the slice aggregation -- 3 writes + 3
+    reads.  Other short keys (16-B records) and canonical UUIDs (16-B records of their 128 bits)
+    take one fused stage-and-split kernel: 2 writes + 2 reads.  Composite keys (hashed records)
+    take the row-order stage, copy each key's bytes into the key heap once, and re-read a record
+    and two keys per row that joins an existing hash group (the exact compare).  Probes are in
+    LDS; the table is written once, occupied slots only (compacted); a UUID group's 36-byte text
+    is written once per group."""
     slot_bytes = 32.0
     rec = {"digits": 8, "alnum": 16, "uuid": 16, "pair": 16}[keys]
-    passes = {"digits": (3, 3), "alnum": (2, 2), "uuid": (3, 3), "pair": (3, 3)}[keys]
-    compacted = keys != "alnum"
+    passes = {"digits": (3, 3), "alnum": (2, 2), "uuid": (2, 2), "pair": (3, 3)}[keys]
+    heap = {"uuid": 40.0}.get(keys, 0.0)
     return {"record_bytes": rec, "record_writes_per_row": passes[0], "record_reads_per_row": passes[1],
             "global_table_probes_per_row": 0,
-            "table_bytes_written_per_row": (groups if compacted else _c4_table_slots(groups)) * slot_bytes / float(rows),
-            "table_write": "occupied slots only" if compacted else "whole slot image",
-            "key_heap_copy": keys in ("uuid", "pair")}
-
-
-def _c4_table_slots(groups: float) -> float:
-    """Slots of the table the partition path sizes for `groups` (power of two, load <= 0.5 of 1.15 x the
-    estimate; dq_freq_api.inc materialize)."""
-    cap = 65536.0
-    while groups * 1.15 + 4096 > 0.5 * cap:
-        cap *= 2
-    return cap
+            "table_bytes_written_per_row": groups * (slot_bytes + heap) / float(rows),
+            "table_write": "occupied slots only" + (" + each group's text (40 B)" if heap else ""),
+            "key_heap_copy": keys == "pair"}
 
 
 def _strings_from_ints(ids, width: int, prefix: bytes, dev):

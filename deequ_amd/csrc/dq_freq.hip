@@ -3533,9 +3533,26 @@ struct AggLdsU {
   uint32_t hist[kAggLdsHist];
 };
 
-__global__ __launch_bounds__(kAggUThreads) void dq_freq_agg_uuid_kernel(
-    FreqTable T, const UuidRec* __restrict__ recs, const unsigned long long* __restrict__ fill, uint64_t cap,
+// The record's two key words and its table hash (UuidRec: the UUID's 128 bits; FreqRec: the
+// inline key bytes with the length in k1's top byte -- the same words make the same key).
+__device__ inline uint64_t agg_w0(const UuidRec& r) { return r.lo; }
+__device__ inline uint64_t agg_w1(const UuidRec& r) { return r.hi; }
+__device__ inline uint64_t agg_w0(const FreqRec& r) { return r.k0; }
+__device__ inline uint64_t agg_w1(const FreqRec& r) { return r.k1; }
+__device__ inline uint64_t agg_hash(uint64_t w0, uint64_t w1, const UuidRec*) { return hash_uuid(w0, w1); }
+__device__ inline uint64_t agg_hash(uint64_t w0, uint64_t w1, const FreqRec*) {
+  const uint32_t len = (uint32_t)(w1 >> kRecLenShift);
+  return hash_inline(w0, w1 & ((1ull << kRecLenShift) - 1ull), len);
+}
+
+// R = UuidRec: canonical UUID records (text into the heap at write-out); R = FreqRec: 16-byte
+// records of keys of <= 15 bytes (round 6: the same hash-CAS + LDS compare in place of
+// dq_freq_agg_region_kernel's two-word publish protocol, for fresh tables).
+template <typename R>
+__global__ __launch_bounds__(kAggUThreads) void dq_freq_agg_keys_kernel(
+    FreqTable T, const R* __restrict__ recs, const unsigned long long* __restrict__ fill, uint64_t cap,
     uint64_t n_slices, FreqRec* retry, unsigned long long* n_retry, unsigned long long* new_groups, AggTrack tr) {
+  constexpr bool kUuid = std::is_same<R, UuidRec>::value;
   constexpr uint32_t S = (uint32_t)kFreqSliceSlots;
   constexpr int NT = kAggUThreads;
   constexpr uint32_t kChunk = (uint32_t)kAggUPer * NT;
@@ -3572,7 +3589,7 @@ __global__ __launch_bounds__(kAggUThreads) void dq_freq_agg_uuid_kernel(
     }
     lds_barrier();
     for (uint64_t c0 = r0; c0 < r1; c0 += kChunk) {
-      UuidRec rb[kAggUPer];
+      R rb[kAggUPer];
       uint32_t sl[kAggUPer];
 #pragma unroll
       for (int j = 0; j < kAggUPer; ++j) {
@@ -3584,15 +3601,15 @@ __global__ __launch_bounds__(kAggUThreads) void dq_freq_agg_uuid_kernel(
       for (int j = 0; j < kAggUPer; ++j) {
         sl[j] = 0u;
         if (c0 + (uint64_t)j * NT + t >= r1) continue;
-        const uint64_t h = hash_uuid(rb[j].lo, rb[j].hi);
+        const uint64_t h = agg_hash(agg_w0(rb[j]), agg_w1(rb[j]), (const R*)nullptr);
         const unsigned long long kk = h ? h : 1ull;
         uint32_t s = (uint32_t)h & (S - 1u);
         uint32_t probe = 0;
         for (; probe < S; ++probe) {
           const unsigned long long c = atomicCAS(&L.K[s], 0ull, kk);
           if (c == 0ull) {
-            L.KL[s] = rb[j].lo;
-            L.KH[s] = rb[j].hi;
+            L.KL[s] = agg_w0(rb[j]);
+            L.KH[s] = agg_w1(rb[j]);
             atomicAdd(&L.C[s], 1u);
             break;
           }
@@ -3609,7 +3626,7 @@ __global__ __launch_bounds__(kAggUThreads) void dq_freq_agg_uuid_kernel(
       lds_barrier();  // every group's first key words are in place (later claims touch other slots)
 #pragma unroll
       for (int j = 0; j < kAggUPer; ++j)
-        if (((joined >> j) & 1u) && (L.KL[sl[j]] != rb[j].lo || L.KH[sl[j]] != rb[j].hi)) L.overflow = 2;
+        if (((joined >> j) & 1u) && (L.KL[sl[j]] != agg_w0(rb[j]) || L.KH[sl[j]] != agg_w1(rb[j]))) L.overflow = 2;
     }
     lds_barrier();
     // this thread's eight slots: occupancy, the slice's group count, one heap reservation
@@ -3620,7 +3637,7 @@ __global__ __launch_bounds__(kAggUThreads) void dq_freq_agg_uuid_kernel(
     for (int j = 0; j < 4; ++j) occ |= (cs[j] ? 1u : 0u) << j;
     uint32_t tot;
     const uint32_t k = block_prefix<NT>((uint32_t)__builtin_popcount(occ), L.wsum, &tot);
-    if (t == 0 && !L.overflow) {
+    if (kUuid && t == 0 && !L.overflow) {
       const unsigned long long need = (unsigned long long)tot * kUuidHeap;
       const unsigned long long hb = atomicAdd(T.heap_used, need);
       if (hb + need > T.heap_cap) L.overflow = 3;  // (the host sized the heap from the sketch; it clamps heap_used)
@@ -3676,16 +3693,25 @@ __global__ __launch_bounds__(kAggUThreads) void dq_freq_agg_uuid_kernel(
         }
         continue;
       }
-      const uint64_t lo = L.KL[s], hi = L.KH[s];
-      uuid_store_text(T.heap, hoff, lo, hi);
-      const unsigned long long ctrl = ((unsigned long long)tag_of(hash_uuid(lo, hi)) << 32) | kReady | kHeapKey | kUuidLen;
+      const uint64_t w0 = L.KL[s], w1 = L.KH[s];
+      unsigned long long ctrl, k0, k1;
+      if constexpr (kUuid) {
+        uuid_store_text(T.heap, hoff, w0, w1);
+        ctrl = ((unsigned long long)tag_of(hash_uuid(w0, w1)) << 32) | kReady | kHeapKey | kUuidLen;
+        k0 = hoff;
+        k1 = 0ull;
+        hoff += kUuidHeap;
+      } else {
+        ctrl = ((unsigned long long)tag_of(agg_hash(w0, w1, (const R*)nullptr)) << 32) | kReady | (w1 >> kRecLenShift);
+        k0 = w0;
+        k1 = w1 & ((1ull << kRecLenShift) - 1ull);
+      }
       if (compact) {
-        *out++ = FreqSlot{ctrl, (unsigned long long)cs[j], hoff, 0ull};
+        *out++ = FreqSlot{ctrl, (unsigned long long)cs[j], k0, k1};
       } else {
         halves[2u * s] = ulonglong2{ctrl, (unsigned long long)cs[j]};
-        halves[2u * s + 1u] = ulonglong2{hoff, 0ull};
+        halves[2u * s + 1u] = ulonglong2{k0, k1};
       }
-      hoff += kUuidHeap;
     }
     if (t == 0) {
       if (tot) atomicAdd(new_groups, (unsigned long long)tot);
@@ -4117,6 +4143,13 @@ hipError_t launch_freq_compact(const void* d_in, bool packed, const unsigned lon
   return hipGetLastError();
 }
 
+// 16-byte records into a fresh table take dq_freq_agg_keys_kernel<FreqRec> (round 6);
+// DQ_FREQ_AGG16=0 keeps dq_freq_agg_region_kernel (A/B knob).
+static const bool g_agg_keys_free = [] {
+  const char* e = std::getenv("DQ_FREQ_AGG16");
+  return e == nullptr || e[0] != '0';
+}();
+
 hipError_t launch_freq_agg_region(const FreqTable& T, const void* d_recs, int rec_kind, const unsigned long long* d_fill,
                                   uint64_t cap, uint64_t n_slices, int table_empty, FreqRec* d_retry,
                                   unsigned long long* d_n_retry, unsigned long long* d_new_groups,
@@ -4131,8 +4164,11 @@ hipError_t launch_freq_agg_region(const FreqTable& T, const void* d_recs, int re
   if ((rec_kind == kRecHashed || rec_kind == kRecUuid) && !table_empty) return hipErrorInvalidValue;  // (fresh tables only)
   AggTrack tr{d_hist, d_big, d_n_big, big_cap, d_smax, write_all, compact ? *compact : FreqCompact{}};
   if (rec_kind == kRecUuid)
-    hipLaunchKernelGGL(dq_freq_agg_uuid_kernel, dim3((unsigned)blocks), dim3(kAggUThreads), 0, stream, T,
+    hipLaunchKernelGGL(dq_freq_agg_keys_kernel<UuidRec>, dim3((unsigned)blocks), dim3(kAggUThreads), 0, stream, T,
                        static_cast<const UuidRec*>(d_recs), d_fill, cap, n_slices, d_retry, d_n_retry, d_new_groups, tr);
+  else if (rec_kind == kRecFree && table_empty && g_agg_keys_free)
+    hipLaunchKernelGGL(dq_freq_agg_keys_kernel<FreqRec>, dim3((unsigned)blocks), dim3(kAggUThreads), 0, stream, T,
+                       static_cast<const FreqRec*>(d_recs), d_fill, cap, n_slices, d_retry, d_n_retry, d_new_groups, tr);
   else if (rec_kind == kRecHashed)
     hipLaunchKernelGGL(dq_freq_agg_hashed_kernel, dim3((unsigned)blocks), dim3(kAggHThreads), 0, stream, T,
                        static_cast<const HashRec*>(d_recs), d_fill, cap, n_slices, d_retry, d_n_retry, d_new_groups, tr);
