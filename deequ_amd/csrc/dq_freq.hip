@@ -1644,7 +1644,7 @@ __device__ inline void part_tile(PartLdsT<MAXB, R, SUBN>& L, const R (&rec)[PER]
 #endif
 // MAXB: LDS bin arrays for up to that many bins (512 when bin_bits <= 9: more LDS for the image).
 template <typename R, int MAXB>
-__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(sizeof(R) == 8 && MAXB <= 512 ? DQ_PARTP_WAVES : 1))) void dq_freq_part_kernel(
+__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(MAXB <= 512 ? DQ_PARTP_WAVES : 1))) void dq_freq_part_kernel(
     const R* __restrict__ in, uint64_t in_n, const unsigned long long* __restrict__ in_fill, uint64_t in_cap,
     int id_bits, int bin_bits, R* __restrict__ out, uint64_t out_cap, unsigned long long* out_fill,
     FreqRec* ovf, unsigned long long* ovf_n, uint64_t ovf_cap, unsigned int* flag, unsigned long long* staged) {
@@ -3518,7 +3518,7 @@ __global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(D
 // the slot image, and their text as 40 consecutive heap bytes each at one heap reservation per
 // slice.
 constexpr int kAggUThreads = 512;  // (the 58 KB image allows two workgroups per CU: 4 waves per SIMD)
-constexpr int kAggUPer = 8;
+constexpr int kAggUPer = 4;  // (<= 128 VGPRs: two workgroups per CU)
 struct AggLdsU {
   unsigned long long K[kFreqSliceSlots];
   unsigned long long KL[kFreqSliceSlots];
@@ -3549,7 +3549,7 @@ __device__ inline uint64_t agg_hash(uint64_t w0, uint64_t w1, const FreqRec*) {
 // records of keys of <= 15 bytes (round 6: the same hash-CAS + LDS compare in place of
 // dq_freq_agg_region_kernel's two-word publish protocol, for fresh tables).
 template <typename R>
-__global__ __launch_bounds__(kAggUThreads) void dq_freq_agg_keys_kernel(
+__global__ __launch_bounds__(kAggUThreads) __attribute__((amdgpu_waves_per_eu(4))) void dq_freq_agg_keys_kernel(
     FreqTable T, const R* __restrict__ recs, const unsigned long long* __restrict__ fill, uint64_t cap,
     uint64_t n_slices, FreqRec* retry, unsigned long long* n_retry, unsigned long long* new_groups, AggTrack tr) {
   constexpr bool kUuid = std::is_same<R, UuidRec>::value;
@@ -3596,32 +3596,45 @@ __global__ __launch_bounds__(kAggUThreads) void dq_freq_agg_keys_kernel(
         const uint64_t idx = c0 + (uint64_t)j * NT + t;
         if (idx < r1) rb[j] = recs[idx];
       }
+      // every record's first probe is issued before any result is looked at (independent LDS
+      // round trips, as dq_freq_agg_packed_kernel); at the table's ~0.4 load most records are
+      // counted there
       uint32_t joined = 0u;
+      unsigned long long kk[kAggUPer], cv[kAggUPer];
 #pragma unroll
       for (int j = 0; j < kAggUPer; ++j) {
-        sl[j] = 0u;
-        if (c0 + (uint64_t)j * NT + t >= r1) continue;
+        const bool in = c0 + (uint64_t)j * NT + t < r1;
         const uint64_t h = agg_hash(agg_w0(rb[j]), agg_w1(rb[j]), (const R*)nullptr);
-        const unsigned long long kk = h ? h : 1ull;
-        uint32_t s = (uint32_t)h & (S - 1u);
+        kk[j] = h ? h : 1ull;
+        sl[j] = (uint32_t)h & (S - 1u);
+        cv[j] = in ? atomicCAS(&L.K[sl[j]], 0ull, kk[j]) : ~0ull;
+      }
+#pragma unroll
+      for (int j = 0; j < kAggUPer; ++j) {
+        if (c0 + (uint64_t)j * NT + t >= r1) continue;
+        uint32_t s = sl[j];
+        unsigned long long c = cv[j];
         uint32_t probe = 0;
-        for (; probe < S; ++probe) {
-          const unsigned long long c = atomicCAS(&L.K[s], 0ull, kk);
+        while (true) {
           if (c == 0ull) {
             L.KL[s] = agg_w0(rb[j]);
             L.KH[s] = agg_w1(rb[j]);
             atomicAdd(&L.C[s], 1u);
             break;
           }
-          if (c == kk) {
+          if (c == kk[j]) {
             atomicAdd(&L.C[s], 1u);
             joined |= 1u << j;
             sl[j] = s;
             break;
           }
+          if (++probe == S) {
+            L.overflow = 1;
+            break;
+          }
           s = (s + 1u) & (S - 1u);
+          c = atomicCAS(&L.K[s], 0ull, kk[j]);
         }
-        if (probe == S) L.overflow = 1;
       }
       lds_barrier();  // every group's first key words are in place (later claims touch other slots)
 #pragma unroll
@@ -3637,11 +3650,20 @@ __global__ __launch_bounds__(kAggUThreads) void dq_freq_agg_keys_kernel(
     for (int j = 0; j < 4; ++j) occ |= (cs[j] ? 1u : 0u) << j;
     uint32_t tot;
     const uint32_t k = block_prefix<NT>((uint32_t)__builtin_popcount(occ), L.wsum, &tot);
-    if (kUuid && t == 0 && !L.overflow) {
+    if (t == 0 && !L.overflow) {
+      // the slice's heap text (UUIDs) and compacted slots, both reserved before one barrier (a
+      // slice that then hands its records back leaves an unused range: readers go by base / num)
+      unsigned long long hb = 0ull, at = 0ull;
       const unsigned long long need = (unsigned long long)tot * kUuidHeap;
-      const unsigned long long hb = atomicAdd(T.heap_used, need);
-      if (hb + need > T.heap_cap) L.overflow = 3;  // (the host sized the heap from the sketch; it clamps heap_used)
+      if (kUuid) hb = atomicAdd(T.heap_used, need);
+      if (compact) at = atomicAdd(tr.cmp.cursor, (unsigned long long)tot);
+      if (kUuid && hb + need > T.heap_cap) L.overflow = 3;  // (the host sized the heap from the sketch; it clamps heap_used)
       L.hbase = hb;
+      L.cbase = at;
+      if (compact) {
+        tr.cmp.base[b] = at;
+        tr.cmp.num[b] = L.overflow ? 0u : tot;
+      }
     }
     lds_barrier();
     if (L.overflow) {  // hand the region's records back (their bits: the host converts, then inserts globally)
@@ -3673,14 +3695,8 @@ __global__ __launch_bounds__(kAggUThreads) void dq_freq_agg_keys_kernel(
     if (compact) {
       const uint32_t pair = occ | ((uint32_t)__shfl_down((int)occ, 1, 64) << 4);  // (byte t / 2: slots 4t .. 4t + 7)
       if (!(t & 1u)) tr.cmp.bits[(b << 8) + (t >> 1)] = (uint8_t)pair;
-      if (t == 0) {
-        const unsigned long long at = atomicAdd(tr.cmp.cursor, (unsigned long long)tot);
-        L.cbase = at;
-        tr.cmp.base[b] = at;
-        tr.cmp.num[b] = tot;
-      }
     }
-    lds_barrier();  // (L.cbase; every thread's cmax update before thread 0 reads it)
+    lds_barrier();  // (every thread's cmax update before thread 0 reads it)
     unsigned long long hoff = L.hbase + (unsigned long long)k * kUuidHeap;
     FreqSlot* out = compact ? tr.cmp.slots + L.cbase + k : nullptr;
 #pragma unroll
@@ -3955,6 +3971,18 @@ hipError_t launch_freq_part(const void* d_in, uint64_t in_n, const unsigned long
     hipLaunchKernelGGL((dq_freq_part_kernel<uint64_t, (1 << kPartMaxBinBits)>), grid, dim3(kPartThreads), 0, stream,
                        static_cast<const uint64_t*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
                        static_cast<uint64_t*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag, d_staged);
+  else if (bin_bits <= kStageBinBits && rec_kind == kRecHashed)  // (512 bins: a smaller LDS image, 2 workgroups per CU)
+    hipLaunchKernelGGL((dq_freq_part_kernel<HashRec, (1 << kStageBinBits)>), grid, dim3(kPartThreads), 0, stream,
+                       static_cast<const HashRec*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
+                       static_cast<HashRec*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag, d_staged);
+  else if (bin_bits <= kStageBinBits && rec_kind == kRecUuid)
+    hipLaunchKernelGGL((dq_freq_part_kernel<UuidRec, (1 << kStageBinBits)>), grid, dim3(kPartThreads), 0, stream,
+                       static_cast<const UuidRec*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
+                       static_cast<UuidRec*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag, d_staged);
+  else if (bin_bits <= kStageBinBits && rec_kind == kRecFree)
+    hipLaunchKernelGGL((dq_freq_part_kernel<FreqRec, (1 << kStageBinBits)>), grid, dim3(kPartThreads), 0, stream,
+                       static_cast<const FreqRec*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
+                       static_cast<FreqRec*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag, d_staged);
   else if (rec_kind == kRecHashed)
     hipLaunchKernelGGL((dq_freq_part_kernel<HashRec, (1 << kPartMaxBinBits)>), grid, dim3(kPartThreads), 0, stream,
                        static_cast<const HashRec*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
@@ -3976,10 +4004,11 @@ hipError_t launch_freq_part(const void* d_in, uint64_t in_n, const unsigned long
 // not pack would fill the packed stage's overflow list and be staged twice.
 constexpr int kPackProbe = 16384;
 __global__ __launch_bounds__(kBlock) void dq_freq_pack_probe_kernel(FreqKeySpec ks, const DevColumn* __restrict__ cols,
-                                                                    int64_t n_rows, unsigned long long* out) {
+                                                                    int64_t n_rows, unsigned long long* out,
+                                                                    unsigned long long* n_long) {
   const DevColumn& c = cols[ks.key_cols[0]];
   const int64_t samples = n_rows < kPackProbe ? n_rows : kPackProbe;
-  uint32_t bad = 0u;
+  uint32_t bad = 0u, longer = 0u;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < samples; i += (int64_t)gridDim.x * kBlock) {
     // scattered rows (a multiplicative hash of i), not a fixed stride: a periodic key pattern
     // would alias with a stride
@@ -3989,6 +4018,7 @@ __global__ __launch_bounds__(kBlock) void dq_freq_pack_probe_kernel(FreqKeySpec 
     const uint32_t n = (uint32_t)(c.offsets[row + 1] - c.offsets[row]);
     if (n > 15u) {
       ++bad;
+      ++longer;
       continue;
     }
     uint64_t k0 = 0ull, k1 = 0ull, p;
@@ -4000,13 +4030,14 @@ __global__ __launch_bounds__(kBlock) void dq_freq_pack_probe_kernel(FreqKeySpec 
     if (!kp_pack_record(k0, k1, n, &p)) ++bad;
   }
   if (bad) atomicAdd(out, (unsigned long long)bad);
+  if (longer && n_long) atomicAdd(n_long, (unsigned long long)longer);
 }
 
 hipError_t launch_freq_pack_probe(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, unsigned long long* d_out,
-                                  hipStream_t stream) {
+                                  hipStream_t stream, unsigned long long* d_long) {
   if (n_rows <= 0) return hipSuccess;
   hipLaunchKernelGGL(dq_freq_pack_probe_kernel, dim3((kPackProbe + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, ks,
-                     d_cols, n_rows, d_out);
+                     d_cols, n_rows, d_out, d_long);
   return hipGetLastError();
 }
 

@@ -364,7 +364,7 @@ constexpr int kRecFree = 0, kRecPacked = 1, kRecHashed = 2, kRecUuid = 3;  // Fr
 // one_string: the only key column is utf8 (the kernel's batched-load fast path); packed (needs
 // one_string): digit keys staged as packed words, other keys onto the overflow list.
 hipError_t launch_freq_pack_probe(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, unsigned long long* d_out,
-                                  hipStream_t stream);
+                                  hipStream_t stream, unsigned long long* d_long = nullptr);
 // dq_profile.hip: ApproxCountDistinct registers (ranks, 512) and the five DataType counts of a
 // utf8 column from its flat groups (dq_profile_string_groups); both zeroed by the caller.
 hipError_t launch_string_groups(const int64_t* d_counts, const int64_t* d_offs, const uint8_t* d_bytes, int64_t n,
