@@ -1389,6 +1389,10 @@ constexpr uint32_t kStageTile = (uint32_t)kStageThreads * kStagePer;
 #define DQ_STAGEP_SUB kStageTile
 #endif
 constexpr uint32_t kStageSubP = DQ_STAGEP_SUB;  // packed records per LDS round of the fused stage
+#ifndef DQ_STAGE_SUB16
+#define DQ_STAGE_SUB16 3072  // (2048: 33.3 ms per alnum C4 step, 3072: 32.4, 6144: 32.8 -- profiles/r06g_c4_alnum_stage_sub_ab.txt)
+#endif
+constexpr uint32_t kStageSub16 = DQ_STAGE_SUB16;  // 16-byte records per LDS round of the fused stage
 
 // R: the record type of the regions -- FreqRec (16 B: key bytes + length) or, for a staging of
 // digit keys, its packed word (uint64_t, dq_keypack.h).
@@ -2011,7 +2015,7 @@ __global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(D
     uint32_t* hll, unsigned long long* long_key, unsigned long long* staged) {
   static_assert(ONE_STRING || !PACK, "packed records are staged from one string key column");
   using R = typename std::conditional<PACK, uint64_t, FreqRec>::type;
-  __shared__ PartLdsT<(1 << kStageBinBits), R, (PACK ? kStageSubP : kPartSub)> L;
+  __shared__ PartLdsT<(1 << kStageBinBits), R, (PACK ? kStageSubP : kStageSub16)> L;
   __shared__ uint32_t regs[kHllM];
   __shared__ uint4 psel[16];  // stage_pack's byte selectors by key length
   const uint32_t t = threadIdx.x;
@@ -2195,7 +2199,7 @@ __global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(D
       if constexpr (PACK)
         if (t == 0) abort_v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
-    part_tile<kStagePer, (1 << kStageBinBits), R, (PACK ? kStageSubP : kPartSub), kProf, DQ_STAGE_WOUT_UNROLL,
+    part_tile<kStagePer, (1 << kStageBinBits), R, (PACK ? kStageSubP : kStageSub16), kProf, DQ_STAGE_WOUT_UNROLL,
               PACK, kStageThreads, decltype(flag_read)>(
         L, rec, bin, nb, 0, out, cap1, fill1, ovf, ovf_n, ovf_cap, flag, staged, nullptr, prof_t_, flag_read);
   }

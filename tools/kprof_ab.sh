@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 for lib in ${LIBS:-x0}; do
   D=gpurun_out/kprof_$lib
   DEEQU_AMD_LIB=gpurun_ab/lib_$lib.so timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $D -o run --output-format csv \
-    -- python -u bench.py --workload ${WL:-c4} --steps ${STEPS:-2} --warmup 1 --no-cpu-baseline > $D.log 2>&1
+    -- python -u bench.py --workload ${WL:-c4} --steps ${STEPS:-2} --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > $D.log 2>&1
   st=$?
   if [ $st -ge 124 ]; then echo "STOP $lib: exit $st (fault / abort / time limit)"; tail -3 $D.log; exit $st; fi
   if [ $st -ne 0 ]; then echo "FAILED $lib (exit $st: an exception, timing still in the trace)"; grep -v "^[WE]2026" $D.log | tail -2; fi
