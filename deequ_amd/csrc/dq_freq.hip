@@ -3525,8 +3525,7 @@ constexpr int kAggUThreads = 512;  // (the 58 KB image allows two workgroups per
 constexpr int kAggUPer = 4;  // (<= 128 VGPRs: two workgroups per CU)
 struct AggLdsU {
   unsigned long long K[kFreqSliceSlots];
-  unsigned long long KL[kFreqSliceSlots];
-  unsigned long long KH[kFreqSliceSlots];
+  ulonglong2 KW[kFreqSliceSlots];  // the group's key words {w0, w1}: one 16-byte LDS access
   uint32_t C[kFreqSliceSlots];
   uint32_t wsum[8];
   int overflow;
@@ -3621,8 +3620,7 @@ __global__ __launch_bounds__(kAggUThreads) __attribute__((amdgpu_waves_per_eu(4)
         uint32_t probe = 0;
         while (true) {
           if (c == 0ull) {
-            L.KL[s] = agg_w0(rb[j]);
-            L.KH[s] = agg_w1(rb[j]);
+            L.KW[s] = ulonglong2{agg_w0(rb[j]), agg_w1(rb[j])};
             atomicAdd(&L.C[s], 1u);
             break;
           }
@@ -3643,7 +3641,10 @@ __global__ __launch_bounds__(kAggUThreads) __attribute__((amdgpu_waves_per_eu(4)
       lds_barrier();  // every group's first key words are in place (later claims touch other slots)
 #pragma unroll
       for (int j = 0; j < kAggUPer; ++j)
-        if (((joined >> j) & 1u) && (L.KL[sl[j]] != agg_w0(rb[j]) || L.KH[sl[j]] != agg_w1(rb[j]))) L.overflow = 2;
+        if ((joined >> j) & 1u) {
+          const ulonglong2 w = L.KW[sl[j]];
+          if (w.x != agg_w0(rb[j]) || w.y != agg_w1(rb[j])) L.overflow = 2;
+        }
     }
     lds_barrier();
     // this thread's eight slots: occupancy, the slice's group count, one heap reservation
@@ -3700,7 +3701,6 @@ __global__ __launch_bounds__(kAggUThreads) __attribute__((amdgpu_waves_per_eu(4)
       const uint32_t pair = occ | ((uint32_t)__shfl_down((int)occ, 1, 64) << 4);  // (byte t / 2: slots 4t .. 4t + 7)
       if (!(t & 1u)) tr.cmp.bits[(b << 8) + (t >> 1)] = (uint8_t)pair;
     }
-    lds_barrier();  // (every thread's cmax update before thread 0 reads it)
     unsigned long long hoff = L.hbase + (unsigned long long)k * kUuidHeap;
     FreqSlot* out = compact ? tr.cmp.slots + L.cbase + k : nullptr;
 #pragma unroll
@@ -3713,7 +3713,8 @@ __global__ __launch_bounds__(kAggUThreads) __attribute__((amdgpu_waves_per_eu(4)
         }
         continue;
       }
-      const uint64_t w0 = L.KL[s], w1 = L.KH[s];
+      const ulonglong2 kw = L.KW[s];
+      const uint64_t w0 = kw.x, w1 = kw.y;
       unsigned long long ctrl, k0, k1;
       if constexpr (kUuid) {
         uuid_store_text(T.heap, hoff, w0, w1);
@@ -3733,11 +3734,11 @@ __global__ __launch_bounds__(kAggUThreads) __attribute__((amdgpu_waves_per_eu(4)
         halves[2u * s + 1u] = ulonglong2{k0, k1};
       }
     }
-    if (t == 0) {
+    lds_barrier();  // LDS is reused by the next slice (every cmax update is in)
+    if (t == 0) {  // (thread 0 resets L.cmax only at the next slice's start, after this read)
       if (tot) atomicAdd(new_groups, (unsigned long long)tot);
       if (tr.smax) tr.smax[b] = L.cmax;
     }
-    lds_barrier();  // LDS is reused by the next slice
   }
   if (track) {
     lds_barrier();
