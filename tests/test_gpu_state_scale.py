@@ -83,6 +83,24 @@ def test_flat_import_rejects_bad_offsets(gpu):
     with pytest.raises(L.DeequAmdError):
         t.import_flat(np.array([1, 1]), np.array([0, 5, 3]), np.zeros(8, np.uint8))
     assert t.summary().num_groups == 0
+    assert t.num_rows == 0  # (a failing import adds no numRows)
+    t.close()
+
+
+def test_flat_import_tensor_inputs(gpu):
+    """Device tensors: a CPU tensor is refused (ValueError, nothing imported); int32 offsets and
+    int32 counts -- Arrow's string offsets -- are converted, not misread as int64."""
+    import torch
+    t = FrequencyTable(["s"], {"s": "string"})
+    dev = t.torch_device
+    blob = torch.tensor(list(b"abxyz"), dtype=torch.uint8, device=dev)
+    with pytest.raises(ValueError):
+        t.import_flat(torch.tensor([2, 3]), torch.tensor([0, 2, 5], device=dev), blob, 5)
+    assert t.summary().num_groups == 0 and t.num_rows == 0
+    t.import_flat(torch.tensor([2, 3], dtype=torch.int32, device=dev),
+                  torch.tensor([0, 2, 5], dtype=torch.int32, device=dev), blob, 5)
+    assert _flat_dict(t) == {b"ab": 2, b"xyz": 3}
+    assert t.num_rows == 5
     t.close()
 
 
