@@ -25,6 +25,7 @@
 #include "dq_uuidpack.h"
 
 #include <cstdio>
+#include <cstring>
 #include <type_traits>
 
 namespace dq {
@@ -3020,6 +3021,98 @@ __global__ __launch_bounds__(kBlock) void dq_freq_stage_hashed_kernel(FreqKeySpe
     if (regs[i] != 0xFFFFFFFFu) atomicMax(&hll[i], stage_sketch_rank(regs[i]));
 }
 
+// The hashed stage of a multi-column key (round 6): dq_freq_stage_hashed_kernel<false>'s
+// unrolled 16-row body held 251 VGPRs (two waves per SIMD) and ran 9.5 ms per 125M (int64, utf8)
+// rows.  Here the same tile layout (heap and records in row order, one heap reservation per
+// tile) with rolled loops: the rows' heap offsets wait in LDS between the length pass and the
+// copy pass, so a thread holds one row's key at a time.
+__global__ __launch_bounds__(kBlock) void dq_freq_stage_hashed_multi_kernel(FreqKeySpec ks, const DevColumn* __restrict__ cols,
+                                                                            int64_t n_rows, HashRec* __restrict__ out,
+                                                                            FreqTable T, uint32_t* hll,
+                                                                            unsigned long long* too_long,
+                                                                            unsigned long long* staged,
+                                                                            unsigned long long* max_len) {
+  static_assert(kBlock / 64 <= 4, "four waves");
+  __shared__ uint32_t regs[kHllM];
+  __shared__ uint32_t offs[kHashPer][kBlock];
+  __shared__ uint32_t wsum[4];
+  __shared__ unsigned long long tile_base;
+  for (uint32_t i = threadIdx.x; i < (uint32_t)kHllM; i += kBlock) regs[i] = 0xFFFFFFFFu;  // (stage_sketch)
+  __syncthreads();
+  const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+  unsigned long long n_keys = 0;
+  uint32_t longest = 0u;
+  bool tl_any = false;
+  const int64_t n_tiles = (n_rows + kHashTile - 1) / kHashTile;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const int64_t rw = tile * (int64_t)kHashTile + (int64_t)wave * 64 * kHashPer + lane;  // row of j = 0
+    uint32_t run = 0u;
+#pragma unroll 1
+    for (int j = 0; j < kHashPer; ++j) {
+      const int64_t row = rw + 64 * j;
+      uint32_t n = 0u, m8 = 0u;
+      if (row < n_rows && key_len_of(ks, cols, row, &n)) m8 = (n + 7u) & ~7u;
+      uint32_t x = m8;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+      }
+      offs[j][t] = run + x - m8;
+      run += __shfl(x, 63, 64);
+    }
+    if (lane == 0u) wsum[wave] = run;
+    __syncthreads();
+    uint32_t before = 0u, total = 0u;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+      before += (uint32_t)w < wave ? wsum[w] : 0u;
+      total += wsum[w];
+    }
+    if (t == 0) tile_base = total ? atomicAdd(T.heap_used, (unsigned long long)total) : 0ull;
+    __syncthreads();
+    const unsigned long long base = tile_base + before;
+    const bool room = tile_base + total <= T.heap_cap;  // (the host sized the heap: never false)
+    if (!room && t == 0) atomicOr(T.overflow, 2u);
+#pragma unroll 1
+    for (int j = 0; j < kHashPer; ++j) {
+      const int64_t row = rw + 64 * j;
+      if (row >= n_rows) break;
+      const unsigned long long at = base + offs[j][t];
+      HashRec r;
+      uint64_t kw[kHashWords];
+      uint32_t nm = 0u;
+      if (room && key_words<kHashWords>(ks, cols, row, kw, &nm) && nm) {
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(T.heap + at);
+#pragma unroll
+        for (int i = 0; i < kHashWords; ++i)
+          if (8u * (uint32_t)i < nm) dst[i] = kw[i];
+        r.h = nm <= 16u ? hash_inline(kw[0], kw[1], nm) : hash_long_words<kHashWords>(kw, nm);
+        r.ref = (at << 24) | nm;
+        longest = max(longest, nm);
+      } else {
+        bool tl = false;
+        if (room) stage_hashed_row(ks, cols, row, T, at, &r, &tl);
+        else { r.h = 0ull; r.ref = kHashHole; }
+        tl_any |= tl;
+        if (r.ref != kHashHole) longest = max(longest, (uint32_t)(r.ref & kLenMask));
+      }
+      if (r.ref != kHashHole) {
+        stage_sketch(regs, r.h);
+        ++n_keys;
+      }
+      out[row] = r;
+    }
+    __syncthreads();  // (offs, wsum and tile_base are rewritten by the next tile)
+  }
+  for (int d = 32; d >= 1; d >>= 1) n_keys += __shfl_xor(n_keys, d, 64);
+  if (staged && lane == 0u && n_keys) atomicAdd(staged, n_keys);
+  if (max_len && longest) atomicMax(max_len, (unsigned long long)longest);
+  if (tl_any) atomicMax(too_long, (unsigned long long)kMaxLocalKey + 1ull);
+  for (uint32_t i = t; i < (uint32_t)kHllM; i += kBlock)
+    if (regs[i] != 0xFFFFFFFFu) atomicMax(&hll[i], stage_sketch_rank(regs[i]));
+}
+
 // The key of a hashed record, its bytes read from (and, when long, left in) T's heap.
 __device__ inline Key hashed_key(const FreqTable& T, const FreqRec& r) {
   Key k;
@@ -4298,6 +4391,13 @@ hipError_t launch_freq_key_bytes(const FreqKeySpec& ks, const DevColumn* d_cols,
   return hipGetLastError();
 }
 
+// Multi-column keys take dq_freq_stage_hashed_multi_kernel; DQ_FREQ_HSTAGE=unrolled the round's
+// first (unrolled) body (A/B knob).
+static const bool g_hstage_unrolled = [] {
+  const char* e = std::getenv("DQ_FREQ_HSTAGE");
+  return e != nullptr && std::strcmp(e, "unrolled") == 0;
+}();
+
 hipError_t launch_freq_stage_hashed(const FreqKeySpec& ks, bool one_string, const DevColumn* d_cols, int64_t n_rows, HashRec* d_out,
                                     const FreqTable& T, uint32_t* d_hll, unsigned long long* d_too_long,
                                     unsigned long long* d_staged, unsigned long long* d_max_len, hipStream_t stream) {
@@ -4307,8 +4407,11 @@ hipError_t launch_freq_stage_hashed(const FreqKeySpec& ks, bool one_string, cons
   if (one_string)
     hipLaunchKernelGGL(dq_freq_stage_hashed_kernel<true>, dim3((unsigned)blocks), dim3(kBlock), 0, stream, ks, d_cols,
                        n_rows, d_out, T, d_hll, d_too_long, d_staged, d_max_len);
-  else
+  else if (g_hstage_unrolled)
     hipLaunchKernelGGL(dq_freq_stage_hashed_kernel<false>, dim3((unsigned)blocks), dim3(kBlock), 0, stream, ks, d_cols,
+                       n_rows, d_out, T, d_hll, d_too_long, d_staged, d_max_len);
+  else
+    hipLaunchKernelGGL(dq_freq_stage_hashed_multi_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, ks, d_cols,
                        n_rows, d_out, T, d_hll, d_too_long, d_staged, d_max_len);
   return hipGetLastError();
 }

@@ -7,9 +7,11 @@ fused pass of the gfx950 kernels, and `dq_plan_finish` returns one POD state per
 """
 from __future__ import annotations
 
+import collections
 import contextvars
 import ctypes
 import os
+import threading
 from typing import Dict, List, Optional, Sequence
 
 from . import _lib as L
@@ -239,8 +241,65 @@ LAUNCH_GATE: "contextvars.ContextVar" = contextvars.ContextVar("deequ_amd_launch
 LAUNCH_SIGNAL: "contextvars.ContextVar" = contextvars.ContextVar("deequ_amd_launch_signal", default=None)
 
 
+# Idle plans by (device, schema, packed analyzer list): dq_plan_create allocates the plan's
+# device state (task table, per-block partials, HLL registers) and a profiler run builds five or
+# six plans -- the same ones on every run.  A finished plan goes back here and the next run of the
+# same analyzers over the same schema takes it (dq_plan_reset) instead of creating one; each plan
+# is used by one thread at a time.  DEEQU_AMD_PLAN_CACHE=0 turns it off.
+_PLAN_POOL: "collections.OrderedDict[tuple, List[Plan]]" = collections.OrderedDict()
+_PLAN_POOL_LOCK = threading.Lock()
+_PLAN_POOL_IDLE = 32  # idle plans kept (least recently returned dropped first)
+
+
+def _take_plan(specs: Sequence[OpSpec], schema: Dict[str, str]):
+    if os.environ.get("DEEQU_AMD_PLAN_CACHE", "1") == "0":
+        return Plan(specs, schema), None
+    key = (current_device(), tuple(schema.items()), pack_ops(specs))
+    plan = None
+    with _PLAN_POOL_LOCK:
+        idle = _PLAN_POOL.get(key)
+        if idle:
+            plan = idle.pop()
+    if plan is not None:
+        try:
+            plan.reset()
+        except Exception:  # noqa: BLE001 - a plan that cannot be reset is dropped, a fresh one made
+            plan.close()
+            plan = None
+    return (plan if plan is not None else Plan(specs, schema)), key
+
+
+def _return_plan(plan: "Plan", key) -> None:
+    if key is None:
+        plan.close()
+        return
+    drop = []
+    with _PLAN_POOL_LOCK:
+        _PLAN_POOL.setdefault(key, []).append(plan)
+        _PLAN_POOL.move_to_end(key)
+        n = sum(len(v) for v in _PLAN_POOL.values())
+        while n > _PLAN_POOL_IDLE:
+            k, v = next(iter(_PLAN_POOL.items()))
+            drop.append(v.pop(0))
+            n -= 1
+            if not v:
+                del _PLAN_POOL[k]
+    for p in drop:
+        p.close()
+
+
+def clear_plan_cache() -> None:
+    """Releases every idle plan (their device memory)."""
+    with _PLAN_POOL_LOCK:
+        plans = [p for v in _PLAN_POOL.values() for p in v]
+        _PLAN_POOL.clear()
+    for p in plans:
+        p.close()
+
+
 def _scan_local(specs: Sequence[OpSpec], data) -> List:
-    plan = Plan(specs, data.schema)
+    plan, key = _take_plan(specs, data.schema)
+    ok = False
     try:
         gate = LAUNCH_GATE.get()
         if gate is not None:
@@ -258,9 +317,13 @@ def _scan_local(specs: Sequence[OpSpec], data) -> List:
                 res.append(L.DqState.from_buffer_copy(out[i]))
             except L.DeequAmdError as e:
                 res.append(OpUnsupported(e))
+        ok = True
         return res
     finally:
-        plan.close()
+        if ok:
+            _return_plan(plan, key)  # (the next run of the same analyzers resets and reuses it)
+        else:
+            plan.close()  # (a failed run's plan may hold a half-consumed batch)
 
 
 def run_scan_raw(specs: Sequence[OpSpec], data) -> List:
