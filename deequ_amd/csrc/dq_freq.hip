@@ -4338,6 +4338,27 @@ hipError_t launch_freq_uuid_to_hashed(const FreqTable& T, FreqRec* d_recs, uint6
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(kBlock) void dq_freq_len_probe_kernel(FreqKeySpec ks, const DevColumn* __restrict__ cols,
+                                                                   int64_t n_rows, unsigned long long* out) {
+  constexpr int64_t kProbe = 16384;  // (as kPackProbe)
+  const int64_t samples = n_rows < kProbe ? n_rows : kProbe;
+  uint32_t longer = 0u;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < samples; i += (int64_t)gridDim.x * kBlock) {
+    const int64_t row = samples == n_rows ? i : (int64_t)(((uint64_t)i * 11400714819323198485ull) % (uint64_t)n_rows);
+    uint32_t n;
+    if (key_len_of(ks, cols, row, &n) && n > 15u) ++longer;
+  }
+  if (longer) atomicAdd(out, (unsigned long long)longer);
+}
+
+hipError_t launch_freq_len_probe(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, unsigned long long* d_out,
+                                 hipStream_t stream) {
+  if (n_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(dq_freq_len_probe_kernel, dim3((16384 + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, ks, d_cols,
+                     n_rows, d_out);
+  return hipGetLastError();
+}
+
 hipError_t launch_freq_uuid_probe(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, unsigned long long* d_out,
                                   hipStream_t stream) {
   if (n_rows <= 0) return hipSuccess;

@@ -414,6 +414,10 @@ hipError_t launch_freq_stage_uuid(const FreqKeySpec& ks, const DevColumn* d_cols
                                   uint64_t ovf_cap, unsigned int* d_flag, uint32_t* d_hll, unsigned long long* d_bad,
                                   unsigned long long* d_staged, hipStream_t stream);
 hipError_t launch_freq_uuid_to_hashed(const FreqTable& T, FreqRec* d_recs, uint64_t n, hipStream_t stream);
+// Sampled rows (16384 scattered, as the pack probe) whose encoded key (make_key) is longer than
+// 15 bytes, added to *d_out: a multi-column table's choice of hashed records from the start.
+hipError_t launch_freq_len_probe(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, unsigned long long* d_out,
+                                 hipStream_t stream);
 hipError_t launch_freq_uuid_probe(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, unsigned long long* d_out,
                                   hipStream_t stream);
 // Global inserts of n hashed records (the list form: FreqRec bits of HashRec), their key bytes
