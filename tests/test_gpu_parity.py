@@ -371,3 +371,22 @@ def test_hll_rare_rank_branches(gpu):
     st = d.run_scan([d.ApproxCountDistinct(c) for c in cols], product_table(cols))
     for c in cols:
         assert list(st[d.ApproxCountDistinct(c)].words) == list(O.approx_count_distinct_state(ot, c).words), c
+
+
+def test_pooled_plan_reuse_equals_fresh_plan(gpu, monkeypatch):
+    """A finished plan goes back to the pool and the next run of the same analyzers over the same
+    schema resets and reuses it: every state equals a fresh plan's, across tables of different
+    sizes and NULL fractions (host and device batches), and the pool holds the plan afterwards."""
+    from deequ_amd import engine
+    engine.clear_plan_cache()
+    rng = np.random.default_rng(77)
+    analyzers = _analyzers()
+    tables = [product_table(random_table(rng, n, f)) for n, f in ((9000, 0.1), (17, 0.0), (40001, 0.5))]
+    tables[1] = tables[1].to_device(0)
+    pooled = [d.run_scan(analyzers, t) for t in tables]
+    assert sum(len(v) for v in engine._PLAN_POOL.values()) == 1
+    monkeypatch.setenv("DEEQU_AMD_PLAN_CACHE", "0")
+    for t, got in zip(tables, pooled):
+        fresh = d.run_scan(analyzers, t)
+        for a in analyzers:
+            assert got[a] == fresh[a], a
