@@ -63,13 +63,14 @@ def parse_args():
     p.add_argument("--c4-rows", type=int, default=1_000_000_000, help="rows per GPU")
     p.add_argument("--c4-batch", type=int, default=125_000_000, help="rows per string batch")
     p.add_argument("--c4-distinct", type=int, default=201_500_000)
-    p.add_argument("--c4-keys", default="digits", choices=["digits", "alnum", "uuid", "pair"],
+    p.add_argument("--c4-keys", default="digits", choices=["digits", "alnum", "uuid", "pair", "pair64"],
                    help="C4 key text: 12 decimal digits (packs into one word: 8-byte records), 'k' + 11 "
                         "digits (not a digit string: the 16-byte record path, after the packed staging gives up), "
-                        "uuid (36-character UUID text of the same ids: the hashed record path, isPrimaryKey's "
-                        "shape) or pair (a two-column key (int64 id / 1000, 8-digit id % 1000): 20 encoded "
+                        "uuid (36-character UUID text of the same ids: 128-bit records, isPrimaryKey's "
+                        "shape), pair (a two-column key (int64 id / 1000, 8-digit id % 1000): 20 encoded "
                         "bytes, the hashed record path; Uniqueness / Distinctness / UniqueValueRatio / "
-                        "CountDistinct of the pair)")
+                        "CountDistinct of the pair) or pair64 (the same pair as (int64, int64): 16 encoded "
+                        "bytes, the 16-byte-key records)")
     p.add_argument("--c4-verify", action="store_true",
                    help="after timing, check the C4 metrics against torch.unique over the integer ids on the "
                         "device (an independent sort-based group-by; 1 rank); adds `verify` to the line")
@@ -360,7 +361,7 @@ def make_c3_string_table(rows: int, n_cols: int, rank: int, device: int):
 def c4_batch_rows(batch: int, keys_kind: str) -> int:
     """Arrow utf8 offsets are int32: one batch holds at most 2^31 - 1 bytes of chars.  36-char
     UUIDs fit 59.6M rows, so the 125M-row default is cut to 50M-row batches for them."""
-    width = {"uuid": 36, "pair": 8}.get(keys_kind, 12)
+    width = {"uuid": 36, "pair": 8, "pair64": 0}.get(keys_kind, 12)
     if batch * width >= 2 ** 31:
         return 50_000_000 if width * 50_000_000 < 2 ** 31 else (2 ** 31 - 1) // width
     return batch
@@ -476,14 +477,15 @@ def make_c4_batches(rows: int, batch: int, distinct: int, rank: int, device: int
     gen = torch.Generator(device=dev)
     gen.manual_seed(7 + 1000 * rank)
     pow10 = torch.tensor([10 ** (11 - i) for i in range(12)], dtype=torch.int64, device=dev)
-    width = {"uuid": 36, "pair": 8}.get(keys_kind, 12)
+    width = {"uuid": 36, "pair": 8, "pair64": 0}.get(keys_kind, 12)
     batch = c4_batch_rows(batch, keys_kind)
     parts = []
     for b0 in range(0, rows, batch):
         m = min(batch, rows - b0)
         chars = torch.empty(m * width + 16, dtype=torch.uint8, device=dev)
         valid = torch.empty((m + 7) // 8 + 64, dtype=torch.uint8, device=dev)
-        avals = torch.empty(m, dtype=torch.int64, device=dev) if keys_kind == "pair" else None
+        avals = torch.empty(m, dtype=torch.int64, device=dev) if keys_kind in ("pair", "pair64") else None
+        bvals = torch.empty(m, dtype=torch.int64, device=dev) if keys_kind == "pair64" else None
         sub = 1 << 24
         for s in range(0, m, sub):
             e = min(m, s + sub)
@@ -493,6 +495,9 @@ def make_c4_batches(rows: int, batch: int, distinct: int, rank: int, device: int
             elif keys_kind == "pair":
                 avals[s:e] = keys // 1000
                 chars[s * width: e * width] = _strings_from_ints(keys % 1000, 8, b"", dev)
+            elif keys_kind == "pair64":
+                avals[s:e] = keys // 1000
+                bvals[s:e] = keys % 1000
             else:
                 digits = (keys[:, None] // pow10[None, :]) % 10 + 48
                 if keys_kind == "alnum":
@@ -500,8 +505,11 @@ def make_c4_batches(rows: int, batch: int, distinct: int, rank: int, device: int
                 chars[s * 12: e * 12] = digits.to(torch.uint8).reshape(-1)
             packed = _valid_bits(e - s, gen, dev, 0.01)
             valid[s // 8: s // 8 + packed.numel()] = packed
-        offsets = torch.arange(0, width * (m + 1), width, dtype=torch.int32, device=dev)
-        if keys_kind == "pair":
+        offsets = torch.arange(0, width * (m + 1), width, dtype=torch.int32, device=dev) if width else None
+        if keys_kind == "pair64":
+            parts.append(d.Table({"a": d.Column("int64", m, avals, valid, device=True),
+                                  "b": d.Column("int64", m, bvals, None, device=True)}))
+        elif keys_kind == "pair":
             parts.append(d.Table({"a": d.Column("int64", m, avals, valid, device=True),
                                   "b": d.Column("string", m, chars, None, offsets=offsets, device=True)}))
         else:
@@ -717,7 +725,7 @@ def run_c4(args, world, rank, local):
     from deequ_amd.distributed import ShardedTable
     shard = make_c4_batches(args.c4_rows, args.c4_batch, args.c4_distinct, rank, local, args.c4_keys)
     data = ShardedTable(shard) if world > 1 else shard
-    pair = args.c4_keys == "pair"
+    pair = args.c4_keys in ("pair", "pair64")
     if pair:  # a composite key: the pair's frequency analyzers (Check.hasUniqueness / isPrimaryKey shape)
         cols = ["a", "b"]
         analyzers = [d.Uniqueness(cols), d.Distinctness(cols), d.UniqueValueRatio(cols), d.CountDistinct(cols)]
@@ -747,7 +755,8 @@ def run_c4(args, world, rank, local):
         "dtype": "utf8 keys, int64 counts",
         "data": "synthetic %s keys of ids uniform in [0, %d), 1%% NULL, generated in HBM"
                 % ({"digits": "12-digit", "alnum": "'k' + 11-digit", "uuid": "36-character UUID",
-                    "pair": "(int64, 8-digit utf8) pair"}[args.c4_keys], args.c4_distinct),
+                    "pair": "(int64, 8-digit utf8) pair", "pair64": "(int64, int64) pair"}[args.c4_keys],
+                   args.c4_distinct),
         "config": {"workload": ("C4: %d rows/GPU in %d-row batches; Uniqueness, Distinctness, UniqueValueRatio, "
                                 "CountDistinct of the two-column key (a, b), one GPU group-by%s" if pair else
                                 "C4: %d rows/GPU in %d-row utf8 batches; Uniqueness, Distinctness, Entropy, "
@@ -804,8 +813,8 @@ def _c4_table_access(keys: str, groups: float, rows: int):
     LDS; the table is written once, occupied slots only (compacted); a UUID group's 36-byte text
     is written once per group."""
     slot_bytes = 32.0
-    rec = {"digits": 8, "alnum": 16, "uuid": 16, "pair": 16}[keys]
-    passes = {"digits": (3, 3), "alnum": (2, 2), "uuid": (2, 2), "pair": (3, 3)}[keys]
+    rec = {"digits": 8, "alnum": 16, "uuid": 16, "pair": 16, "pair64": 16}[keys]
+    passes = {"digits": (3, 3), "alnum": (2, 2), "uuid": (2, 2), "pair": (3, 3), "pair64": (2, 2)}[keys]
     heap = {"uuid": 40.0}.get(keys, 0.0)
     return {"record_bytes": rec, "record_writes_per_row": passes[0], "record_reads_per_row": passes[1],
             "global_table_probes_per_row": 0,

@@ -1429,6 +1429,10 @@ __device__ inline uint64_t rec_hash(const UuidRec& r, bool* hole) {
   *hole = false;  // (the UUID stage is fused with the level-1 split: no row-order holes)
   return hash_uuid(r.lo, r.hi);
 }
+__device__ inline uint64_t rec_hash(const Raw16Rec& r, bool* hole) {
+  *hole = false;  // (as UuidRec)
+  return hash_inline(r.lo, r.hi, 16u);
+}
 
 // A record in the 16-byte form (what the overflow and retry lists and the sort path hold; a
 // hashed record keeps its bits: the hashed path's lists are read by dq_freq_insert_hashed_kernel).
@@ -1440,6 +1444,12 @@ __device__ inline FreqRec rec_raw(const HashRec& r) {
   return f;
 }
 __device__ inline FreqRec rec_raw(const UuidRec& r) {  // (its bits; the host converts such lists)
+  FreqRec f;
+  f.k0 = r.lo;
+  f.k1 = r.hi;
+  return f;
+}
+__device__ inline FreqRec rec_raw(const Raw16Rec& r) {  // (as UuidRec)
   FreqRec f;
   f.k0 = r.lo;
   f.k1 = r.hi;
@@ -3604,6 +3614,97 @@ __global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(D
     if (regs[i] != 0xFFFFFFFFu) atomicMax(&hll[i], stage_sketch_rank(regs[i]));
 }
 
+// Stage + level-1 split of 16-byte keys as Raw16Rec (round 6): STRING -- one utf8 column whose
+// non-NULL keys are all 16 bytes (one 16-byte load per row; any other length is counted in
+// bad_keys and the host rolls the batch back to hashed records); otherwise two 8-byte fixed-width
+// columns, the record being their value bits (make_key's encoding), a NULL in either dropping the
+// row.  The tile layout, the split and the sketch are the UUID stage's.
+template <bool STRING>
+__global__ __launch_bounds__(kStageThreads) __attribute__((amdgpu_waves_per_eu(DQ_STAGEP_WAVES))) void dq_freq_stage_raw16_kernel(
+    FreqKeySpec ks, const DevColumn* __restrict__ cols, int64_t n_rows, int b1, Raw16Rec* __restrict__ out,
+    uint64_t cap1, unsigned long long* fill1, FreqRec* ovf, unsigned long long* ovf_n, uint64_t ovf_cap,
+    unsigned int* flag, uint32_t* hll, unsigned long long* bad_keys, unsigned long long* staged) {
+  __shared__ PartLdsT<(1 << kStageBinBits), Raw16Rec, kPartSub> L;
+  __shared__ uint32_t regs[kHllM];
+  const uint32_t t = threadIdx.x;
+  const uint32_t nb = 1u << b1;
+  for (uint32_t i = t; i < (uint32_t)kHllM; i += kStageThreads) regs[i] = 0xFFFFFFFFu;  // (stage_sketch)
+  lds_barrier();
+  const DevColumn& c0 = cols[ks.key_cols[0]];
+  const DevColumn& c1 = cols[ks.key_cols[STRING ? 0 : 1]];
+  const int32_t* offs = STRING ? uniform_ptr(c0.offsets) : nullptr;
+  const uint32_t heap_end = STRING ? __builtin_amdgcn_readfirstlane((uint32_t)offs[n_rows]) : 0u;
+  const __amdgpu_buffer_rsrc_t rs_vals = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(static_cast<const uint8_t*>(uniform_ptr(c0.values))), 0, (int)heap_end, 0x00020000);
+  const uint8_t* validity0 = uniform_ptr(c0.validity);
+  const uint8_t* validity1 = STRING ? nullptr : uniform_ptr(c1.validity);
+  const unsigned long long* v0 = static_cast<const unsigned long long*>(uniform_ptr(c0.values));
+  const unsigned long long* v1 = static_cast<const unsigned long long*>(uniform_ptr(c1.values));
+  const int64_t n_tiles = (n_rows + kUuidTile - 1) / kUuidTile;
+  uint32_t n_bad = 0u;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const int64_t r0 = tile * (int64_t)kUuidTile;
+    const int64_t left = n_rows - r0;
+    const uint32_t m = (uint32_t)(left < (int64_t)kUuidTile ? left : (int64_t)kUuidTile);
+    const uint32_t vword0 = tile_valid_word<kStageThreads, kUuidPer>(validity0, r0, m);
+    const uint32_t vword1 = STRING ? 0u : tile_valid_word<kStageThreads, kUuidPer>(validity1, r0, m);
+    Raw16Rec rec[kUuidPer];
+    uint32_t bin[kUuidPer];
+    if constexpr (STRING) {
+      const __amdgpu_buffer_rsrc_t rs_off =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(offs + r0), 0, (int)(4u * (m + 1u)), 0x00020000);
+      uint32_t pob[kUuidPer], len[kUuidPer];
+#pragma unroll
+      for (int j = 0; j < kUuidPer; ++j) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs_off, (int)(4u * ((uint32_t)j * kStageThreads + t)), 0, 0);
+        pob[j] = v[0];
+        len[j] = v[1] - v[0];
+      }
+#pragma unroll
+      for (int j = 0; j < kUuidPer; ++j) {
+        const auto w = __builtin_amdgcn_raw_buffer_load_b128(rs_vals, (int)pob[j], 0, 0);
+        rec[j].lo = (unsigned long long)w[0] | ((unsigned long long)w[1] << 32);
+        rec[j].hi = (unsigned long long)w[2] | ((unsigned long long)w[3] << 32);
+        bin[j] = len[j];  // (the length, until the row is checked below)
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < kUuidPer; ++j) {
+        const int64_t row = r0 + (int64_t)j * kStageThreads + t;
+        rec[j].lo = rec[j].hi = 0ull;
+        if (row < n_rows) {
+          rec[j].lo = v0[row];
+          rec[j].hi = v1[row];
+        }
+        bin[j] = 16u;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kUuidPer; ++j) {
+      const uint32_t i = (uint32_t)j * kStageThreads + t;
+      const bool valid = (validity0 == nullptr || ((stage_valid_mask(vword0, j) >> (t & 63u)) & 1u)) &&
+                         (STRING || validity1 == nullptr || ((stage_valid_mask(vword1, j) >> (t & 63u)) & 1u));
+      const uint32_t n = bin[j];
+      bin[j] = kPartNoBin;
+      if (i >= m || !valid) continue;
+      if (n != 16u) {
+        ++n_bad;
+        continue;
+      }
+      const uint64_t h = hash_inline(rec[j].lo, rec[j].hi, 16u);
+      bin[j] = (uint32_t)(h >> (64 - b1)) & (nb - 1u);
+      stage_sketch(regs, h);
+    }
+    part_tile<kUuidPer, (1 << kStageBinBits), Raw16Rec, kPartSub, false, DQ_STAGE_WOUT_UNROLL, false, kStageThreads>(
+        L, rec, bin, nb, 0, out, cap1, fill1, ovf, ovf_n, ovf_cap, flag, staged);
+  }
+  for (int d = 32; d >= 1; d >>= 1) n_bad += __shfl_xor(n_bad, d, 64);
+  if ((t & 63u) == 0u && n_bad) atomicAdd(bad_keys, (unsigned long long)n_bad);
+  lds_barrier();
+  for (uint32_t i = t; i < (uint32_t)kHllM; i += kStageThreads)
+    if (regs[i] != 0xFFFFFFFFu) atomicMax(&hll[i], stage_sketch_rank(regs[i]));
+}
+
 // The owner aggregation of slice regions of UUID records into a FRESH table.  LDS image: the
 // table hash (0 kept as 1; the claimed mark), the group's key words and its count.  A chunk of
 // kAggUPer records per thread is counted by hash (one CAS per probe; the claimer stores its key
@@ -3635,6 +3736,9 @@ __device__ inline uint64_t agg_w0(const UuidRec& r) { return r.lo; }
 __device__ inline uint64_t agg_w1(const UuidRec& r) { return r.hi; }
 __device__ inline uint64_t agg_w0(const FreqRec& r) { return r.k0; }
 __device__ inline uint64_t agg_w1(const FreqRec& r) { return r.k1; }
+__device__ inline uint64_t agg_w0(const Raw16Rec& r) { return r.lo; }
+__device__ inline uint64_t agg_w1(const Raw16Rec& r) { return r.hi; }
+__device__ inline uint64_t agg_hash(uint64_t w0, uint64_t w1, const Raw16Rec*) { return hash_inline(w0, w1, 16u); }
 __device__ inline uint64_t agg_hash(uint64_t w0, uint64_t w1, const UuidRec*) { return hash_uuid(w0, w1); }
 __device__ inline uint64_t agg_hash(uint64_t w0, uint64_t w1, const FreqRec*) {
   const uint32_t len = (uint32_t)(w1 >> kRecLenShift);
@@ -3815,6 +3919,10 @@ __global__ __launch_bounds__(kAggUThreads) __attribute__((amdgpu_waves_per_eu(4)
         k0 = hoff;
         k1 = 0ull;
         hoff += kUuidHeap;
+      } else if constexpr (std::is_same<R, Raw16Rec>::value) {  // (a 16-byte key, inline)
+        ctrl = ((unsigned long long)tag_of(agg_hash(w0, w1, (const R*)nullptr)) << 32) | kReady | 16ull;
+        k0 = w0;
+        k1 = w1;
       } else {
         ctrl = ((unsigned long long)tag_of(agg_hash(w0, w1, (const R*)nullptr)) << 32) | kReady | (w1 >> kRecLenShift);
         k0 = w0;
@@ -3844,7 +3952,9 @@ __global__ __launch_bounds__(kAggUThreads) __attribute__((amdgpu_waves_per_eu(4)
 // turned in place into hashed records {table hash, heap reference}: each key's text written to
 // the heap (one reservation per wave), so dq_freq_insert_hashed_kernel can insert them.  The host
 // reserved the room; a record that finds none raises the heap-full bit.
+template <bool UUID>
 __global__ __launch_bounds__(kBlock) void dq_freq_uuid_to_hashed_kernel(FreqTable T, FreqRec* recs, uint64_t n) {
+  constexpr unsigned long long kBytes = UUID ? kUuidHeap : 16ull;  // (a Raw16Rec's key: 16 bytes)
   const uint32_t lane = threadIdx.x & 63u;
   for (uint64_t i0 = (uint64_t)blockIdx.x * kBlock; i0 < n; i0 += (uint64_t)gridDim.x * kBlock) {
     const uint64_t i = i0 + threadIdx.x;
@@ -3853,19 +3963,27 @@ __global__ __launch_bounds__(kBlock) void dq_freq_uuid_to_hashed_kernel(FreqTabl
     if (!ball) continue;
     const uint32_t first = (uint32_t)__builtin_ctzll(ball);
     unsigned long long base = 0ull;
-    if (lane == first) base = atomicAdd(T.heap_used, (unsigned long long)__popcll(ball) * kUuidHeap);
+    if (lane == first) base = atomicAdd(T.heap_used, (unsigned long long)__popcll(ball) * kBytes);
     base = __shfl(base, (int)first, 64);
     if (!act) continue;
     const FreqRec r = recs[i];
-    const unsigned long long off = base + (unsigned long long)__popcll(ball & ((1ull << lane) - 1ull)) * kUuidHeap;
-    if (off + kUuidHeap > T.heap_cap) {
+    const unsigned long long off = base + (unsigned long long)__popcll(ball & ((1ull << lane) - 1ull)) * kBytes;
+    if (off + kBytes > T.heap_cap) {
       atomicOr(T.overflow, 2u);
       continue;
     }
-    uuid_store_text(T.heap, off, r.k0, r.k1);
     FreqRec o;
-    o.k0 = hash_uuid(r.k0, r.k1);
-    o.k1 = (off << 24) | kUuidLen;
+    if constexpr (UUID) {
+      uuid_store_text(T.heap, off, r.k0, r.k1);
+      o.k0 = hash_uuid(r.k0, r.k1);
+      o.k1 = (off << 24) | kUuidLen;
+    } else {
+      unsigned long long* dst = reinterpret_cast<unsigned long long*>(T.heap + off);
+      dst[0] = r.k0;
+      dst[1] = r.k1;
+      o.k0 = hash_inline(r.k0, r.k1, 16u);
+      o.k1 = (off << 24) | 16ull;
+    }
     recs[i] = o;
   }
 }
@@ -4077,6 +4195,14 @@ hipError_t launch_freq_part(const void* d_in, uint64_t in_n, const unsigned long
     hipLaunchKernelGGL((dq_freq_part_kernel<UuidRec, (1 << kStageBinBits)>), grid, dim3(kPartThreads), 0, stream,
                        static_cast<const UuidRec*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
                        static_cast<UuidRec*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag, d_staged);
+  else if (bin_bits <= kStageBinBits && rec_kind == kRecRaw16)
+    hipLaunchKernelGGL((dq_freq_part_kernel<Raw16Rec, (1 << kStageBinBits)>), grid, dim3(kPartThreads), 0, stream,
+                       static_cast<const Raw16Rec*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
+                       static_cast<Raw16Rec*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag, d_staged);
+  else if (rec_kind == kRecRaw16)
+    hipLaunchKernelGGL((dq_freq_part_kernel<Raw16Rec, (1 << kPartMaxBinBits)>), grid, dim3(kPartThreads), 0, stream,
+                       static_cast<const Raw16Rec*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
+                       static_cast<Raw16Rec*>(d_out), out_cap, d_out_fill, d_ovf, d_ovf_n, ovf_cap, d_flag, d_staged);
   else if (bin_bits <= kStageBinBits && rec_kind == kRecFree)
     hipLaunchKernelGGL((dq_freq_part_kernel<FreqRec, (1 << kStageBinBits)>), grid, dim3(kPartThreads), 0, stream,
                        static_cast<const FreqRec*>(d_in), in_n, d_in_fill, in_cap, id_bits, bin_bits,
@@ -4290,11 +4416,15 @@ hipError_t launch_freq_agg_region(const FreqTable& T, const void* d_recs, int re
   if (!table_empty && (d_hist || d_smax || write_all)) return hipErrorInvalidValue;
   const bool packed = rec_kind == kRecPacked;
   if (compact && !table_empty) return hipErrorInvalidValue;
-  if ((rec_kind == kRecHashed || rec_kind == kRecUuid) && !table_empty) return hipErrorInvalidValue;  // (fresh tables only)
+  if ((rec_kind == kRecHashed || rec_kind == kRecUuid || rec_kind == kRecRaw16) && !table_empty)
+    return hipErrorInvalidValue;  // (fresh tables only)
   AggTrack tr{d_hist, d_big, d_n_big, big_cap, d_smax, write_all, compact ? *compact : FreqCompact{}};
   if (rec_kind == kRecUuid)
     hipLaunchKernelGGL(dq_freq_agg_keys_kernel<UuidRec>, dim3((unsigned)blocks), dim3(kAggUThreads), 0, stream, T,
                        static_cast<const UuidRec*>(d_recs), d_fill, cap, n_slices, d_retry, d_n_retry, d_new_groups, tr);
+  else if (rec_kind == kRecRaw16)
+    hipLaunchKernelGGL(dq_freq_agg_keys_kernel<Raw16Rec>, dim3((unsigned)blocks), dim3(kAggUThreads), 0, stream, T,
+                       static_cast<const Raw16Rec*>(d_recs), d_fill, cap, n_slices, d_retry, d_n_retry, d_new_groups, tr);
   else if (rec_kind == kRecFree && table_empty && g_agg_keys_free)
     hipLaunchKernelGGL(dq_freq_agg_keys_kernel<FreqRec>, dim3((unsigned)blocks), dim3(kAggUThreads), 0, stream, T,
                        static_cast<const FreqRec*>(d_recs), d_fill, cap, n_slices, d_retry, d_n_retry, d_new_groups, tr);
@@ -4330,11 +4460,14 @@ hipError_t launch_freq_stage_uuid(const FreqKeySpec& ks, const DevColumn* d_cols
   return hipGetLastError();
 }
 
-hipError_t launch_freq_uuid_to_hashed(const FreqTable& T, FreqRec* d_recs, uint64_t n, hipStream_t stream) {
+hipError_t launch_freq_uuid_to_hashed(const FreqTable& T, FreqRec* d_recs, uint64_t n, hipStream_t stream, int rec_kind) {
   if (n == 0) return hipSuccess;
   uint64_t blocks = (n + kBlock - 1) / kBlock;
   if (blocks > 65536) blocks = 65536;
-  hipLaunchKernelGGL(dq_freq_uuid_to_hashed_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, d_recs, n);
+  if (rec_kind == kRecRaw16)
+    hipLaunchKernelGGL(dq_freq_uuid_to_hashed_kernel<false>, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, d_recs, n);
+  else
+    hipLaunchKernelGGL(dq_freq_uuid_to_hashed_kernel<true>, dim3((unsigned)blocks), dim3(kBlock), 0, stream, T, d_recs, n);
   return hipGetLastError();
 }
 
@@ -4356,6 +4489,54 @@ hipError_t launch_freq_len_probe(const FreqKeySpec& ks, const DevColumn* d_cols,
   if (n_rows <= 0) return hipSuccess;
   hipLaunchKernelGGL(dq_freq_len_probe_kernel, dim3((16384 + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, ks, d_cols,
                      n_rows, d_out);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(kBlock) void dq_freq_len16_probe_kernel(FreqKeySpec ks, const DevColumn* __restrict__ cols,
+                                                                     int64_t n_rows, unsigned long long* out) {
+  const DevColumn& c = cols[ks.key_cols[0]];
+  constexpr int64_t kProbe = 16384;  // (as kPackProbe)
+  const int64_t samples = n_rows < kProbe ? n_rows : kProbe;
+  uint32_t other = 0u;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < samples; i += (int64_t)gridDim.x * kBlock) {
+    const int64_t row = samples == n_rows ? i : (int64_t)(((uint64_t)i * 11400714819323198485ull) % (uint64_t)n_rows);
+    if (c.validity != nullptr && !((c.validity[row >> 3] >> (row & 7)) & 1u)) continue;
+    if (c.offsets[row + 1] - c.offsets[row] != 16) ++other;
+  }
+  if (other) atomicAdd(out, (unsigned long long)other);
+}
+
+hipError_t launch_freq_len16_probe(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
+                                   unsigned long long* d_out, hipStream_t stream) {
+  if (n_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(dq_freq_len16_probe_kernel, dim3((16384 + kBlock - 1) / kBlock), dim3(kBlock), 0, stream, ks, d_cols,
+                     n_rows, d_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_freq_stage_raw16(const FreqKeySpec& ks, bool one_string, const DevColumn* d_cols, int64_t n_rows,
+                                   int b1, void* d_out, uint64_t cap1, unsigned long long* d_fill1, FreqRec* d_ovf,
+                                   unsigned long long* d_ovf_n, uint64_t ovf_cap, unsigned int* d_flag, uint32_t* d_hll,
+                                   unsigned long long* d_bad, unsigned long long* d_staged, hipStream_t stream) {
+  if (n_rows <= 0) return hipSuccess;
+  if (b1 < 1 || b1 > kStageBinBits || (!one_string && ks.n_keys != 2)) return hipErrorInvalidValue;
+  const int64_t tiles = (n_rows + kUuidTile - 1) / kUuidTile;
+  int dev = 0, cus = 256, per_cu = 2;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (one_string)
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dq_freq_stage_raw16_kernel<true>, kStageThreads, 0);
+  else
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dq_freq_stage_raw16_kernel<false>, kStageThreads, 0);
+  const int64_t resident = (int64_t)cus * (per_cu > 0 ? per_cu : 1);
+  const int64_t blocks = tiles < resident ? tiles : resident;
+  if (one_string)
+    hipLaunchKernelGGL(dq_freq_stage_raw16_kernel<true>, dim3((unsigned)blocks), dim3(kStageThreads), 0, stream, ks, d_cols,
+                       n_rows, b1, static_cast<Raw16Rec*>(d_out), cap1, d_fill1, d_ovf, d_ovf_n, ovf_cap, d_flag, d_hll,
+                       d_bad, d_staged);
+  else
+    hipLaunchKernelGGL(dq_freq_stage_raw16_kernel<false>, dim3((unsigned)blocks), dim3(kStageThreads), 0, stream, ks, d_cols,
+                       n_rows, b1, static_cast<Raw16Rec*>(d_out), cap1, d_fill1, d_ovf, d_ovf_n, ovf_cap, d_flag, d_hll,
+                       d_bad, d_staged);
   return hipGetLastError();
 }
 

@@ -193,6 +193,13 @@ struct alignas(16) UuidRec {
   unsigned long long lo, hi;
 };
 
+// A staged row of a 16-byte key (round 6): a single string column of 16-byte keys, or two 8-byte
+// fixed-width columns (make_key's encoding: the two values' little-endian bits) -- the key bytes
+// themselves, hashed as every 16-byte key is (hash_inline) and written inline into its slot.
+struct alignas(16) Raw16Rec {
+  unsigned long long lo, hi;
+};
+
 struct FreqTable {
   FreqSlot* slots;
   uint64_t mask;                   // capacity - 1 (capacity: a power of two >= kFreqSliceSlots)
@@ -355,7 +362,7 @@ hipError_t launch_freq_part(const void* d_in, uint64_t in_n, const unsigned long
                             unsigned long long* d_out_fill, FreqRec* d_ovf, unsigned long long* d_ovf_n,
                             uint64_t ovf_cap, unsigned int* d_flag, int rec_kind, hipStream_t stream,
                             unsigned long long* d_staged = nullptr);
-constexpr int kRecFree = 0, kRecPacked = 1, kRecHashed = 2, kRecUuid = 3;  // FreqRec, packed word, HashRec, UuidRec
+constexpr int kRecFree = 0, kRecPacked = 1, kRecHashed = 2, kRecUuid = 3, kRecRaw16 = 4;  // FreqRec, packed word, HashRec, UuidRec, Raw16Rec
 // With an empty table it can also produce the count-of-counts histogram (d_hist, counts >=
 // kFreqHist into d_big), each slice's largest count (d_smax) and write every slot (write_all:
 // the table needs no clearing).
@@ -413,7 +420,17 @@ hipError_t launch_freq_stage_uuid(const FreqKeySpec& ks, const DevColumn* d_cols
                                   uint64_t cap1, unsigned long long* d_fill1, FreqRec* d_ovf, unsigned long long* d_ovf_n,
                                   uint64_t ovf_cap, unsigned int* d_flag, uint32_t* d_hll, unsigned long long* d_bad,
                                   unsigned long long* d_staged, hipStream_t stream);
-hipError_t launch_freq_uuid_to_hashed(const FreqTable& T, FreqRec* d_recs, uint64_t n, hipStream_t stream);
+hipError_t launch_freq_uuid_to_hashed(const FreqTable& T, FreqRec* d_recs, uint64_t n, hipStream_t stream,
+                                      int rec_kind = kRecUuid);
+// The 16-byte-key form (Raw16Rec): stage + level-1 split of one string column of 16-byte keys
+// (d_bad: non-NULL keys of another length) or of two 8-byte fixed-width columns.
+hipError_t launch_freq_stage_raw16(const FreqKeySpec& ks, bool one_string, const DevColumn* d_cols, int64_t n_rows,
+                                   int b1, void* d_out, uint64_t cap1, unsigned long long* d_fill1, FreqRec* d_ovf,
+                                   unsigned long long* d_ovf_n, uint64_t ovf_cap, unsigned int* d_flag, uint32_t* d_hll,
+                                   unsigned long long* d_bad, unsigned long long* d_staged, hipStream_t stream);
+// Sampled non-NULL keys of a single string column whose length is not 16, added to d_out[0].
+hipError_t launch_freq_len16_probe(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows,
+                                   unsigned long long* d_out, hipStream_t stream);
 // Sampled rows (16384 scattered, as the pack probe) whose encoded key (make_key) is longer than
 // 15 bytes, added to *d_out: a multi-column table's choice of hashed records from the start.
 hipError_t launch_freq_len_probe(const FreqKeySpec& ks, const DevColumn* d_cols, int64_t n_rows, unsigned long long* d_out,

@@ -298,12 +298,12 @@ class FrequencyTable:
 
     def paths(self) -> Dict[str, int]:
         """Which group-by paths this table's groupings took (dq_diag_freq_paths; tests)."""
-        out = (ctypes.c_int64 * 13)()
+        out = (ctypes.c_int64 * 14)()
         L.check(L.lib().dq_diag_freq_paths(self.handle, out))
         return {"slots": out[0], "partition_runs": out[1], "slice_bits": out[2], "sort_records": out[3],
                 "packed_runs": out[4], "small_runs": out[5], "wait_timeouts": out[6],
                 "import_coarse_runs": out[7], "import_skipped_runs": out[8], "hashed_runs": out[9],
-                "hashed_inserts": out[10], "compacted": out[11], "uuid_runs": out[12]}
+                "hashed_inserts": out[10], "compacted": out[11], "uuid_runs": out[12], "raw16_runs": out[13]}
 
     def merge_from(self, other: "FrequencyTable") -> None:
         """self += other, device to device."""

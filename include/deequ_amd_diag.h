@@ -32,7 +32,8 @@ dq_status dq_diag_hash_rate(int device, int with_hll, int reps, double* hashes_p
  * aggregations of hashed records (long or multi-column keys), out[10] = hashed records inserted
  * globally (slices handed back, tables that already held groups), out[11] = 1 while the table is
  * compacted (occupied slots only), out[12] = partition-path aggregations of canonical UUID records
- * (dq_uuidpack.h).  `out` holds 13 values. */
+ * (dq_uuidpack.h), out[13] = partition-path aggregations of 16-byte-key records (16-byte strings,
+ * two 8-byte key columns).  `out` holds 14 values. */
 dq_status dq_diag_freq_paths(dq_freq* f, int64_t* out);
 
 /* Test hooks of one table (tests only; never set by the product): flags = 1 makes claimed

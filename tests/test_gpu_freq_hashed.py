@@ -271,3 +271,62 @@ def test_uuid_slices_handed_back(gpu, part, monkeypatch):
     assert set(c.tolist()) == {2} and len(c) == len(range(0, n, 7))  # (top-N keeps the ties)
     assert sorted(k) == sorted(_uuid(v).encode() for v in range(0, n, 7))
     t.close()
+
+
+# ---- 16-byte keys (Raw16Rec): a single string column of 16-byte keys, or two 8-byte key columns
+# (make_key's encoding is then the two values' 16 bytes): the record is the key, compared in LDS
+# and written inline into its slot.
+
+def test_int64_pair_keys_against_oracle(gpu, part, monkeypatch):
+    """(int64, int64) keys with NULLs in either column and negative values: 16-byte-key records,
+    groups equal to the oracle's FrequenciesAndNumRows (GroupingAnalyzers.scala:53-80)."""
+    monkeypatch.setenv("DQ_FREQ_PART_SLOTS", str(1 << 20))
+    rng = np.random.default_rng(83)
+    n = 150_000
+    a = rng.integers(-2000, 2000, n)
+    b = rng.integers(0, 300, n)
+    spec = {"a": ["int64", [None if i % 29 == 0 else int(a[i]) for i in range(n)]],
+            "b": ["int64", [None if i % 31 == 0 else int(b[i]) * 1_000_000_007 for i in range(n)]]}
+    table = product_table(spec)
+    t = FrequencyTable(["a", "b"], dict(table.schema))
+    t.reserve(n)
+    t.consume(table)
+    st = O.frequencies_state(oracle_table(spec), ["a", "b"])
+    want = {encode_key(list(k), ["int64", "int64"]): c for k, c in st.frequencies.items()}
+    assert _export(t) == want
+    paths = t.paths()
+    assert paths["raw16_runs"] >= 1 and paths["hashed_inserts"] == 0, paths
+    k = next(iter(want))
+    assert t.lookup(k) == want[k]
+    t.close()
+
+
+def test_16_byte_string_keys_against_hashed(gpu, part, monkeypatch):
+    """16-character keys (hex ids) with NULLs: 16-byte-key records against hashed records
+    (DQ_FREQ_UUID=0): equal exports, summaries and top-N, exact against Python counts; then a
+    batch with a 17-byte key is rolled back to hashed records."""
+    monkeypatch.setenv("DQ_FREQ_PART_SLOTS", str(1 << 20))
+    rng = np.random.default_rng(89)
+    keys = [None if i % 43 == 0 else "%016x" % (int(v) * 0x9E3779B97F4A7C15 % 2 ** 64)
+            for i, v in enumerate(rng.integers(0, 300_000, 700_000))]
+    want = _count(keys)
+    got = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("DQ_FREQ_UUID", mode)
+        t = _consume(keys, False, 2)
+        paths = t.paths()
+        assert (paths["raw16_runs"] >= 1) == (mode == "1"), paths
+        s = t.summary()
+        top_c, top_k = t.top(5)
+        got[mode] = (_export(t), (s.num_groups, s.num_unique, s.grouped_rows), sorted(zip(top_c.tolist(), top_k)))
+        t.close()
+    assert got["1"][0] == want and got["1"] == got["0"]
+    monkeypatch.setenv("DQ_FREQ_UUID", "1")
+    b2 = keys[:200_000] + ["x" * 17]
+    t = FrequencyTable(["key"], {"key": "string"})
+    t.reserve(len(keys) + len(b2))
+    t.consume(d.Table.from_pydict({"key": ("string", keys)}))
+    t.consume(d.Table.from_pydict({"key": ("string", b2)}))
+    assert _export(t) == _count(keys + b2)
+    assert t.paths()["raw16_runs"] >= 1
+    t.close()
