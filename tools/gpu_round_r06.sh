@@ -13,7 +13,7 @@ TAG=${TAG:-r06}
 case "${PART:-a}" in
   a) TAG=$TAG bash tools/gpu_check.sh || exit $? ;;
   b)
-    for v in ${SET:-c1: c3: c4: c4_alnum:--c4-keys,alnum c4_uuid:--c4-keys,uuid c4_pair:--c4-keys,pair c5:}; do
+    for v in ${SET:-c1: c3: c4: c4_alnum:--c4-keys,alnum c4_uuid:--c4-keys,uuid c4_pair:--c4-keys,pair c4_pair64:--c4-keys,pair64 c5:}; do
       name=${v%%:*}; args=$(echo "${v#*:}" | tr ',' ' '); W=${name%%_*}
       timeout -k 10 400 python -u bench.py --workload $W --steps ${STEPS:-5} --warmup 2 $args \
         > "$OUT/bench_${name}_$TAG.log" 2>&1
