@@ -224,20 +224,19 @@ class ApproxCountDistinctState(State):
     KIND = L.DQ_OP_APPROX_COUNT_DISTINCT
 
     def __init__(self, words: Sequence[int]):
-        words = tuple(int(w) for w in words)
+        words = tuple(map(int, words))
         if len(words) != L.DQ_HLL_NUM_WORDS:
             raise ValueError("requirement failed: expected %d words" % L.DQ_HLL_NUM_WORDS)
         self.words: Tuple[int, ...] = words
 
     def to_dq(self):
         s = self._dq()
-        for i, w in enumerate(self.words):
-            s.words[i] = w
+        s.words[:] = self.words
         return s
 
     @classmethod
     def from_dq(cls, s):
-        return cls(list(s.words))
+        return cls(s.words[:])
 
     def to_bytes(self) -> bytes:
         """DeequHyperLogLogPlusPlusUtils.wordsToBytes (StatefulHyperloglogPlus.scala:170-178)."""
