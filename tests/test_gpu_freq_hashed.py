@@ -14,6 +14,8 @@ each record of a hash group compared byte for byte with the group's first.  Chec
   reserved rows) and tables of fewer than 2^20 slots: the global inserts (exact, slower);
 * every operation after it (summary, top, export, lookup, merge, further batches).
 """
+import struct
+
 import numpy as np
 import pytest
 
@@ -329,4 +331,48 @@ def test_16_byte_string_keys_against_hashed(gpu, part, monkeypatch):
     t.consume(d.Table.from_pydict({"key": ("string", b2)}))
     assert _export(t) == _count(keys + b2)
     assert t.paths()["raw16_runs"] >= 1
+    t.close()
+
+
+def _oracle_float_key(k, dtypes):
+    # the oracle keys floats by their bits (-0.0 and 0.0 apart): back to the float of those bits
+    return [struct.unpack("<d", struct.pack("<Q", v[1]))[0] if t == "float64" else v for v, t in zip(k, dtypes)]
+
+
+@pytest.mark.parametrize("dtypes", [("int64", "float64"), ("float64", "float64")])
+def test_float_pair_keys_group_by_bits(gpu, part, monkeypatch, dtypes):
+    """Two 8-byte key columns with a float64 among them, holding 0.0 and -0.0, NaN, +-inf and
+    NULLs: 16-byte-key records; groups equal to the oracle's, which keys floats by their bits
+    (Spark 2.2 groups by the UnsafeRow bytes: -0.0 and 0.0 are different groups)."""
+    monkeypatch.setenv("DQ_FREQ_PART_SLOTS", str(1 << 20))
+    rng = np.random.default_rng(97)
+    n = 160_000
+    special = [0.0, -0.0, float("nan"), float("inf"), -float("inf")]
+
+    def col(t, salt):
+        out = []
+        for i, v in enumerate(rng.integers(0, 3000, n)):
+            if (i + salt) % 37 == 0:
+                out.append(None)
+            elif t == "int64":
+                out.append(int(v) - 1500)
+            elif v % 11 == 0:
+                out.append(special[int(v) % len(special)])
+            else:
+                out.append(float(v % 700) * 0.25 - 40.0)
+        return out
+    spec = {"a": [dtypes[0], col(dtypes[0], 0)], "b": [dtypes[1], col(dtypes[1], 5)]}
+    table = product_table(spec)
+    t = FrequencyTable(["a", "b"], dict(table.schema))
+    t.reserve(n)
+    t.consume(table)
+    st = O.frequencies_state(oracle_table(spec), ["a", "b"])
+    want = {encode_key(_oracle_float_key(k, dtypes), list(dtypes)): c for k, c in st.frequencies.items()}
+    assert _export(t) == want
+    zero = {k[8:] for k in want} if dtypes[0] == "int64" else {k[:8] for k in want}
+    assert struct.pack("<d", 0.0) in zero and struct.pack("<d", -0.0) in zero
+    paths = t.paths()
+    assert paths["raw16_runs"] >= 1 and paths["hashed_inserts"] == 0, paths
+    s = t.summary()
+    assert (s.num_groups, s.num_rows) == (len(want), n)
     t.close()
